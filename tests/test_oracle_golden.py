@@ -1,0 +1,90 @@
+"""Pin the CPU oracle against the reference's own outputs (CPU only).
+
+The golden vectors were produced by running the reference
+``FedAvgTrainer.aggregate`` (fedavg_trainer.py:441-458) in the build
+container (oracle/gen_golden.py).  Both oracle restatements -- the torch loop
+(also the bench's CPU baseline) and the numpy one -- must reproduce them bit
+for bit.
+"""
+import copy
+import hashlib
+
+import numpy as np
+import pytest
+import torch
+
+import fedavg_oracle as O
+from golden_io import bits_equal, case_names, load_case
+
+CASES = case_names()
+
+
+def test_golden_present():
+    assert len(CASES) >= 20
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_golden_sha256(name):
+    meta, _, expected = load_case(name)
+    for k in meta["out_keys"]:
+        t = expected[k["name"]]
+        if t.dtype == torch.bfloat16:
+            raw = t.view(torch.int16).numpy()
+        else:
+            raw = t.numpy()
+        assert hashlib.sha256(np.ascontiguousarray(raw).tobytes()).hexdigest() == k["sha256"]
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_torch_restatement_matches_reference(name):
+    meta, w_locals, expected = load_case(name)
+    if meta["K"] == 0:
+        pytest.skip("empty w_locals is covered by test_empty_case")
+    first = w_locals[0][1]
+    out = O.aggregate_torch(w_locals)
+    assert out is first  # fedavg_trainer.py:449 aliasing
+    assert list(out.keys()) == list(expected.keys())
+    for k in expected:
+        assert bits_equal(out[k], expected[k]), k
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_numpy_restatement_matches_reference(name):
+    meta, w_locals, expected = load_case(name)
+    if meta["K"] == 0:
+        pytest.skip("empty")
+    bf16 = [k["name"] for k in meta["in_keys"] if k["dtype"] == "bfloat16"]
+    np_locals = []
+    for n, sd in w_locals:
+        np_locals.append((n, {k: (v.view(torch.int16).numpy() if v.dtype == torch.bfloat16 else v.numpy())
+                              for k, v in sd.items()}))
+    out = O.aggregate_numpy(np_locals, bf16_keys=bf16)
+    for k, exp in expected.items():
+        got = out[k]
+        if exp.dtype == torch.bfloat16:
+            got_t = torch.from_numpy(np.asarray(got).astype(np.uint16).view(np.int16).copy()).view(torch.bfloat16)
+        else:
+            got_t = torch.from_numpy(np.array(got))
+        assert bits_equal(got_t.reshape(exp.shape), exp), k
+
+
+def test_empty_case():
+    meta, w_locals, expected = load_case("empty_w_locals")
+    assert meta["K"] == 0 and not meta["aliased"]
+    torch.manual_seed(0)
+    glob = torch.nn.Linear(5, 3)
+    out = O.empty_result(glob)
+    for k in expected:
+        assert bits_equal(out[k], expected[k])
+
+
+def test_zero_total_raises():
+    with pytest.raises(ZeroDivisionError):
+        O.sample_weights([0, 0])
+
+
+def test_int64_example_value():
+    # survey-verified: nbt 7, 8, 9 with n = 10, 20, 30 -> 8.3333 (fp32)
+    _, _, expected = load_case("int64_nbt_example")
+    assert expected["nbt"].dtype == torch.float32
+    assert abs(float(expected["nbt"]) - 8.333333) < 1e-5
