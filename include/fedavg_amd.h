@@ -1,0 +1,114 @@
+/*
+ * fedavg_amd.h -- C ABI of the MI355X (gfx950) FedAvg weighted reduction.
+ *
+ * Replaces the inner loop of the reference's
+ *     FedAvgTrainer.aggregate(self, w_locals)        src/fedavg_trainer.py:441-458
+ * i.e. for every parameter element p:
+ *     out[p] = (((x[0][p]*w[0]) + x[1][p]*w[1]) + ...) + x[K-1][p]*w[K-1]
+ * computed in the reference's order (client 0 first, a multiply then an add
+ * per client, never fused), so fp32 results are bit-identical to the
+ * reference's torch CPU loop (fedavg_trainer.py:451-457).
+ *
+ * The reference has no FFI: its boundary is the Python method above.  These
+ * entry points are what the Python drop-in (mobile-federated-learning_amd/)
+ * binds through ctypes; INTEGRATION.md shows the binding.  The weight vector
+ * w[i] = float(n_i / sum(n)) is formed on the host exactly as
+ * fedavg_trainer.py:444-447,453 forms it (Python double, rounded to fp32 by
+ * ATen), see fedavg_weights_f32() below.
+ *
+ * Conventions (all functions):
+ *   - every buffer argument is DEVICE memory owned by the caller; nothing is
+ *     allocated inside; calls are asynchronous and ordered on `stream`
+ *     (a hipStream_t; NULL = the default stream), reentrant across streams;
+ *   - return 0 on success, a negative FEDAVG_E* code for a rejected argument,
+ *     or -(hipError_t) for a launch failure; fedavg_last_error() gives a
+ *     thread-local message for the last failing call on this thread;
+ *   - K == 0 is rejected (the reference returns the global model then,
+ *     fedavg_trainer.py:442-443 -- the host layer handles that case);
+ *     P == 0 is a no-op.
+ */
+#ifndef FEDAVG_AMD_H
+#define FEDAVG_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FEDAVG_OK 0
+#define FEDAVG_EINVAL (-10001)   /* bad size / stride / null pointer     */
+#define FEDAVG_EALIGN (-10002)   /* misaligned buffer for this entry     */
+#define FEDAVG_EMODE (-10003)    /* unknown mode / variant               */
+
+/* ABI version: bumped on any signature change. */
+int fedavg_abi_version(void);
+
+/* Thread-local message for the last failing call on this thread ("" if none). */
+const char* fedavg_last_error(void);
+
+/*
+ * fp32 sequential (bit-exact) reduce over a client-major packed buffer.
+ *   clients : [K, ld] row-major fp32, row i = client i's flattened state_dict
+ *             (fedavg_trainer.py:199 w_locals[i][1], keys concatenated in the
+ *             order of w_locals[0][1].keys(), :450)
+ *   weights : [K] fp32, weights[i] = fp32(n_i / N)                (:453)
+ *   out     : [P] fp32
+ *   ld      : row stride in elements, ld >= P.
+ * Fast path: clients 16-B aligned and ld % 4 == 0 (float4 streaming); any
+ * other alignment takes a scalar path with identical results.
+ */
+int fedavg_reduce_f32(const float* clients, int64_t K, int64_t P, int64_t ld,
+                      const float* weights, float* out, void* stream);
+
+/*
+ * Same reduction over K separate device buffers (no packing):
+ *   client_ptrs : DEVICE array [K] of device pointers, each to >= P floats.
+ * Each pointer may have any 4-byte alignment (checked per client on device).
+ */
+int fedavg_reduce_ptrs_f32(const float* const* client_ptrs, int64_t K, int64_t P,
+                           const float* weights, float* out, void* stream);
+
+/*
+ * fp64 keys keep fp64 (reference: `tensor_f64 * python_float` stays double,
+ * the weight is not rounded to fp32).  weights : [K] double.
+ */
+int fedavg_reduce_f64(const double* clients, int64_t K, int64_t P, int64_t ld,
+                      const double* weights, double* out, void* stream);
+
+/*
+ * fp16 / bf16 keys keep their dtype; each multiply and each add is computed
+ * in fp32 and rounded to the storage type (ATen opmath), as the reference's
+ * `acc += p * w` does for a half tensor.  Values are passed as raw 16-bit
+ * patterns.  weights : [K] fp32.
+ */
+int fedavg_reduce_f16(const uint16_t* clients, int64_t K, int64_t P, int64_t ld,
+                      const float* weights, uint16_t* out, void* stream);
+int fedavg_reduce_bf16(const uint16_t* clients, int64_t K, int64_t P, int64_t ld,
+                       const float* weights, uint16_t* out, void* stream);
+
+/*
+ * Tolerance-gated split-client variant (NOT bit-exact with the reference):
+ * the client axis is cut into `splits` contiguous groups (1, 2, 4 or 8),
+ * each group's partial sum is kept in registers, staged through LDS and the
+ * groups are combined in a fixed order.  Deterministic run to run; matches
+ * the reference within norm-wise relative 1e-6 on model-like data.  Useful
+ * where P is too small to fill the GPU.  splits == 1 is the exact kernel.
+ */
+int fedavg_reduce_splitk_f32(const float* clients, int64_t K, int64_t P, int64_t ld,
+                             const float* weights, float* out, int splits, void* stream);
+
+/*
+ * Host helper: weights[i] = (float)((double)n_i / (double)sum(n)) for integer
+ * sample counts, exactly as Python's int/int true division followed by ATen's
+ * double->float cast (fedavg_trainer.py:444-447,453).  Counts must be >= 0
+ * and sum to a value <= 2^53; returns FEDAVG_EINVAL on a zero sum (the
+ * reference raises ZeroDivisionError).  `weights` is HOST memory.
+ */
+int fedavg_weights_f32(const int64_t* sample_nums, int64_t K, float* weights);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FEDAVG_AMD_H */

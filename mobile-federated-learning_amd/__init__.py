@@ -1,0 +1,43 @@
+"""MI355X-native FedAvg server-side weighted reduction (drop-in for the
+reference's ``FedAvgTrainer.aggregate``, src/fedavg_trainer.py:441-458).
+
+Importable as ``mfl_amd`` (see ``/mfl_amd.py`` at the repo root; the
+directory name itself is not a Python identifier).
+
+Layers:
+  csrc/fedavg_reduce.hip   gfx950 kernels + C ABI (include/fedavg_amd.h)
+  _lib                     ctypes binding, fails loudly if the .so is missing
+  reduce                   device-resident entry points (torch tensors in HBM)
+  layout                   state_dict <-> packed [K, ld] client-major buffers
+  aggregate                the drop-in (DeviceAggregator, install, mixin)
+  distributed              P-sharded multi-GPU reduce + RCCL all-gather
+"""
+from ._lib import FedAvgLibraryError, library_path
+from .aggregate import (
+    DeviceAggregator,
+    FedAvgAggregateMixin,
+    aggregate,
+    default_aggregator,
+    install,
+    sample_weights,
+)
+from .layout import KeyTable, ShapeMismatchError, result_dtype
+from .reduce import ALIGN_ELEMS, reduce_packed, reduce_tensors, weights_tensor
+
+__all__ = [
+    "FedAvgLibraryError",
+    "library_path",
+    "DeviceAggregator",
+    "FedAvgAggregateMixin",
+    "aggregate",
+    "default_aggregator",
+    "install",
+    "sample_weights",
+    "KeyTable",
+    "ShapeMismatchError",
+    "result_dtype",
+    "ALIGN_ELEMS",
+    "reduce_packed",
+    "reduce_tensors",
+    "weights_tensor",
+]

@@ -1,0 +1,82 @@
+"""ctypes binding of libfedavg_amd.so (the C ABI in include/fedavg_amd.h).
+
+There is no fallback: if the HIP library is missing or does not export the
+declared entry points, every product call raises ``FedAvgLibraryError``.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+from pathlib import Path
+
+from .build import LIB_PATH
+
+_c_i64 = ctypes.c_int64
+_c_int = ctypes.c_int
+_vp = ctypes.c_void_p
+
+# name -> (restype, argtypes); mirrors include/fedavg_amd.h + fedavg_amd_tuning.h
+SIGNATURES = {
+    "fedavg_abi_version": (_c_int, []),
+    "fedavg_last_error": (ctypes.c_char_p, []),
+    "fedavg_reduce_f32": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp]),
+    "fedavg_reduce_ptrs_f32": (_c_int, [_vp, _c_i64, _c_i64, _vp, _vp, _vp]),
+    "fedavg_reduce_f64": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp]),
+    "fedavg_reduce_f16": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp]),
+    "fedavg_reduce_bf16": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp]),
+    "fedavg_reduce_splitk_f32": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_int, _vp]),
+    "fedavg_weights_f32": (_c_int, [_vp, _c_i64, _vp]),
+    "fedavg_reduce_f32_tuned": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_int, _c_int, _vp]),
+}
+
+ABI_VERSION = 1
+
+FEDAVG_EINVAL = -10001
+FEDAVG_EALIGN = -10002
+FEDAVG_EMODE = -10003
+
+
+class FedAvgLibraryError(RuntimeError):
+    """libfedavg_amd.so is missing, stale, or a call into it failed."""
+
+
+_lock = threading.Lock()
+_lib = None
+
+
+def library_path() -> Path:
+    return LIB_PATH
+
+
+def load() -> ctypes.CDLL:
+    """Load (once) and type the HIP library; raise loudly if unavailable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not LIB_PATH.exists():
+            raise FedAvgLibraryError(
+                f"{LIB_PATH} not built: run __graft_entry__.build() (hipcc --offload-arch=gfx950); "
+                "there is no CPU fallback for the FedAvg reduction"
+            )
+        lib = ctypes.CDLL(str(LIB_PATH))
+        for name, (res, args) in SIGNATURES.items():
+            try:
+                fn = getattr(lib, name)
+            except AttributeError as e:
+                raise FedAvgLibraryError(f"{LIB_PATH} does not export {name}") from e
+            fn.restype = res
+            fn.argtypes = args
+        ver = lib.fedavg_abi_version()
+        if ver != ABI_VERSION:
+            raise FedAvgLibraryError(f"ABI version {ver} != expected {ABI_VERSION}; rebuild the library")
+        _lib = lib
+    return _lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load().fedavg_last_error().decode(errors="replace")
+        raise FedAvgLibraryError(f"{what} failed (rc={rc}): {msg}")

@@ -1,0 +1,235 @@
+"""Drop-in replacement for ``FedAvgTrainer.aggregate`` (fedavg_trainer.py:441-458).
+
+Same signature, same return object, same dtypes and same fp32 bits as the
+reference's torch CPU loop; the weighted sum itself runs in the gfx950 HIP
+kernel (libfedavg_amd.so).  Host code stays Python on PyTorch-ROCm.
+
+Use it in the reference's standalone loop without touching ``main_fedavg.py``::
+
+    import mfl_amd
+    from fedavg_trainer import FedAvgTrainer       # reference class
+    mfl_amd.install(FedAvgTrainer)                 # patches .aggregate
+
+or subclass: ``class Trainer(mfl_amd.FedAvgAggregateMixin, FedAvgTrainer)``.
+
+Contract kept from the reference:
+* ``w_locals`` is a list of ``(sample_num, state_dict)`` (fedavg_trainer.py:199);
+* empty list -> ``deepcopy(self.model_global.cpu().state_dict())`` (:442-443);
+* weights ``n_i / sum(n)`` are Python doubles (:444-447, :453), rounded to
+  fp32 once (ATen's scalar cast) for fp32/fp16/bf16 keys, kept double for fp64;
+* the returned object IS ``w_locals[0][1]`` (:449), its values replaced by new
+  tensors of the key's shape in the reference's result dtype (integer keys come
+  back fp32, :455); other clients' dicts are untouched;
+* a key missing in a later client raises ``KeyError``; a zero sample total
+  raises ``ZeroDivisionError``.
+Deliberate tightening: differing shapes or dtypes for one key raise
+(``ShapeMismatchError`` / ``TypeError``) instead of broadcasting.
+Representation difference: the returned tensors of one dtype group are views
+of one freshly allocated host buffer (values and shapes are the reference's;
+``load_state_dict`` at fedavg_trainer.py:219 copies them out).
+"""
+from __future__ import annotations
+
+import copy
+import threading
+import time
+from collections import OrderedDict
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from . import _lib
+from .layout import KeyTable
+from .reduce import reduce_packed, weights_tensor
+
+__all__ = [
+    "sample_weights",
+    "prepare",
+    "DeviceAggregator",
+    "aggregate",
+    "FedAvgAggregateMixin",
+    "install",
+    "default_aggregator",
+]
+
+
+def sample_weights(sample_nums: Sequence) -> List[float]:
+    """``n_i / sum(n)`` as Python numbers (fedavg_trainer.py:444-447, :453)."""
+    training_num = 0
+    for n in sample_nums:
+        training_num += n
+    return [n / training_num for n in sample_nums]
+
+
+class _Prepared(tuple):
+    """(acc_dict, KeyTable, state_dicts, weights) for a non-trivial call."""
+
+
+def prepare(w_locals, model_global=None):
+    """Host-side part of ``aggregate``: the reference's early returns and errors.
+
+    Returns either the final answer (empty ``w_locals`` -> copy of the global
+    model state, fedavg_trainer.py:442-443; state_dicts without keys -> the
+    untouched ``w_locals[0][1]``) or a ``_Prepared`` tuple for the device.
+    Raises what the reference raises (``ZeroDivisionError`` on a zero sample
+    total, ``KeyError`` on a missing key) and refuses inputs it would have
+    broadcast (``ShapeMismatchError``).  Touches no GPU.
+    """
+    if not w_locals:
+        if model_global is None:
+            raise ValueError("empty w_locals needs model_global (fedavg_trainer.py:442-443)")
+        return copy.deepcopy(model_global.cpu().state_dict())
+    sample_nums = [n for n, _ in w_locals]
+    acc_dict = w_locals[0][1]
+    if len(acc_dict) == 0:
+        sum(sample_nums)  # the reference still forms training_num (:444-447)
+        return acc_dict
+    weights = sample_weights(sample_nums)  # ZeroDivisionError like the reference
+    dicts = [sd for _, sd in w_locals]
+    for i in range(1, len(dicts)):
+        if dicts[i] is acc_dict:
+            raise ValueError(
+                f"w_locals[{i}][1] is the same dict object as w_locals[0][1]; the reference would read "
+                "its own partial sums there (fedavg_trainer.py:199 deep-copies to avoid this)")
+    table = KeyTable(acc_dict)
+    table.validate(dicts)
+    return _Prepared((acc_dict, table, dicts, weights))
+
+
+class _Staging:
+    """Reusable pinned host rows + device buffer for one dtype group."""
+
+    def __init__(self, K: int, ld: int, dtype: torch.dtype, device: torch.device):
+        self.K, self.ld, self.dtype = K, ld, dtype
+        self.host = torch.empty((K, ld), dtype=dtype, pin_memory=True)
+        self.dev = torch.empty((K, ld), dtype=dtype, device=device)
+
+
+class DeviceAggregator:
+    """Runs the FedAvg reduction of host state_dicts on one GPU.
+
+    Keeps pinned staging and device buffers between rounds (a round's K and
+    model are usually stable), packs client ``i`` into its pinned row and
+    starts its H2D copy on a side stream before packing client ``i+1``, so the
+    host packing overlaps the PCIe transfer.
+    """
+
+    def __init__(self, device: Optional[torch.device] = None):
+        if device is None:
+            if not torch.cuda.is_available():
+                raise _lib.FedAvgLibraryError("no HIP device visible: the FedAvg reduction has no CPU fallback")
+            device = torch.device("cuda", torch.cuda.current_device())
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise ValueError("DeviceAggregator needs a cuda (HIP) device")
+        _lib.load()  # fail loudly and early if the HIP library is missing
+        self._staging: Dict[torch.dtype, _Staging] = {}
+        self._copy_stream = None
+        self.last_profile: Dict[str, float] = {}
+
+    # ------------------------------------------------------------------
+    def _staging_for(self, dtype: torch.dtype, K: int, ld: int) -> _Staging:
+        st = self._staging.get(dtype)
+        if st is None or st.K < K or st.ld != ld:
+            st = _Staging(K, ld, dtype, self.device)
+            self._staging[dtype] = st
+        return st
+
+    def aggregate(self, w_locals, model_global=None):
+        """``FedAvgTrainer.aggregate`` semantics; see the module docstring."""
+        prep = prepare(w_locals, model_global)
+        if not isinstance(prep, _Prepared):
+            return prep  # empty list / no keys: answered on the host like the reference
+        acc_dict, table, dicts, weights = prep
+        results = self._reduce_groups(table, dicts, weights)
+        # replace values in place, keeping client 0's key order (fedavg_trainer.py:450-457)
+        for e in table.entries:
+            acc_dict[e.name] = results[e.name]
+        return acc_dict
+
+    def _reduce_groups(self, table: KeyTable, dicts, weights) -> "OrderedDict[str, torch.Tensor]":
+        K = len(dicts)
+        dev = self.device
+        prof = {"pack_h2d_ms": 0.0, "kernel_d2h_ms": 0.0}
+        results: "OrderedDict[str, torch.Tensor]" = OrderedDict()
+        with torch.cuda.device(dev):
+            compute = torch.cuda.current_stream(dev)
+            if self._copy_stream is None:
+                self._copy_stream = torch.cuda.Stream(dev)
+            copy_s = self._copy_stream
+            copy_s.wait_stream(compute)  # previous users of the device buffers are done
+            t0 = time.perf_counter()
+            staged = []
+            for g in table.groups.values():
+                st = self._staging_for(g.dtype, K, g.ld)
+                host, devbuf = st.host[:K], st.dev[:K]
+                for i, sd in enumerate(dicts):
+                    table.pack_into(g, host[i:i + 1], [sd])
+                    with torch.cuda.stream(copy_s):
+                        devbuf[i].copy_(host[i], non_blocking=True)
+                w_dev = weights_tensor(weights, g.dtype, dev)
+                staged.append((g, devbuf, w_dev))
+            compute.wait_stream(copy_s)
+            t1 = time.perf_counter()
+            outs = []
+            for g, devbuf, w_dev in staged:
+                out_dev = reduce_packed(devbuf, w_dev, g.P)
+                out_host = torch.empty(g.P, dtype=g.dtype, pin_memory=True)
+                out_host.copy_(out_dev, non_blocking=True)
+                outs.append((g, out_host))
+            compute.synchronize()
+            t2 = time.perf_counter()
+        for g, out_host in outs:
+            results.update(table.unpack(g, out_host))
+        prof["pack_h2d_ms"] = (t1 - t0) * 1e3
+        prof["kernel_d2h_ms"] = (t2 - t1) * 1e3
+        self.last_profile = prof
+        return results
+
+
+_default: Dict[int, DeviceAggregator] = {}
+_default_lock = threading.Lock()
+
+
+def default_aggregator(device: Optional[torch.device] = None) -> DeviceAggregator:
+    if device is None:
+        if not torch.cuda.is_available():
+            raise _lib.FedAvgLibraryError("no HIP device visible: the FedAvg reduction has no CPU fallback")
+        device = torch.device("cuda", torch.cuda.current_device())
+    device = torch.device(device)
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    with _default_lock:
+        agg = _default.get(idx)
+        if agg is None:
+            agg = DeviceAggregator(torch.device("cuda", idx))
+            _default[idx] = agg
+    return agg
+
+
+def aggregate(w_locals, model_global=None, device: Optional[torch.device] = None):
+    """Functional form of ``FedAvgTrainer.aggregate``."""
+    prep = prepare(w_locals, model_global)
+    if not isinstance(prep, _Prepared):
+        return prep
+    return default_aggregator(device).aggregate(w_locals, model_global=model_global)
+
+
+class FedAvgAggregateMixin:
+    """Mix in ahead of the reference ``FedAvgTrainer`` to run ``aggregate`` on the GPU."""
+
+    fedavg_device: Optional[torch.device] = None
+
+    def aggregate(self, w_locals):  # fedavg_trainer.py:441
+        return aggregate(w_locals, getattr(self, "model_global", None), self.fedavg_device)
+
+
+def install(trainer_cls, device: Optional[torch.device] = None):
+    """Patch ``trainer_cls.aggregate`` (e.g. the reference ``FedAvgTrainer``) in place."""
+
+    def aggregate_method(self, w_locals):
+        return aggregate(w_locals, getattr(self, "model_global", None), device)
+
+    aggregate_method.__doc__ = FedAvgAggregateMixin.aggregate.__doc__
+    aggregate_method.__wrapped_reference__ = getattr(trainer_cls, "aggregate", None)
+    trainer_cls.aggregate = aggregate_method
+    return trainer_cls

@@ -1,0 +1,73 @@
+"""Build recipe for libfedavg_amd.so (gfx950 only).
+
+    python -m mfl_amd.build           # or __graft_entry__.build()
+
+Compiles ``csrc/fedavg_reduce.hip`` with hipcc for ``--offload-arch=gfx950``
+into ``lib/libfedavg_amd.so`` inside the package (in-tree, so the built
+library travels with the repo snapshot to the GPU box).  ``-ffp-contract=off``
+keeps every multiply and add separately rounded (bit parity with the
+reference's ATen CPU ops, fedavg_trainer.py:455-457).
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+PKG_DIR = Path(__file__).resolve().parent
+REPO_DIR = PKG_DIR.parent
+CSRC = PKG_DIR / "csrc" / "fedavg_reduce.hip"
+INCLUDE = REPO_DIR / "include"
+LIB_DIR = PKG_DIR / "lib"
+LIB_PATH = LIB_DIR / "libfedavg_amd.so"
+ARCH = "gfx950"
+
+HIPCC_FLAGS = [
+    f"--offload-arch={ARCH}",
+    "-O3",
+    "-std=c++17",
+    "-fPIC",
+    "-shared",
+    "-ffp-contract=off",
+    "-fno-fast-math",
+    "-Wall",
+]
+
+
+def hipcc_path() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and Path(cand).exists():
+            return cand
+    raise RuntimeError("hipcc not found (ROCm toolchain required to build libfedavg_amd.so)")
+
+
+def sources():
+    return [CSRC, INCLUDE / "fedavg_amd.h", INCLUDE / "fedavg_amd_tuning.h"]
+
+
+def up_to_date() -> bool:
+    if not LIB_PATH.exists():
+        return False
+    t = LIB_PATH.stat().st_mtime
+    return all(p.stat().st_mtime <= t for p in sources())
+
+
+def build(force: bool = False, verbose: bool = False) -> Path:
+    if not force and up_to_date():
+        return LIB_PATH
+    LIB_DIR.mkdir(parents=True, exist_ok=True)
+    tmp = LIB_PATH.with_suffix(".so.tmp")
+    cmd = [hipcc_path(), *HIPCC_FLAGS, f"-I{INCLUDE}", "-o", str(tmp), str(CSRC)]
+    if verbose:
+        print(" ".join(cmd))
+    proc = subprocess.run(cmd, capture_output=True, text=True)
+    if proc.returncode != 0:
+        raise RuntimeError(f"hipcc failed ({proc.returncode}):\n{proc.stdout}\n{proc.stderr}")
+    os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

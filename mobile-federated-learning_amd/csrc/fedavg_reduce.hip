@@ -1,0 +1,536 @@
+// fedavg_reduce.hip -- gfx950 (MI355X / CDNA4) kernels for the FedAvg
+// server-side weighted reduction, plus the C ABI declared in
+// include/fedavg_amd.h.
+//
+// Reference semantics (src/fedavg_trainer.py:441-458): for each element p,
+//     acc = x[0][p] * w[0];  acc = acc + x[i][p] * w[i]  for i = 1..K-1
+// evaluated left to right, one rounding per multiply and per add.  This file
+// is compiled with -ffp-contract=off and also pins `fp contract(off)` below so
+// the multiply+add pair is never fused into v_fma/v_fmac (a fused form rounds
+// once and would not be bit-identical to the reference's ATen CPU ops).
+//
+// Roofline: 2 flops per 4-byte element read -> 0.5 flop/B; the kernels are
+// HBM-read bound (4*K*P bytes in, 4*P out), never MFMA work.  Layout in HBM:
+// one client-major [K, ld] buffer, each row one client's flattened
+// state_dict; thread t owns the 16-byte column slice [4t, 4t+4) of every row
+// and walks the client axis in order, so each wave-instruction reads 1 KiB of
+// one row and a thread keeps UNROLL independent 16-B loads in flight.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+
+#include "fedavg_amd.h"
+#include "fedavg_amd_tuning.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr int kBlock = 256;  // 4 waves of 64
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+
+thread_local char g_err[512] = "";
+
+int set_error(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+int launch_status(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    return set_error(-static_cast<int>(e), "%s: launch failed: %s", what, hipGetErrorString(e));
+  }
+  g_err[0] = '\0';
+  return FEDAVG_OK;
+}
+
+__host__ __device__ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+__host__ __device__ inline bool aligned4(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 3u) == 0; }
+
+template <bool NT, typename T>
+__device__ __forceinline__ T ld(const T* p) {
+  if constexpr (NT) {
+    return __builtin_nontemporal_load(p);
+  } else {
+    return *p;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// fp32, bit-exact, float4 path.  One thread = one 16-B column slice.
+//   X    : [K, ld] fp32 viewed as [K, ld4] float4 (16-B aligned, ld % 4 == 0)
+//   nvec : ceil(P / 4) column slices; the last one stores only `tail` lanes
+//          when P % 4 != 0 (its extra lanes read row padding, never stored).
+// ---------------------------------------------------------------------------
+template <int UNROLL, bool NT, bool OUT_VEC>
+__global__ __launch_bounds__(kBlock) void reduce_f32x4_kernel(
+    const f32x4* __restrict__ X, int K, int64_t ld4, int64_t nvec, int tail,
+    const float* __restrict__ W, float* __restrict__ out) {
+  const int64_t v = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (v >= nvec) return;
+  const f32x4* col = X + v;
+
+  f32x4 acc = ld<NT>(col) * W[0];  // fedavg_trainer.py:455  (i == 0)
+  int k = 1;
+  for (; k + UNROLL <= K; k += UNROLL) {
+    f32x4 xs[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) xs[u] = ld<NT>(col + static_cast<int64_t>(k + u) * ld4);
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const f32x4 term = xs[u] * W[k + u];  // fl32(p_i * w_i)
+      acc = acc + term;                     // fedavg_trainer.py:457
+    }
+  }
+  for (; k < K; ++k) {
+    const f32x4 term = ld<NT>(col + static_cast<int64_t>(k) * ld4) * W[k];
+    acc = acc + term;
+  }
+
+  float* o = out + v * 4;
+  if (tail == 0 || v != nvec - 1) {
+    if constexpr (OUT_VEC) {
+      *reinterpret_cast<f32x4*>(o) = acc;
+    } else {
+      o[0] = acc.x; o[1] = acc.y; o[2] = acc.z; o[3] = acc.w;
+    }
+  } else {
+    o[0] = acc.x;
+    if (tail > 1) o[1] = acc.y;
+    if (tail > 2) o[2] = acc.z;
+  }
+}
+
+// fp32, bit-exact, scalar path for buffers that are not 16-B aligned.
+__global__ __launch_bounds__(kBlock) void reduce_f32_scalar_kernel(
+    const float* __restrict__ X, int K, int64_t ld, int64_t P,
+    const float* __restrict__ W, float* __restrict__ out) {
+  const int64_t p = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (p >= P) return;
+  float acc = X[p] * W[0];
+  for (int k = 1; k < K; ++k) {
+    const float term = X[static_cast<int64_t>(k) * ld + p] * W[k];
+    acc = acc + term;
+  }
+  out[p] = acc;
+}
+
+// fp32, bit-exact, pointer-array path: client k lives at ptrs[k] (device).
+// Alignment is a per-client property, so the branch is wave-uniform.
+template <bool OUT_VEC>
+__global__ __launch_bounds__(kBlock) void reduce_ptrs_f32_kernel(
+    const float* const* __restrict__ ptrs, int K, int64_t P,
+    const float* __restrict__ W, float* __restrict__ out) {
+  const int64_t v = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  const int64_t p0 = v * 4;
+  if (p0 >= P) return;
+  const int n = (P - p0) >= 4 ? 4 : static_cast<int>(P - p0);
+  f32x4 acc;
+  for (int k = 0; k < K; ++k) {
+    const float* base = ptrs[k];
+    f32x4 x;
+    if (n == 4 && aligned16(base)) {
+      x = *reinterpret_cast<const f32x4*>(base + p0);
+    } else {
+      x.x = base[p0];
+      x.y = n > 1 ? base[p0 + 1] : 0.f;
+      x.z = n > 2 ? base[p0 + 2] : 0.f;
+      x.w = n > 3 ? base[p0 + 3] : 0.f;
+    }
+    const f32x4 term = x * W[k];
+    acc = (k == 0) ? term : acc + term;
+  }
+  float* o = out + p0;
+  if (n == 4) {
+    if constexpr (OUT_VEC) {
+      *reinterpret_cast<f32x4*>(o) = acc;
+    } else {
+      o[0] = acc.x; o[1] = acc.y; o[2] = acc.z; o[3] = acc.w;
+    }
+  } else {
+    o[0] = acc.x;
+    if (n > 1) o[1] = acc.y;
+    if (n > 2) o[2] = acc.z;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// fp64: the weight stays a double (ATen opmath for double).  16 B per thread.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void reduce_f64x2_kernel(
+    const f64x2* __restrict__ X, int K, int64_t ld2, int64_t nvec, int tail,
+    const double* __restrict__ W, double* __restrict__ out) {
+  const int64_t v = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (v >= nvec) return;
+  const f64x2* col = X + v;
+  f64x2 acc = col[0] * W[0];
+  int k = 1;
+  for (; k + 4 <= K; k += 4) {
+    f64x2 xs[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) xs[u] = col[static_cast<int64_t>(k + u) * ld2];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const f64x2 term = xs[u] * W[k + u];
+      acc = acc + term;
+    }
+  }
+  for (; k < K; ++k) {
+    const f64x2 term = col[static_cast<int64_t>(k) * ld2] * W[k];
+    acc = acc + term;
+  }
+  double* o = out + v * 2;
+  o[0] = acc.x;
+  if (tail == 0 || v != nvec - 1) o[1] = acc.y;
+}
+
+__global__ __launch_bounds__(kBlock) void reduce_f64_scalar_kernel(
+    const double* __restrict__ X, int K, int64_t ld, int64_t P,
+    const double* __restrict__ W, double* __restrict__ out) {
+  const int64_t p = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (p >= P) return;
+  double acc = X[p] * W[0];
+  for (int k = 1; k < K; ++k) {
+    const double term = X[static_cast<int64_t>(k) * ld + p] * W[k];
+    acc = acc + term;
+  }
+  out[p] = acc;
+}
+
+// ---------------------------------------------------------------------------
+// fp16 / bf16: storage type kept, each op computed in fp32 and rounded back
+// (ATen opmath float):  term = rh(f32(x) * w);  acc = rh(f32(acc) + f32(term)).
+// ---------------------------------------------------------------------------
+struct F16Rule {
+  __device__ static float to_f32(unsigned short h) {
+    _Float16 v;
+    __builtin_memcpy(&v, &h, 2);
+    return static_cast<float>(v);
+  }
+  __device__ static unsigned short from_f32(float f) {
+    const _Float16 v = static_cast<_Float16>(f);  // v_cvt_f16_f32, round to nearest even
+    unsigned short h;
+    __builtin_memcpy(&h, &v, 2);
+    return h;
+  }
+};
+
+struct BF16Rule {
+  __device__ static float to_f32(unsigned short h) {
+    return __uint_as_float(static_cast<unsigned int>(h) << 16);
+  }
+  // c10::BFloat16 round_to_nearest_even: NaN -> 0x7FC0.
+  __device__ static unsigned short from_f32(float f) {
+    if (f != f) return 0x7FC0u;
+    const unsigned int u = __float_as_uint(f);
+    return static_cast<unsigned short>((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+  }
+};
+
+// The fp32 intermediate is made opaque to the instruction selector: without
+// it gfx950 folds fpext -> fmul -> fptrunc into one v_fma_mixlo_f16, which
+// rounds the exact product straight to f16 instead of f32-then-f16.
+__device__ __forceinline__ float opaque(float v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
+template <typename R>
+__device__ __forceinline__ unsigned short half_step(unsigned short acc, unsigned short x, float w, bool first) {
+  const unsigned short term = R::from_f32(opaque(R::to_f32(x) * w));
+  if (first) return term;
+  return R::from_f32(opaque(R::to_f32(acc) + R::to_f32(term)));
+}
+
+// 8 halves (16 B) per thread when aligned; scalar elements otherwise.
+template <typename R>
+__global__ __launch_bounds__(kBlock) void reduce_half_kernel(
+    const unsigned short* __restrict__ X, int K, int64_t ld, int64_t P, bool vec,
+    const float* __restrict__ W, unsigned short* __restrict__ out) {
+  const int64_t v = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (vec) {
+    const int64_t p0 = v * 8;
+    if (p0 >= P) return;
+    const int n = (P - p0) >= 8 ? 8 : static_cast<int>(P - p0);
+    u16x8 acc;
+    for (int k = 0; k < K; ++k) {
+      const u16x8 x = *reinterpret_cast<const u16x8*>(X + static_cast<int64_t>(k) * ld + p0);
+      const float w = W[k];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = half_step<R>(acc[j], x[j], w, k == 0);
+    }
+    if (n == 8) {
+      *reinterpret_cast<u16x8*>(out + p0) = acc;
+    } else {
+      for (int j = 0; j < n; ++j) out[p0 + j] = acc[j];
+    }
+  } else {
+    const int64_t p = v;
+    if (p >= P) return;
+    unsigned short acc = 0;
+    for (int k = 0; k < K; ++k) acc = half_step<R>(acc, X[static_cast<int64_t>(k) * ld + p], W[k], k == 0);
+    out[p] = acc;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Split-client variant (tolerance-gated).  Block = SPLITS waves over the same
+// 64 column slices; wave g owns the contiguous client range
+// [g*K/SPLITS, (g+1)*K/SPLITS), keeps its partial sum in registers, stages
+// it in LDS, and wave 0 combines the partials in group order.
+// ---------------------------------------------------------------------------
+template <int SPLITS>
+__global__ __launch_bounds__(64 * SPLITS) void reduce_splitk_f32x4_kernel(
+    const f32x4* __restrict__ X, int K, int64_t ld4, int64_t nvec, int tail,
+    const float* __restrict__ W, float* __restrict__ out) {
+  __shared__ f32x4 partial[SPLITS][64];
+  const int lane = threadIdx.x & 63;
+  const int g = threadIdx.x >> 6;
+  const int64_t v = static_cast<int64_t>(blockIdx.x) * 64 + lane;
+  const int k0 = static_cast<int>((static_cast<int64_t>(K) * g) / SPLITS);
+  const int k1 = static_cast<int>((static_cast<int64_t>(K) * (g + 1)) / SPLITS);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (v < nvec && k1 > k0) {
+    const f32x4* col = X + v;
+    acc = col[static_cast<int64_t>(k0) * ld4] * W[k0];
+    int k = k0 + 1;
+    for (; k + 8 <= k1; k += 8) {
+      f32x4 xs[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) xs[u] = col[static_cast<int64_t>(k + u) * ld4];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const f32x4 term = xs[u] * W[k + u];
+        acc = acc + term;
+      }
+    }
+    for (; k < k1; ++k) {
+      const f32x4 term = col[static_cast<int64_t>(k) * ld4] * W[k];
+      acc = acc + term;
+    }
+  }
+  partial[g][lane] = acc;
+  __syncthreads();
+  if (g != 0 || v >= nvec) return;
+  f32x4 s = partial[0][lane];
+#pragma unroll
+  for (int j = 1; j < SPLITS; ++j) {
+    // groups with an empty client range (K < SPLITS) contribute nothing
+    const int a = static_cast<int>((static_cast<int64_t>(K) * j) / SPLITS);
+    const int b = static_cast<int>((static_cast<int64_t>(K) * (j + 1)) / SPLITS);
+    if (b > a) s = s + partial[j][lane];
+  }
+  float* o = out + v * 4;
+  if (tail == 0 || v != nvec - 1) {
+    o[0] = s.x; o[1] = s.y; o[2] = s.z; o[3] = s.w;
+  } else {
+    o[0] = s.x;
+    if (tail > 1) o[1] = s.y;
+    if (tail > 2) o[2] = s.z;
+  }
+}
+
+inline unsigned grid_for(int64_t items, int per_block) {
+  return static_cast<unsigned>((items + per_block - 1) / per_block);
+}
+
+int check_common(const void* clients, int64_t K, int64_t P, int64_t ld, const void* weights,
+                 const void* out, const char* what) {
+  if (K <= 0) return set_error(FEDAVG_EINVAL, "%s: K must be >= 1 (got %lld)", what, (long long)K);
+  if (K > INT32_MAX) return set_error(FEDAVG_EINVAL, "%s: K too large", what);
+  if (P < 0) return set_error(FEDAVG_EINVAL, "%s: P must be >= 0", what);
+  if (ld < P) return set_error(FEDAVG_EINVAL, "%s: ld (%lld) < P (%lld)", what, (long long)ld, (long long)P);
+  if (P > 0 && (!clients || !weights || !out)) return set_error(FEDAVG_EINVAL, "%s: null buffer", what);
+  return FEDAVG_OK;
+}
+
+template <int U, bool NT>
+void launch_f32x4(const float* clients, int K, int64_t ld, int64_t P, const float* W, float* out,
+                  hipStream_t s) {
+  const int64_t nvec = (P + 3) / 4;
+  const int tail = static_cast<int>(P & 3);
+  const f32x4* X = reinterpret_cast<const f32x4*>(clients);
+  if (aligned16(out)) {
+    hipLaunchKernelGGL((reduce_f32x4_kernel<U, NT, true>), dim3(grid_for(nvec, kBlock)), dim3(kBlock), 0, s,
+                       X, K, ld / 4, nvec, tail, W, out);
+  } else {
+    hipLaunchKernelGGL((reduce_f32x4_kernel<U, NT, false>), dim3(grid_for(nvec, kBlock)), dim3(kBlock), 0, s,
+                       X, K, ld / 4, nvec, tail, W, out);
+  }
+}
+
+int reduce_f32_impl(const float* clients, int64_t K, int64_t P, int64_t ld, const float* weights,
+                    float* out, hipStream_t s, int unroll, int nontemporal, const char* what) {
+  int rc = check_common(clients, K, P, ld, weights, out, what);
+  if (rc) return rc;
+  if (P == 0) return FEDAVG_OK;
+  if (!aligned4(clients) || !aligned4(out) || !aligned4(weights))
+    return set_error(FEDAVG_EALIGN, "%s: fp32 buffers must be 4-byte aligned", what);
+  const int k = static_cast<int>(K);
+  if (aligned16(clients) && (ld % 4) == 0) {
+    switch (unroll * 2 + (nontemporal ? 1 : 0)) {
+      case 4 * 2 + 0: launch_f32x4<4, false>(clients, k, ld, P, weights, out, s); break;
+      case 4 * 2 + 1: launch_f32x4<4, true>(clients, k, ld, P, weights, out, s); break;
+      case 8 * 2 + 0: launch_f32x4<8, false>(clients, k, ld, P, weights, out, s); break;
+      case 8 * 2 + 1: launch_f32x4<8, true>(clients, k, ld, P, weights, out, s); break;
+      case 16 * 2 + 0: launch_f32x4<16, false>(clients, k, ld, P, weights, out, s); break;
+      case 16 * 2 + 1: launch_f32x4<16, true>(clients, k, ld, P, weights, out, s); break;
+      default: return set_error(FEDAVG_EMODE, "%s: unsupported unroll %d", what, unroll);
+    }
+  } else {
+    hipLaunchKernelGGL(reduce_f32_scalar_kernel, dim3(grid_for(P, kBlock)), dim3(kBlock), 0, s,
+                       clients, k, ld, P, weights, out);
+  }
+  return launch_status(what);
+}
+
+}  // namespace
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+extern "C" {
+
+int fedavg_abi_version(void) { return 1; }
+
+const char* fedavg_last_error(void) { return g_err; }
+
+int fedavg_reduce_f32(const float* clients, int64_t K, int64_t P, int64_t ld, const float* weights,
+                      float* out, void* stream) {
+  return reduce_f32_impl(clients, K, P, ld, weights, out, static_cast<hipStream_t>(stream),
+                         FEDAVG_DEFAULT_UNROLL, FEDAVG_DEFAULT_NONTEMPORAL, "fedavg_reduce_f32");
+}
+
+int fedavg_reduce_f32_tuned(const float* clients, int64_t K, int64_t P, int64_t ld, const float* weights,
+                            float* out, int unroll, int nontemporal, void* stream) {
+  return reduce_f32_impl(clients, K, P, ld, weights, out, static_cast<hipStream_t>(stream), unroll,
+                         nontemporal, "fedavg_reduce_f32_tuned");
+}
+
+int fedavg_reduce_ptrs_f32(const float* const* client_ptrs, int64_t K, int64_t P, const float* weights,
+                           float* out, void* stream) {
+  const char* what = "fedavg_reduce_ptrs_f32";
+  int rc = check_common(client_ptrs, K, P, P, weights, out, what);
+  if (rc) return rc;
+  if (P == 0) return FEDAVG_OK;
+  if (!aligned4(out) || !aligned4(weights)) return set_error(FEDAVG_EALIGN, "%s: out/weights misaligned", what);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t nvec = (P + 3) / 4;
+  if (aligned16(out)) {
+    hipLaunchKernelGGL(reduce_ptrs_f32_kernel<true>, dim3(grid_for(nvec, kBlock)), dim3(kBlock), 0, s,
+                       client_ptrs, static_cast<int>(K), P, weights, out);
+  } else {
+    hipLaunchKernelGGL(reduce_ptrs_f32_kernel<false>, dim3(grid_for(nvec, kBlock)), dim3(kBlock), 0, s,
+                       client_ptrs, static_cast<int>(K), P, weights, out);
+  }
+  return launch_status(what);
+}
+
+int fedavg_reduce_f64(const double* clients, int64_t K, int64_t P, int64_t ld, const double* weights,
+                      double* out, void* stream) {
+  const char* what = "fedavg_reduce_f64";
+  int rc = check_common(clients, K, P, ld, weights, out, what);
+  if (rc) return rc;
+  if (P == 0) return FEDAVG_OK;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const uintptr_t m = 7u;
+  if ((reinterpret_cast<uintptr_t>(clients) | reinterpret_cast<uintptr_t>(out) |
+       reinterpret_cast<uintptr_t>(weights)) & m)
+    return set_error(FEDAVG_EALIGN, "%s: fp64 buffers must be 8-byte aligned", what);
+  if (aligned16(clients) && aligned16(out) && (ld % 2) == 0) {
+    const int64_t nvec = (P + 1) / 2;
+    hipLaunchKernelGGL(reduce_f64x2_kernel, dim3(grid_for(nvec, kBlock)), dim3(kBlock), 0, s,
+                       reinterpret_cast<const f64x2*>(clients), static_cast<int>(K), ld / 2, nvec,
+                       static_cast<int>(P & 1), weights, out);
+  } else {
+    hipLaunchKernelGGL(reduce_f64_scalar_kernel, dim3(grid_for(P, kBlock)), dim3(kBlock), 0, s, clients,
+                       static_cast<int>(K), ld, P, weights, out);
+  }
+  return launch_status(what);
+}
+
+static int reduce_half_entry(bool bf16, const uint16_t* clients, int64_t K, int64_t P, int64_t ld,
+                             const float* weights, uint16_t* out, void* stream, const char* what) {
+  int rc = check_common(clients, K, P, ld, weights, out, what);
+  if (rc) return rc;
+  if (P == 0) return FEDAVG_OK;
+  if ((reinterpret_cast<uintptr_t>(clients) | reinterpret_cast<uintptr_t>(out)) & 1u)
+    return set_error(FEDAVG_EALIGN, "%s: 16-bit buffers must be 2-byte aligned", what);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const bool vec = aligned16(clients) && aligned16(out) && (ld % 8) == 0;
+  const int64_t items = vec ? (P + 7) / 8 : P;
+  const auto* X = reinterpret_cast<const unsigned short*>(clients);
+  auto* O = reinterpret_cast<unsigned short*>(out);
+  if (bf16) {
+    hipLaunchKernelGGL(reduce_half_kernel<BF16Rule>, dim3(grid_for(items, kBlock)), dim3(kBlock), 0, s, X,
+                       static_cast<int>(K), ld, P, vec, weights, O);
+  } else {
+    hipLaunchKernelGGL(reduce_half_kernel<F16Rule>, dim3(grid_for(items, kBlock)), dim3(kBlock), 0, s, X,
+                       static_cast<int>(K), ld, P, vec, weights, O);
+  }
+  return launch_status(what);
+}
+
+int fedavg_reduce_f16(const uint16_t* clients, int64_t K, int64_t P, int64_t ld, const float* weights,
+                      uint16_t* out, void* stream) {
+  return reduce_half_entry(false, clients, K, P, ld, weights, out, stream, "fedavg_reduce_f16");
+}
+
+int fedavg_reduce_bf16(const uint16_t* clients, int64_t K, int64_t P, int64_t ld, const float* weights,
+                       uint16_t* out, void* stream) {
+  return reduce_half_entry(true, clients, K, P, ld, weights, out, stream, "fedavg_reduce_bf16");
+}
+
+int fedavg_reduce_splitk_f32(const float* clients, int64_t K, int64_t P, int64_t ld, const float* weights,
+                             float* out, int splits, void* stream) {
+  const char* what = "fedavg_reduce_splitk_f32";
+  if (splits == 1) return fedavg_reduce_f32(clients, K, P, ld, weights, out, stream);
+  int rc = check_common(clients, K, P, ld, weights, out, what);
+  if (rc) return rc;
+  if (P == 0) return FEDAVG_OK;
+  if (!aligned16(clients) || (ld % 4) != 0 || !aligned4(out))
+    return set_error(FEDAVG_EALIGN, "%s: needs 16-B aligned clients and ld %% 4 == 0", what);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t nvec = (P + 3) / 4;
+  const int tail = static_cast<int>(P & 3);
+  const f32x4* X = reinterpret_cast<const f32x4*>(clients);
+  const unsigned grid = grid_for(nvec, 64);
+  const int k = static_cast<int>(K);
+  switch (splits) {
+    case 2: hipLaunchKernelGGL(reduce_splitk_f32x4_kernel<2>, dim3(grid), dim3(128), 0, s, X, k, ld / 4, nvec, tail, weights, out); break;
+    case 4: hipLaunchKernelGGL(reduce_splitk_f32x4_kernel<4>, dim3(grid), dim3(256), 0, s, X, k, ld / 4, nvec, tail, weights, out); break;
+    case 8: hipLaunchKernelGGL(reduce_splitk_f32x4_kernel<8>, dim3(grid), dim3(512), 0, s, X, k, ld / 4, nvec, tail, weights, out); break;
+    default: return set_error(FEDAVG_EMODE, "%s: splits must be 1, 2, 4 or 8 (got %d)", what, splits);
+  }
+  return launch_status(what);
+}
+
+int fedavg_weights_f32(const int64_t* sample_nums, int64_t K, float* weights) {
+  if (K <= 0 || !sample_nums || !weights) return set_error(FEDAVG_EINVAL, "fedavg_weights_f32: bad arguments");
+  int64_t total = 0;
+  for (int64_t i = 0; i < K; ++i) {
+    if (sample_nums[i] < 0) return set_error(FEDAVG_EINVAL, "fedavg_weights_f32: negative sample count");
+    total += sample_nums[i];
+    if (total > (int64_t(1) << 53)) return set_error(FEDAVG_EINVAL, "fedavg_weights_f32: sum exceeds 2^53");
+  }
+  if (total == 0) return set_error(FEDAVG_EINVAL, "fedavg_weights_f32: sample counts sum to zero (ZeroDivisionError)");
+  const double n = static_cast<double>(total);
+  for (int64_t i = 0; i < K; ++i) {
+    volatile double w = static_cast<double>(sample_nums[i]) / n;  // Python int / int (exact operands)
+    weights[i] = static_cast<float>(w);                             // ATen double -> float scalar cast
+  }
+  g_err[0] = '\0';
+  return FEDAVG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,154 @@
+"""P-sharded FedAvg reduction across the GPUs of one node.
+
+The reference runs everything in one process (no
+collectives).  On MI355X the flattened parameter vector of the global model is
+partitioned over G ranks (one process per GPU, ``torch.distributed`` with the
+``nccl`` backend = RCCL over xGMI).  Every output element depends only on the
+same element of the K clients (fedavg_trainer.py:451-457), so each rank
+reduces its columns with the exact sequential kernel -- no data-path
+communication, bit-identical results -- and ONE exchange step, an all-gather,
+reassembles the averaged model on every rank.
+
+Layout (block-cyclic, so that an all-gather chunk lands contiguously in the
+final vector): with G ranks, C chunks and a block of ``S_c`` columns
+(a multiple of ``ALIGN_ELEMS``), rank ``r`` owns global columns
+
+    [c*G*S_c + r*S_c, c*G*S_c + (r+1)*S_c)    for c = 0..C-1,
+
+stored contiguously as local columns ``[c*S_c, (c+1)*S_c)`` of its
+``[K, C*S_c]`` client buffer.  ``all_gather_into_tensor`` of chunk ``c``
+writes global columns ``[c*G*S_c, (c+1)*G*S_c)`` in order, so the reassembled
+vector needs no permutation.  C = 1 is plain contiguous sharding.
+
+Overlap: the reduce of chunk c+1 runs on the compute stream while RCCL
+gathers chunk c (torch issues the collective on its own stream, ordered after
+the kernel that produced the chunk).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Callable, List, Optional, Sequence
+
+import torch
+import torch.distributed as dist
+
+from .reduce import ALIGN_ELEMS, reduce_packed
+
+__all__ = ["ShardPlan", "plan_shards", "ShardedReducer"]
+
+
+def _round_up(n: int, m: int) -> int:
+    return (n + m - 1) // m * m
+
+
+@dataclass(frozen=True)
+class ShardPlan:
+    P: int  # valid global columns
+    world_size: int
+    rank: int
+    chunks: int
+    block: int  # S_c: columns per (rank, chunk)
+
+    @property
+    def local_cols(self) -> int:
+        return self.chunks * self.block
+
+    @property
+    def padded_P(self) -> int:
+        return self.chunks * self.world_size * self.block
+
+    def global_range(self, chunk: int, rank: Optional[int] = None):
+        r = self.rank if rank is None else rank
+        start = chunk * self.world_size * self.block + r * self.block
+        return start, start + self.block
+
+    def valid_local_cols(self) -> int:
+        """Local columns that map to global columns < P (the rest is padding)."""
+        n = 0
+        for c in range(self.chunks):
+            s, e = self.global_range(c)
+            n += max(0, min(e, self.P) - s)
+        return n
+
+    def local_segments(self):
+        """[(local_start, global_start, length)] of valid columns owned by this rank."""
+        segs = []
+        for c in range(self.chunks):
+            s, e = self.global_range(c)
+            n = max(0, min(e, self.P) - s)
+            if n > 0:
+                segs.append((c * self.block, s, n))
+        return segs
+
+
+def plan_shards(P: int, world_size: int, rank: int, chunks: int = 1, align: int = ALIGN_ELEMS) -> ShardPlan:
+    if P < 0 or world_size < 1 or not (0 <= rank < world_size) or chunks < 1:
+        raise ValueError("bad shard plan arguments")
+    block = max(_round_up(-(-P // (world_size * chunks)), align), align)
+    return ShardPlan(P, world_size, rank, chunks, block)
+
+
+LocalReduce = Callable[[torch.Tensor, torch.Tensor, int, torch.Tensor], None]
+
+
+def _hip_local_reduce(clients: torch.Tensor, weights: torch.Tensor, P: int, out: torch.Tensor) -> None:
+    reduce_packed(clients, weights, P, out)
+
+
+class ShardedReducer:
+    """One rank's part of the P-sharded reduction plus the all-gather.
+
+    ``clients`` is this rank's ``[K, local_cols]`` device buffer (fill it with
+    :meth:`load_from_host` or generate synthetic data in place).  ``step``
+    runs the exact kernel chunk by chunk and all-gathers every chunk into
+    ``self.full`` (``[padded_P]``; the model is ``self.full[:P]``).
+
+    ``local_reduce`` is injectable so the sharding/gather logic can be tested
+    with the ``gloo`` backend on CPU; the product default is the HIP kernel.
+    """
+
+    def __init__(self, K: int, P: int, *, chunks: int = 1, group=None, device=None,
+                 dtype: torch.dtype = torch.float32, local_reduce: Optional[LocalReduce] = None,
+                 gather: bool = True):
+        self.group = group
+        ws = dist.get_world_size(group) if dist.is_initialized() else 1
+        rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.plan = plan_shards(P, ws, rank, chunks)
+        self.K = K
+        self.dtype = dtype
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.local_reduce = local_reduce or _hip_local_reduce
+        self.gather = gather and ws > 1
+        self.clients = torch.empty((K, self.plan.local_cols), dtype=dtype, device=self.device)
+        self.local_out = torch.empty(self.plan.local_cols, dtype=dtype, device=self.device)
+        self.full = (torch.empty(self.plan.padded_P, dtype=dtype, device=self.device)
+                     if self.gather else None)
+
+    # ------------------------------------------------------------------
+    def load_from_host(self, host_clients: torch.Tensor) -> None:
+        """Copy this rank's columns of a host ``[K, >=P]`` buffer (strided H2D)."""
+        if host_clients.shape[0] != self.K:
+            raise ValueError("host buffer has the wrong client count")
+        self.clients.zero_()
+        for lstart, gstart, n in self.plan.local_segments():
+            self.clients[:, lstart:lstart + n].copy_(host_clients[:, gstart:gstart + n], non_blocking=True)
+
+    def step(self, weights: torch.Tensor) -> Optional[torch.Tensor]:
+        """Reduce every local chunk; all-gather each as soon as it is ready."""
+        plan = self.plan
+        S = plan.block
+        works: List = []
+        for c in range(plan.chunks):
+            cols = slice(c * S, (c + 1) * S)
+            out_c = self.local_out[cols]
+            self.local_reduce(self.clients[:, cols], weights, S, out_c)
+            if self.gather:
+                dst = self.full[c * plan.world_size * S:(c + 1) * plan.world_size * S]
+                works.append(dist.all_gather_into_tensor(dst, out_c, group=self.group, async_op=True))
+        for w in works:
+            w.wait()
+        return self.full[:plan.P] if self.gather else None
+
+    def local_model_columns(self):
+        """(local_out views, global ranges) of the valid columns this rank reduced."""
+        return [(self.local_out[l:l + n], (g, g + n)) for l, g, n in self.plan.local_segments()]

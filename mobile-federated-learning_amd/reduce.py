@@ -1,0 +1,147 @@
+"""Device-level entry points: the reduction over device-resident buffers.
+
+These wrap the C ABI (include/fedavg_amd.h) for torch device tensors; torch is
+only plumbing here (HBM allocation and the current HIP stream).  Every call
+is stream-ordered on ``torch.cuda.current_stream()`` unless ``stream`` is
+given, and raises ``FedAvgLibraryError`` if the HIP library is unavailable.
+"""
+from __future__ import annotations
+
+from typing import Optional, Sequence
+
+import torch
+
+from . import _lib
+
+__all__ = ["reduce_packed", "reduce_tensors", "weights_tensor", "ALIGN_ELEMS"]
+
+# Row stride granule of the packed [K, ld] layout: 64 elements (256 B for
+# fp32) keeps every client row 16-B aligned for the float4/double2/8xhalf
+# vector paths and starts each row on its own 256-B boundary.
+ALIGN_ELEMS = 64
+
+_ENTRY = {
+    torch.float32: "fedavg_reduce_f32",
+    torch.float64: "fedavg_reduce_f64",
+    torch.float16: "fedavg_reduce_f16",
+    torch.bfloat16: "fedavg_reduce_bf16",
+}
+
+
+def _stream_handle(stream: Optional[torch.cuda.Stream], device: torch.device) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream(device)
+    return int(s.cuda_stream)
+
+
+def weights_tensor(weights: Sequence[float], dtype: torch.dtype, device) -> torch.Tensor:
+    """Device weight vector: fp32 for fp32/fp16/bf16 groups, fp64 for fp64.
+
+    ``weights`` are the reference's Python doubles ``n_i / N``
+    (fedavg_trainer.py:453); ``torch.tensor(..., float32)`` rounds each one to
+    nearest fp32, exactly the cast ATen applies to the scalar in ``p * w``.
+    """
+    wdt = torch.float64 if dtype == torch.float64 else torch.float32
+    host = torch.tensor([float(w) for w in weights], dtype=wdt)
+    if torch.device(device).type == "cuda":
+        host = host.pin_memory()
+    return host.to(device, non_blocking=True)
+
+
+def _check_device_tensor(t: torch.Tensor, name: str):
+    if not isinstance(t, torch.Tensor) or t.device.type != "cuda":
+        raise ValueError(f"{name} must be a CUDA (HIP) device tensor")
+
+
+def reduce_packed(
+    clients: torch.Tensor,
+    weights: torch.Tensor,
+    P: Optional[int] = None,
+    out: Optional[torch.Tensor] = None,
+    *,
+    splits: int = 1,
+    stream: Optional[torch.cuda.Stream] = None,
+    tuned: Optional[tuple] = None,
+) -> torch.Tensor:
+    """out[p] = sum_i clients[i, p] * weights[i], client 0 first (bit-exact).
+
+    clients : [K, ld] device tensor, row stride ld >= P, unit column stride.
+    weights : [K] device tensor (fp32; fp64 for fp64 clients).
+    P       : number of valid columns (default ``clients.shape[1]``).
+    splits  : 1 = exact sequential kernel; 2/4/8 = split-client fp32 variant
+              (tolerance-gated, not bit-exact).
+    tuned   : (unroll, nontemporal) -- benchmarking hook for the fp32 kernel.
+    """
+    _check_device_tensor(clients, "clients")
+    _check_device_tensor(weights, "weights")
+    if clients.dim() != 2 or clients.stride(1) != 1:
+        raise ValueError("clients must be 2-D [K, ld] with unit column stride")
+    K = clients.shape[0]
+    ld = clients.stride(0) if K > 1 else clients.shape[1]
+    if P is None:
+        P = clients.shape[1]
+    if P > clients.shape[1]:
+        raise ValueError(f"P={P} exceeds clients.shape[1]={clients.shape[1]}")
+    dtype = clients.dtype
+    if dtype not in _ENTRY:
+        raise TypeError(f"unsupported client dtype {dtype}")
+    wdt = torch.float64 if dtype == torch.float64 else torch.float32
+    if weights.dtype != wdt or weights.numel() != K or not weights.is_contiguous():
+        raise ValueError(f"weights must be a contiguous [{K}] {wdt} tensor")
+    if weights.device != clients.device:
+        raise ValueError("weights and clients must be on the same device")
+    if out is None:
+        out = torch.empty(P, dtype=dtype, device=clients.device)
+    else:
+        _check_device_tensor(out, "out")
+        if out.dtype != dtype or out.numel() < P or not out.is_contiguous() or out.device != clients.device:
+            raise ValueError(f"out must be a contiguous device tensor of >= {P} {dtype}")
+    lib = _lib.load()
+    s = _stream_handle(stream, clients.device)
+    if splits != 1:
+        if dtype != torch.float32:
+            raise TypeError("the split-client variant is fp32 only")
+        rc = lib.fedavg_reduce_splitk_f32(clients.data_ptr(), K, P, ld, weights.data_ptr(), out.data_ptr(), splits, s)
+        _lib.check(rc, "fedavg_reduce_splitk_f32")
+    elif tuned is not None:
+        if dtype != torch.float32:
+            raise TypeError("tuned variants are fp32 only")
+        unroll, nt = tuned
+        rc = lib.fedavg_reduce_f32_tuned(clients.data_ptr(), K, P, ld, weights.data_ptr(), out.data_ptr(),
+                                         int(unroll), int(nt), s)
+        _lib.check(rc, "fedavg_reduce_f32_tuned")
+    else:
+        fn = getattr(lib, _ENTRY[dtype])
+        rc = fn(clients.data_ptr(), K, P, ld, weights.data_ptr(), out.data_ptr(), s)
+        _lib.check(rc, _ENTRY[dtype])
+    return out
+
+
+def reduce_tensors(
+    clients: Sequence[torch.Tensor],
+    weights: torch.Tensor,
+    out: Optional[torch.Tensor] = None,
+    *,
+    stream: Optional[torch.cuda.Stream] = None,
+) -> torch.Tensor:
+    """Pointer-array variant: K separate contiguous fp32 device tensors of P elements."""
+    if not clients:
+        raise ValueError("need at least one client")
+    dev = clients[0].device
+    P = clients[0].numel()
+    for i, c in enumerate(clients):
+        _check_device_tensor(c, f"clients[{i}]")
+        if c.dtype != torch.float32 or c.numel() != P or not c.is_contiguous() or c.device != dev:
+            raise ValueError(f"clients[{i}] must be a contiguous fp32 device tensor of {P} elements")
+    _check_device_tensor(weights, "weights")
+    if weights.dtype != torch.float32 or weights.numel() != len(clients):
+        raise ValueError("weights must be [K] fp32")
+    ptrs = torch.tensor([c.data_ptr() for c in clients], dtype=torch.int64).pin_memory().to(dev, non_blocking=True)
+    if out is None:
+        out = torch.empty(P, dtype=torch.float32, device=dev)
+    lib = _lib.load()
+    rc = lib.fedavg_reduce_ptrs_f32(ptrs.data_ptr(), len(clients), P, weights.data_ptr(), out.data_ptr(),
+                                    _stream_handle(stream, dev))
+    _lib.check(rc, "fedavg_reduce_ptrs_f32")
+    # keep the pointer array alive until the kernel has consumed it
+    ptrs.record_stream(stream if stream is not None else torch.cuda.current_stream(dev))
+    return out

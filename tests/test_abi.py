@@ -1,0 +1,98 @@
+"""The C-ABI library loads and exports every symbol include/*.h declares.
+
+CPU only: argument validation runs before any HIP call, so rejected calls and
+the host-side weight helper can be exercised without a GPU.
+"""
+import ctypes
+import re
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import mfl_amd
+from mfl_amd import _lib, build
+
+INCLUDE = Path(__file__).resolve().parents[1] / "include"
+
+
+def declared_functions():
+    names = []
+    for h in sorted(INCLUDE.glob("*.h")):
+        text = re.sub(r"/\*.*?\*/", "", h.read_text(), flags=re.S)
+        names += re.findall(r"^\s*(?:const\s+)?\w+\**\s+\**(fedavg_\w+)\s*\(", text, flags=re.M)
+    return sorted(set(names))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    build.build()
+    return _lib.load()
+
+
+def test_header_parse_finds_entry_points():
+    names = declared_functions()
+    for required in ("fedavg_reduce_f32", "fedavg_reduce_ptrs_f32", "fedavg_reduce_f64", "fedavg_reduce_f16",
+                     "fedavg_reduce_bf16", "fedavg_reduce_splitk_f32", "fedavg_last_error", "fedavg_weights_f32",
+                     "fedavg_abi_version", "fedavg_reduce_f32_tuned"):
+        assert required in names
+
+
+def test_library_exports_every_declared_symbol(lib):
+    raw = ctypes.CDLL(str(_lib.library_path()))
+    for name in declared_functions():
+        assert hasattr(raw, name), name
+        assert name in _lib.SIGNATURES, f"{name} declared but not typed in _lib.SIGNATURES"
+
+
+def test_library_is_gfx950_code_object():
+    data = _lib.library_path().read_bytes()
+    assert b"gfx950" in data
+
+
+def test_abi_version(lib):
+    assert lib.fedavg_abi_version() == _lib.ABI_VERSION
+
+
+@pytest.mark.parametrize("K,P,ld", [(0, 10, 10), (-1, 10, 10), (2, 10, 5), (2, -1, 0)])
+def test_rejects_bad_sizes_without_gpu(lib, K, P, ld):
+    rc = lib.fedavg_reduce_f32(None, K, P, ld, None, None, None)
+    assert rc == _lib.FEDAVG_EINVAL
+    assert lib.fedavg_last_error().startswith(b"fedavg_reduce_f32")
+
+
+def test_null_buffers_rejected(lib):
+    assert lib.fedavg_reduce_f64(None, 2, 8, 8, None, None, None) == _lib.FEDAVG_EINVAL
+    assert lib.fedavg_reduce_bf16(None, 2, 8, 8, None, None, None) == _lib.FEDAVG_EINVAL
+    assert lib.fedavg_reduce_ptrs_f32(None, 2, 8, None, None, None) == _lib.FEDAVG_EINVAL
+
+
+def test_p_zero_is_noop(lib):
+    assert lib.fedavg_reduce_f32(None, 3, 0, 0, None, None, None) == 0
+
+
+def test_splitk_bad_mode(lib):
+    buf = np.zeros(64, np.float32)
+    w = np.ones(2, np.float32)
+    out = np.zeros(32, np.float32)
+    # validation happens before launch; an unsupported split count is refused
+    rc = lib.fedavg_reduce_splitk_f32(buf.ctypes.data, 2, 32, 32, w.ctypes.data, out.ctypes.data, 3, None)
+    assert rc in (_lib.FEDAVG_EMODE, _lib.FEDAVG_EALIGN)
+
+
+def test_weights_helper_matches_python(lib):
+    rng = np.random.default_rng(7)
+    for K in (1, 2, 3, 10, 100, 1000):
+        n = rng.integers(0, 10**6, size=K).astype(np.int64)
+        n[0] = max(n[0], 1)
+        w = np.zeros(K, np.float32)
+        assert lib.fedavg_weights_f32(n.ctypes.data, K, w.ctypes.data) == 0
+        expect = np.array(mfl_amd.sample_weights([int(v) for v in n]), dtype=np.float64).astype(np.float32)
+        assert w.tobytes() == expect.tobytes()
+
+
+def test_weights_helper_zero_total(lib):
+    n = np.zeros(3, np.int64)
+    w = np.zeros(3, np.float32)
+    assert lib.fedavg_weights_f32(n.ctypes.data, 3, w.ctypes.data) == _lib.FEDAVG_EINVAL
+    assert b"ZeroDivisionError" in lib.fedavg_last_error()

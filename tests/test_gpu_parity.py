@@ -1,0 +1,261 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle and the
+reference's golden vectors.  Run on the MI355X box: ``pytest -m gpu``.
+
+Bar: bit-exact for the fp32/fp64/fp16/bf16 exact kernels (NaN positions must
+match; NaN payload bits are not compared -- x86 and gfx950 produce different
+default-NaN patterns and IEEE 754 leaves them unspecified).  The split-client
+fp32 variant is tolerance-gated: norm-wise relative error <= 1e-6 (the
+north-star tolerance) and identical bits run to run.
+"""
+import numpy as np
+import pytest
+import torch
+
+import fedavg_oracle as O
+import mfl_amd
+from golden_io import case_names, load_case
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda", 0)
+
+
+def assert_bits(got: torch.Tensor, exp: torch.Tensor, what=""):
+    got = got.detach().cpu()
+    exp = exp.detach().cpu()
+    assert got.dtype == exp.dtype, (what, got.dtype, exp.dtype)
+    assert tuple(got.shape) == tuple(exp.shape), (what, got.shape, exp.shape)
+    if got.dtype == torch.bool:
+        assert torch.equal(got, exp), what
+        return
+    g = got.reshape(-1)
+    e = exp.reshape(-1)
+    if got.is_floating_point():
+        gn, en = torch.isnan(g), torch.isnan(e)
+        assert torch.equal(gn, en), f"{what}: NaN positions differ"
+        g = g[~gn]
+        e = e[~en]
+    gb = g.contiguous().view(torch.uint8).numpy()
+    eb = e.contiguous().view(torch.uint8).numpy()
+    if gb.tobytes() != eb.tobytes():
+        gv, ev = g.numpy(), e.numpy()
+        diff = np.nonzero(gv.astype(np.float64) != ev.astype(np.float64))[0]
+        raise AssertionError(f"{what}: {len(diff)} mismatching elements, first {diff[:5]}: "
+                             f"{gv[diff[:5]]} vs {ev[diff[:5]]}")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu(gpu_available):
+    mfl_amd._lib.load()
+    torch.cuda.set_device(DEV)
+    yield
+
+
+def _w(weights, dtype=torch.float32):
+    return mfl_amd.weights_tensor(weights, dtype, DEV)
+
+
+# ---------------------------------------------------------------------------
+# golden vectors through the drop-in (host state_dicts in, host state_dict out)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("name", [c for c in case_names() if c != "empty_w_locals"])
+def test_dropin_matches_reference_golden(name):
+    meta, w_locals, expected = load_case(name)
+    first = w_locals[0][1] if w_locals else None
+    others = [dict(sd) for _, sd in w_locals[1:]]
+    out = mfl_amd.aggregate(w_locals)
+    assert out is first  # fedavg_trainer.py:449 aliasing
+    assert list(out.keys()) == list(expected.keys())
+    for k, exp in expected.items():
+        assert out[k].device.type == "cpu"
+        assert_bits(out[k], exp, f"{name}/{k}")
+    for d, (_, sd) in zip(others, w_locals[1:]):  # other clients untouched
+        assert all(d[k] is sd[k] for k in d)
+
+
+def test_dropin_repeated_rounds_reuse_staging():
+    agg = mfl_amd.DeviceAggregator(DEV)
+    for name in ["mnist_lr_k10", "mnist_lr_k100", "mnist_lr_k10", "resnet_like_bn_k5"]:
+        _, w_locals, expected = load_case(name)
+        out = agg.aggregate(w_locals)
+        for k in expected:
+            assert_bits(out[k], expected[k], name)
+
+
+def test_dropin_femnist_cnn_shape():
+    # FEMNIST + CNN_DropOut (P = 1,206,590; 8 keys), K = 10
+    shapes = [("conv2d_1.weight", (32, 1, 5, 5)), ("conv2d_1.bias", (32,)), ("conv2d_2.weight", (64, 32, 5, 5)),
+              ("conv2d_2.bias", (64,)), ("linear_1.weight", (512, 3136)), ("linear_1.bias", (512,)),
+              ("linear_2.weight", (62, 512)), ("linear_2.bias", (62,))]
+    g = torch.Generator().manual_seed(3)
+    base = {k: torch.randn(s, generator=g) * 0.05 for k, s in shapes}
+    w_locals = []
+    for i in range(10):
+        sd = {k: base[k] + torch.randn(s, generator=g) * 1e-3 for k, s in shapes}
+        w_locals.append((int(torch.randint(1, 1000, (1,), generator=g)), sd))
+    import copy
+    ref = O.aggregate_torch(copy.deepcopy(w_locals))
+    out = mfl_amd.aggregate(w_locals)
+    assert sum(t.numel() for t in out.values()) == 1_206_590
+    for k in ref:
+        assert_bits(out[k], ref[k], k)
+
+
+# ---------------------------------------------------------------------------
+# device-resident kernels vs the oracle
+# ---------------------------------------------------------------------------
+def _clients(K, P, ld=None, seed=0, dtype=torch.float32):
+    ld = ld or max((P + 63) // 64 * 64, 64)
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    x = torch.randn((K, ld), generator=g, device=DEV, dtype=torch.float32) * 0.05
+    return x.to(dtype)
+
+
+def _weights(K, seed=1234):
+    n = np.random.default_rng(seed).integers(1, 1001, size=K)
+    return O.sample_weights([int(v) for v in n])
+
+
+@pytest.mark.parametrize("K", [1, 2, 3, 7, 8, 9, 16, 17, 33, 100, 257])
+@pytest.mark.parametrize("P", [1, 3, 4, 5, 63, 64, 65, 1000, 4097])
+def test_reduce_f32_exact(K, P):
+    x = _clients(K, P, seed=K * 1000 + P)
+    w = _weights(K, seed=K + P)
+    out = mfl_amd.reduce_packed(x, _w(w), P)
+    exp = O.reduce_f32(x[:, :P].cpu().numpy(), w)
+    assert_bits(out, torch.from_numpy(exp), f"K={K} P={P}")
+
+
+@pytest.mark.parametrize("K,P", [(10, 1 << 20), (100, 600_372), (37, 3_000_001)])
+def test_reduce_f32_exact_large(K, P):
+    x = _clients(K, P, seed=P)
+    w = _weights(K, seed=K)
+    out = mfl_amd.reduce_packed(x, _w(w), P)
+    exp = O.reduce_f32(x[:, :P].cpu().numpy(), w)
+    assert_bits(out, torch.from_numpy(exp), f"K={K} P={P}")
+
+
+@pytest.mark.parametrize("unroll", [4, 8, 16])
+@pytest.mark.parametrize("nt", [0, 1])
+def test_tuned_variants_bit_identical(unroll, nt):
+    K, P = 45, 123_457
+    x = _clients(K, P, seed=5)
+    w = _w(_weights(K))
+    base = mfl_amd.reduce_packed(x, w, P)
+    got = mfl_amd.reduce_packed(x, w, P, tuned=(unroll, nt))
+    assert_bits(got, base, f"unroll={unroll} nt={nt}")
+
+
+def test_misaligned_clients_take_scalar_path():
+    K, P = 6, 1001
+    big = _clients(K, P + 1, ld=1088, seed=9)
+    x = big[:, 1:]  # 4-byte offset: not 16-B aligned, ld stays 1088
+    w = _weights(K)
+    out = mfl_amd.reduce_packed(x, _w(w), P)
+    exp = O.reduce_f32(x[:, :P].cpu().numpy(), w)
+    assert_bits(out, torch.from_numpy(exp))
+
+
+def test_odd_ld_and_misaligned_out():
+    K, P = 5, 999
+    x = _clients(K, P, ld=1001, seed=10)
+    w = _weights(K)
+    out_big = torch.empty(P + 1, device=DEV)
+    out = mfl_amd.reduce_packed(x, _w(w), P, out=out_big[1:])
+    exp = O.reduce_f32(x[:, :P].cpu().numpy(), w)
+    assert_bits(out[:P], torch.from_numpy(exp))
+
+
+def test_ptrs_variant_mixed_alignment():
+    K, P = 9, 10_003
+    store = _clients(K, P + 4, seed=12)
+    clients = [store[i, (i % 4):(i % 4) + P] for i in range(K)]  # 0/4/8/12-byte offsets
+    w = _weights(K)
+    out = mfl_amd.reduce_tensors(clients, _w(w))
+    exp = O.reduce_f32(np.stack([c.cpu().numpy() for c in clients]), w)
+    assert_bits(out, torch.from_numpy(exp))
+
+
+@pytest.mark.parametrize("K,P", [(3, 33), (10, 4099), (64, 100_000)])
+def test_reduce_f64_exact(K, P):
+    x = _clients(K, P, seed=P, dtype=torch.float64)
+    w = _weights(K)
+    out = mfl_amd.reduce_packed(x, _w(w, torch.float64), P)
+    exp = O.reduce_f64(x[:, :P].cpu().numpy(), w)
+    assert_bits(out, torch.from_numpy(exp))
+
+
+@pytest.mark.parametrize("kind", ["float16", "bfloat16"])
+@pytest.mark.parametrize("K,P", [(3, 70), (10, 4099), (50, 65_536)])
+def test_reduce_half_exact(kind, K, P):
+    dt = torch.float16 if kind == "float16" else torch.bfloat16
+    x = _clients(K, P, seed=P + K, dtype=dt)
+    w = _weights(K)
+    out = mfl_amd.reduce_packed(x, _w(w), P)
+    xs = x[:, :P].cpu()
+    if kind == "float16":
+        exp = torch.from_numpy(O.reduce_half(xs.numpy(), w, kind))
+    else:
+        bits = O.reduce_half(xs.view(torch.int16).numpy(), w, kind)
+        exp = torch.from_numpy(bits.view(np.int16).copy()).view(torch.bfloat16)
+    assert_bits(out, exp, kind)
+
+
+@pytest.mark.parametrize("splits", [2, 4, 8])
+@pytest.mark.parametrize("K,P", [(3, 1000), (10, 7850), (100, 600_372), (500, 65_536)])
+def test_splitk_within_tolerance_and_deterministic(splits, K, P):
+    x = _clients(K, P, seed=P) * 0.02 + _clients(1, P, seed=P + 1)  # model-like: base + per-client noise
+    w = _weights(K)
+    a = mfl_amd.reduce_packed(x, _w(w), P, splits=splits)
+    b = mfl_amd.reduce_packed(x, _w(w), P, splits=splits)
+    assert_bits(a, b, "run-to-run")
+    exp = torch.from_numpy(O.reduce_f32(x[:, :P].cpu().numpy(), w)).double()
+    err = (a.cpu().double() - exp).norm() / exp.norm()
+    assert err <= 1e-6, float(err)
+
+
+# ---------------------------------------------------------------------------
+# BASELINE.json full size (K = 100, P = 25M): sampled-column parity + properties
+# ---------------------------------------------------------------------------
+def test_target_size_sampled_parity():
+    K, P = 100, 25_000_000
+    ld = (P + 63) // 64 * 64
+    g = torch.Generator(device=DEV).manual_seed(0)
+    base = torch.randn(ld, generator=g, device=DEV) * 0.05
+    x = torch.empty((K, ld), device=DEV)
+    for k in range(K):
+        gk = torch.Generator(device=DEV).manual_seed(1000 + k)
+        x[k] = base + torch.randn(ld, generator=gk, device=DEV) * 1e-3
+    w = _weights(K)
+    out = mfl_amd.reduce_packed(x, _w(w), P)
+    rng = np.random.default_rng(0)
+    starts = list(rng.integers(0, P - 8192, size=16)) + [0, P - 4099]
+    for s in starts:
+        s = int(s)
+        e = min(s + 4099, P)
+        exp = O.reduce_f32(x[:, s:e].cpu().numpy(), w)
+        assert_bits(out[s:e], torch.from_numpy(exp), f"window {s}")
+    # every variant gives the same bits at full size (idempotence across launches)
+    for tuned in [(4, 0), (16, 1)]:
+        again = mfl_amd.reduce_packed(x, _w(w), P, tuned=tuned)
+        assert torch.equal(again.view(torch.int32), out.view(torch.int32))
+    # linearity sanity in fp64: |out - sum w_i x_i| small relative to the norm
+    ref64 = torch.zeros(P, dtype=torch.float64, device=DEV)
+    for k in range(K):
+        ref64 += x[k, :P].double() * float(np.float32(w[k]))
+    rel = (out.double() - ref64).norm() / ref64.norm()
+    assert rel < 1e-6
+    del x
+
+
+def test_sharded_reducer_single_rank_chunks():
+    from mfl_amd.distributed import ShardedReducer
+    K, P = 12, 100_003
+    host = torch.randn((K, P)) * 0.05
+    w = _weights(K)
+    red = ShardedReducer(K, P, chunks=3, device=DEV)
+    red.load_from_host(host)
+    assert red.step(_w(w)) is None  # world size 1: no gather
+    exp = O.reduce_f32(host.numpy(), w)
+    got = torch.cat([v for v, _ in red.local_model_columns()])
+    assert_bits(got, torch.from_numpy(exp))

@@ -1,0 +1,156 @@
+"""Host-side logic of the drop-in (no GPU): the reference's early returns and
+errors, key tables, packing/unpacking and dtype promotion rules."""
+import copy
+from collections import OrderedDict
+
+import numpy as np
+import pytest
+import torch
+
+import fedavg_oracle as O
+import mfl_amd
+from mfl_amd.aggregate import _Prepared, prepare
+from mfl_amd.layout import KeyTable, result_dtype
+from golden_io import bits_equal, case_names, load_case
+
+
+def test_empty_w_locals_returns_global_copy():
+    torch.manual_seed(0)
+    glob = torch.nn.Linear(5, 3)
+    _, _, expected = load_case("empty_w_locals")
+    out = mfl_amd.aggregate([], model_global=glob)
+    assert list(out.keys()) == list(expected.keys())
+    for k in expected:
+        assert bits_equal(out[k], expected[k])
+    # a copy, not the live parameters
+    out["weight"].add_(1.0)
+    assert not torch.equal(out["weight"], glob.weight.detach())
+
+
+def test_mixin_empty_path_uses_model_global():
+    class Trainer(mfl_amd.FedAvgAggregateMixin):
+        def __init__(self):
+            torch.manual_seed(0)
+            self.model_global = torch.nn.Linear(5, 3)
+
+    out = Trainer().aggregate([])
+    _, _, expected = load_case("empty_w_locals")
+    assert all(bits_equal(out[k], expected[k]) for k in expected)
+
+
+def test_install_patches_class():
+    class RefLike:
+        def aggregate(self, w_locals):
+            raise AssertionError("reference path must not run")
+
+    mfl_amd.install(RefLike)
+    t = RefLike()
+    t.model_global = torch.nn.Linear(2, 2)
+    out = t.aggregate([])
+    assert set(out.keys()) == {"weight", "bias"}
+    assert RefLike.aggregate.__wrapped_reference__ is not None
+
+
+def test_no_keys_returns_first_dict():
+    meta, w_locals, expected = load_case("no_keys_k2")
+    first = w_locals[0][1]
+    out = mfl_amd.aggregate(w_locals)
+    assert out is first and len(out) == 0
+
+
+def test_zero_total_raises_zero_division():
+    sd = OrderedDict(w=torch.ones(3))
+    with pytest.raises(ZeroDivisionError):
+        prepare([(0, sd), (0, copy.deepcopy(sd))])
+
+
+def test_missing_key_raises_key_error():
+    a = OrderedDict(w=torch.ones(3), b=torch.ones(2))
+    b = OrderedDict(w=torch.ones(3))
+    with pytest.raises(KeyError):
+        prepare([(1, a), (1, b)])
+
+
+def test_extra_keys_in_later_clients_ignored():
+    a = OrderedDict(w=torch.ones(3))
+    b = OrderedDict(w=torch.ones(3), extra=torch.ones(7))
+    prep = prepare([(1, a), (2, b)])
+    assert isinstance(prep, _Prepared)
+    assert [e.name for e in prep[1].entries] == ["w"]
+
+
+def test_shape_mismatch_raises():
+    a = OrderedDict(w=torch.ones(3))
+    b = OrderedDict(w=torch.ones(1))  # the reference would silently broadcast
+    with pytest.raises(mfl_amd.ShapeMismatchError):
+        prepare([(1, a), (1, b)])
+    with pytest.raises(RuntimeError):  # same exception family as the reference's broadcast error
+        prepare([(1, OrderedDict(w=torch.ones(2, 3))), (1, OrderedDict(w=torch.ones(3, 2)))])
+
+
+def test_dtype_mismatch_raises():
+    with pytest.raises(TypeError):
+        prepare([(1, OrderedDict(w=torch.ones(3))), (1, OrderedDict(w=torch.ones(3, dtype=torch.float64)))])
+
+
+def test_same_dict_twice_refused():
+    sd = OrderedDict(w=torch.ones(3))
+    with pytest.raises(ValueError):
+        prepare([(1, sd), (1, sd)])
+
+
+@pytest.mark.parametrize("src,res", [
+    (torch.float32, torch.float32), (torch.float64, torch.float64), (torch.float16, torch.float16),
+    (torch.bfloat16, torch.bfloat16), (torch.int64, torch.float32), (torch.int32, torch.float32),
+    (torch.uint8, torch.float32), (torch.bool, torch.float32),
+])
+def test_result_dtype_matches_aten_promotion(src, res):
+    assert result_dtype(src) == res
+    assert (torch.ones(2, dtype=src) * 0.5).dtype == res
+
+
+def test_key_table_groups_and_alignment():
+    _, w_locals, _ = load_case("resnet_like_bn_k5")
+    table = KeyTable(w_locals[0][1])
+    assert list(table.groups) == [torch.float32]  # int64 buffers join the fp32 group
+    g = table.groups[torch.float32]
+    assert g.P == sum(t.numel() for t in w_locals[0][1].values())
+    assert g.ld % mfl_amd.ALIGN_ELEMS == 0 and g.ld >= g.P
+    offs = [e.offset for e in g.keys]
+    assert offs == sorted(offs) and offs[0] == 0
+
+
+@pytest.mark.parametrize("name", ["resnet_like_bn_k5", "int_dtypes_k3", "float64_key_k3", "mnist_lr_k10",
+                                  "bfloat16_key_k3", "scalar_key_k3"])
+def test_pack_then_cpu_oracle_reproduces_reference(name):
+    """Packing is lossless w.r.t. the reference's promotion: the oracle run on
+    the packed rows reproduces the golden output bit for bit."""
+    meta, w_locals, expected = load_case(name)
+    table = KeyTable(w_locals[0][1])
+    dicts = [sd for _, sd in w_locals]
+    table.validate(dicts)
+    weights = O.sample_weights([n for n, _ in w_locals])
+    for g in table.groups.values():
+        buf = torch.zeros((len(dicts), g.ld), dtype=g.dtype)
+        table.pack_into(g, buf, dicts)
+        if g.dtype == torch.float32:
+            flat = torch.from_numpy(O.reduce_f32(buf[:, :g.P].numpy(), weights))
+        elif g.dtype == torch.float64:
+            flat = torch.from_numpy(O.reduce_f64(buf[:, :g.P].numpy(), weights))
+        elif g.dtype == torch.bfloat16:
+            bits = O.reduce_half(buf[:, :g.P].view(torch.int16).numpy(), weights, "bfloat16")
+            flat = torch.from_numpy(bits.view(np.int16).copy()).view(torch.bfloat16)
+        else:
+            flat = torch.from_numpy(O.reduce_half(buf[:, :g.P].numpy(), weights, "float16"))
+        for k, t in table.unpack(g, flat).items():
+            assert bits_equal(t, expected[k]), k
+
+
+def test_int64_to_fp32_rounding_matches_reference_cast():
+    _, w_locals, expected = load_case("int_dtypes_k3")
+    big = w_locals[0][1]["big"]
+    assert (big > 2**24).all()  # values that do not fit fp32 exactly
+    buf = torch.zeros((1, 64))
+    table = KeyTable(OrderedDict(big=big))
+    table.pack_into(table.groups[torch.float32], buf, [OrderedDict(big=big)])
+    assert torch.equal(buf[0, :40], big.to(torch.float32))
