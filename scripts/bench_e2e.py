@@ -1,0 +1,145 @@
+"""End-to-end rate of the drop-in: host state_dicts in, host state_dict out.
+
+    python scripts/bench_e2e.py [--configs mnist_lr,femnist_cnn,resnet56,target_flat] [--reps 5]
+
+The reference's aggregate starts and ends in host memory (client.py:96
+returns ``net.cpu().state_dict()``; fedavg_trainer.py:219 loads the result
+into the CPU-resident global model), so this measures the whole drop-in:
+validation, packing into pinned staging rows overlapped with per-client H2D,
+the HIP kernel, D2H and unpacking -- next to the reference's torch CPU loop
+(oracle restatement) on the same inputs in the same process, and checks the
+two agree bit for bit.  One JSON line per config.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import sys
+import time
+from collections import OrderedDict
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "oracle"))
+
+import numpy as np
+import torch
+
+import fedavg_oracle as O
+import mfl_amd
+
+
+def resnet56_shapes(num_classes=10):
+    """FedML resnet56 (Bottleneck, [6, 6, 6]) state_dict: 350 keys, 600,372 elements."""
+    shapes = []
+
+    def bn(prefix, c):
+        shapes.extend([(f"{prefix}.weight", (c,)), (f"{prefix}.bias", (c,)), (f"{prefix}.running_mean", (c,)),
+                       (f"{prefix}.running_var", (c,)), (f"{prefix}.num_batches_tracked", ())])
+
+    shapes.append(("conv1.weight", (16, 3, 3, 3)))
+    bn("bn1", 16)
+    inplanes = 16
+    for li, (planes, stride) in enumerate([(16, 1), (32, 2), (64, 2)], 1):
+        for b in range(6):
+            p = f"layer{li}.{b}"
+            shapes.append((f"{p}.conv1.weight", (planes, inplanes, 1, 1)))
+            bn(f"{p}.bn1", planes)
+            shapes.append((f"{p}.conv2.weight", (planes, planes, 3, 3)))
+            bn(f"{p}.bn2", planes)
+            shapes.append((f"{p}.conv3.weight", (planes * 4, planes, 1, 1)))
+            bn(f"{p}.bn3", planes * 4)
+            if b == 0 and (stride != 1 or inplanes != planes * 4):
+                shapes.append((f"{p}.downsample.0.weight", (planes * 4, inplanes, 1, 1)))
+                bn(f"{p}.downsample.1", planes * 4)
+            inplanes = planes * 4
+    shapes.append(("fc.weight", (num_classes, 256)))
+    shapes.append(("fc.bias", (num_classes,)))
+    return shapes
+
+
+CONFIGS = {
+    "mnist_lr": (10, [("linear.weight", (10, 784)), ("linear.bias", (10,))]),
+    "femnist_cnn": (10, [("conv2d_1.weight", (32, 1, 3, 3)), ("conv2d_1.bias", (32,)),
+                         ("conv2d_2.weight", (64, 32, 3, 3)), ("conv2d_2.bias", (64,)),
+                         ("linear_1.weight", (128, 9216)), ("linear_1.bias", (128,)),
+                         ("linear_2.weight", (62, 128)), ("linear_2.bias", (62,))]),
+    "resnet56": (100, resnet56_shapes()),
+    "target_flat": (100, [("w", (25_000_000,))]),
+}
+
+
+def make_clients(K, shapes, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    base = {k: torch.randn(s, generator=g) * 0.05 for k, s in shapes if not k.endswith("num_batches_tracked")}
+    counts = [int(v) for v in np.random.default_rng(1234).integers(1, 1001, size=K)]
+    dicts = []
+    for i in range(K):
+        sd = OrderedDict()
+        for k, s in shapes:
+            if k.endswith("num_batches_tracked"):
+                sd[k] = torch.tensor(1000 + i, dtype=torch.int64)
+            else:
+                sd[k] = base[k] + torch.randn(s, generator=g) * 1e-3
+        dicts.append(sd)
+    return counts, dicts
+
+
+def fresh(counts, dicts):
+    # aggregate mutates w_locals[0][1]; give each rep its own first dict
+    return [(counts[0], OrderedDict(dicts[0]))] + list(zip(counts[1:], dicts[1:]))
+
+
+def run(name, reps):
+    K, shapes = CONFIGS[name]
+    P = sum(math.prod(s) for _, s in shapes)
+    counts, dicts = make_clients(K, shapes)
+    alg = 4 * K * P + 4 * P + 4 * K
+    agg = mfl_amd.DeviceAggregator(torch.device("cuda", 0))
+    gpu_t, prof = [], []
+    for r in range(reps + 1):
+        wl = fresh(counts, dicts)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        out = agg.aggregate(wl)
+        t = time.perf_counter() - t0
+        if r:
+            gpu_t.append(t)
+            prof.append(dict(agg.last_profile))
+    cpu_t = []
+    cpu_reps = max(1, min(reps, int(20.0 / max(alg / 5e9, 1e-3))))
+    for r in range(cpu_reps + 1):
+        wl = fresh(counts, dicts)
+        t0 = time.perf_counter()
+        ref = O.aggregate_torch(wl)
+        t = time.perf_counter() - t0
+        if r:
+            cpu_t.append(t)
+    same = all(torch.equal(out[k].reshape(-1).view(torch.int32), ref[k].reshape(-1).view(torch.int32)) for k in ref)
+    g, c = float(np.median(gpu_t)), float(np.median(cpu_t))
+    return {
+        "config": name, "K": K, "P": P, "keys": len(shapes),
+        "e2e_ms_median": round(g * 1e3, 3), "e2e_ms_min": round(min(gpu_t) * 1e3, 3),
+        "e2e_GBps": round(alg / g / 1e9, 2),
+        "pack_h2d_ms_median": round(float(np.median([p["pack_h2d_ms"] for p in prof])), 3),
+        "kernel_d2h_ms_median": round(float(np.median([p["kernel_d2h_ms"] for p in prof])), 3),
+        "cpu_ref_ms_median": round(c * 1e3, 3), "cpu_ref_GBps": round(alg / c / 1e9, 2),
+        "cpu_threads": torch.get_num_threads(), "speedup_vs_cpu": round(c / g, 2),
+        "bit_exact_vs_cpu_ref": bool(same), "reps": reps,
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="mnist_lr,femnist_cnn,resnet56,target_flat")
+    ap.add_argument("--reps", type=int, default=5)
+    args = ap.parse_args()
+    torch.cuda.set_device(0)
+    for name in args.configs.split(","):
+        print(json.dumps(run(name, args.reps)), flush=True)
+
+
+if __name__ == "__main__":
+    main()

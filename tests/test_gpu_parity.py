@@ -84,9 +84,9 @@ def test_dropin_repeated_rounds_reuse_staging():
 
 def test_dropin_femnist_cnn_shape():
     # FEMNIST + CNN_DropOut (P = 1,206,590; 8 keys), K = 10
-    shapes = [("conv2d_1.weight", (32, 1, 5, 5)), ("conv2d_1.bias", (32,)), ("conv2d_2.weight", (64, 32, 5, 5)),
-              ("conv2d_2.bias", (64,)), ("linear_1.weight", (512, 3136)), ("linear_1.bias", (512,)),
-              ("linear_2.weight", (62, 512)), ("linear_2.bias", (62,))]
+    shapes = [("conv2d_1.weight", (32, 1, 3, 3)), ("conv2d_1.bias", (32,)), ("conv2d_2.weight", (64, 32, 3, 3)),
+              ("conv2d_2.bias", (64,)), ("linear_1.weight", (128, 9216)), ("linear_1.bias", (128,)),
+              ("linear_2.weight", (62, 128)), ("linear_2.bias", (62,))]
     g = torch.Generator().manual_seed(3)
     base = {k: torch.randn(s, generator=g) * 0.05 for k, s in shapes}
     w_locals = []
