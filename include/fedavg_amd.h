@@ -107,6 +107,30 @@ int fedavg_reduce_splitk_f32(const float* clients, int64_t K, int64_t P, int64_t
  */
 int fedavg_weights_f32(const int64_t* sample_nums, int64_t K, float* weights);
 
+/*
+ * Host runtime: pack client state_dicts into pinned client-major rows.
+ *
+ * One item per (client, key): copy `numel` elements from `src` (host, dense)
+ * to element offset `dst_offset` of `dst_base` (host; for the packed [K, ld]
+ * layout dst_offset = row * ld + key offset).  `kind` selects the source
+ * type: 0 = same dtype as the destination (elem_size bytes per element);
+ * 1..6 = int64, int32, int16, int8, uint8, bool promoted to fp32 with the
+ * static_cast ATen applies to `int_tensor * python_float`
+ * (fedavg_trainer.py:455).  Work is split evenly by bytes over `n_threads`
+ * host threads (a persistent pool inside the library).  Replaces the
+ * reference's per-key host loop over w_locals (fedavg_trainer.py:450-452) as
+ * the way parameters reach the reduction.  Returns 0 or FEDAVG_EINVAL.
+ */
+typedef struct fedavg_pack_item {
+  int64_t src;        /* host address of the first source element */
+  int64_t numel;      /* elements to copy                        */
+  int64_t dst_offset; /* destination element offset              */
+  int64_t kind;       /* 0 raw, 1 i64, 2 i32, 3 i16, 4 i8, 5 u8, 6 bool */
+} fedavg_pack_item;
+
+int fedavg_pack_rows(const fedavg_pack_item* items, int64_t n_items, void* dst_base,
+                     int64_t elem_size, int n_threads);
+
 #ifdef __cplusplus
 }
 #endif

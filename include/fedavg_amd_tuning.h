@@ -26,6 +26,34 @@ int fedavg_reduce_f32_tuned(const float* clients, int64_t K, int64_t P, int64_t 
                             const float* weights, float* out, int unroll, int nontemporal,
                             void* stream);
 
+/*
+ * Variant family of the exact fp32 kernel (same bits, different schedule):
+ *   unroll     : client rows per load batch (2, 4, 8, 16)
+ *   cols       : 16-B column slices per thread (1, 2, 4; 8 with unroll <= 4)
+ *   pipelined  : 0 = register batches; 1 = register double-buffered batches
+ *                (2*unroll*cols loads in flight); 2 = LDS-DMA staging
+ *                (global_load_lds_dwordx4 into per-wave LDS slots, unroll*cols <= 16);
+ *                3 = balanced persistent: grid = blocks resident on the chip, each block
+ *                owns an equal contiguous range of 1 KiB wave-slices (unroll*cols <= 32);
+ *                4 = round-split: the plain kernel (mode 0) launched over the fewest
+ *                equal column ranges that each fit in one resident round
+ *   max_blocks : 0 = default grid (one block per column group; for pipelined == 3
+ *                the resident block count); > 0 caps / sets the grid
+ * Needs 16-B aligned clients/out and ld % 4 == 0.
+ */
+int fedavg_reduce_f32_variant(const float* clients, int64_t K, int64_t P, int64_t ld,
+                              const float* weights, float* out, int unroll, int nontemporal,
+                              int cols, int pipelined, int max_blocks, void* stream);
+
+/*
+ * Exact fp32 reduce over the TILED layout [ceil(P/1024)][K][1024]: tile t
+ * holds columns [1024t, 1024t+1024) of every client, client-major inside the
+ * tile (a block then streams K*4 KiB contiguous bytes).  Padding columns of
+ * the last tile are read but never stored.
+ */
+int fedavg_reduce_tiled_f32(const float* tiles, int64_t K, int64_t P, const float* weights,
+                            float* out, int unroll, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -26,7 +26,11 @@ SIGNATURES = {
     "fedavg_reduce_bf16": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp]),
     "fedavg_reduce_splitk_f32": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_int, _vp]),
     "fedavg_weights_f32": (_c_int, [_vp, _c_i64, _vp]),
+    "fedavg_pack_rows": (_c_int, [_vp, _c_i64, _vp, _c_i64, _c_int]),
     "fedavg_reduce_f32_tuned": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_int, _c_int, _vp]),
+    "fedavg_reduce_f32_variant": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_int, _c_int, _c_int, _c_int,
+                                           _c_int, _vp]),
+    "fedavg_reduce_tiled_f32": (_c_int, [_vp, _c_i64, _c_i64, _vp, _vp, _c_int, _vp]),
 }
 
 ABI_VERSION = 1

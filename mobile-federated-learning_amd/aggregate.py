@@ -62,7 +62,7 @@ def sample_weights(sample_nums: Sequence) -> List[float]:
 
 
 class _Prepared(tuple):
-    """(acc_dict, KeyTable, state_dicts, weights) for a non-trivial call."""
+    """(acc_dict, KeyTable, state_dicts, weights, src_ptrs, keepalive) for a non-trivial call."""
 
 
 def prepare(w_locals, model_global=None):
@@ -92,8 +92,8 @@ def prepare(w_locals, model_global=None):
                 f"w_locals[{i}][1] is the same dict object as w_locals[0][1]; the reference would read "
                 "its own partial sums there (fedavg_trainer.py:199 deep-copies to avoid this)")
     table = KeyTable(acc_dict)
-    table.validate(dicts)
-    return _Prepared((acc_dict, table, dicts, weights))
+    ptrs, keepalive = table.collect(dicts)  # validates every client (KeyError / ShapeMismatchError / TypeError)
+    return _Prepared((acc_dict, table, dicts, weights, ptrs, keepalive))
 
 
 class _Staging:
@@ -140,33 +140,44 @@ class DeviceAggregator:
         prep = prepare(w_locals, model_global)
         if not isinstance(prep, _Prepared):
             return prep  # empty list / no keys: answered on the host like the reference
-        acc_dict, table, dicts, weights = prep
-        results = self._reduce_groups(table, dicts, weights)
+        acc_dict, table, dicts, weights, ptrs, keepalive = prep
+        results = self._reduce_groups(table, ptrs, weights)
+        del keepalive
         # replace values in place, keeping client 0's key order (fedavg_trainer.py:450-457)
         for e in table.entries:
             acc_dict[e.name] = results[e.name]
         return acc_dict
 
-    def _reduce_groups(self, table: KeyTable, dicts, weights) -> "OrderedDict[str, torch.Tensor]":
-        K = len(dicts)
+    # rows per H2D chunk: big enough to amortise a copy launch, small enough
+    # that the first chunk's DMA starts while the host still packs the rest
+    CHUNK_BYTES = 32 << 20
+
+    def _reduce_groups(self, table: KeyTable, ptrs, weights) -> "OrderedDict[str, torch.Tensor]":
+        K = ptrs.shape[0]
         dev = self.device
-        prof = {"pack_h2d_ms": 0.0, "kernel_d2h_ms": 0.0}
+        lib = _lib.load()
+        threads = max(1, torch.get_num_threads())
         results: "OrderedDict[str, torch.Tensor]" = OrderedDict()
         with torch.cuda.device(dev):
             compute = torch.cuda.current_stream(dev)
             if self._copy_stream is None:
                 self._copy_stream = torch.cuda.Stream(dev)
             copy_s = self._copy_stream
-            copy_s.wait_stream(compute)  # previous users of the device buffers are done
+            copy_s.wait_stream(compute)  # earlier users of the device staging are done
             t0 = time.perf_counter()
             staged = []
             for g in table.groups.values():
                 st = self._staging_for(g.dtype, K, g.ld)
                 host, devbuf = st.host[:K], st.dev[:K]
-                for i, sd in enumerate(dicts):
-                    table.pack_into(g, host[i:i + 1], [sd])
+                esize = host.element_size()
+                rows = max(1, min(K, self.CHUNK_BYTES // max(1, g.ld * esize)))
+                for i0 in range(0, K, rows):
+                    i1 = min(K, i0 + rows)
+                    items = table.pack_items(g, ptrs[i0:i1], i0, g.ld)
+                    _lib.check(lib.fedavg_pack_rows(items.ctypes.data, items.shape[0], host.data_ptr(), esize,
+                                                    threads), "fedavg_pack_rows")
                     with torch.cuda.stream(copy_s):
-                        devbuf[i].copy_(host[i], non_blocking=True)
+                        devbuf[i0:i1].copy_(host[i0:i1], non_blocking=True)
                 w_dev = weights_tensor(weights, g.dtype, dev)
                 staged.append((g, devbuf, w_dev))
             compute.wait_stream(copy_s)
@@ -181,9 +192,7 @@ class DeviceAggregator:
             t2 = time.perf_counter()
         for g, out_host in outs:
             results.update(table.unpack(g, out_host))
-        prof["pack_h2d_ms"] = (t1 - t0) * 1e3
-        prof["kernel_d2h_ms"] = (t2 - t1) * 1e3
-        self.last_profile = prof
+        self.last_profile = {"pack_issue_ms": (t1 - t0) * 1e3, "h2d_kernel_d2h_ms": (t2 - t1) * 1e3}
         return results
 
 

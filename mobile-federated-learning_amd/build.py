@@ -2,7 +2,8 @@
 
     python -m mfl_amd.build           # or __graft_entry__.build()
 
-Compiles ``csrc/fedavg_reduce.hip`` with hipcc for ``--offload-arch=gfx950``
+Compiles ``csrc/fedavg_reduce.hip`` (kernels + C ABI) and
+``csrc/fedavg_host.cpp`` (native host packer) with hipcc for ``--offload-arch=gfx950``
 into ``lib/libfedavg_amd.so`` inside the package (in-tree, so the built
 library travels with the repo snapshot to the GPU box).  ``-ffp-contract=off``
 keeps every multiply and add separately rounded (bit parity with the
@@ -19,6 +20,7 @@ from pathlib import Path
 PKG_DIR = Path(__file__).resolve().parent
 REPO_DIR = PKG_DIR.parent
 CSRC = PKG_DIR / "csrc" / "fedavg_reduce.hip"
+CSRC_HOST = PKG_DIR / "csrc" / "fedavg_host.cpp"
 INCLUDE = REPO_DIR / "include"
 LIB_DIR = PKG_DIR / "lib"
 LIB_PATH = LIB_DIR / "libfedavg_amd.so"
@@ -33,6 +35,7 @@ HIPCC_FLAGS = [
     "-ffp-contract=off",
     "-fno-fast-math",
     "-Wall",
+    "-pthread",
 ]
 
 
@@ -44,7 +47,7 @@ def hipcc_path() -> str:
 
 
 def sources():
-    return [CSRC, INCLUDE / "fedavg_amd.h", INCLUDE / "fedavg_amd_tuning.h"]
+    return [CSRC, CSRC_HOST, INCLUDE / "fedavg_amd.h", INCLUDE / "fedavg_amd_tuning.h", Path(__file__)]
 
 
 def up_to_date() -> bool:
@@ -59,7 +62,7 @@ def build(force: bool = False, verbose: bool = False) -> Path:
         return LIB_PATH
     LIB_DIR.mkdir(parents=True, exist_ok=True)
     tmp = LIB_PATH.with_suffix(".so.tmp")
-    cmd = [hipcc_path(), *HIPCC_FLAGS, f"-I{INCLUDE}", "-o", str(tmp), str(CSRC)]
+    cmd = [hipcc_path(), *HIPCC_FLAGS, f"-I{INCLUDE}", "-o", str(tmp), str(CSRC), str(CSRC_HOST)]
     if verbose:
         print(" ".join(cmd))
     proc = subprocess.run(cmd, capture_output=True, text=True)

@@ -25,6 +25,7 @@ from collections import OrderedDict
 from dataclasses import dataclass, field
 from typing import Dict, List, Mapping, Sequence, Tuple
 
+import numpy as np
 import torch
 
 from .reduce import ALIGN_ELEMS
@@ -72,10 +73,18 @@ class Group:
     dtype: torch.dtype
     P: int = 0  # valid elements per client row
     keys: List[KeyEntry] = field(default_factory=list)
+    key_index: "np.ndarray" = None  # positions of this group's keys in the table
+    numel: "np.ndarray" = None
+    offset: "np.ndarray" = None
+    kind: "np.ndarray" = None  # fedavg_pack_item.kind per key
 
     @property
     def ld(self) -> int:
         return max(_round_up(self.P, ALIGN_ELEMS), ALIGN_ELEMS)
+
+
+# fedavg_pack_item.kind codes (include/fedavg_amd.h)
+_PACK_KIND = {torch.int64: 1, torch.int32: 2, torch.int16: 3, torch.int8: 4, torch.uint8: 5, torch.bool: 6}
 
 
 class KeyTable:
@@ -93,6 +102,56 @@ class KeyTable:
             g.P += e.numel
             g.keys.append(e)
             self.entries.append(e)
+        self._names = [e.name for e in self.entries]
+        self._shapes = [torch.Size(e.shape) for e in self.entries]
+        self._dtypes = [e.src_dtype for e in self.entries]
+        # per group: column indices into the entry list + pack metadata
+        index = {id(e): i for i, e in enumerate(self.entries)}
+        for g in self.groups.values():
+            g.key_index = np.array([index[id(e)] for e in g.keys], dtype=np.int64)
+            g.numel = np.array([e.numel for e in g.keys], dtype=np.int64)
+            g.offset = np.array([e.offset for e in g.keys], dtype=np.int64)
+            g.kind = np.array([0 if e.src_dtype == g.dtype else _PACK_KIND[e.src_dtype] for e in g.keys],
+                              dtype=np.int64)
+
+    def collect(self, state_dicts: Sequence[Mapping[str, torch.Tensor]]):
+        """Validate every client against client 0 and gather source addresses.
+
+        Returns ``(ptrs, keepalive)``: ``ptrs`` is an int64 ``[K, n_keys]``
+        array of host data pointers in table order; ``keepalive`` holds
+        contiguous copies made for non-contiguous sources.  Raises like
+        :meth:`validate`.  One list comprehension per attribute per client keeps
+        the per-key Python cost to a few hundred ns.
+        """
+        names, shapes, dtypes = self._names, self._shapes, self._dtypes
+        ptrs = np.empty((len(state_dicts), len(names)), dtype=np.int64)
+        keepalive = []
+        for i, sd in enumerate(state_dicts):
+            ts = [sd[n] for n in names]  # KeyError, as in the reference
+            if [t.shape for t in ts] != shapes or [t.dtype for t in ts] != dtypes:
+                self.validate([sd], first_index=i)
+                raise AssertionError("unreachable")  # validate raised
+            if not all([t.is_cpu for t in ts]):
+                raise TypeError(f"client {i}: state_dict tensors must be host (CPU) tensors, as client.py:96 "
+                                "returns them (net.cpu().state_dict()); use reduce_packed/reduce_tensors for "
+                                "device-resident updates")
+            if not all([t.is_contiguous() for t in ts]):
+                ts = [t if t.is_contiguous() else t.contiguous() for t in ts]
+                keepalive.append(ts)
+            ptrs[i] = [t.data_ptr() for t in ts]
+        return ptrs, keepalive
+
+    def pack_items(self, group: "Group", ptrs: np.ndarray, row0: int, ld: int) -> np.ndarray:
+        """fedavg_pack_item rows [(src, numel, dst_offset, kind)] for clients
+        ``row0 .. row0+len(ptrs)-1`` of ``group`` (dst offsets in elements from
+        the start of the [K, ld] staging buffer)."""
+        nc, nk = ptrs.shape[0], len(group.keys)
+        items = np.empty((nc, nk, 4), dtype=np.int64)
+        items[:, :, 0] = ptrs[:, group.key_index]
+        items[:, :, 1] = group.numel
+        items[:, :, 2] = (np.arange(row0, row0 + nc, dtype=np.int64) * ld)[:, None] + group.offset[None, :]
+        items[:, :, 3] = group.kind
+        return items.reshape(nc * nk, 4)
 
     @property
     def total_elements(self) -> int:
@@ -101,14 +160,14 @@ class KeyTable:
     def signature(self):
         return tuple((e.name, e.shape, e.src_dtype) for e in self.entries)
 
-    def validate(self, state_dicts: Sequence[Mapping[str, torch.Tensor]]) -> None:
+    def validate(self, state_dicts: Sequence[Mapping[str, torch.Tensor]], first_index: int = 0) -> None:
         """Every client must hold every key of client 0 with the same shape/dtype.
 
         A missing key raises ``KeyError`` like the reference's
         ``local_model_params[k]`` (fedavg_trainer.py:457); keys only present in
         later clients are ignored, as the reference iterates client 0's keys.
         """
-        for i, sd in enumerate(state_dicts):
+        for i, sd in enumerate(state_dicts, start=first_index):
             for e in self.entries:
                 t = sd[e.name]  # KeyError, as in the reference
                 if tuple(t.shape) != e.shape:

@@ -69,7 +69,9 @@ def reduce_packed(
     P       : number of valid columns (default ``clients.shape[1]``).
     splits  : 1 = exact sequential kernel; 2/4/8 = split-client fp32 variant
               (tolerance-gated, not bit-exact).
-    tuned   : (unroll, nontemporal) -- benchmarking hook for the fp32 kernel.
+    tuned   : benchmarking hook for the fp32 kernel: (unroll, nontemporal) or
+              (unroll, nontemporal, cols, pipelined, max_blocks), see
+              include/fedavg_amd_tuning.h.  Every variant gives the same bits.
     """
     _check_device_tensor(clients, "clients")
     _check_device_tensor(weights, "weights")
@@ -105,10 +107,16 @@ def reduce_packed(
     elif tuned is not None:
         if dtype != torch.float32:
             raise TypeError("tuned variants are fp32 only")
-        unroll, nt = tuned
-        rc = lib.fedavg_reduce_f32_tuned(clients.data_ptr(), K, P, ld, weights.data_ptr(), out.data_ptr(),
-                                         int(unroll), int(nt), s)
-        _lib.check(rc, "fedavg_reduce_f32_tuned")
+        if len(tuned) == 2:
+            unroll, nt = tuned
+            rc = lib.fedavg_reduce_f32_tuned(clients.data_ptr(), K, P, ld, weights.data_ptr(), out.data_ptr(),
+                                             int(unroll), int(nt), s)
+            _lib.check(rc, "fedavg_reduce_f32_tuned")
+        else:
+            unroll, nt, cols, pipe, max_blocks = tuned
+            rc = lib.fedavg_reduce_f32_variant(clients.data_ptr(), K, P, ld, weights.data_ptr(), out.data_ptr(),
+                                               int(unroll), int(nt), int(cols), int(pipe), int(max_blocks), s)
+            _lib.check(rc, "fedavg_reduce_f32_variant")
     else:
         fn = getattr(lib, _ENTRY[dtype])
         rc = fn(clients.data_ptr(), K, P, ld, weights.data_ptr(), out.data_ptr(), s)

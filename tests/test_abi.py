@@ -96,3 +96,19 @@ def test_weights_helper_zero_total(lib):
     w = np.zeros(3, np.float32)
     assert lib.fedavg_weights_f32(n.ctypes.data, 3, w.ctypes.data) == _lib.FEDAVG_EINVAL
     assert b"ZeroDivisionError" in lib.fedavg_last_error()
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    """No silent fallback: without the .so every product entry raises."""
+    import torch
+
+    monkeypatch.setattr(_lib, "LIB_PATH", tmp_path / "libfedavg_amd.so")
+    monkeypatch.setattr(_lib, "_lib", None)
+    with pytest.raises(_lib.FedAvgLibraryError):
+        _lib.load()
+    # the drop-in refuses too (before or at device use), never computing on the CPU
+    from collections import OrderedDict
+    w_locals = [(1, OrderedDict(w=torch.ones(4))), (3, OrderedDict(w=torch.zeros(4)))]
+    with pytest.raises((_lib.FedAvgLibraryError, RuntimeError)):
+        mfl_amd.aggregate(w_locals)
+    assert torch.equal(w_locals[0][1]["w"], torch.ones(4))  # nothing was written

@@ -146,6 +146,38 @@ def test_tuned_variants_bit_identical(unroll, nt):
     assert_bits(got, base, f"unroll={unroll} nt={nt}")
 
 
+def _all_variants():
+    out = []
+    for U in (2, 4, 8, 16):
+        for C in (1, 2, 4, 8):
+            if C == 8 and U > 4:
+                continue
+            for nt in (0, 1):
+                for pipe in (0, 1, 2, 3, 4):
+                    if pipe in (1, 3) and U * C > 32:
+                        continue
+                    if pipe == 2 and U * C > 16:
+                        continue
+                    out.append((U, nt, C, pipe, 0))
+    return out + [(8, 1, 4, 0, 2048), (4, 1, 1, 2, 300), (16, 0, 2, 1, 7), (4, 1, 8, 3, 5), (2, 1, 8, 3, 333),
+                  (4, 1, 8, 4, 3), (8, 1, 4, 4, 17), (8, 0, 1, 4, 1)]
+
+
+def test_schedule_variants_bit_identical():
+    """Every schedule of the exact kernel (register batches, double-buffered,
+    LDS-DMA staging, multi-column, capped grid) gives the default's bits,
+    including a ragged last column group and a P % 4 tail."""
+    for K, P in [(37, 123_457), (1, 4099), (9, 1_000_003), (3, 64 * 64 * 3 + 5), (5, 190)]:
+        x = _clients(K, P, seed=K + P)
+        w = _w(_weights(K))
+        base = mfl_amd.reduce_packed(x, w, P)
+        exp = O.reduce_f32(x[:, :P].cpu().numpy(), _weights(K))
+        assert_bits(base, torch.from_numpy(exp), f"default K={K} P={P}")
+        for v in _all_variants():
+            got = mfl_amd.reduce_packed(x, w, P, tuned=v)
+            assert torch.equal(got.view(torch.int32), base.view(torch.int32)), (K, P, v)
+
+
 def test_misaligned_clients_take_scalar_path():
     K, P = 6, 1001
     big = _clients(K, P + 1, ld=1088, seed=9)

@@ -154,3 +154,28 @@ def test_int64_to_fp32_rounding_matches_reference_cast():
     table = KeyTable(OrderedDict(big=big))
     table.pack_into(table.groups[torch.float32], buf, [OrderedDict(big=big)])
     assert torch.equal(buf[0, :40], big.to(torch.float32))
+
+
+def test_launch_patches_reference_module_before_script_runs(tmp_path):
+    """mfl_amd.launch: the script's own `from fedavg_trainer import FedAvgTrainer`
+    (main_fedavg.py:16) must bind the patched class."""
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    (tmp_path / "fedavg_trainer.py").write_text(
+        "class FedAvgTrainer:\n"
+        "    def aggregate(self, w_locals):\n"
+        "        return 'reference'\n")
+    (tmp_path / "main_fedavg.py").write_text(
+        "import sys, torch\n"
+        "from fedavg_trainer import FedAvgTrainer\n"
+        "t = FedAvgTrainer(); t.model_global = torch.nn.Linear(2, 2)\n"
+        "out = t.aggregate([])\n"
+        "print('PATCHED' if isinstance(out, dict) and set(out) == {'weight', 'bias'} else 'NOT', sys.argv[1:])\n")
+    repo = Path(__file__).resolve().parents[1]
+    env = dict(__import__("os").environ, PYTHONPATH=str(repo))
+    proc = subprocess.run([sys.executable, "-m", "mfl_amd.launch", str(tmp_path / "main_fedavg.py"), "--gpu", "0"],
+                          cwd=tmp_path, env=env, capture_output=True, text=True, timeout=120)
+    assert proc.returncode == 0, proc.stderr
+    assert "PATCHED ['--gpu', '0']" in proc.stdout
