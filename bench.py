@@ -80,15 +80,18 @@ def fill_synthetic(clients: torch.Tensor, rank: int):
     del base
 
 
-def cpu_baseline(target_seconds: float = 12.0):
+def cpu_baseline(P: int, target_seconds: float = 12.0):
     """The reference's torch CPU loop (fedavg_trainer.py:444-458, restated in
-    oracle/fedavg_oracle.py) on a bounded sample: K = 100 clients x one flat
-    2.5M-param key (1 GB of client data); repeated until ~target_seconds."""
+    oracle/fedavg_oracle.py) on a bounded sample of the bench workload: a
+    K-slice -- 10 clients with the workload's full P-element key (1 GB at
+    P = 25M), so every tensor has the workload's size and the same cache
+    behaviour (a P-slice of 10 MB tensors can sit in a large host L3 and
+    overstate the CPU); repeated until ~target_seconds."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import fedavg_oracle as O
 
     threads = torch.get_num_threads()
-    K, P = 100, 2_500_000
+    K = 10
     g = torch.Generator().manual_seed(0)
     base = torch.randn(P, generator=g) * 0.05
     clients = [base + torch.randn(P, generator=g) * 1e-3 for _ in range(K)]
@@ -108,7 +111,7 @@ def cpu_baseline(target_seconds: float = 12.0):
         "unit": "GB/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"K={K} x P={P} fp32, one flat key; reference torch CPU loop restated "
+        "sample": f"K-slice: K={K} x P={P} fp32 (the workload's key size), one flat key; reference torch CPU loop restated "
                   f"(oracle/fedavg_oracle.py aggregate_torch); best of {len(times) - 1} reps "
                   f"after 1 warm-up, {best * 1e3:.1f} ms/reduce, torch threads={threads}",
     }
@@ -175,6 +178,8 @@ def main():
         tuned = (args.unroll or 8, max(args.nt, 0))
 
     S = red.plan.block
+    sched = mfl_amd._lib.f32_schedule(K, S) if tuned is None else None
+    launches_per_call = sched["launches"] if sched else 1
     ev_pairs = []
 
     def local_reduce(clients, w, P, out):
@@ -222,8 +227,15 @@ def main():
     if rank == 0:
         bytes_step = algorithmic_bytes(K, P_total)
         value = bytes_step * args.steps / elapsed_max / 1e9
-        bytes_launch = algorithmic_bytes(K, S)  # one launch = one chunk of one rank's shard
-        achieved = bytes_launch / (kernel_ms_max * 1e-3) / 1e9
+        # one reduce call = one chunk of one rank's shard = `launches_per_call`
+        # round-split kernel launches of equal size
+        bytes_call = algorithmic_bytes(K, S)
+        achieved = bytes_call / (kernel_ms_max * 1e-3) / 1e9
+        if sched:
+            kname = (f"reduce_f32x4_var_kernel<U={sched['unroll']},C={sched['cols']},nt={sched['nontemporal']}> "
+                     f"(exact, sequential client order; round-split x{launches_per_call})")
+        else:
+            kname = f"tuned variant {tuned}"
         roofline = {
             "bound": "hbm",
             "achieved": round(achieved, 1),
@@ -231,10 +243,10 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": None,
-            "kernel": "reduce_f32x4_kernel (exact, sequential client order)",
-            "bytes_per_launch": bytes_launch,
-            "avg_launch_ms": round(kernel_ms_max, 4),
-            "launches": len(kernel_ms),
+            "kernel": kname,
+            "bytes_per_launch": bytes_call // launches_per_call,
+            "avg_launch_ms": round(kernel_ms_max / launches_per_call, 4),
+            "launches": len(kernel_ms) * launches_per_call,
         }
         tj = args.traffic_json or str(ROOT / "profiles" / f"traffic_{args.workload}.json")
         if Path(tj).exists():
@@ -272,7 +284,7 @@ def main():
             "parity": parity,
         }
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline()
+            out["cpu_baseline"] = cpu_baseline(P_local)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

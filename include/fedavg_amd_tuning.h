@@ -12,9 +12,17 @@
 extern "C" {
 #endif
 
-/* Defaults used by fedavg_reduce_f32(). */
+/* Defaults of the first-version kernel (fedavg_reduce_f32_tuned; also the
+ * path fedavg_reduce_f32 takes for buffers that are not 16-B aligned). */
 #define FEDAVG_DEFAULT_UNROLL 8
 #define FEDAVG_DEFAULT_NONTEMPORAL 0
+
+/*
+ * The schedule fedavg_reduce_f32() uses for an aligned [K, P] problem:
+ * rows per load batch, 16-B column slices per thread, nontemporal loads, and
+ * the number of round-split launches.  Host-only query.
+ */
+int fedavg_f32_schedule(int64_t K, int64_t P, int* unroll, int* cols, int* nontemporal, int* launches);
 
 /*
  * fedavg_reduce_f32 with explicit variant knobs:

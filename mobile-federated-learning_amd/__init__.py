@@ -10,6 +10,7 @@ Layers:
   reduce                   device-resident entry points (torch tensors in HBM)
   layout                   state_dict <-> packed [K, ld] client-major buffers
   aggregate                the drop-in (DeviceAggregator, install, mixin)
+  session                  streaming rounds: pack + upload each client as it arrives
   distributed              P-sharded multi-GPU reduce + RCCL all-gather
 """
 from ._lib import FedAvgLibraryError, library_path
@@ -23,6 +24,7 @@ from .aggregate import (
 )
 from .layout import KeyTable, ShapeMismatchError, result_dtype
 from .reduce import ALIGN_ELEMS, reduce_packed, reduce_tensors, weights_tensor
+from .session import RoundSession
 
 __all__ = [
     "FedAvgLibraryError",
@@ -40,4 +42,5 @@ __all__ = [
     "reduce_packed",
     "reduce_tensors",
     "weights_tensor",
+    "RoundSession",
 ]

@@ -27,6 +27,7 @@ SIGNATURES = {
     "fedavg_reduce_splitk_f32": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_int, _vp]),
     "fedavg_weights_f32": (_c_int, [_vp, _c_i64, _vp]),
     "fedavg_pack_rows": (_c_int, [_vp, _c_i64, _vp, _c_i64, _c_int]),
+    "fedavg_f32_schedule": (_c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp]),
     "fedavg_reduce_f32_tuned": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_int, _c_int, _vp]),
     "fedavg_reduce_f32_variant": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_int, _c_int, _c_int, _c_int,
                                            _c_int, _vp]),
@@ -78,6 +79,13 @@ def load() -> ctypes.CDLL:
             raise FedAvgLibraryError(f"ABI version {ver} != expected {ABI_VERSION}; rebuild the library")
         _lib = lib
     return _lib
+
+
+def f32_schedule(K: int, P: int) -> dict:
+    """The schedule fedavg_reduce_f32 picks for an aligned [K, P] problem."""
+    vals = [ctypes.c_int() for _ in range(4)]
+    check(load().fedavg_f32_schedule(K, P, *[ctypes.byref(v) for v in vals]), "fedavg_f32_schedule")
+    return dict(zip(("unroll", "cols", "nontemporal", "launches"), (v.value for v in vals)))
 
 
 def check(rc: int, what: str) -> None:

@@ -128,6 +128,17 @@ class DeviceAggregator:
         self.last_profile: Dict[str, float] = {}
 
     # ------------------------------------------------------------------
+    def begin_round(self, template, max_clients: int):
+        """Start a streaming round (see ``session.RoundSession``)."""
+        from .session import RoundSession
+
+        return RoundSession(self, template, max_clients)
+
+    def _copy_stream_for(self):
+        if self._copy_stream is None:
+            self._copy_stream = torch.cuda.Stream(self.device)
+        return self._copy_stream
+
     def _staging_for(self, dtype: torch.dtype, K: int, ld: int) -> _Staging:
         st = self._staging.get(dtype)
         if st is None or st.K < K or st.ld != ld:
@@ -160,9 +171,7 @@ class DeviceAggregator:
         results: "OrderedDict[str, torch.Tensor]" = OrderedDict()
         with torch.cuda.device(dev):
             compute = torch.cuda.current_stream(dev)
-            if self._copy_stream is None:
-                self._copy_stream = torch.cuda.Stream(dev)
-            copy_s = self._copy_stream
+            copy_s = self._copy_stream_for()
             copy_s.wait_stream(compute)  # earlier users of the device staging are done
             t0 = time.perf_counter()
             staged = []

@@ -21,6 +21,8 @@ PKG_DIR = Path(__file__).resolve().parent
 REPO_DIR = PKG_DIR.parent
 CSRC = PKG_DIR / "csrc" / "fedavg_reduce.hip"
 CSRC_HOST = PKG_DIR / "csrc" / "fedavg_host.cpp"
+CSRC_COLLECT = PKG_DIR / "csrc" / "fedavg_collect_ext.cpp"
+COLLECT_NAME = "fedavg_collect_ext"
 INCLUDE = REPO_DIR / "include"
 LIB_DIR = PKG_DIR / "lib"
 LIB_PATH = LIB_DIR / "libfedavg_amd.so"
@@ -55,6 +57,23 @@ def up_to_date() -> bool:
         return False
     t = LIB_PATH.stat().st_mtime
     return all(p.stat().st_mtime <= t for p in sources())
+
+
+def collect_ext_path() -> Path:
+    return LIB_DIR / f"{COLLECT_NAME}.so"
+
+
+def build_collect_ext(force: bool = False, verbose: bool = False) -> Path:
+    """torch C++ extension for the host-side state_dict walk (layout.KeyTable.collect)."""
+    out = collect_ext_path()
+    if not force and out.exists() and out.stat().st_mtime >= CSRC_COLLECT.stat().st_mtime:
+        return out
+    from torch.utils.cpp_extension import load
+
+    LIB_DIR.mkdir(parents=True, exist_ok=True)
+    load(name=COLLECT_NAME, sources=[str(CSRC_COLLECT)], build_directory=str(LIB_DIR),
+         extra_cflags=["-O2"], verbose=verbose)
+    return out
 
 
 def build(force: bool = False, verbose: bool = False) -> Path:

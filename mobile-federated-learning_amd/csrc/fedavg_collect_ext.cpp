@@ -1,0 +1,62 @@
+// fedavg_collect_ext.cpp -- native walk over the clients' state_dicts.
+//
+// aggregate() must check every client's tensor for every key of client 0
+// (fedavg_trainer.py:450-457 reads p_i[k] for all i, k) and gather its host
+// address for the packer (csrc/fedavg_host.cpp).  In Python that costs about
+// 0.75 us per tensor (26 ms for resnet56 x 100 clients, 35,000 tensors); here
+// the dict lookups and tensor metadata are read through the torch C++ API.
+//
+// collect(dicts, names, template) -> (ptrs[K, N] int64, bad_client, bad_key)
+//   template[j] is client 0's tensor for names[j].  A client tensor passes
+//   when it has the template's sizes and dtype and is a contiguous CPU tensor.
+//   On the first one that does not (or a missing key), the scan stops and
+//   returns its (client, key) index so the Python layer can raise the
+//   reference's exception or take its general path; otherwise (-1, -1).
+#include <torch/csrc/autograd/python_variable.h>
+#include <torch/extension.h>
+
+#include <vector>
+
+namespace py = pybind11;
+
+static py::tuple collect(py::list dicts, py::list names, py::list templ) {
+  const Py_ssize_t K = PyList_GET_SIZE(dicts.ptr());
+  const Py_ssize_t N = PyList_GET_SIZE(names.ptr());
+  if (PyList_GET_SIZE(templ.ptr()) != N) throw std::invalid_argument("template/names length mismatch");
+  std::vector<std::vector<int64_t>> sizes(N);
+  std::vector<at::ScalarType> dtypes(N);
+  for (Py_ssize_t j = 0; j < N; ++j) {
+    PyObject* t = PyList_GET_ITEM(templ.ptr(), j);
+    if (!THPVariable_Check(t)) throw std::invalid_argument("template entries must be tensors");
+    const at::Tensor& ten = THPVariable_Unpack(t);
+    sizes[j] = ten.sizes().vec();
+    dtypes[j] = ten.scalar_type();
+  }
+  auto ptrs = torch::empty({static_cast<int64_t>(K), static_cast<int64_t>(N)}, torch::kInt64);
+  int64_t* out = ptrs.data_ptr<int64_t>();
+  for (Py_ssize_t i = 0; i < K; ++i) {
+    PyObject* d = PyList_GET_ITEM(dicts.ptr(), i);
+    for (Py_ssize_t j = 0; j < N; ++j) {
+      PyObject* t = PyObject_GetItem(d, PyList_GET_ITEM(names.ptr(), j));  // new reference
+      if (!t) {
+        PyErr_Clear();
+        return py::make_tuple(py::none(), i, j);
+      }
+      bool ok = THPVariable_Check(t);
+      if (ok) {
+        const at::Tensor& ten = THPVariable_Unpack(t);
+        ok = ten.scalar_type() == dtypes[j] && ten.sizes() == c10::IntArrayRef(sizes[j]) && ten.is_cpu() &&
+             ten.is_contiguous();
+        if (ok) out[i * N + j] = reinterpret_cast<int64_t>(ten.data_ptr());
+      }
+      Py_DECREF(t);  // the dict keeps the tensor alive
+      if (!ok) return py::make_tuple(py::none(), i, j);
+    }
+  }
+  return py::make_tuple(ptrs, -1, -1);
+}
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "native state_dict walk for mfl_amd (host metadata only)";
+  m.def("collect", &collect, "validate clients against client 0 and gather data pointers");
+}

@@ -779,6 +779,50 @@ var_launcher pick_var(int unroll, int cols, int nt, int pipe) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Production schedule for the exact fp32 reduce (fedavg_reduce_f32), chosen
+// from the in-process A/B sweeps in profiles/ (scripts/kernel_variants.py):
+//   * column slices per thread C: the widest of 8/4/2/1 that still gives a
+//     launch >= 512 blocks (a block then reads C*4 KiB contiguous bytes of
+//     each client row per step); U (rows per load batch) = 4 for C = 8, else 8
+//     (32 and 32/16/8 16-B loads in flight per thread);
+//   * round-split dispatch: the column range is cut into the fewest equal
+//     launches of <= 768 blocks (2-3 blocks per CU) -- one resident round
+//     each, so every launch's blocks start together and sweep one compact
+//     window of every row (88% of HBM peak at K=100 x P=25M vs 76% for one
+//     multi-round launch of the same kernel);
+//   * nontemporal loads (the rows are read once), except for working sets of
+//     64-240 MiB, which stay resident in the 256 MiB Infinity Cache across
+//     back-to-back rounds when loaded with the default policy.
+// ---------------------------------------------------------------------------
+struct Schedule {
+  int unroll, cols, nt, blocks_per_launch;
+};
+
+constexpr int kBlocksPerLaunch = 768;
+
+Schedule choose_schedule(int64_t K, int64_t P) {
+  const int64_t nvec = (P + 3) / 4;
+  Schedule sc{8, 1, 1, kBlocksPerLaunch};
+  if (nvec >= int64_t(512) * kBlock * 8) {
+    sc.unroll = 4, sc.cols = 8;
+  } else if (nvec >= int64_t(512) * kBlock * 4) {
+    sc.cols = 4;
+  } else if (nvec >= int64_t(512) * kBlock * 2) {
+    sc.cols = 2;
+  }
+  const double bytes = 4.0 * static_cast<double>(K) * static_cast<double>(P);
+  if (bytes > 64.0 * (1 << 20) && bytes <= 240.0 * (1 << 20)) sc.nt = 0;
+  return sc;
+}
+
+void launch_production_f32(const float* clients, int K, int64_t ld, int64_t P, const float* W, float* out,
+                           hipStream_t s) {
+  const Schedule sc = choose_schedule(K, P);
+  var_launcher fn = pick_var(sc.unroll, sc.cols, sc.nt, 4);
+  fn(clients, K, ld, P, W, out, sc.blocks_per_launch, s);
+}
+
 }  // namespace
 
 // ===========================================================================
@@ -792,8 +836,30 @@ const char* fedavg_last_error(void) { return g_err; }
 
 int fedavg_reduce_f32(const float* clients, int64_t K, int64_t P, int64_t ld, const float* weights,
                       float* out, void* stream) {
+  const char* what = "fedavg_reduce_f32";
+  if (aligned16(clients) && aligned16(out) && (ld % 4) == 0 && P > 0 && K > 0) {
+    int rc = check_common(clients, K, P, ld, weights, out, what);
+    if (rc) return rc;
+    if (!aligned4(weights)) return set_error(FEDAVG_EALIGN, "%s: weights must be 4-byte aligned", what);
+    launch_production_f32(clients, static_cast<int>(K), ld, P, weights, out, static_cast<hipStream_t>(stream));
+    return launch_status(what);
+  }
+  // unaligned buffers / odd row stride: the first-version kernels (same bits)
   return reduce_f32_impl(clients, K, P, ld, weights, out, static_cast<hipStream_t>(stream),
-                         FEDAVG_DEFAULT_UNROLL, FEDAVG_DEFAULT_NONTEMPORAL, "fedavg_reduce_f32");
+                         FEDAVG_DEFAULT_UNROLL, FEDAVG_DEFAULT_NONTEMPORAL, what);
+}
+
+int fedavg_f32_schedule(int64_t K, int64_t P, int* unroll, int* cols, int* nontemporal, int* launches) {
+  if (K <= 0 || P < 0) return set_error(FEDAVG_EINVAL, "fedavg_f32_schedule: bad sizes");
+  const Schedule sc = choose_schedule(K, P);
+  const int64_t nvec = (P + 3) / 4;
+  const int64_t span = static_cast<int64_t>(kBlock) * sc.cols;
+  const int64_t blocks = (nvec + span - 1) / span;
+  if (unroll) *unroll = sc.unroll;
+  if (cols) *cols = sc.cols;
+  if (nontemporal) *nontemporal = sc.nt;
+  if (launches) *launches = static_cast<int>((blocks + sc.blocks_per_launch - 1) / sc.blocks_per_launch);
+  return FEDAVG_OK;
 }
 
 int fedavg_reduce_f32_tuned(const float* clients, int64_t K, int64_t P, int64_t ld, const float* weights,
@@ -811,7 +877,7 @@ int fedavg_reduce_f32_variant(const float* clients, int64_t K, int64_t P, int64_
   if (P == 0) return FEDAVG_OK;
   if (!aligned16(clients) || !aligned16(out) || (ld % 4) != 0)
     return set_error(FEDAVG_EALIGN, "%s: needs 16-B aligned clients/out and ld %% 4 == 0", what);
-  var_launcher fn = pick_var(unroll, cols, nontemporal ? 1 : 0, pipelined ? 1 : 0);
+  var_launcher fn = pick_var(unroll, cols, nontemporal ? 1 : 0, pipelined);
   if (!fn) return set_error(FEDAVG_EMODE, "%s: unsupported unroll=%d cols=%d", what, unroll, cols);
   fn(clients, static_cast<int>(K), ld, P, weights, out, max_blocks, static_cast<hipStream_t>(stream));
   return launch_status(what);

@@ -83,6 +83,31 @@ class Group:
         return max(_round_up(self.P, ALIGN_ELEMS), ALIGN_ELEMS)
 
 
+_COLLECT = []
+
+
+def _collect_ext():
+    """The native state_dict walk (csrc/fedavg_collect_ext.cpp), or None if it
+    was not built -- it only speeds up host bookkeeping; the Python walk below
+    computes the same pointers and raises the same errors."""
+    if not _COLLECT:
+        mod = None
+        try:
+            import importlib.util
+
+            from .build import collect_ext_path
+
+            path = collect_ext_path()
+            if path.exists():
+                spec = importlib.util.spec_from_file_location("fedavg_collect_ext", path)
+                mod = importlib.util.module_from_spec(spec)
+                spec.loader.exec_module(mod)
+        except (ImportError, OSError):
+            mod = None
+        _COLLECT.append(mod)
+    return _COLLECT[0]
+
+
 # fedavg_pack_item.kind codes (include/fedavg_amd.h)
 _PACK_KIND = {torch.int64: 1, torch.int32: 2, torch.int16: 3, torch.int8: 4, torch.uint8: 5, torch.bool: 6}
 
@@ -103,6 +128,7 @@ class KeyTable:
             g.keys.append(e)
             self.entries.append(e)
         self._names = [e.name for e in self.entries]
+        self._template = [template[n] for n in self._names]
         self._shapes = [torch.Size(e.shape) for e in self.entries]
         self._dtypes = [e.src_dtype for e in self.entries]
         # per group: column indices into the entry list + pack metadata
@@ -124,6 +150,14 @@ class KeyTable:
         the per-key Python cost to a few hundred ns.
         """
         names, shapes, dtypes = self._names, self._shapes, self._dtypes
+        ext = _collect_ext()
+        if ext is not None:
+            got, bad_i, _bad_j = ext.collect(list(state_dicts), names, self._template)
+            if got is not None:
+                return got.numpy(), []
+            # something unusual at client bad_i (missing key, other shape/dtype,
+            # non-contiguous or non-CPU tensor): the general path below raises
+            # the reference's exception or handles it
         ptrs = np.empty((len(state_dicts), len(names)), dtype=np.int64)
         keepalive = []
         for i, sd in enumerate(state_dicts):

@@ -1,0 +1,121 @@
+"""Streaming aggregation: pack and upload each client as it arrives.
+
+In the reference round loop (fedavg_trainer.py:172-217) clients train one
+after another and each result is appended to ``w_locals`` at :199; the
+reduction only starts at :217.  With the drop-in's ``aggregate`` every client
+row is packed and copied to HBM at :217, so the whole PCIe transfer sits on
+the round's critical path.  A ``RoundSession`` moves that work next to the
+client loop: ``add`` validates the client, packs its row into pinned staging
+with the native packer and starts the row's H2D on a side stream, while the
+next client trains; ``finish`` then only forms the weights, runs the kernel
+and copies the averaged model back.
+
+Integration (two lines in the reference loop)::
+
+    session = aggregator.begin_round(self.model_global.state_dict(), len(client_indexes))
+    ...
+    w_locals.append((client.get_sample_number(), copy.deepcopy(w)))       # :199
+    session.add(*w_locals[-1])                                              # new
+    ...
+    w_glob = session.finish(w_locals)                                       # :217, replaces aggregate
+
+``finish(w_locals)`` keeps ``aggregate``'s contract: it returns
+``w_locals[0][1]`` with its values replaced, raises ``ZeroDivisionError`` on
+a zero sample total, and checks that ``w_locals`` holds exactly the clients
+that were added (same count, sample numbers and dict objects, in order).
+Results are bit-identical to ``aggregate`` (and to the reference).
+"""
+from __future__ import annotations
+
+import time
+from collections import OrderedDict
+from typing import Mapping, Optional
+
+import torch
+
+from . import _lib
+from .layout import KeyTable
+from .reduce import reduce_packed, weights_tensor
+
+__all__ = ["RoundSession"]
+
+
+class RoundSession:
+    """One round's streaming reduction on a ``DeviceAggregator``'s device."""
+
+    def __init__(self, aggregator, template: Mapping[str, torch.Tensor], max_clients: int):
+        if max_clients < 1:
+            raise ValueError("max_clients must be >= 1")
+        self.agg = aggregator
+        self.table = KeyTable(template)
+        self.max_clients = max_clients
+        self.counts = []
+        self.dicts = []
+        self._keepalive = []
+        self._finished = False
+        self.dev = aggregator.device
+        self._lib = _lib.load()
+        self._threads = max(1, torch.get_num_threads())
+        with torch.cuda.device(self.dev):
+            self._compute = torch.cuda.current_stream(self.dev)
+            self._copy = aggregator._copy_stream_for()
+            self._copy.wait_stream(self._compute)
+        self._staging = {g.dtype: aggregator._staging_for(g.dtype, max_clients, g.ld)
+                         for g in self.table.groups.values()}
+        self.add_ms = 0.0
+
+    def add(self, sample_num, state_dict: Mapping[str, torch.Tensor]) -> None:
+        """Validate, pack and start uploading one client's row (fedavg_trainer.py:199)."""
+        if self._finished:
+            raise RuntimeError("session already finished")
+        i = len(self.counts)
+        if i >= self.max_clients:
+            raise ValueError(f"more than max_clients={self.max_clients} clients added")
+        t0 = time.perf_counter()
+        ptrs, keep = self.table.collect([state_dict])
+        for g in self.table.groups.values():
+            st = self._staging[g.dtype]
+            items = self.table.pack_items(g, ptrs, i, g.ld)
+            _lib.check(self._lib.fedavg_pack_rows(items.ctypes.data, items.shape[0], st.host.data_ptr(),
+                                                  st.host.element_size(), self._threads), "fedavg_pack_rows")
+            with torch.cuda.stream(self._copy):
+                st.dev[i].copy_(st.host[i], non_blocking=True)
+        self.counts.append(sample_num)
+        self.dicts.append(state_dict)
+        if keep:
+            self._keepalive.append(keep)
+        self.add_ms += (time.perf_counter() - t0) * 1e3
+
+    def finish(self, w_locals=None):
+        """Reduce the added clients; ``aggregate``'s contract (fedavg_trainer.py:441-458)."""
+        if self._finished:
+            raise RuntimeError("session already finished")
+        self._finished = True
+        if w_locals is not None:
+            if len(w_locals) != len(self.counts):
+                raise ValueError(f"w_locals has {len(w_locals)} clients, session has {len(self.counts)}")
+            for i, ((n, sd), n2, sd2) in enumerate(zip(w_locals, self.counts, self.dicts)):
+                if sd is not sd2 or n != n2:
+                    raise ValueError(f"w_locals[{i}] is not the client added as #{i}")
+        if not self.counts:
+            raise ValueError("no clients added (the reference returns the global model then: use aggregate([]))")
+        K = len(self.counts)
+        acc_dict = w_locals[0][1] if w_locals is not None else OrderedDict()
+        from .aggregate import sample_weights
+
+        weights = sample_weights(self.counts)  # ZeroDivisionError like the reference
+        outs = []
+        with torch.cuda.device(self.dev):
+            self._compute.wait_stream(self._copy)
+            for g in self.table.groups.values():
+                st = self._staging[g.dtype]
+                out_dev = reduce_packed(st.dev[:K], weights_tensor(weights, g.dtype, self.dev), g.P)
+                out_host = torch.empty(g.P, dtype=g.dtype, pin_memory=True)
+                out_host.copy_(out_dev, non_blocking=True)
+                outs.append((g, out_host))
+            self._compute.synchronize()
+        for g, out_host in outs:
+            for name, t in self.table.unpack(g, out_host).items():
+                acc_dict[name] = t
+        self._keepalive.clear()
+        return acc_dict

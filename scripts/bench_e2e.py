@@ -8,7 +8,11 @@ into the CPU-resident global model), so this measures the whole drop-in:
 validation, packing into pinned staging rows overlapped with per-client H2D,
 the HIP kernel, D2H and unpacking -- next to the reference's torch CPU loop
 (oracle restatement) on the same inputs in the same process, and checks the
-two agree bit for bit.  One JSON line per config.
+two agree bit for bit.  It also times the streaming form (RoundSession):
+clients added one by one as they would arrive from the round loop (with a
+simulated per-client training time, --train-ms, between arrivals), and the
+time from the last arrival to the averaged model (the part left on the
+round's critical path).  One JSON line per config.
 """
 from __future__ import annotations
 
@@ -92,7 +96,7 @@ def fresh(counts, dicts):
     return [(counts[0], OrderedDict(dicts[0]))] + list(zip(counts[1:], dicts[1:]))
 
 
-def run(name, reps):
+def run(name, reps, train_ms=0.0):
     K, shapes = CONFIGS[name]
     P = sum(math.prod(s) for _, s in shapes)
     counts, dicts = make_clients(K, shapes)
@@ -117,17 +121,40 @@ def run(name, reps):
         t = time.perf_counter() - t0
         if r:
             cpu_t.append(t)
+    # streaming rounds (mfl_amd.RoundSession): clients are added as they
+    # "arrive"; what remains after the last arrival is the round's critical path
+    crit, add_ms = [], []
+    for r in range(reps + 1):
+        wl = fresh(counts, dicts)
+        torch.cuda.synchronize()
+        sess = agg.begin_round(wl[0][1], K)
+        for n, sd in wl:
+            if train_ms:
+                time.sleep(train_ms / 1e3)  # the client's local training (client.py:38-96) would run here
+            sess.add(n, sd)
+        t0 = time.perf_counter()
+        sout = sess.finish(wl)
+        t = time.perf_counter() - t0
+        if r:
+            crit.append(t)
+            add_ms.append(sess.add_ms)
+    same_stream = all(torch.equal(sout[k].reshape(-1).view(torch.int32), out[k].reshape(-1).view(torch.int32))
+                      for k in out)
     same = all(torch.equal(out[k].reshape(-1).view(torch.int32), ref[k].reshape(-1).view(torch.int32)) for k in ref)
     g, c = float(np.median(gpu_t)), float(np.median(cpu_t))
     return {
         "config": name, "K": K, "P": P, "keys": len(shapes),
         "e2e_ms_median": round(g * 1e3, 3), "e2e_ms_min": round(min(gpu_t) * 1e3, 3),
         "e2e_GBps": round(alg / g / 1e9, 2),
-        "pack_h2d_ms_median": round(float(np.median([p["pack_h2d_ms"] for p in prof])), 3),
-        "kernel_d2h_ms_median": round(float(np.median([p["kernel_d2h_ms"] for p in prof])), 3),
+        "pack_issue_ms_median": round(float(np.median([p["pack_issue_ms"] for p in prof])), 3),
+        "h2d_kernel_d2h_ms_median": round(float(np.median([p["h2d_kernel_d2h_ms"] for p in prof])), 3),
         "cpu_ref_ms_median": round(c * 1e3, 3), "cpu_ref_GBps": round(alg / c / 1e9, 2),
         "cpu_threads": torch.get_num_threads(), "speedup_vs_cpu": round(c / g, 2),
         "bit_exact_vs_cpu_ref": bool(same), "reps": reps,
+        "stream_finish_ms_median": round(float(np.median(crit)) * 1e3, 3),
+        "stream_add_ms_total_median": round(float(np.median(add_ms)), 3),
+        "stream_bit_exact": bool(same_stream),
+        "stream_train_ms_per_client": train_ms,
     }
 
 
@@ -135,10 +162,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="mnist_lr,femnist_cnn,resnet56,target_flat")
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--train-ms", type=float, default=5.0,
+                    help="simulated per-client training time between streaming arrivals")
     args = ap.parse_args()
     torch.cuda.set_device(0)
     for name in args.configs.split(","):
-        print(json.dumps(run(name, args.reps)), flush=True)
+        print(json.dumps(run(name, args.reps, args.train_ms)), flush=True)
 
 
 if __name__ == "__main__":

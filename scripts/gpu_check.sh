@@ -21,6 +21,11 @@ fi
 timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > "$OUT/bench.json" 2> "$OUT/bench.err"
 echo "[gpu_check] bench ok: $(cat "$OUT/bench.json")" | tee -a "$OUT/progress.log"
 
+if [[ "${E2E:-0}" == 1 ]]; then
+  timeout -k 10 600 python scripts/bench_e2e.py --reps 5 > "$OUT/e2e.jsonl" 2> "$OUT/e2e.err"
+  echo "[gpu_check] e2e ok" | tee -a "$OUT/progress.log"
+fi
+
 if [[ "${SKIP_PROF:-0}" != 1 ]]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_stats" -o run \
       -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline ${BENCH_ARGS:-} > "$OUT/prof_stats.log" 2>&1

@@ -60,8 +60,10 @@ def main():
         for U, C in [(8, 4), (4, 8), (8, 2), (8, 1)]:
             for nt in (0, 1):
                 variants.append((f"var U{U} C{C} nt{nt} pipe0 mb0", (U, nt, C, 0, 0)))
-        for U, C in [(8, 4), (4, 4)]:
+        for U, C in [(8, 4), (4, 4), (4, 8), (8, 2)]:
             variants.append((f"bal U{U} C{C} nt1 mb0", (U, 1, C, 3, 0)))
+        for U, C in [(4, 4), (2, 4), (8, 2), (4, 2), (8, 1), (16, 1), (2, 8)]:
+            variants.append((f"glds U{U} C{C} nt1", (U, 1, C, 2, 0)))
         for U, C in [(2, 4), (4, 4), (8, 4), (16, 4), (2, 8), (4, 8), (8, 2), (16, 2), (4, 2), (8, 1), (16, 1)]:
             for nt in (0, 1):
                 for mb in (0, 512, 768):

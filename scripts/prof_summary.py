@@ -58,6 +58,7 @@ def main():
     ap.add_argument("--workload", default="target")
     ap.add_argument("--K", type=int, default=100)
     ap.add_argument("--P", type=int, default=25_000_000)
+    ap.add_argument("--launches", type=int, default=1, help="round-split launches per reduce call")
     args = ap.parse_args()
     base = Path(args.outdir)
     prof = ROOT / "profiles"
@@ -90,7 +91,7 @@ def main():
     if best:
         name, fv, wv = best
         hbm = (2.0 * fv + wv) * 1024.0
-        alg = 4 * args.K * args.P + 4 * args.P + 4 * args.K
+        alg = (4 * args.K * args.P + 4 * args.P + 4 * args.K) // args.launches
         traffic = {
             "kernel": name,
             "FETCH_SIZE_KiB": fv,

@@ -291,3 +291,26 @@ def test_sharded_reducer_single_rank_chunks():
     exp = O.reduce_f32(host.numpy(), w)
     got = torch.cat([v for v, _ in red.local_model_columns()])
     assert_bits(got, torch.from_numpy(exp))
+
+
+def test_round_session_streaming_matches_golden():
+    for name in ["mnist_lr_k100", "resnet_like_bn_k5", "int_dtypes_k3", "float64_key_k3", "bfloat16_key_k3"]:
+        meta, w_locals, expected = load_case(name)
+        agg = mfl_amd.DeviceAggregator(DEV)
+        sess = agg.begin_round(w_locals[0][1], len(w_locals) + 3)
+        for n, sd in w_locals:
+            sess.add(n, sd)
+        out = sess.finish(w_locals)
+        assert out is w_locals[0][1]
+        for k, exp in expected.items():
+            assert_bits(out[k], exp, f"{name}/{k}")
+
+
+def test_round_session_checks_w_locals():
+    _, w_locals, _ = load_case("mnist_lr_k10")
+    agg = mfl_amd.DeviceAggregator(DEV)
+    sess = agg.begin_round(w_locals[0][1], 10)
+    for n, sd in w_locals[:5]:
+        sess.add(n, sd)
+    with pytest.raises(ValueError):
+        sess.finish(w_locals)

@@ -179,3 +179,54 @@ def test_launch_patches_reference_module_before_script_runs(tmp_path):
                           cwd=tmp_path, env=env, capture_output=True, text=True, timeout=120)
     assert proc.returncode == 0, proc.stderr
     assert "PATCHED ['--gpu', '0']" in proc.stdout
+
+
+def _python_collect(table, dicts, monkeypatch):
+    from mfl_amd import layout
+    monkeypatch.setattr(layout, "_COLLECT", [None])
+    try:
+        return table.collect(dicts)
+    finally:
+        monkeypatch.setattr(layout, "_COLLECT", [])
+
+
+def test_native_collect_matches_python_walk(monkeypatch):
+    from mfl_amd.layout import _collect_ext
+    if _collect_ext() is None:
+        pytest.skip("collect extension not built")
+    for name in ["resnet_like_bn_k5", "int_dtypes_k3", "mnist_lr_k100", "float64_key_k3", "bfloat16_key_k3"]:
+        _, w_locals, _ = load_case(name)
+        dicts = [sd for _, sd in w_locals]
+        table = KeyTable(dicts[0])
+        native, keep = table.collect(dicts)
+        assert keep == []
+        py, _ = _python_collect(table, dicts, monkeypatch)
+        assert (native == py).all(), name
+
+
+@pytest.mark.parametrize("case", ["missing", "shape", "dtype", "noncontig", "notensor"])
+def test_native_collect_falls_back_for_unusual_clients(case):
+    a = OrderedDict(w=torch.arange(6, dtype=torch.float32).reshape(2, 3), b=torch.ones(2))
+    if case == "missing":
+        b = OrderedDict(w=torch.ones(2, 3))
+        err = KeyError
+    elif case == "shape":
+        b = OrderedDict(w=torch.ones(3, 2), b=torch.ones(2))
+        err = mfl_amd.ShapeMismatchError
+    elif case == "dtype":
+        b = OrderedDict(w=torch.ones(2, 3, dtype=torch.float64), b=torch.ones(2))
+        err = TypeError
+    elif case == "notensor":
+        b = OrderedDict(w=[[1.0] * 3] * 2, b=torch.ones(2))
+        err = AttributeError
+    else:
+        b = OrderedDict(w=torch.ones(3, 2).t(), b=torch.ones(2))  # non-contiguous: handled, not an error
+        err = None
+    table = KeyTable(a)
+    if err is None:
+        ptrs, keep = table.collect([a, b])
+        assert len(keep) == 1 and ptrs[1, 0] == keep[0][0].data_ptr()
+        assert torch.equal(keep[0][0], b["w"])
+    else:
+        with pytest.raises(err):
+            table.collect([a, b])
