@@ -148,6 +148,7 @@ def main():
     ap.add_argument("--unroll", type=int, default=0, help="kernel variant: loads in flight per thread")
     ap.add_argument("--nt", type=int, default=-1, help="kernel variant: 1 = nontemporal loads")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--graph", action="store_true", help="N=1: replay each step from a captured hipGraph")
     ap.add_argument("--traffic-json", default="", help="PMC traffic summary (profiles/*.json) to attach")
     args = ap.parse_args()
 
@@ -157,10 +158,18 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus > 1 needs torch.distributed.run (one process per GPU)")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # Rehearsal knobs (a 1-GPU box): FEDAVG_DIST_BACKEND=gloo and
+    # FEDAVG_SAME_DEVICE=1 run N ranks on cuda:0.  The driver's runs use the
+    # defaults: RCCL ("nccl") with one GPU per rank.
+    backend = os.environ.get("FEDAVG_DIST_BACKEND", "nccl")
+    dev_index = 0 if os.environ.get("FEDAVG_SAME_DEVICE") == "1" else local_rank
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     mfl_amd._lib.load()
 
     K, P_local, desc = WORKLOADS[args.workload]
@@ -201,10 +210,41 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
 
-    red.local_reduce = timed_local_reduce
+    step = lambda: red.step(w_dev)  # noqa: E731
+    if args.graph:
+        # one step captured into a hipGraph and replayed: removes the per-step
+        # host launch path (Python + ctypes + hipLaunchKernel) that dominates
+        # small, cache-resident workloads
+        if world > 1:
+            raise SystemExit("--graph is single-GPU only (RCCL capture is not used)")
+        graph = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            red.step(w_dev)  # warm the capture stream
+            torch.cuda.synchronize()
+            with torch.cuda.graph(graph, stream=s):
+                red.step(w_dev)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+
+        def step():
+            st = torch.cuda.Event(enable_timing=True)
+            en = torch.cuda.Event(enable_timing=True)
+            st.record()
+            graph.replay()
+            en.record()
+            ev_pairs.append((st, en))
+
+        for _ in range(args.warmup):
+            graph.replay()
+        torch.cuda.synchronize()
+        ev_pairs.clear()
+    else:
+        red.local_reduce = timed_local_reduce
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        red.step(w_dev)
+        step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -279,6 +319,7 @@ def main():
                              if red.gather else "none (single GPU or --no-gather)"),
                 "parallelism": f"p-shard{world}",
                 "kernel_variant": {"unroll": tuned[0], "nt": tuned[1]} if tuned else "default",
+                "launch": "hipGraph replay" if args.graph else "eager (stream-ordered)",
             },
             "roofline": roofline,
             "parity": parity,

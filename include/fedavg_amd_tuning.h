@@ -36,15 +36,17 @@ int fedavg_reduce_f32_tuned(const float* clients, int64_t K, int64_t P, int64_t 
 
 /*
  * Variant family of the exact fp32 kernel (same bits, different schedule):
- *   unroll     : client rows per load batch (2, 4, 8, 16)
- *   cols       : 16-B column slices per thread (1, 2, 4; 8 with unroll <= 4)
+ *   unroll     : client rows per load batch (1, 2, 4, 8, 16)
+ *   cols       : 16-B column slices per thread (1, 2, 4; 8 with unroll <= 8; 16 with unroll <= 2)
  *   pipelined  : 0 = register batches; 1 = register double-buffered batches
  *                (2*unroll*cols loads in flight); 2 = LDS-DMA staging
  *                (global_load_lds_dwordx4 into per-wave LDS slots, unroll*cols <= 16);
  *                3 = balanced persistent: grid = blocks resident on the chip, each block
  *                owns an equal contiguous range of 1 KiB wave-slices (unroll*cols <= 32);
  *                4 = round-split: the plain kernel (mode 0) launched over the fewest
- *                equal column ranges that each fit in one resident round
+ *                equal column ranges that each fit in one resident round;
+ *                5 = windowed balanced: equal windows, each launched with exactly
+ *                max_blocks blocks (0 = 3 x CUs), split evenly at 1 KiB granularity
  *   max_blocks : 0 = default grid (one block per column group; for pipelined == 3
  *                the resident block count); > 0 caps / sets the grid
  * Needs 16-B aligned clients/out and ld % 4 == 0.

@@ -31,7 +31,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--quick", action="store_true")
-    ap.add_argument("--set", default="all", choices=["all", "focus"])
+    ap.add_argument("--set", default="all", choices=["all", "focus", "wide", "window"])
     ap.add_argument("--no-tiled", action="store_true")
     args = ap.parse_args()
     K, P = args.K, args.P
@@ -43,7 +43,7 @@ def main():
     x = torch.randn((K, ld), generator=g, device=dev) * 0.05
     ntiles = (P + 1023) // 1024
     tiled = None
-    if args.set != "focus" and not args.no_tiled:
+    if args.set == "all" and not args.no_tiled:
         tiled = torch.zeros((ntiles, K, 1024), device=dev)
         full_cols = min(ntiles * 1024, ld) // 1024 * 1024
         tiled[: full_cols // 1024] = x[:, :full_cols].reshape(K, full_cols // 1024, 1024).permute(1, 0, 2)
@@ -56,7 +56,19 @@ def main():
     ref = mfl_amd.reduce_packed(x, w, P)
 
     variants = [("default", None)]
-    if args.set == "focus":
+    if args.set == "window":
+        for U, C in [(4, 8), (8, 8), (8, 4), (2, 16), (4, 4)]:
+            for G in (512, 768, 1024):
+                variants.append((f"window U{U} C{C} nt1 G{G}", (U, 1, C, 5, G)))
+        for U, C, mb in [(4, 8, 768), (8, 8, 768), (8, 4, 512)]:
+            variants.append((f"split U{U} C{C} nt1 mb{mb}", (U, 1, C, 4, mb)))
+        unrolls = []
+    elif args.set == "wide":
+        for U, C in [(4, 8), (2, 8), (8, 8), (2, 16), (1, 16), (8, 4)]:
+            for mb in (384, 512, 640, 768, 896, 1024, 1280):
+                variants.append((f"split U{U} C{C} nt1 mb{mb}", (U, 1, C, 4, mb)))
+        unrolls = []
+    elif args.set == "focus":
         for U, C in [(8, 4), (4, 8), (8, 2), (8, 1)]:
             for nt in (0, 1):
                 variants.append((f"var U{U} C{C} nt{nt} pipe0 mb0", (U, nt, C, 0, 0)))
@@ -80,7 +92,7 @@ def main():
                         continue  # spills
                     for mb in ((0,) if args.quick else (0, 2048)):
                         variants.append((f"var U{U} C{C} nt{nt} pipe{pipe} mb{mb}", (U, nt, C, pipe, mb)))
-    if args.set != "focus":
+    if args.set == "all":
         for U in (2, 4):
             for nt in (0, 1):
                 variants.append((f"var U{U} C8 nt{nt} pipe0 mb0", (U, nt, 8, 0, 0)))

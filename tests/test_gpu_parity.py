@@ -148,19 +148,20 @@ def test_tuned_variants_bit_identical(unroll, nt):
 
 def _all_variants():
     out = []
-    for U in (2, 4, 8, 16):
-        for C in (1, 2, 4, 8):
-            if C == 8 and U > 4:
+    for U in (1, 2, 4, 8, 16):
+        for C in (1, 2, 4, 8, 16):
+            if (C == 8 and U > 8) or (C == 16 and U > 2):
                 continue
             for nt in (0, 1):
-                for pipe in (0, 1, 2, 3, 4):
+                for pipe in (0, 1, 2, 3, 4, 5):
                     if pipe in (1, 3) and U * C > 32:
                         continue
                     if pipe == 2 and U * C > 16:
                         continue
                     out.append((U, nt, C, pipe, 0))
     return out + [(8, 1, 4, 0, 2048), (4, 1, 1, 2, 300), (16, 0, 2, 1, 7), (4, 1, 8, 3, 5), (2, 1, 8, 3, 333),
-                  (4, 1, 8, 4, 3), (8, 1, 4, 4, 17), (8, 0, 1, 4, 1)]
+                  (4, 1, 8, 4, 3), (8, 1, 4, 4, 17), (8, 0, 1, 4, 1), (4, 1, 8, 5, 7), (8, 1, 8, 5, 256),
+                  (2, 1, 16, 5, 1), (8, 1, 4, 5, 1000)]
 
 
 def test_schedule_variants_bit_identical():
