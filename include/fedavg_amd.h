@@ -99,6 +99,20 @@ int fedavg_reduce_splitk_f32(const float* clients, int64_t K, int64_t P, int64_t
                              const float* weights, float* out, int splits, void* stream);
 
 /*
+ * Post-aggregate client distances (fedavg_trainer.py:291, feeding delta at
+ * :293): sumsq[i] = sum_p fl32(clients[i][p] - glob[p])^2, the difference
+ * rounded to fp32 as the reference's `w[para] - w_glob[para]` does, squares
+ * exact in fp64 and summed in fp64 in a fixed order (deterministic).  The
+ * norm is fl32(sqrt(sumsq[i])).  glob : [P] fp32 (the reduce's output);
+ * sumsq : [K] double; workspace : fedavg_client_sqdist_workspace(K, P)
+ * doubles of device scratch.  Needs 16-B aligned clients/glob, ld % 4 == 0.
+ */
+int64_t fedavg_client_sqdist_workspace(int64_t K, int64_t P);
+int fedavg_client_sqdist_f32(const float* clients, int64_t K, int64_t P, int64_t ld,
+                             const float* glob, double* workspace, int64_t workspace_elems,
+                             double* sumsq, void* stream);
+
+/*
  * Host helper: weights[i] = (float)((double)n_i / (double)sum(n)) for integer
  * sample counts, exactly as Python's int/int true division followed by ATen's
  * double->float cast (fedavg_trainer.py:444-447,453).  Counts must be >= 0

@@ -18,12 +18,14 @@ from .aggregate import (
     DeviceAggregator,
     FedAvgAggregateMixin,
     aggregate,
+    client_distances,
+    estimate_delta,
     default_aggregator,
     install,
     sample_weights,
 )
 from .layout import KeyTable, ShapeMismatchError, result_dtype
-from .reduce import ALIGN_ELEMS, reduce_packed, reduce_tensors, weights_tensor
+from .reduce import ALIGN_ELEMS, client_sqdist, reduce_packed, reduce_tensors, weights_tensor
 from .session import RoundSession
 
 __all__ = [
@@ -32,6 +34,9 @@ __all__ = [
     "DeviceAggregator",
     "FedAvgAggregateMixin",
     "aggregate",
+    "client_distances",
+    "estimate_delta",
+    "client_sqdist",
     "default_aggregator",
     "install",
     "sample_weights",

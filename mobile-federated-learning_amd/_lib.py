@@ -27,6 +27,8 @@ SIGNATURES = {
     "fedavg_reduce_splitk_f32": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_int, _vp]),
     "fedavg_weights_f32": (_c_int, [_vp, _c_i64, _vp]),
     "fedavg_pack_rows": (_c_int, [_vp, _c_i64, _vp, _c_i64, _c_int]),
+    "fedavg_client_sqdist_workspace": (_c_i64, [_c_i64, _c_i64]),
+    "fedavg_client_sqdist_f32": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_i64, _vp, _vp]),
     "fedavg_f32_schedule": (_c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp]),
     "fedavg_reduce_f32_tuned": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_int, _c_int, _vp]),
     "fedavg_reduce_f32_variant": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_int, _c_int, _c_int, _c_int,

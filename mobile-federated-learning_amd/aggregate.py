@@ -33,6 +33,7 @@ from __future__ import annotations
 import copy
 import threading
 import time
+import weakref
 from collections import OrderedDict
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -40,11 +41,13 @@ import torch
 
 from . import _lib
 from .layout import KeyTable
-from .reduce import reduce_packed, weights_tensor
+from .reduce import client_sqdist, reduce_packed, weights_tensor
 
 __all__ = [
     "sample_weights",
     "prepare",
+    "client_distances",
+    "estimate_delta",
     "DeviceAggregator",
     "aggregate",
     "FedAvgAggregateMixin",
@@ -126,6 +129,9 @@ class DeviceAggregator:
         self._staging: Dict[torch.dtype, _Staging] = {}
         self._copy_stream = None
         self.last_profile: Dict[str, float] = {}
+        # device state of the last aggregate call (client rows + averaged model per
+        # dtype group), reused by client_distances for the same round
+        self._last: Dict[str, object] = {}
 
     # ------------------------------------------------------------------
     def begin_round(self, template, max_clients: int):
@@ -154,6 +160,13 @@ class DeviceAggregator:
         acc_dict, table, dicts, weights, ptrs, keepalive = prep
         results = self._reduce_groups(table, ptrs, weights)
         del keepalive
+        # weak references: the round's dicts are the caller's (the reference drops
+        # them at the next round); a dead or replaced dict simply misses the cache
+        try:
+            self._last["refs"] = [weakref.ref(sd) for sd in dicts]
+            self._last["acc"] = weakref.ref(acc_dict)
+        except TypeError:  # plain dicts cannot be weakly referenced: no reuse
+            self._last.pop("dev", None)
         # replace values in place, keeping client 0's key order (fedavg_trainer.py:450-457)
         for e in table.entries:
             acc_dict[e.name] = results[e.name]
@@ -192,17 +205,84 @@ class DeviceAggregator:
             compute.wait_stream(copy_s)
             t1 = time.perf_counter()
             outs = []
+            self._last = {"table": table, "K": K, "dev": {}}
             for g, devbuf, w_dev in staged:
                 out_dev = reduce_packed(devbuf, w_dev, g.P)
                 out_host = torch.empty(g.P, dtype=g.dtype, pin_memory=True)
                 out_host.copy_(out_dev, non_blocking=True)
                 outs.append((g, out_host))
+                self._last["dev"][g.dtype] = (devbuf, out_dev)
             compute.synchronize()
             t2 = time.perf_counter()
         for g, out_host in outs:
             results.update(table.unpack(g, out_host))
         self.last_profile = {"pack_issue_ms": (t1 - t0) * 1e3, "h2d_kernel_d2h_ms": (t2 - t1) * 1e3}
         return results
+
+
+    # ------------------------------------------------------------------
+    def client_distances(self, w_locals, w_glob) -> "np.ndarray":
+        """``[torch.norm(cat(w[k] - w_glob[k])).item() for _, w in w_locals]``
+        (fedavg_trainer.py:291) on the GPU.
+
+        Reuses the client rows and the averaged model left in HBM by the last
+        ``aggregate`` when called with that round's ``w_locals``/``w_glob``
+        (the reference's order: :217 then :291); otherwise uploads them.
+        A client whose dict IS ``w_glob`` (client 0 after aggregate, :449)
+        gets ``w_glob - w_glob``: 0.0, or NaN where ``w_glob`` holds inf/NaN.
+        Norms are accumulated in fp64 and rounded to fp32 like torch.norm's
+        fp32 result (the reference's fp32 SIMD accumulation is
+        within its own rounding error of this value).
+        """
+        import numpy as np
+
+        if not w_locals:
+            return np.zeros(0)
+        last = self._last
+        refs = last.get("refs")
+        cached = (refs is not None and last["acc"]() is w_glob and len(refs) == len(w_locals)
+                  and all(r() is sd for r, (_, sd) in zip(refs, w_locals))
+                  and set(last.get("dev", {})) == {torch.float32})
+        if cached:
+            devbuf, out_dev = last["dev"][torch.float32]
+            P = last["table"].groups[torch.float32].P
+        else:
+            devbuf, out_dev, P = self._upload_for_distances(w_locals, w_glob)
+        with torch.cuda.device(self.device):
+            sumsq = client_sqdist(devbuf, out_dev, P).cpu().numpy()
+            glob_finite = bool(torch.isfinite(out_dev[:P]).all())
+        norms = np.sqrt(sumsq).astype(np.float32).astype(np.float64)
+        for i, (_, sd) in enumerate(w_locals):
+            if sd is w_glob:
+                norms[i] = 0.0 if glob_finite else float("nan")
+        return norms
+
+    def _upload_for_distances(self, w_locals, w_glob):
+        others = [sd for _, sd in w_locals if sd is not w_glob]
+        template = others[0] if others else w_glob
+        table = KeyTable(template)
+        if set(table.groups) != {torch.float32}:
+            raise NotImplementedError("client_distances supports fp32/integer state_dicts (fp64/fp16/bf16 keys "
+                                      "change torch.cat's result dtype at fedavg_trainer.py:291)")
+        g = table.groups[torch.float32]
+        K = len(w_locals)
+        rows = [sd if sd is not w_glob else template for _, sd in w_locals]  # aliased rows are overridden
+        ptrs, keep = table.collect(rows)
+        gtable = KeyTable(w_glob)
+        gptrs, gkeep = gtable.collect([w_glob])
+        gg = gtable.groups[torch.float32]
+        lib = _lib.load()
+        host = torch.empty((K + 1, g.ld), dtype=torch.float32, pin_memory=True)
+        items = table.pack_items(g, ptrs, 0, g.ld)
+        _lib.check(lib.fedavg_pack_rows(items.ctypes.data, items.shape[0], host.data_ptr(), 4,
+                                        max(1, torch.get_num_threads())), "fedavg_pack_rows")
+        gitems = gtable.pack_items(gg, gptrs, K, g.ld)
+        _lib.check(lib.fedavg_pack_rows(gitems.ctypes.data, gitems.shape[0], host.data_ptr(), 4, 1),
+                   "fedavg_pack_rows")
+        dev = host.to(self.device, non_blocking=True)
+        torch.cuda.current_stream(self.device).synchronize()
+        del keep, gkeep
+        return dev[:K], dev[K], g.P
 
 
 _default: Dict[int, DeviceAggregator] = {}
@@ -230,6 +310,20 @@ def aggregate(w_locals, model_global=None, device: Optional[torch.device] = None
     if not isinstance(prep, _Prepared):
         return prep
     return default_aggregator(device).aggregate(w_locals, model_global=model_global)
+
+
+def client_distances(w_locals, w_glob, device: Optional[torch.device] = None):
+    """Functional form of fedavg_trainer.py:291 (see DeviceAggregator.client_distances)."""
+    return default_aggregator(device).client_distances(w_locals, w_glob)
+
+
+def estimate_delta(w_locals, w_glob, lr, device: Optional[torch.device] = None):
+    """fedavg_trainer.py:289-293: ``sum(n_i * ||w_i - w_glob||) / sum(n_i) / lr``."""
+    import numpy as np
+
+    sample_nums = np.array([n for n, _ in w_locals])
+    norms = client_distances(w_locals, w_glob, device)
+    return np.sum(sample_nums * norms) / np.sum(sample_nums) / lr
 
 
 class FedAvgAggregateMixin:

@@ -13,7 +13,7 @@ import torch
 
 from . import _lib
 
-__all__ = ["reduce_packed", "reduce_tensors", "weights_tensor", "ALIGN_ELEMS"]
+__all__ = ["reduce_packed", "reduce_tensors", "weights_tensor", "client_sqdist", "ALIGN_ELEMS"]
 
 # Row stride granule of the packed [K, ld] layout: 64 elements (256 B for
 # fp32) keeps every client row 16-B aligned for the float4/double2/8xhalf
@@ -152,4 +152,33 @@ def reduce_tensors(
     _lib.check(rc, "fedavg_reduce_ptrs_f32")
     # keep the pointer array alive until the kernel has consumed it
     ptrs.record_stream(stream if stream is not None else torch.cuda.current_stream(dev))
+    return out
+
+
+def client_sqdist(clients: torch.Tensor, glob: torch.Tensor, P: Optional[int] = None, *,
+                  stream: Optional[torch.cuda.Stream] = None) -> torch.Tensor:
+    """sumsq[i] = sum_p fl32(clients[i, p] - glob[p])^2 in fp64 (device [K] float64).
+
+    The squared distance behind fedavg_trainer.py:291; the norm is
+    ``fl32(sqrt(sumsq))``.  ``clients`` [K, ld] fp32 (16-B aligned rows),
+    ``glob`` [>= P] fp32 on the same device.
+    """
+    _check_device_tensor(clients, "clients")
+    _check_device_tensor(glob, "glob")
+    if clients.dtype != torch.float32 or glob.dtype != torch.float32:
+        raise TypeError("client_sqdist is fp32 only")
+    if clients.dim() != 2 or clients.stride(1) != 1:
+        raise ValueError("clients must be 2-D [K, ld] with unit column stride")
+    K = clients.shape[0]
+    ld = clients.stride(0) if K > 1 else clients.shape[1]
+    P = clients.shape[1] if P is None else P
+    if glob.numel() < P or not glob.is_contiguous():
+        raise ValueError("glob must be a contiguous tensor of >= P elements")
+    lib = _lib.load()
+    n_ws = lib.fedavg_client_sqdist_workspace(K, P)
+    work = torch.empty(max(n_ws, 1), dtype=torch.float64, device=clients.device)
+    out = torch.empty(K, dtype=torch.float64, device=clients.device)
+    rc = lib.fedavg_client_sqdist_f32(clients.data_ptr(), K, P, ld, glob.data_ptr(), work.data_ptr(), n_ws,
+                                      out.data_ptr(), _stream_handle(stream, clients.device))
+    _lib.check(rc, "fedavg_client_sqdist_f32")
     return out

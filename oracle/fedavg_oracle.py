@@ -50,6 +50,9 @@ __all__ = [
     "aggregate_torch",
     "aggregate_numpy",
     "empty_result",
+    "client_distances_torch",
+    "client_distances_exact",
+    "delta_from_norms",
 ]
 
 
@@ -186,3 +189,36 @@ def aggregate_numpy(w_locals, bf16_keys: Iterable[str] = ()) -> "OrderedDict[str
 def empty_result(model_global):
     """fedavg_trainer.py:442-443: deep copy of the global model's CPU state."""
     return copy.deepcopy(model_global.cpu().state_dict())
+
+
+def client_distances_torch(w_locals, w_glob, keys=None):
+    """fedavg_trainer.py:291 restated: torch.norm(torch.cat([w[k] - w_glob[k]])).item().
+
+    Uses ATen's CPU fp32 norm, which accumulates in fp32 SIMD lanes, so the
+    value depends on the host's vector width; it approximates the exact norm
+    to within its own rounding error.
+    """
+    import torch
+
+    keys = list(w_glob.keys()) if keys is None else list(keys)
+    return np.array([torch.norm(torch.cat([w[k].reshape((-1,)) - w_glob[k].reshape((-1,)) for k in keys])).item()
+                     for _, w in w_locals])
+
+
+def client_distances_exact(w_locals, w_glob, keys=None):
+    """Accurate form of :291: fp32 differences (as the reference forms them),
+    exact fp64 squares and sum, fp32-rounded sqrt."""
+    import torch
+
+    keys = list(w_glob.keys()) if keys is None else list(keys)
+    out = []
+    for _, w in w_locals:
+        d = torch.cat([w[k].reshape((-1,)) - w_glob[k].reshape((-1,)) for k in keys])
+        out.append(float(np.float32(np.sqrt(np.sum(np.square(d.numpy().astype(np.float64)))))))
+    return np.array(out)
+
+
+def delta_from_norms(sample_nums, norms, lr):
+    """fedavg_trainer.py:293."""
+    sample_nums = np.asarray(sample_nums)
+    return np.sum(sample_nums * np.asarray(norms)) / np.sum(sample_nums) / lr

@@ -315,3 +315,61 @@ def test_round_session_checks_w_locals():
         sess.add(n, sd)
     with pytest.raises(ValueError):
         sess.finish(w_locals)
+
+
+# ---------------------------------------------------------------------------
+# post-aggregate client distances (fedavg_trainer.py:291) and delta (:293)
+# ---------------------------------------------------------------------------
+def _fp32_ulp(x):
+    return np.spacing(np.float32(abs(x))).astype(np.float64)
+
+
+@pytest.mark.parametrize("name", ["mnist_lr_k10", "mnist_lr_k100", "resnet_like_bn_k5", "adversarial_k10",
+                                  "flat_k10_p65", "int_dtypes_k3", "thirds_k3", "single_client_k1"])
+def test_client_distances_after_aggregate(name):
+    import copy
+    _, w_locals, _ = load_case(name)
+    ref_locals = copy.deepcopy(w_locals)
+    ref_glob = O.aggregate_torch(ref_locals)  # reference order: :217 aggregate ...
+    agg = mfl_amd.DeviceAggregator(DEV)
+    w_glob = agg.aggregate(w_locals)
+    norms = agg.client_distances(w_locals, w_glob)  # ... then :291 (cached device rows)
+    exact = O.client_distances_exact(ref_locals, ref_glob)
+    torch_ref = O.client_distances_torch(ref_locals, ref_glob)
+    assert norms[0] == 0.0 and exact[0] == 0.0 and torch_ref[0] == 0.0  # aliasing quirk: w_locals[0][1] is w_glob
+    for a, e, t in zip(norms, exact, torch_ref):
+        assert abs(a - e) <= _fp32_ulp(e), (name, a, e)
+        assert abs(a - t) <= 1e-5 * max(abs(t), 1e-30) + 1e-30, (name, a, t)
+    # the uncached path (fresh upload) agrees with the cached one
+    again = mfl_amd.DeviceAggregator(DEV).client_distances(w_locals, w_glob)
+    assert np.array_equal(again, norms)
+    lr = 0.03
+    d = mfl_amd.estimate_delta(w_locals, w_glob, lr, device=DEV)
+    d_ref = O.delta_from_norms([n for n, _ in ref_locals], torch_ref, lr)
+    assert abs(d - d_ref) <= 1e-5 * abs(d_ref) + 1e-30
+
+
+def test_client_sqdist_large_vs_fp64():
+    K, P = 100, 25_000_000 + 3
+    ld = (P + 63) // 64 * 64
+    g = torch.Generator(device=DEV).manual_seed(5)
+    x = torch.randn((K, ld), generator=g, device=DEV) * 0.05
+    glob = torch.randn(ld, generator=g, device=DEV) * 0.05
+    got = mfl_amd.client_sqdist(x, glob, P)
+    ref = torch.stack([((x[k, :P] - glob[:P]).double() ** 2).sum() for k in range(K)])
+    rel = ((got - ref).abs() / ref).max().item()
+    assert rel < 1e-12, rel
+    again = mfl_amd.client_sqdist(x, glob, P)
+    assert torch.equal(got, again)  # deterministic
+    del x
+
+
+def test_client_sqdist_padding_nan_ignored():
+    K, P = 3, 1001  # P % 4 == 1: the last float4 holds 3 padding lanes
+    x = torch.full((K, 1024), float("nan"), device=DEV)
+    x[:, :P] = torch.arange(P, device=DEV, dtype=torch.float32) * 1e-3
+    glob = torch.full((1024,), float("nan"), device=DEV)
+    glob[:P] = 0.0
+    got = mfl_amd.client_sqdist(x, glob, P)
+    assert torch.isfinite(got).all()
+    assert abs(got[0].item() - float(((torch.arange(P, device=DEV, dtype=torch.float32) * 1e-3).double() ** 2).sum())) < 1e-9

@@ -88,3 +88,17 @@ def test_int64_example_value():
     _, _, expected = load_case("int64_nbt_example")
     assert expected["nbt"].dtype == torch.float32
     assert abs(float(expected["nbt"]) - 8.333333) < 1e-5
+
+
+@pytest.mark.parametrize("name", ["mnist_lr_k10", "resnet_like_bn_k5", "adversarial_k10", "int_dtypes_k3"])
+def test_distance_oracles_agree(name):
+    """fedavg_trainer.py:291: ATen's fp32 norm and the fp64-accurate restatement
+    agree to ATen's rounding error; client 0 (aliased to w_glob) is 0."""
+    _, w_locals, _ = load_case(name)
+    w_glob = O.aggregate_torch(w_locals)
+    t = O.client_distances_torch(w_locals, w_glob)
+    e = O.client_distances_exact(w_locals, w_glob)
+    assert t[0] == 0.0 and e[0] == 0.0
+    assert np.allclose(t, e, rtol=1e-5, atol=0)
+    d = O.delta_from_norms([n for n, _ in w_locals], t, 0.03)
+    assert np.isfinite(d)
