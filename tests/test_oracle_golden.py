@@ -90,7 +90,7 @@ def test_int64_example_value():
     assert abs(float(expected["nbt"]) - 8.333333) < 1e-5
 
 
-@pytest.mark.parametrize("name", ["mnist_lr_k10", "resnet_like_bn_k5", "adversarial_k10", "int_dtypes_k3"])
+@pytest.mark.parametrize("name", ["mnist_lr_k10", "resnet_like_bn_k5", "adversarial_k10", "sixths_k3"])
 def test_distance_oracles_agree(name):
     """fedavg_trainer.py:291: ATen's fp32 norm and the fp64-accurate restatement
     agree to ATen's rounding error; client 0 (aliased to w_glob) is 0."""
@@ -102,3 +102,10 @@ def test_distance_oracles_agree(name):
     assert np.allclose(t, e, rtol=1e-5, atol=0)
     d = O.delta_from_norms([n for n, _ in w_locals], t, 0.03)
     assert np.isfinite(d)
+
+
+def test_distance_with_bool_buffer_raises_like_reference():
+    _, w_locals, _ = load_case("int_dtypes_k3")  # has a bool key
+    w_glob = O.aggregate_torch(w_locals)
+    with pytest.raises(RuntimeError):
+        O.client_distances_torch(w_locals, w_glob)
