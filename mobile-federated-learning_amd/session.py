@@ -28,6 +28,7 @@ Results are bit-identical to ``aggregate`` (and to the reference).
 from __future__ import annotations
 
 import time
+import weakref
 from collections import OrderedDict
 from typing import Mapping, Optional
 
@@ -105,6 +106,7 @@ class RoundSession:
 
         weights = sample_weights(self.counts)  # ZeroDivisionError like the reference
         outs = []
+        dev_state = {}
         with torch.cuda.device(self.dev):
             self._compute.wait_stream(self._copy)
             for g in self.table.groups.values():
@@ -113,9 +115,16 @@ class RoundSession:
                 out_host = torch.empty(g.P, dtype=g.dtype, pin_memory=True)
                 out_host.copy_(out_dev, non_blocking=True)
                 outs.append((g, out_host))
+                dev_state[g.dtype] = (st.dev[:K], out_dev)
             self._compute.synchronize()
         for g, out_host in outs:
             for name, t in self.table.unpack(g, out_host).items():
                 acc_dict[name] = t
         self._keepalive.clear()
+        # leave the round's device rows + averaged model for client_distances (:291)
+        try:
+            self.agg._last = {"table": self.table, "K": K, "dev": dev_state,
+                              "refs": [weakref.ref(sd) for sd in self.dicts], "acc": weakref.ref(acc_dict)}
+        except TypeError:
+            self.agg._last = {}
         return acc_dict

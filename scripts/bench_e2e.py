@@ -112,15 +112,32 @@ def run(name, reps, train_ms=0.0):
         if r:
             gpu_t.append(t)
             prof.append(dict(agg.last_profile))
-    cpu_t = []
+    # post-aggregate distances (fedavg_trainer.py:291) on the round's device rows
+    has_bool = any(t.dtype == torch.bool for t in dicts[0].values())
+    dist_t = []
+    if not has_bool:
+        for r in range(reps + 1):
+            t0 = time.perf_counter()
+            norms = agg.client_distances(wl, out)
+            t = time.perf_counter() - t0
+            if r:
+                dist_t.append(t)
+    cpu_t, cpu_dist_t = [], []
     cpu_reps = max(1, min(reps, int(20.0 / max(alg / 5e9, 1e-3))))
     for r in range(cpu_reps + 1):
-        wl = fresh(counts, dicts)
+        wl_ref = fresh(counts, dicts)
         t0 = time.perf_counter()
-        ref = O.aggregate_torch(wl)
+        ref = O.aggregate_torch(wl_ref)
         t = time.perf_counter() - t0
         if r:
             cpu_t.append(t)
+    for r in range(min(cpu_reps, 2) + 1):
+        t0 = time.perf_counter()
+        ref_norms = O.client_distances_torch(wl_ref, ref)
+        t = time.perf_counter() - t0
+        if r:
+            cpu_dist_t.append(t)
+    dist_rel = float(np.max(np.abs(norms - ref_norms) / np.maximum(np.abs(ref_norms), 1e-30))) if dist_t else None
     # streaming rounds (mfl_amd.RoundSession): clients are added as they
     # "arrive"; what remains after the last arrival is the round's critical path
     crit, add_ms = [], []
@@ -155,6 +172,9 @@ def run(name, reps, train_ms=0.0):
         "stream_add_ms_total_median": round(float(np.median(add_ms)), 3),
         "stream_bit_exact": bool(same_stream),
         "stream_train_ms_per_client": train_ms,
+        "dist_ms_median": round(float(np.median(dist_t)) * 1e3, 3) if dist_t else None,
+        "cpu_dist_ms_median": round(float(np.median(cpu_dist_t)) * 1e3, 3),
+        "dist_max_rel_vs_cpu_ref": dist_rel,
     }
 
 

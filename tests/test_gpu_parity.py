@@ -380,3 +380,19 @@ def test_client_distances_bool_buffer_raises():
     w_glob = mfl_amd.aggregate(w_locals)
     with pytest.raises(RuntimeError):
         mfl_amd.client_distances(w_locals, w_glob)
+
+
+def test_client_distances_after_streaming_round():
+    import copy
+    _, w_locals, _ = load_case("mnist_lr_k100")
+    ref_locals = copy.deepcopy(w_locals)
+    ref_glob = O.aggregate_torch(ref_locals)
+    agg = mfl_amd.DeviceAggregator(DEV)
+    sess = agg.begin_round(w_locals[0][1], len(w_locals))
+    for n, sd in w_locals:
+        sess.add(n, sd)
+    w_glob = sess.finish(w_locals)
+    norms = agg.client_distances(w_locals, w_glob)
+    exact = O.client_distances_exact(ref_locals, ref_glob)
+    assert norms[0] == 0.0
+    assert np.all(np.abs(norms - exact) <= np.spacing(exact.astype(np.float32)).astype(np.float64))
