@@ -238,16 +238,20 @@ class DeviceAggregator:
 
         if not w_locals:
             return np.zeros(0)
-        for _, sd in w_locals:
-            if sd is not w_glob and any(t.dtype == torch.bool for t in sd.values()):
-                # the reference's `w[para] - w_glob[para]` raises here too
-                raise RuntimeError("Subtraction, the `-` operator, with a bool tensor is not supported "
-                                   "(fedavg_trainer.py:291 on a state_dict with bool buffers)")
         last = self._last
         refs = last.get("refs")
         cached = (refs is not None and last["acc"]() is w_glob and len(refs) == len(w_locals)
                   and all(r() is sd for r, (_, sd) in zip(refs, w_locals))
                   and set(last.get("dev", {})) == {torch.float32})
+        # the reference's `w[para] - w_glob[para]` raises on bool buffers; the
+        # round's key table already holds every client's (validated) dtypes
+        if cached:
+            has_bool = any(e.src_dtype == torch.bool for e in last["table"].entries)
+        else:
+            has_bool = any(t.dtype == torch.bool for _, sd in w_locals if sd is not w_glob for t in sd.values())
+        if has_bool and any(sd is not w_glob for _, sd in w_locals):
+            raise RuntimeError("Subtraction, the `-` operator, with a bool tensor is not supported "
+                               "(fedavg_trainer.py:291 on a state_dict with bool buffers)")
         if cached:
             devbuf, out_dev = last["dev"][torch.float32]
             P = last["table"].groups[torch.float32].P
