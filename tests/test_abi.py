@@ -112,3 +112,14 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
     with pytest.raises((_lib.FedAvgLibraryError, RuntimeError)):
         mfl_amd.aggregate(w_locals)
     assert torch.equal(w_locals[0][1]["w"], torch.ones(4))  # nothing was written
+
+
+def test_plain_c_consumer_builds(lib):
+    """examples/c_abi_demo.c links against the library with only the C header
+    (no Python, no torch): the boundary is usable from a non-Python host."""
+    import subprocess
+    root = INCLUDE.parent
+    proc = subprocess.run(["make", "-s", "-B", "-C", str(root / "examples"), "c_abi_demo"],
+                          capture_output=True, text=True, timeout=120)
+    assert proc.returncode == 0, proc.stderr
+    assert (root / "examples" / "c_abi_demo").exists()

@@ -396,3 +396,36 @@ def test_client_distances_after_streaming_round():
     exact = O.client_distances_exact(ref_locals, ref_glob)
     assert norms[0] == 0.0
     assert np.all(np.abs(norms - exact) <= np.spacing(exact.astype(np.float32)).astype(np.float64))
+
+
+def test_plain_c_consumer_runs():
+    import subprocess
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    subprocess.run(["make", "-s", "-C", str(root / "examples"), "c_abi_demo"], check=True, timeout=120)
+    proc = subprocess.run([str(root / "examples" / "c_abi_demo"), "37", "1000003"], capture_output=True,
+                          text=True, timeout=120)
+    assert proc.returncode == 0, proc.stdout + proc.stderr
+    assert "C ABI demo OK" in proc.stdout
+
+
+def test_int64_indexing_beyond_2_31_elements():
+    """A row longer than 2^31 elements (8.6 GB): every offset in the kernels is
+    64-bit.  Sampled windows at the start, around 2^31 and at the ragged end."""
+    K = 2
+    P = (1 << 31) + 4099
+    ld = (P + 63) // 64 * 64
+    x = torch.empty((K, ld), device=DEV)
+    for k in range(K):
+        g = torch.Generator(device=DEV).manual_seed(70 + k)
+        x[k].normal_(0.0, 0.05, generator=g)
+    w = _weights(K)
+    out = mfl_amd.reduce_packed(x, _w(w), P)
+    for s in (0, (1 << 31) - 2048, (1 << 31) - 3, P - 4099):
+        e = min(s + 4099, P)
+        exp = O.reduce_f32(x[:, s:e].cpu().numpy(), w)
+        assert_bits(out[s:e], torch.from_numpy(exp), f"window {s}")
+    sq = mfl_amd.client_sqdist(x, out, P)
+    ref = torch.stack([((x[k, :P] - out[:P]).double() ** 2).sum() for k in range(K)])
+    assert ((sq - ref).abs() / ref).max().item() < 1e-12
+    del x, out
