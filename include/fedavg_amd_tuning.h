@@ -36,7 +36,7 @@ int fedavg_reduce_f32_tuned(const float* clients, int64_t K, int64_t P, int64_t 
 
 /*
  * Variant family of the exact fp32 kernel (same bits, different schedule):
- *   unroll     : client rows per load batch (1, 2, 4, 8, 16)
+ *   unroll     : client rows per load batch (1, 2, 4, 8, 16; 32 with cols <= 2)
  *   cols       : 16-B column slices per thread (1, 2, 4; 8 with unroll <= 8; 16 with unroll <= 2)
  *   pipelined  : 0 = register batches; 1 = register double-buffered batches
  *                (2*unroll*cols loads in flight); 2 = LDS-DMA staging

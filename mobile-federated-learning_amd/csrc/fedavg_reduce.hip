@@ -924,6 +924,10 @@ var_launcher pick_var1(int cols, int nt, int pipe) {
 
 var_launcher pick_var(int unroll, int cols, int nt, int pipe) {
   switch (unroll) {
+    case 32:  // deep batches for short rows / many clients (latency-bound shapes)
+      if (cols == 1) return pick_var2<32, 1>(nt, pipe);
+      if (cols == 2) return pick_var2<32, 2>(nt, pipe);
+      return nullptr;
     case 1: return pick_var1<1>(cols, nt, pipe);
     case 2: return pick_var1<2>(cols, nt, pipe);
     case 4: return pick_var1<4>(cols, nt, pipe);
@@ -959,15 +963,26 @@ constexpr int kBlocksPerLaunch = 768;
 Schedule choose_schedule(int64_t K, int64_t P) {
   const int64_t nvec = (P + 3) / 4;
   Schedule sc{8, 1, 1, kBlocksPerLaunch};
-  if (nvec >= int64_t(512) * kBlock * 8) {
+  if (K <= 4) {
+    // a block's work is tiny (K rows): one launch, many short blocks; round
+    // splitting would only add launch boundaries (K=2..3 sweeps: +14-22 %)
+    sc.cols = 1;
+    sc.blocks_per_launch = 1 << 30;
+  } else if (nvec >= int64_t(512) * kBlock * 8) {
     sc.unroll = 4, sc.cols = 8;
   } else if (nvec >= int64_t(512) * kBlock * 4) {
     sc.cols = 4;
   } else if (nvec >= int64_t(512) * kBlock * 2) {
     sc.cols = 2;
+  } else {
+    // short rows: few blocks, so each thread's client chain is the critical
+    // path; deeper batches (16 rows) cut its round trips (+11-12 %), and with
+    // many clients 4 slices per thread keep 64 loads in flight
+    sc.unroll = 16;
+    sc.cols = (K >= 500 && nvec >= int64_t(128) * kBlock * 4) ? 4 : 1;
   }
   const double bytes = 4.0 * static_cast<double>(K) * static_cast<double>(P);
-  if (bytes > 64.0 * (1 << 20) && bytes <= 240.0 * (1 << 20)) {
+  if (K > 4 && bytes > 64.0 * (1 << 20) && bytes <= 240.0 * (1 << 20)) {
     // Infinity-Cache-resident band: default-policy loads, and a deep, wide
     // per-thread batch (16 rows x 4 slices) measured fastest there
     sc.nt = 0;

@@ -31,7 +31,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--quick", action="store_true")
-    ap.add_argument("--set", default="all", choices=["all", "focus", "wide", "window"])
+    ap.add_argument("--set", default="all", choices=["all", "focus", "wide", "window", "small"])
     ap.add_argument("--no-tiled", action="store_true")
     args = ap.parse_args()
     K, P = args.K, args.P
@@ -56,7 +56,12 @@ def main():
     ref = mfl_amd.reduce_packed(x, w, P)
 
     variants = [("default", None)]
-    if args.set == "window":
+    if args.set == "small":
+        for U, C in [(8, 1), (16, 1), (32, 1), (8, 2), (16, 2), (32, 2), (8, 4), (16, 4), (4, 8)]:
+            for mb in (768, 100000):
+                variants.append((f"split U{U} C{C} nt1 mb{mb}", (U, 1, C, 4, mb)))
+        unrolls = []
+    elif args.set == "window":
         for U, C in [(4, 8), (8, 8), (8, 4), (2, 16), (4, 4)]:
             for G in (512, 768, 1024):
                 variants.append((f"window U{U} C{C} nt1 G{G}", (U, 1, C, 5, G)))

@@ -159,6 +159,7 @@ def _all_variants():
                     if pipe == 2 and U * C > 16:
                         continue
                     out.append((U, nt, C, pipe, 0))
+    out += [(32, nt, C, pipe, 0) for nt in (0, 1) for C in (1, 2) for pipe in (0, 4)]
     return out + [(8, 1, 4, 0, 2048), (4, 1, 1, 2, 300), (16, 0, 2, 1, 7), (4, 1, 8, 3, 5), (2, 1, 8, 3, 333),
                   (4, 1, 8, 4, 3), (8, 1, 4, 4, 17), (8, 0, 1, 4, 1), (4, 1, 8, 5, 7), (8, 1, 8, 5, 256),
                   (2, 1, 16, 5, 1), (8, 1, 4, 5, 1000)]
