@@ -132,13 +132,26 @@ class DeviceAggregator:
         # device state of the last aggregate call (client rows + averaged model per
         # dtype group), reused by client_distances for the same round
         self._last: Dict[str, object] = {}
+        self._session = None  # weakref to the open RoundSession, if any
 
     # ------------------------------------------------------------------
     def begin_round(self, template, max_clients: int):
-        """Start a streaming round (see ``session.RoundSession``)."""
+        """Start a streaming round (see ``session.RoundSession``).
+
+        A session owns this aggregator's staging buffers until ``finish``;
+        ``aggregate`` and a second ``begin_round`` refuse to run meanwhile.
+        """
         from .session import RoundSession
 
-        return RoundSession(self, template, max_clients)
+        self._check_no_open_session("begin_round")
+        sess = RoundSession(self, template, max_clients)
+        self._session = weakref.ref(sess)
+        return sess
+
+    def _check_no_open_session(self, what: str):
+        sess = self._session() if self._session is not None else None
+        if sess is not None and not sess._finished:
+            raise RuntimeError(f"{what}: a RoundSession on this aggregator is still open (call finish first)")
 
     def _copy_stream_for(self):
         if self._copy_stream is None:
@@ -157,6 +170,7 @@ class DeviceAggregator:
         prep = prepare(w_locals, model_global)
         if not isinstance(prep, _Prepared):
             return prep  # empty list / no keys: answered on the host like the reference
+        self._check_no_open_session("aggregate")
         acc_dict, table, dicts, weights, ptrs, keepalive = prep
         results = self._reduce_groups(table, ptrs, weights)
         del keepalive

@@ -645,6 +645,107 @@ __global__ __launch_bounds__(kBlock) void reduce_half_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// fp64 / fp16 / bf16 production kernels: the fp32 schedule (U-row batches,
+// C 16-B slices per thread, nontemporal loads, round-split dispatch) over an
+// element-op policy carrying each dtype's exact per-element rule.
+// ---------------------------------------------------------------------------
+struct OpF64 {
+  using vec = f64x2;
+  using wt = double;
+  using elem = double;
+  static constexpr int kLanes = 2;
+  __device__ static vec first(vec x, wt w) { return x * w; }
+  __device__ static vec step(vec acc, vec x, wt w) {
+    const vec t = x * w;
+    return acc + t;
+  }
+};
+
+template <typename R>
+struct OpHalf {
+  using vec = u16x8;
+  using wt = float;
+  using elem = unsigned short;
+  static constexpr int kLanes = 8;
+  __device__ static vec first(vec x, wt w) {
+    vec r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = half_step<R>(0, x[j], w, true);
+    return r;
+  }
+  __device__ static vec step(vec acc, vec x, wt w) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = half_step<R>(acc[j], x[j], w, false);
+    return acc;
+  }
+};
+
+template <class Op, int U, int C, bool NT>
+__device__ __forceinline__ void reduce_vec_group(typename Op::vec (&acc)[C], const typename Op::vec* col, int K,
+                                                 int64_t ldv, const typename Op::wt* __restrict__ W) {
+  using vec = typename Op::vec;
+  const typename Op::wt w0 = W[0];
+#pragma unroll
+  for (int j = 0; j < C; ++j) acc[j] = Op::first(ld<NT>(col + j * kBlock), w0);
+  int k = 1;
+  for (; k + U <= K; k += U) {
+    vec xs[U][C];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < C; ++j) xs[u][j] = ld<NT>(col + static_cast<int64_t>(k + u) * ldv + j * kBlock);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const typename Op::wt w = W[k + u];
+#pragma unroll
+      for (int j = 0; j < C; ++j) acc[j] = Op::step(acc[j], xs[u][j], w);
+    }
+  }
+  for (; k < K; ++k) {
+    const typename Op::wt w = W[k];
+#pragma unroll
+    for (int j = 0; j < C; ++j) acc[j] = Op::step(acc[j], ld<NT>(col + static_cast<int64_t>(k) * ldv + j * kBlock), w);
+  }
+}
+
+template <class Op>
+__device__ __forceinline__ void store_vec(typename Op::elem* out, int64_t v, int64_t nvec, int tail,
+                                          typename Op::vec a) {
+  typename Op::elem* o = out + v * Op::kLanes;
+  if (tail == 0 || v != nvec - 1) {
+    *reinterpret_cast<typename Op::vec*>(o) = a;
+  } else {
+#pragma unroll
+    for (int j = 0; j < Op::kLanes; ++j)
+      if (j < tail) o[j] = a[j];
+  }
+}
+
+template <class Op, int U, int C, bool NT>
+__global__ __launch_bounds__(kBlock) void reduce_vec_kernel(
+    const typename Op::vec* __restrict__ X, int K, int64_t ldv, int64_t nvec, int tail,
+    const typename Op::wt* __restrict__ W, typename Op::elem* __restrict__ out) {
+  const int64_t span = static_cast<int64_t>(kBlock) * C;
+  for (int64_t base = static_cast<int64_t>(blockIdx.x) * span; base < nvec;
+       base += static_cast<int64_t>(gridDim.x) * span) {
+    if (base + span <= nvec) {
+      typename Op::vec acc[C];
+      reduce_vec_group<Op, U, C, NT>(acc, X + base + threadIdx.x, K, ldv, W);
+#pragma unroll
+      for (int j = 0; j < C; ++j) store_vec<Op>(out, base + threadIdx.x + j * kBlock, nvec, tail, acc[j]);
+    } else {
+      for (int j = 0; j < C; ++j) {
+        const int64_t v = base + threadIdx.x + j * kBlock;
+        if (v >= nvec) break;
+        typename Op::vec acc1[1];
+        reduce_vec_group<Op, U, 1, NT>(acc1, X + v, K, ldv, W);
+        store_vec<Op>(out, v, nvec, tail, acc1[0]);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Split-client variant (tolerance-gated).  Block = SPLITS waves over the same
 // 64 column slices; wave g owns the contiguous client range
 // [g*K/SPLITS, (g+1)*K/SPLITS), keeps its partial sum in registers, stages
@@ -999,6 +1100,69 @@ void launch_production_f32(const float* clients, int K, int64_t ld, int64_t P, c
   fn(clients, K, ld, P, W, out, sc.blocks_per_launch, s);
 }
 
+// Round-split launches of reduce_vec_kernel (fp64 / fp16 / bf16).  The
+// schedule is the fp32 one for the same number of 16-B column slices and the
+// same byte footprint (choose_schedule takes fp32-equivalent element counts).
+template <class Op, int U, int C, bool NT>
+void launch_vec_split(const void* clients, int K, int64_t ld, int64_t P, const void* W, void* out, int bpl,
+                      hipStream_t s) {
+  using vec = typename Op::vec;
+  const int64_t lanes = Op::kLanes;
+  const int64_t nvec = (P + lanes - 1) / lanes;
+  const int64_t span = static_cast<int64_t>(kBlock) * C;
+  const int64_t blocks = (nvec + span - 1) / span;
+  const int64_t nl = (blocks + bpl - 1) / bpl;
+  const int64_t per = ((nvec + nl - 1) / nl + span - 1) / span * span;
+  const vec* X = reinterpret_cast<const vec*>(clients);
+  auto* O = reinterpret_cast<typename Op::elem*>(out);
+  for (int64_t v0 = 0; v0 < nvec; v0 += per) {
+    const int64_t n = (nvec - v0) < per ? (nvec - v0) : per;
+    const int tail = (v0 + n == nvec) ? static_cast<int>(P % lanes) : 0;
+    hipLaunchKernelGGL((reduce_vec_kernel<Op, U, C, NT>), dim3(static_cast<unsigned>((n + span - 1) / span)),
+                       dim3(kBlock), 0, s, X + v0, K, ld / lanes, n, tail,
+                       reinterpret_cast<const typename Op::wt*>(W), O + v0 * lanes);
+  }
+}
+
+template <class Op, bool NT>
+void launch_vec_nt(const Schedule& sc, const void* clients, int K, int64_t ld, int64_t P, const void* W, void* out,
+                   hipStream_t s) {
+  int key = sc.unroll * 100 + sc.cols;
+  if constexpr (Op::kLanes == 8) {
+    // fp16/bf16 unpack every 16-B vector into 8 fp32 lanes of work: halve the
+    // rows per batch so the schedule stays spill-free (same bytes per block-step)
+    switch (key) {
+      case 408: key = 208; break;
+      case 804: case 1604: key = 404; break;
+      case 1601: key = 801; break;
+      default: break;
+    }
+  }
+  switch (key) {
+    case 408: launch_vec_split<Op, 4, 8, NT>(clients, K, ld, P, W, out, sc.blocks_per_launch, s); break;
+    case 208: launch_vec_split<Op, 2, 8, NT>(clients, K, ld, P, W, out, sc.blocks_per_launch, s); break;
+    case 804: launch_vec_split<Op, 8, 4, NT>(clients, K, ld, P, W, out, sc.blocks_per_launch, s); break;
+    case 404: launch_vec_split<Op, 4, 4, NT>(clients, K, ld, P, W, out, sc.blocks_per_launch, s); break;
+    case 802: launch_vec_split<Op, 8, 2, NT>(clients, K, ld, P, W, out, sc.blocks_per_launch, s); break;
+    case 801: launch_vec_split<Op, 8, 1, NT>(clients, K, ld, P, W, out, sc.blocks_per_launch, s); break;
+    case 1604: launch_vec_split<Op, 16, 4, NT>(clients, K, ld, P, W, out, sc.blocks_per_launch, s); break;
+    default: launch_vec_split<Op, 16, 1, NT>(clients, K, ld, P, W, out, sc.blocks_per_launch, s); break;
+  }
+}
+
+// elem_bytes: 8 (fp64) or 2 (fp16/bf16).  The fp32 schedule is chosen for the
+// problem with the same 16-B slice count and byte footprint.
+template <class Op>
+void launch_production_vec(const void* clients, int K, int64_t ld, int64_t P, const void* W, void* out,
+                           hipStream_t s) {
+  const int64_t f32_equiv = P * static_cast<int64_t>(16 / Op::kLanes) / 4;  // same bytes per row
+  const Schedule sc = choose_schedule(K, f32_equiv);
+  if (sc.nt)
+    launch_vec_nt<Op, true>(sc, clients, K, ld, P, W, out, s);
+  else
+    launch_vec_nt<Op, false>(sc, clients, K, ld, P, W, out, s);
+}
+
 }  // namespace
 
 // ===========================================================================
@@ -1138,10 +1302,7 @@ int fedavg_reduce_f64(const double* clients, int64_t K, int64_t P, int64_t ld, c
        reinterpret_cast<uintptr_t>(weights)) & m)
     return set_error(FEDAVG_EALIGN, "%s: fp64 buffers must be 8-byte aligned", what);
   if (aligned16(clients) && aligned16(out) && (ld % 2) == 0) {
-    const int64_t nvec = (P + 1) / 2;
-    hipLaunchKernelGGL(reduce_f64x2_kernel, dim3(grid_for(nvec, kBlock)), dim3(kBlock), 0, s,
-                       reinterpret_cast<const f64x2*>(clients), static_cast<int>(K), ld / 2, nvec,
-                       static_cast<int>(P & 1), weights, out);
+    launch_production_vec<OpF64>(clients, static_cast<int>(K), ld, P, weights, out, s);
   } else {
     hipLaunchKernelGGL(reduce_f64_scalar_kernel, dim3(grid_for(P, kBlock)), dim3(kBlock), 0, s, clients,
                        static_cast<int>(K), ld, P, weights, out);
@@ -1158,7 +1319,14 @@ static int reduce_half_entry(bool bf16, const uint16_t* clients, int64_t K, int6
     return set_error(FEDAVG_EALIGN, "%s: 16-bit buffers must be 2-byte aligned", what);
   hipStream_t s = static_cast<hipStream_t>(stream);
   const bool vec = aligned16(clients) && aligned16(out) && (ld % 8) == 0;
-  const int64_t items = vec ? (P + 7) / 8 : P;
+  if (vec) {
+    if (bf16)
+      launch_production_vec<OpHalf<BF16Rule>>(clients, static_cast<int>(K), ld, P, weights, out, s);
+    else
+      launch_production_vec<OpHalf<F16Rule>>(clients, static_cast<int>(K), ld, P, weights, out, s);
+    return launch_status(what);
+  }
+  const int64_t items = P;
   const auto* X = reinterpret_cast<const unsigned short*>(clients);
   auto* O = reinterpret_cast<unsigned short*>(out);
   if (bf16) {

@@ -430,3 +430,46 @@ def test_int64_indexing_beyond_2_31_elements():
     ref = torch.stack([((x[k, :P] - out[:P]).double() ** 2).sum() for k in range(K)])
     assert ((sq - ref).abs() / ref).max().item() < 1e-12
     del x, out
+
+
+@pytest.mark.parametrize("dtype,K,P", [(torch.float64, 8, 10_000_003), (torch.float16, 6, 40_000_005),
+                                       (torch.bfloat16, 5, 40_000_001), (torch.float64, 600, 200_001),
+                                       (torch.bfloat16, 3, 1_000_003)])
+def test_reduce_vec_dtypes_multilaunch(dtype, K, P):
+    """fp64/fp16/bf16 production schedule (round-split, multi-slice, nt) is
+    bit-exact on sampled windows incl. launch boundaries and the ragged tail."""
+    from mfl_amd import _lib
+    x = _clients(K, P, seed=P % 1000 + K, dtype=dtype)
+    w = _weights(K, seed=K)
+    out = mfl_amd.reduce_packed(x, _w(w, torch.float64 if dtype == torch.float64 else torch.float32), P)
+    lanes = 16 // x.element_size()
+    f32_equiv = P * (16 // lanes) // 4
+    launches = _lib.f32_schedule(K, f32_equiv)["launches"]
+    starts = [0, P // 2, P - 4099] + [int(P * i / max(launches, 1)) - 2048 for i in range(1, launches)]
+    for s in starts:
+        s = max(0, min(s, P - 4099))
+        xs = x[:, s:s + 4099].cpu()
+        if dtype == torch.float64:
+            exp = torch.from_numpy(O.reduce_f64(xs.numpy(), w))
+        elif dtype == torch.float16:
+            exp = torch.from_numpy(O.reduce_half(xs.numpy(), w, "float16"))
+        else:
+            bits = O.reduce_half(xs.view(torch.int16).numpy(), w, "bfloat16")
+            exp = torch.from_numpy(bits.view(np.int16).copy()).view(torch.bfloat16)
+        assert_bits(out[s:s + 4099], exp, f"{dtype} window {s}")
+    del x
+
+
+def test_open_session_blocks_aggregate():
+    _, w_locals, _ = load_case("mnist_lr_k10")
+    agg = mfl_amd.DeviceAggregator(DEV)
+    sess = agg.begin_round(w_locals[0][1], 10)
+    sess.add(*w_locals[0])
+    with pytest.raises(RuntimeError):
+        agg.aggregate(w_locals)
+    with pytest.raises(RuntimeError):
+        agg.begin_round(w_locals[0][1], 10)
+    for n, sd in w_locals[1:]:
+        sess.add(n, sd)
+    sess.finish(w_locals)
+    agg.begin_round(w_locals[0][1], 10)  # allowed again
