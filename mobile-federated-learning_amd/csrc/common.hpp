@@ -1,0 +1,297 @@
+// common.hpp -- shared device code of libfedavg_amd.so (gfx950 / MI355X).
+//
+// Reference semantics (src/fedavg_trainer.py:441-458): for each element p,
+//     acc = x[0][p] * w[0];  acc = acc + x[i][p] * w[i]  for i = 1..K-1
+// evaluated left to right, one rounding per multiply and per add.  Every
+// translation unit is compiled with -ffp-contract=off and this header pins
+// `fp contract(off)` as well, so the multiply+add pair is never fused into
+// v_fma/v_fmac (a fused form rounds once and is not bit-identical to the
+// reference's ATen CPU ops).
+//
+// Roofline: 2 flops per 4-byte element read -> 0.5 flop/B; the kernels are
+// HBM-read bound (4*K*P bytes in, 4*P out), never MFMA work.  Layout in HBM:
+// one client-major [K, ld] buffer, each row one client's flattened
+// state_dict.  A thread owns C 16-byte column slices (slice j at
+// base + tid + 256*j) and walks the client axis in order, U rows per batch.
+//
+// Translation units: fedavg_reduce.hip (production kernels, schedule, C ABI),
+// fedavg_variants.hip (benchmarking variants), fedavg_dist.hip (the :291
+// distance pass).  Templates and inline helpers live here.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <utility>
+
+#include "fedavg_amd.h"
+#include "fedavg_amd_tuning.h"
+
+#pragma clang fp contract(off)
+
+namespace fedavg_impl {
+
+constexpr int kBlock = 256;  // 4 waves of 64
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+
+// Error state (thread-local message), defined in fedavg_reduce.hip.
+int set_error(int code, const char* fmt, ...);
+int launch_status(const char* what);
+const char* last_error_message();
+int check_common(const void* clients, int64_t K, int64_t P, int64_t ld, const void* weights, const void* out,
+                 const char* what);
+
+__host__ __device__ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+__host__ __device__ inline bool aligned4(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 3u) == 0; }
+
+inline unsigned grid_for(int64_t items, int per_block) {
+  return static_cast<unsigned>((items + per_block - 1) / per_block);
+}
+
+template <bool NT, typename T>
+__device__ __forceinline__ T ld(const T* p) {
+  if constexpr (NT) {
+    return __builtin_nontemporal_load(p);
+  } else {
+    return *p;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// fp32, bit-exact, float4 path.  One thread = one 16-B column slice.
+//   X    : [K, ld] fp32 viewed as [K, ld4] float4 (16-B aligned, ld % 4 == 0)
+//   nvec : ceil(P / 4) column slices; the last one stores only `tail` lanes
+//          when P % 4 != 0 (its extra lanes read row padding, never stored).
+// ---------------------------------------------------------------------------
+template <int UNROLL, bool NT, bool OUT_VEC>
+__global__ __launch_bounds__(kBlock) void reduce_f32x4_kernel(
+    const f32x4* __restrict__ X, int K, int64_t ld4, int64_t nvec, int tail,
+    const float* __restrict__ W, float* __restrict__ out) {
+  const int64_t v = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (v >= nvec) return;
+  const f32x4* col = X + v;
+
+  f32x4 acc = ld<NT>(col) * W[0];  // fedavg_trainer.py:455  (i == 0)
+  int k = 1;
+  for (; k + UNROLL <= K; k += UNROLL) {
+    f32x4 xs[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) xs[u] = ld<NT>(col + static_cast<int64_t>(k + u) * ld4);
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const f32x4 term = xs[u] * W[k + u];  // fl32(p_i * w_i)
+      acc = acc + term;                     // fedavg_trainer.py:457
+    }
+  }
+  for (; k < K; ++k) {
+    const f32x4 term = ld<NT>(col + static_cast<int64_t>(k) * ld4) * W[k];
+    acc = acc + term;
+  }
+
+  float* o = out + v * 4;
+  if (tail == 0 || v != nvec - 1) {
+    if constexpr (OUT_VEC) {
+      *reinterpret_cast<f32x4*>(o) = acc;
+    } else {
+      o[0] = acc.x; o[1] = acc.y; o[2] = acc.z; o[3] = acc.w;
+    }
+  } else {
+    o[0] = acc.x;
+    if (tail > 1) o[1] = acc.y;
+    if (tail > 2) o[2] = acc.z;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// fp32, bit-exact, variant family (benchmarking / tuning).  Same per-element
+// order as reduce_f32x4_kernel; what changes is how much each thread keeps in
+// flight and how the grid walks the columns:
+//   U     client rows loaded per batch,
+//   C     column slices per thread (slice j at base + tid + j*256, so a block
+//         covers C*4 KiB contiguous bytes of every row),
+//   PIPE  register double-buffering: batch b+1's loads are issued before
+//         batch b is consumed, so 2*U*C loads can be in flight per thread,
+//   grid  may be capped (grid-stride over column groups).
+// ---------------------------------------------------------------------------
+template <int U, int C, bool NT>
+__device__ __forceinline__ void load_batch(f32x4 (&xs)[U][C], const f32x4* col, int k, int64_t ld4) {
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int j = 0; j < C; ++j) xs[u][j] = ld<NT>(col + static_cast<int64_t>(k + u) * ld4 + j * kBlock);
+}
+
+template <int U, int C>
+__device__ __forceinline__ void consume_batch(f32x4 (&acc)[C], const f32x4 (&xs)[U][C], const float* W, int k) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const float w = W[k + u];
+#pragma unroll
+    for (int j = 0; j < C; ++j) {
+      const f32x4 term = xs[u][j] * w;
+      acc[j] = acc[j] + term;
+    }
+  }
+}
+
+template <int U, int C, bool NT, bool PIPE>
+__device__ __forceinline__ void reduce_full_group(f32x4 (&acc)[C], const f32x4* col, int K, int64_t ld4,
+                                                  const float* __restrict__ W) {
+  const float w0 = W[0];
+#pragma unroll
+  for (int j = 0; j < C; ++j) acc[j] = ld<NT>(col + j * kBlock) * w0;
+  const int nb = (K - 1) / U;  // full batches after client 0
+  int k = 1;
+  if constexpr (PIPE) {
+    f32x4 xa[U][C], xb[U][C];
+    int b = 0;
+    if (nb > 0) load_batch<U, C, NT>(xa, col, k, ld4);
+    while (b < nb) {
+      if (b + 1 < nb) load_batch<U, C, NT>(xb, col, k + U, ld4);
+      consume_batch<U, C>(acc, xa, W, k);
+      k += U;
+      if (++b >= nb) break;
+      if (b + 1 < nb) load_batch<U, C, NT>(xa, col, k + U, ld4);
+      consume_batch<U, C>(acc, xb, W, k);
+      k += U;
+      ++b;
+    }
+  } else {
+    for (int b = 0; b < nb; ++b, k += U) {
+      f32x4 xs[U][C];
+      load_batch<U, C, NT>(xs, col, k, ld4);
+      consume_batch<U, C>(acc, xs, W, k);
+    }
+  }
+  for (; k < K; ++k) {
+    const float w = W[k];
+#pragma unroll
+    for (int j = 0; j < C; ++j) {
+      const f32x4 term = ld<NT>(col + static_cast<int64_t>(k) * ld4 + j * kBlock) * w;
+      acc[j] = acc[j] + term;
+    }
+  }
+}
+
+__device__ __forceinline__ void store_slice(float* out, int64_t v, int64_t nvec, int tail, f32x4 a) {
+  float* o = out + v * 4;
+  if (tail == 0 || v != nvec - 1) {
+    *reinterpret_cast<f32x4*>(o) = a;
+  } else {
+    o[0] = a.x;
+    if (tail > 1) o[1] = a.y;
+    if (tail > 2) o[2] = a.z;
+  }
+}
+
+template <int U, int C, bool NT, bool PIPE>
+__global__ __launch_bounds__(kBlock) void reduce_f32x4_var_kernel(
+    const f32x4* __restrict__ X, int K, int64_t ld4, int64_t nvec, int tail,
+    const float* __restrict__ W, float* __restrict__ out) {
+  const int64_t span = static_cast<int64_t>(kBlock) * C;
+  for (int64_t base = static_cast<int64_t>(blockIdx.x) * span; base < nvec;
+       base += static_cast<int64_t>(gridDim.x) * span) {
+    if (base + span <= nvec) {
+      f32x4 acc[C];
+      reduce_full_group<U, C, NT, PIPE>(acc, X + base + threadIdx.x, K, ld4, W);
+#pragma unroll
+      for (int j = 0; j < C; ++j) store_slice(out, base + threadIdx.x + j * kBlock, nvec, tail, acc[j]);
+    } else {
+      for (int j = 0; j < C; ++j) {
+        const int64_t v = base + threadIdx.x + j * kBlock;
+        if (v >= nvec) break;
+        f32x4 acc[1];
+        reduce_full_group<U, 1, NT, false>(acc, X + v, K, ld4, W);
+        store_slice(out, v, nvec, tail, acc[0]);
+      }
+    }
+  }
+}
+
+template <int U, bool NT>
+void launch_f32x4(const float* clients, int K, int64_t ld, int64_t P, const float* W, float* out,
+                  hipStream_t s) {
+  const int64_t nvec = (P + 3) / 4;
+  const int tail = static_cast<int>(P & 3);
+  const f32x4* X = reinterpret_cast<const f32x4*>(clients);
+  if (aligned16(out)) {
+    hipLaunchKernelGGL((reduce_f32x4_kernel<U, NT, true>), dim3(grid_for(nvec, kBlock)), dim3(kBlock), 0, s,
+                       X, K, ld / 4, nvec, tail, W, out);
+  } else {
+    hipLaunchKernelGGL((reduce_f32x4_kernel<U, NT, false>), dim3(grid_for(nvec, kBlock)), dim3(kBlock), 0, s,
+                       X, K, ld / 4, nvec, tail, W, out);
+  }
+}
+
+// Blocks of a kernel the whole chip holds at once (occupancy x CUs), cached
+// per (device, kernel) -- kernels of one signature share a template
+// instantiation of this function, so the cache must be keyed by the kernel.
+template <typename Kern>
+int64_t resident_blocks(Kern kernel) {
+  static std::mutex mu;
+  static std::map<std::pair<int, const void*>, int64_t> cache;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 1024;
+  const auto key = std::make_pair(dev, reinterpret_cast<const void*>(kernel));
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+  }
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, 0) != hipSuccess || per_cu <= 0) per_cu = 1;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  const int64_t n = static_cast<int64_t>(per_cu) * cus;
+  std::lock_guard<std::mutex> lk(mu);
+  cache[key] = n;
+  return n;
+}
+
+inline int cu_count() {
+  static std::mutex mu;
+  static std::map<int, int> cache;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(dev);
+  if (it != cache.end()) return it->second;
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  cache[dev] = cus;
+  return cus;
+}
+
+// Round-split dispatch: the column range is cut into the fewest EQUAL
+// launches whose blocks all fit on the chip at once (one resident round
+// each).  Within a launch every block starts together and the running blocks
+// sweep one compact window of every client row; the stream boundary between
+// launches re-aligns them (a multi-round launch lets blocks drift apart and
+// leaves a half-empty last round).
+template <int U, int C, bool NT>
+void launch_split(const float* clients, int K, int64_t ld, int64_t P, const float* W, float* out, int max_blocks,
+                  hipStream_t s) {
+  const int64_t nvec = (P + 3) / 4;
+  const int64_t span = static_cast<int64_t>(kBlock) * C;
+  const int64_t resident = max_blocks > 0 ? max_blocks : resident_blocks(reduce_f32x4_var_kernel<U, C, NT, false>);
+  const int64_t blocks = (nvec + span - 1) / span;
+  const int64_t nl = (blocks + resident - 1) / resident;
+  const int64_t per = ((nvec + nl - 1) / nl + span - 1) / span * span;  // float4 columns per launch
+  const f32x4* X = reinterpret_cast<const f32x4*>(clients);
+  for (int64_t v0 = 0; v0 < nvec; v0 += per) {
+    const int64_t n = (nvec - v0) < per ? (nvec - v0) : per;
+    const int tail = (v0 + n == nvec) ? static_cast<int>(P & 3) : 0;
+    hipLaunchKernelGGL((reduce_f32x4_var_kernel<U, C, NT, false>), dim3(static_cast<unsigned>((n + span - 1) / span)),
+                       dim3(kBlock), 0, s, X + v0, K, ld / 4, n, tail, W, out + v0 * 4);
+  }
+}
+
+}  // namespace fedavg_impl

@@ -1,0 +1,358 @@
+// fedavg_variants.hip -- benchmarking variants of the exact fp32 kernel
+// (include/fedavg_amd_tuning.h): first-version kernel, multi-column /
+// double-buffered / LDS-DMA / balanced / round-split / windowed schedules and
+// the tiled layout.  All produce the same bits as fedavg_reduce_f32; the
+// production schedule is chosen in fedavg_reduce.hip from their sweeps
+// (profiles/sweeps/).
+#include "common.hpp"
+
+namespace {
+using namespace fedavg_impl;
+
+// ---------------------------------------------------------------------------
+// fp32, bit-exact, BALANCED PERSISTENT schedule.  The column axis is cut into
+// wave-slices (64 float4 = 1 KiB of one client row); the grid is the number
+// of blocks the chip holds at once and block b owns the contiguous range
+// [b*N/G, (b+1)*N/G) of the N full wave-slices.  It walks its range in steps
+// of 4*C slices (wave w takes slices s+w, s+w+4, ..., so a step reads 4*C KiB
+// contiguous bytes of each client row); in the last, partial step each wave
+// takes the cw <= C slices still inside its range (cw is wave-uniform).  Every
+// block therefore streams the same number of bytes (+-1 KiB x K) and the
+// launch has no tail of half-empty block rounds, whatever K and P are.  The
+// trailing partial wave-slice (nvec % 64 lanes) goes to the last block.
+// ---------------------------------------------------------------------------
+template <int U, int CW, bool NT>
+__device__ __forceinline__ void balanced_body(const f32x4* col, int K, int64_t ld4, const float* W, float* out,
+                                              int64_t v0, int64_t nvec, int tail) {
+  f32x4 acc[CW];
+  reduce_full_group<U, CW, NT, false>(acc, col, K, ld4, W);
+#pragma unroll
+  for (int j = 0; j < CW; ++j) store_slice(out, v0 + j * kBlock, nvec, tail, acc[j]);
+}
+
+template <int U, int C, bool NT, int CW>
+__device__ __forceinline__ void balanced_dispatch(int cw, const f32x4* col, int K, int64_t ld4, const float* W,
+                                                  float* out, int64_t v0, int64_t nvec, int tail) {
+  if constexpr (CW >= 1) {
+    if (cw == CW) {
+      balanced_body<U, CW, NT>(col, K, ld4, W, out, v0, nvec, tail);
+      return;
+    }
+    balanced_dispatch<U, C, NT, CW - 1>(cw, col, K, ld4, W, out, v0, nvec, tail);
+  }
+}
+
+template <int U, int C, bool NT>
+__global__ __launch_bounds__(kBlock) void reduce_balanced_f32x4_kernel(
+    const f32x4* __restrict__ X, int K, int64_t ld4, int64_t nvec, int tail,
+    const float* __restrict__ W, float* __restrict__ out) {
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int64_t nws = nvec / 64;  // full wave-slices
+  const int64_t G = gridDim.x, b = blockIdx.x;
+  const int64_t ws0 = nws * b / G, ws1 = nws * (b + 1) / G;
+  for (int64_t s = ws0; s < ws1; s += 4 * C) {
+    const int64_t rem = ws1 - s;
+    int cw = C;
+    if (rem < 4 * C) cw = rem > wave ? static_cast<int>((rem - wave + 3) / 4) : 0;
+    if (cw == 0) continue;
+    const int64_t v0 = (s + wave) * 64 + lane;
+    balanced_dispatch<U, C, NT, C>(cw, X + v0, K, ld4, W, out, v0, nvec, tail);
+  }
+  if (b == G - 1 && wave == 0 && nws * 64 < nvec) {
+    const int64_t v = nws * 64 + lane;
+    if (v < nvec) {
+      f32x4 acc[1];
+      reduce_full_group<U, 1, NT, false>(acc, X + v, K, ld4, W);
+      store_slice(out, v, nvec, tail, acc[0]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// fp32, bit-exact, LDS-DMA staging: every client-row load is a
+// global_load_lds_dwordx4 (1 KiB per wave-instruction, `nt` when AUX == 2)
+// into the wave's own LDS slots; after its own vmcnt(0) the wave reads the
+// 16 B it loaded back with ds_read_b128 (lane l reads bytes [16l, 16l+16),
+// conflict-free) and accumulates in the reference order.  No cross-wave LDS
+// sharing, so no barrier: only the issuing wave's vmcnt orders its reads.
+// ---------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef const __attribute__((address_space(1))) void* gbl_ptr_t;
+
+template <int U, int C, int AUX>
+__global__ __launch_bounds__(kBlock) void reduce_glds_f32x4_kernel(
+    const f32x4* __restrict__ X, int K, int64_t ld4, int64_t nvec, int tail,
+    const float* __restrict__ W, float* __restrict__ out) {
+  constexpr int kSlot = 1024;  // bytes one wave-instruction lands
+  __shared__ __attribute__((aligned(16))) char lds[(kBlock / 64) * U * C * kSlot];
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  char* mine = lds + wave * (U * C * kSlot);
+  const int64_t span = static_cast<int64_t>(kBlock) * C;
+  for (int64_t base = static_cast<int64_t>(blockIdx.x) * span; base < nvec;
+       base += static_cast<int64_t>(gridDim.x) * span) {
+    if (base + span > nvec) {
+      for (int j = 0; j < C; ++j) {
+        const int64_t v = base + threadIdx.x + j * kBlock;
+        if (v >= nvec) break;
+        f32x4 acc1[1];
+        reduce_full_group<8, 1, true, false>(acc1, X + v, K, ld4, W);
+        store_slice(out, v, nvec, tail, acc1[0]);
+      }
+      continue;
+    }
+    const f32x4* col = X + base + threadIdx.x;
+    f32x4 acc[C];
+    const float w0 = W[0];
+#pragma unroll
+    for (int j = 0; j < C; ++j) acc[j] = ld<true>(col + j * kBlock) * w0;
+    int k = 1;
+    for (; k + U <= K; k += U) {
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int j = 0; j < C; ++j)
+          __builtin_amdgcn_global_load_lds(
+              (gbl_ptr_t)(col + static_cast<int64_t>(k + u) * ld4 + j * kBlock),
+              (lds_ptr_t)(mine + (u * C + j) * kSlot), 16, 0, AUX);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const float w = W[k + u];
+#pragma unroll
+        for (int j = 0; j < C; ++j) {
+          const f32x4 x = *reinterpret_cast<const f32x4*>(mine + (u * C + j) * kSlot + lane * 16);
+          const f32x4 term = x * w;
+          acc[j] = acc[j] + term;
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slots free before the next batch lands
+    }
+    for (; k < K; ++k) {
+      const float w = W[k];
+#pragma unroll
+      for (int j = 0; j < C; ++j) {
+        const f32x4 term = ld<true>(col + static_cast<int64_t>(k) * ld4 + j * kBlock) * w;
+        acc[j] = acc[j] + term;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < C; ++j) store_slice(out, base + threadIdx.x + j * kBlock, nvec, tail, acc[j]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// fp32, bit-exact, TILED layout: X is [ntiles][K][1024] (tile t holds columns
+// [1024t, 1024t+1024) of every client, client-major inside the tile), so a
+// block streams K * 4 KiB of contiguous memory instead of K rows 4*ld apart.
+// ---------------------------------------------------------------------------
+constexpr int kTile = kBlock * 4;  // floats per tile row (4 KiB)
+
+template <int U, bool NT>
+__global__ __launch_bounds__(kBlock) void reduce_tiled_f32x4_kernel(
+    const f32x4* __restrict__ X, int K, int64_t P, const float* __restrict__ W, float* __restrict__ out) {
+  const int64_t t = blockIdx.x;
+  const f32x4* col = X + t * static_cast<int64_t>(K) * kBlock + threadIdx.x;
+  f32x4 acc[1];
+  reduce_full_group<U, 1, NT, true>(acc, col, K, kBlock, W);
+  const int64_t p0 = t * kTile + static_cast<int64_t>(threadIdx.x) * 4;
+  if (p0 + 4 <= P) {
+    *reinterpret_cast<f32x4*>(out + p0) = acc[0];
+  } else if (p0 < P) {
+    out[p0] = acc[0].x;
+    if (p0 + 1 < P) out[p0 + 1] = acc[0].y;
+    if (p0 + 2 < P) out[p0 + 2] = acc[0].z;
+  }
+}
+
+int reduce_f32_tuned_impl(const float* clients, int64_t K, int64_t P, int64_t ld, const float* weights,
+                    float* out, hipStream_t s, int unroll, int nontemporal, const char* what) {
+  int rc = check_common(clients, K, P, ld, weights, out, what);
+  if (rc) return rc;
+  if (P == 0) return FEDAVG_OK;
+  if (!aligned4(clients) || !aligned4(out) || !aligned4(weights))
+    return set_error(FEDAVG_EALIGN, "%s: fp32 buffers must be 4-byte aligned", what);
+  const int k = static_cast<int>(K);
+  if (aligned16(clients) && (ld % 4) == 0) {
+    switch (unroll * 2 + (nontemporal ? 1 : 0)) {
+      case 4 * 2 + 0: launch_f32x4<4, false>(clients, k, ld, P, weights, out, s); break;
+      case 4 * 2 + 1: launch_f32x4<4, true>(clients, k, ld, P, weights, out, s); break;
+      case 8 * 2 + 0: launch_f32x4<8, false>(clients, k, ld, P, weights, out, s); break;
+      case 8 * 2 + 1: launch_f32x4<8, true>(clients, k, ld, P, weights, out, s); break;
+      case 16 * 2 + 0: launch_f32x4<16, false>(clients, k, ld, P, weights, out, s); break;
+      case 16 * 2 + 1: launch_f32x4<16, true>(clients, k, ld, P, weights, out, s); break;
+      default: return set_error(FEDAVG_EMODE, "%s: unsupported unroll %d", what, unroll);
+    }
+  } else {
+    return set_error(FEDAVG_EALIGN, "%s: the tuning hook needs 16-B aligned clients and ld %% 4 == 0", what);
+  }
+  return launch_status(what);
+}
+
+template <int U, int C, bool NT, bool PIPE>
+void launch_var(const float* clients, int K, int64_t ld, int64_t P, const float* W, float* out, int max_blocks,
+                hipStream_t s) {
+  const int64_t nvec = (P + 3) / 4;
+  const int64_t span = static_cast<int64_t>(kBlock) * C;
+  int64_t grid = (nvec + span - 1) / span;
+  if (max_blocks > 0 && grid > max_blocks) grid = max_blocks;
+  hipLaunchKernelGGL((reduce_f32x4_var_kernel<U, C, NT, PIPE>), dim3(static_cast<unsigned>(grid)), dim3(kBlock), 0,
+                     s, reinterpret_cast<const f32x4*>(clients), K, ld / 4, nvec, static_cast<int>(P & 3), W, out);
+}
+
+template <int U, int C, int AUX>
+void launch_glds(const float* clients, int K, int64_t ld, int64_t P, const float* W, float* out, int max_blocks,
+                 hipStream_t s) {
+  const int64_t nvec = (P + 3) / 4;
+  const int64_t span = static_cast<int64_t>(kBlock) * C;
+  int64_t grid = (nvec + span - 1) / span;
+  if (max_blocks > 0 && grid > max_blocks) grid = max_blocks;
+  hipLaunchKernelGGL((reduce_glds_f32x4_kernel<U, C, AUX>), dim3(static_cast<unsigned>(grid)), dim3(kBlock), 0, s,
+                     reinterpret_cast<const f32x4*>(clients), K, ld / 4, nvec, static_cast<int>(P & 3), W, out);
+}
+
+template <int U, int C, bool NT>
+void launch_balanced(const float* clients, int K, int64_t ld, int64_t P, const float* W, float* out, int max_blocks,
+                     hipStream_t s) {
+  const int64_t nvec = (P + 3) / 4;
+  const int64_t nws = nvec / 64;
+  int64_t grid = max_blocks > 0 ? max_blocks : resident_blocks(reduce_balanced_f32x4_kernel<U, C, NT>);
+  if (grid > nws) grid = nws > 0 ? nws : 1;
+  hipLaunchKernelGGL((reduce_balanced_f32x4_kernel<U, C, NT>), dim3(static_cast<unsigned>(grid)), dim3(kBlock), 0, s,
+                     reinterpret_cast<const f32x4*>(clients), K, ld / 4, nvec, static_cast<int>(P & 3), W, out);
+}
+
+// Windowed balanced dispatch: every launch has EXACTLY G blocks (a multiple
+// of the CU count, so each CU gets the same number of equal-work blocks) and
+// covers one window of ~G*4C wave-slices; inside the window the balanced
+// kernel gives each block an equal contiguous share (+-1 KiB x K).  Windows
+// are equal-sized and processed in order, so each launch sweeps one compact
+// window of every client row.  max_blocks = G (0 = 3 x CUs).
+template <int U, int C, bool NT>
+void launch_window(const float* clients, int K, int64_t ld, int64_t P, const float* W, float* out, int max_blocks,
+                   hipStream_t s) {
+  const int64_t nvec = (P + 3) / 4;
+  const int64_t G = max_blocks > 0 ? max_blocks : 3 * static_cast<int64_t>(cu_count());
+  const int64_t win_ws = G * 4 * C;                   // wave-slices one window holds at full steps
+  const int64_t nws = (nvec + 63) / 64;               // wave-slices incl. a partial last one
+  const int64_t nl = (nws + win_ws - 1) / win_ws;
+  const int64_t per_ws = (nws + nl - 1) / nl;         // equal windows, in wave-slices
+  const f32x4* X = reinterpret_cast<const f32x4*>(clients);
+  for (int64_t w0 = 0; w0 < nws; w0 += per_ws) {
+    const int64_t v0 = w0 * 64;
+    const int64_t n = std::min<int64_t>(per_ws * 64, nvec - v0);
+    const int tail = (v0 + n == nvec) ? static_cast<int>(P & 3) : 0;
+    int64_t grid = std::min<int64_t>(G, std::max<int64_t>(1, n / 64));
+    hipLaunchKernelGGL((reduce_balanced_f32x4_kernel<U, C, NT>), dim3(static_cast<unsigned>(grid)), dim3(kBlock), 0,
+                       s, X + v0, K, ld / 4, n, tail, W, out + v0 * 4);
+  }
+}
+
+typedef void (*var_launcher)(const float*, int, int64_t, int64_t, const float*, float*, int, hipStream_t);
+
+// pipe: 0 = plain register batches, 1 = register double-buffering, 2 = LDS-DMA staging,
+//       3 = balanced persistent (grid = resident blocks unless max_blocks > 0),
+//       4 = round-split launches of the plain kernel (max_blocks = blocks per round, 0 = resident),
+//       5 = windowed balanced launches of exactly max_blocks blocks (0 = 3 x CUs)
+template <int U, int C>
+var_launcher pick_var2(int nt, int pipe) {
+  if (pipe == 3) {
+    if constexpr (U * C <= 32) return nt ? launch_balanced<U, C, true> : launch_balanced<U, C, false>;
+    return nullptr;
+  }
+  if (pipe == 4) return nt ? launch_split<U, C, true> : launch_split<U, C, false>;
+  if (pipe == 5) {
+    if constexpr (U * C <= 64) return nt ? launch_window<U, C, true> : launch_window<U, C, false>;
+    return nullptr;
+  }
+  if (pipe == 2) {
+    if constexpr (U * C <= 16) return nt ? launch_glds<U, C, 2> : launch_glds<U, C, 0>;
+    return nullptr;
+  }
+  if constexpr (U * C <= 32) {
+    if (nt) return pipe ? launch_var<U, C, true, true> : launch_var<U, C, true, false>;
+    return pipe ? launch_var<U, C, false, true> : launch_var<U, C, false, false>;
+  } else {
+    if (pipe) return nullptr;  // would spill
+    return nt ? launch_var<U, C, true, false> : launch_var<U, C, false, false>;
+  }
+}
+
+template <int U>
+var_launcher pick_var1(int cols, int nt, int pipe) {
+  switch (cols) {
+    case 1: return pick_var2<U, 1>(nt, pipe);
+    case 2: return pick_var2<U, 2>(nt, pipe);
+    case 4: return pick_var2<U, 4>(nt, pipe);
+    case 8:
+      if constexpr (U <= 8) return pick_var2<U, 8>(nt, pipe);
+      return nullptr;
+    case 16:
+      if constexpr (U <= 2) return pick_var2<U, 16>(nt, pipe);
+      return nullptr;
+    default: return nullptr;
+  }
+}
+
+var_launcher pick_var(int unroll, int cols, int nt, int pipe) {
+  switch (unroll) {
+    case 32:  // deep batches for short rows / many clients (latency-bound shapes)
+      if (cols == 1) return pick_var2<32, 1>(nt, pipe);
+      if (cols == 2) return pick_var2<32, 2>(nt, pipe);
+      return nullptr;
+    case 1: return pick_var1<1>(cols, nt, pipe);
+    case 2: return pick_var1<2>(cols, nt, pipe);
+    case 4: return pick_var1<4>(cols, nt, pipe);
+    case 8: return pick_var1<8>(cols, nt, pipe);
+    case 16: return pick_var1<16>(cols, nt, pipe);
+    default: return nullptr;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int fedavg_reduce_f32_tuned(const float* clients, int64_t K, int64_t P, int64_t ld, const float* weights,
+                            float* out, int unroll, int nontemporal, void* stream) {
+  return reduce_f32_tuned_impl(clients, K, P, ld, weights, out, static_cast<hipStream_t>(stream), unroll,
+                         nontemporal, "fedavg_reduce_f32_tuned");
+}
+
+int fedavg_reduce_f32_variant(const float* clients, int64_t K, int64_t P, int64_t ld, const float* weights,
+                              float* out, int unroll, int nontemporal, int cols, int pipelined, int max_blocks,
+                              void* stream) {
+  const char* what = "fedavg_reduce_f32_variant";
+  int rc = check_common(clients, K, P, ld, weights, out, what);
+  if (rc) return rc;
+  if (P == 0) return FEDAVG_OK;
+  if (!aligned16(clients) || !aligned16(out) || (ld % 4) != 0)
+    return set_error(FEDAVG_EALIGN, "%s: needs 16-B aligned clients/out and ld %% 4 == 0", what);
+  var_launcher fn = pick_var(unroll, cols, nontemporal ? 1 : 0, pipelined);
+  if (!fn) return set_error(FEDAVG_EMODE, "%s: unsupported unroll=%d cols=%d", what, unroll, cols);
+  fn(clients, static_cast<int>(K), ld, P, weights, out, max_blocks, static_cast<hipStream_t>(stream));
+  return launch_status(what);
+}
+
+int fedavg_reduce_tiled_f32(const float* tiles, int64_t K, int64_t P, const float* weights, float* out,
+                            int unroll, void* stream) {
+  const char* what = "fedavg_reduce_tiled_f32";
+  int rc = check_common(tiles, K, P, P, weights, out, what);
+  if (rc) return rc;
+  if (P == 0) return FEDAVG_OK;
+  if (!aligned16(tiles) || !aligned4(out)) return set_error(FEDAVG_EALIGN, "%s: tiles must be 16-B aligned", what);
+  const int64_t ntiles = (P + kTile - 1) / kTile;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const f32x4* X = reinterpret_cast<const f32x4*>(tiles);
+  const int k = static_cast<int>(K);
+  switch (unroll) {
+    case 4: hipLaunchKernelGGL((reduce_tiled_f32x4_kernel<4, false>), dim3(ntiles), dim3(kBlock), 0, s, X, k, P, weights, out); break;
+    case 8: hipLaunchKernelGGL((reduce_tiled_f32x4_kernel<8, false>), dim3(ntiles), dim3(kBlock), 0, s, X, k, P, weights, out); break;
+    case 16: hipLaunchKernelGGL((reduce_tiled_f32x4_kernel<16, false>), dim3(ntiles), dim3(kBlock), 0, s, X, k, P, weights, out); break;
+    default: return set_error(FEDAVG_EMODE, "%s: unsupported unroll %d", what, unroll);
+  }
+  return launch_status(what);
+}
+
+}  // extern "C"
