@@ -1,6 +1,8 @@
 """Benchmark: device-resident FedAvg weighted reduction on MI355X.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME]
+    python bench.py --e2e [...]   # host state_dicts in/out vs the CPU loop (scripts/bench_e2e.py)
+    python bench.py --fpf [...]   # FPF2 bookkeeping per round (scripts/bench_fpf.py)
 
 Metric (BASELINE.json): "aggregated GB/s device-resident, K-client x P-param
 fp32 weighted reduce".  A step is one pass of the hot path
@@ -332,5 +334,28 @@ def main():
         dist.destroy_process_group()
 
 
+def side_bench(argv) -> bool:
+    """``bench.py --e2e ...`` / ``bench.py --fpf ...``: the host-in/host-out
+    rate of the drop-in (scripts/bench_e2e.py) and the FPF2 bookkeeping per
+    round (scripts/bench_fpf.py), each beside its CPU baseline -- the
+    reference's torch expressions (oracle/), handed in from here."""
+    if not argv or argv[0] not in ("--e2e", "--fpf"):
+        return False
+    sys.path.insert(0, str(ROOT / "scripts"))
+    sys.path.insert(0, str(ROOT / "oracle"))
+    if argv[0] == "--e2e":
+        import bench_e2e
+        import fedavg_oracle as O
+
+        bench_e2e.main(O.aggregate_torch, O.client_distances_torch, argv[1:])
+    else:
+        import bench_fpf
+        import fpf_oracle
+
+        bench_fpf.main(fpf_oracle.FPFOracle, argv[1:])
+    return True
+
+
 if __name__ == "__main__":
-    main()
+    if not side_bench(sys.argv[1:]):
+        main()

@@ -113,6 +113,45 @@ int fedavg_client_sqdist_f32(const float* clients, int64_t K, int64_t P, int64_t
                              double* sumsq, void* stream);
 
 /*
+ * FPF2 bookkeeping (fedavg_trainer.py:108-119 state, :209-210, :271-278,
+ * :314-327), on device-resident state owned by the caller:
+ *   diffs   : local_w_diffs, [n_rows, ld] fp32 (n_rows = client_num_in_total),
+ *             zero-initialised; columns P..ld stay 0
+ *   a_mat   : A_mat, [ld] fp32, initialised to ones
+ *   g_mat   : G_mat, [n_rows] fp32, zeros; itr_row : row round_idx of
+ *             local_itr_lst [comm_round, n_rows]; lru_itr : LRU_itr_lst or NULL
+ * All updates are the reference's fp32 expressions, bit-identical, except
+ * global_w_diff.mean() (:319) and the row norms (:272), which are summed in
+ * fp64 in a fixed order and rounded once (within the reference's own fp32
+ * rounding error).  Needs 16-B aligned diffs/rows/last_w/w_glob/a_mat and
+ * ld % 4 == 0.
+ *
+ * set_rows (:210): diffs[row_idx[k]] = rows[k] - last_w for k < K (row_idx
+ *   is DEVICE int64; out-of-range entries are skipped -- validate on the host).
+ * end_round (:316-319): rows with keep_rows[r] == 0 (device uint8; 1 = in
+ *   client_indexes) get diffs[r] -= (w_glob - last_w); A_mat EMA with the
+ *   mean of (w_glob - last_w).  workspace: fedavg_fpf_workspace(P) doubles.
+ * update_g (:321-327): if `record`, itr_row[selected] = local_itr and (when
+ *   lru_itr != NULL) lru_itr = selected ? 0 : lru_itr + local_itr; then
+ *   G_mat = G_mat * (1 - 1/g1) + itr_row / g1.
+ * index (:272/:274, :276-278): fpf[r] = norm(diffs[r] * a_mat) / g_mat[r]
+ *   (or lru_itr[r] / g_mat[r]), NaN/inf replaced by 0.  fpf is DEVICE fp32.
+ */
+int fedavg_fpf_set_rows_f32(float* diffs, int64_t n_rows, int64_t ld, const int64_t* row_idx,
+                            int64_t K, const float* rows, int64_t ld_rows, const float* last_w,
+                            int64_t P, void* stream);
+int64_t fedavg_fpf_workspace(int64_t P);
+int fedavg_fpf_end_round_f32(float* diffs, int64_t n_rows, int64_t ld, const uint8_t* keep_rows,
+                             float* a_mat, const float* w_glob, const float* last_w, int64_t P,
+                             float g2, double* workspace, int64_t workspace_elems, void* stream);
+int fedavg_fpf_update_g(float* g_mat, float* itr_row, float* lru_itr, const uint8_t* selected,
+                        int64_t n_rows, float local_itr, int record, float g1, void* stream);
+int fedavg_fpf_index_f32(const float* diffs, int64_t n_rows, int64_t ld, int64_t P,
+                         const float* a_mat, const float* g_mat, float* fpf, void* stream);
+int fedavg_fpf_index_lru(const float* lru_itr, const float* g_mat, int64_t n_rows, float* fpf,
+                         void* stream);
+
+/*
  * Host helper: weights[i] = (float)((double)n_i / (double)sum(n)) for integer
  * sample counts, exactly as Python's int/int true division followed by ATen's
  * double->float cast (fedavg_trainer.py:444-447,453).  Counts must be >= 0

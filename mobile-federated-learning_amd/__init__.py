@@ -12,6 +12,7 @@ Layers:
   aggregate                the drop-in (DeviceAggregator, install, mixin)
   session                  streaming rounds: pack + upload each client as it arrives
   distributed              P-sharded multi-GPU reduce + RCCL all-gather
+  fpf                      FPF2 bookkeeping (local_w_diffs / A_mat / G_mat) in HBM
 """
 from ._lib import FedAvgLibraryError, library_path
 from .aggregate import (
@@ -27,6 +28,7 @@ from .aggregate import (
 from .layout import KeyTable, ShapeMismatchError, result_dtype
 from .reduce import ALIGN_ELEMS, client_sqdist, reduce_packed, reduce_tensors, weights_tensor
 from .session import RoundSession
+from .fpf import FPFTracker
 
 __all__ = [
     "FedAvgLibraryError",
@@ -48,4 +50,5 @@ __all__ = [
     "reduce_tensors",
     "weights_tensor",
     "RoundSession",
+    "FPFTracker",
 ]

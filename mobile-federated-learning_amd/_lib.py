@@ -14,6 +14,7 @@ from .build import LIB_PATH
 _c_i64 = ctypes.c_int64
 _c_int = ctypes.c_int
 _vp = ctypes.c_void_p
+_c_float = ctypes.c_float
 
 # name -> (restype, argtypes); mirrors include/fedavg_amd.h + fedavg_amd_tuning.h
 SIGNATURES = {
@@ -29,6 +30,13 @@ SIGNATURES = {
     "fedavg_pack_rows": (_c_int, [_vp, _c_i64, _vp, _c_i64, _c_int]),
     "fedavg_client_sqdist_workspace": (_c_i64, [_c_i64, _c_i64]),
     "fedavg_client_sqdist_f32": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_i64, _vp, _vp]),
+    "fedavg_fpf_set_rows_f32": (_c_int, [_vp, _c_i64, _c_i64, _vp, _c_i64, _vp, _c_i64, _vp, _c_i64, _vp]),
+    "fedavg_fpf_workspace": (_c_i64, [_c_i64]),
+    "fedavg_fpf_end_round_f32": (_c_int, [_vp, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _c_i64, _c_float, _vp, _c_i64,
+                                          _vp]),
+    "fedavg_fpf_update_g": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_float, _c_int, _c_float, _vp]),
+    "fedavg_fpf_index_f32": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _vp]),
+    "fedavg_fpf_index_lru": (_c_int, [_vp, _vp, _c_i64, _vp, _vp]),
     "fedavg_f32_schedule": (_c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp]),
     "fedavg_reduce_f32_tuned": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_int, _c_int, _vp]),
     "fedavg_reduce_f32_variant": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_int, _c_int, _c_int, _c_int,

@@ -1,0 +1,281 @@
+// fedavg_fpf.hip -- the FPF2 bookkeeping of the round loop
+// (fedavg_trainer.py:108-119, :209-210, :271-278, :314-327) on device-resident
+// state: local_w_diffs [n_rows, ld], A_mat [ld], G_mat / local_itr_lst row /
+// LRU_itr_lst [n_rows], all fp32 like the reference's tensors.
+//
+// Elementwise updates reproduce the reference's fp32 expressions operation by
+// operation (no FMA: the library is built with -ffp-contract=off), so
+// local_w_diffs, G_mat, local_itr_lst and LRU_itr_lst are bit-identical.  The
+// two reductions -- global_w_diff.mean() (:319) and the row norms (:272) --
+// accumulate in fp64 in a fixed order and round once; the reference's fp32
+// reductions are within their own rounding error of that value.
+//
+// Padding lanes (columns P..ld) never contribute: every load past P is
+// replaced by a select, so whatever the padding holds cannot leak in.
+#include "common.hpp"
+
+#include <math.h>
+
+namespace {
+using namespace fedavg_impl;
+
+constexpr int kFpfRowsPerBlock = 16;
+constexpr int kFpfMaxPartials = 1024;
+
+__device__ __forceinline__ f32x4 masked(f32x4 v, int nv) {
+  if (nv < 4) {
+    v.x = nv > 0 ? v.x : 0.f;
+    v.y = nv > 1 ? v.y : 0.f;
+    v.z = nv > 2 ? v.z : 0.f;
+    v.w = 0.f;
+  }
+  return v;
+}
+
+__device__ __forceinline__ int lanes_valid(int64_t v, int64_t P) {
+  const int64_t rem = P - v * 4;
+  return rem >= 4 ? 4 : (rem > 0 ? static_cast<int>(rem) : 0);
+}
+
+__device__ __forceinline__ double block_sum(double v, double* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) red[wave] = v;
+  __syncthreads();
+  double s = 0.0;
+  if (threadIdx.x == 0)
+    for (int w = 0; w < kBlock / 64; ++w) s += red[w];
+  return s;  // valid in thread 0
+}
+
+// :210  local_w_diffs[row_idx[k], :] = rows[k, :] - last_w   (fp32 difference)
+__global__ __launch_bounds__(kBlock) void fpf_set_rows_kernel(f32x4* __restrict__ D, int64_t ld4, int64_t n_rows,
+                                                              const int64_t* __restrict__ row_idx,
+                                                              const f32x4* __restrict__ rows, int64_t ld_rows4,
+                                                              const f32x4* __restrict__ last_w, int64_t P) {
+  const int64_t r = row_idx[blockIdx.y];
+  if (r < 0 || r >= n_rows) return;  // the host layer raises IndexError before launching
+  const int64_t nvec = (P + 3) / 4;
+  const f32x4* src = rows + static_cast<int64_t>(blockIdx.y) * ld_rows4;
+  f32x4* dst = D + r * ld4;
+  for (int64_t v = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; v < nvec;
+       v += static_cast<int64_t>(gridDim.x) * kBlock)
+    dst[v] = masked(src[v] - last_w[v], lanes_valid(v, P));
+}
+
+// :319 (first half): per-block fp64 partial sums of global_w_diff = w_glob - last_w.
+__global__ __launch_bounds__(kBlock) void fpf_gdiff_partials_kernel(const f32x4* __restrict__ w_glob,
+                                                                    const f32x4* __restrict__ last_w, int64_t P,
+                                                                    double* __restrict__ partials) {
+  __shared__ double red[kBlock / 64];
+  const int64_t nvec = (P + 3) / 4;
+  double s = 0.0;
+  for (int64_t v = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; v < nvec;
+       v += static_cast<int64_t>(gridDim.x) * kBlock) {
+    const f32x4 g = masked(w_glob[v] - last_w[v], lanes_valid(v, P));
+    s += static_cast<double>(g.x) + static_cast<double>(g.y) + static_cast<double>(g.z) + static_cast<double>(g.w);
+  }
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) partials[blockIdx.x] = s;
+}
+
+// :316-319  rows not in client_indexes: local_w_diffs -= global_w_diff;
+//           A_mat = A_mat * (1 - 1/G2) + global_w_diff / G2 / global_w_diff.mean()
+// Every block reduces the same partials in the same order, so all blocks see
+// the same mean without another launch.
+__global__ __launch_bounds__(kBlock) void fpf_end_round_kernel(f32x4* __restrict__ D, int64_t ld4, int64_t n_rows,
+                                                               const uint8_t* __restrict__ keep_rows,
+                                                               f32x4* __restrict__ A, const f32x4* __restrict__ w_glob,
+                                                               const f32x4* __restrict__ last_w, int64_t P,
+                                                               const double* __restrict__ partials, int nparts,
+                                                               float g2, float c2) {
+  __shared__ double red[kBlock / 64];
+  __shared__ float mean_s;
+  double s = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += kBlock) s += partials[i];
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) mean_s = static_cast<float>(s / static_cast<double>(P));
+  __syncthreads();
+  const float mean = mean_s;
+  const int64_t nvec = (P + 3) / 4;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.y) * kFpfRowsPerBlock;
+  const int64_t r1 = r0 + kFpfRowsPerBlock < n_rows ? r0 + kFpfRowsPerBlock : n_rows;
+  for (int64_t v = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; v < nvec;
+       v += static_cast<int64_t>(gridDim.x) * kBlock) {
+    const int nv = lanes_valid(v, P);
+    const f32x4 g = masked(w_glob[v] - last_w[v], nv);
+    if (blockIdx.y == 0) {
+      const f32x4 a = A[v];
+      f32x4 na;
+      na.x = a.x * c2 + (g.x / g2) / mean;
+      na.y = a.y * c2 + (g.y / g2) / mean;
+      na.z = a.z * c2 + (g.z / g2) / mean;
+      na.w = a.w * c2 + (g.w / g2) / mean;
+      A[v] = nv == 4 ? na : f32x4{nv > 0 ? na.x : a.x, nv > 1 ? na.y : a.y, nv > 2 ? na.z : a.z, a.w};
+    }
+    for (int64_t r = r0; r < r1; ++r) {
+      if (keep_rows[r]) continue;
+      f32x4* p = D + r * ld4 + v;
+      *p = *p - g;  // padding lanes: g == 0, D stays 0
+    }
+  }
+}
+
+// :321-327  local_itr_lst[round_idx, selected] = float(local_itr);
+//           LRU_itr_lst += float(local_itr); LRU_itr_lst[selected] = 0   (LRU mode)
+//           G_mat = G_mat * (1 - 1/G1) + local_itr_lst[round_idx, :] / G1
+__global__ __launch_bounds__(kBlock) void fpf_update_g_kernel(float* __restrict__ G, float* __restrict__ itr_row,
+                                                              float* __restrict__ lru,
+                                                              const uint8_t* __restrict__ selected, int64_t n,
+                                                              float local_itr, int record, float g1, float c1) {
+  const int64_t r = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (r >= n) return;
+  float it = itr_row[r];
+  if (record) {
+    if (selected[r]) it = local_itr;
+    itr_row[r] = it;
+    if (lru) lru[r] = selected[r] ? 0.f : lru[r] + local_itr;
+  }
+  G[r] = G[r] * c1 + it / g1;
+}
+
+// :272, :276-278  fpf[r] = norm(local_w_diffs[r] * A_mat) / G_mat[r], NaN/inf -> 0.
+// One block per row; products rounded to fp32 like the reference's
+// `local_w_diffs * A_mat`, squares and sum in fp64, one rounding at the end.
+__global__ __launch_bounds__(kBlock) void fpf_index_kernel(const f32x4* __restrict__ D, int64_t ld4, int64_t P,
+                                                           const f32x4* __restrict__ A, const float* __restrict__ G,
+                                                           float* __restrict__ out) {
+  __shared__ double red[kBlock / 64];
+  const int64_t r = blockIdx.x;
+  const int64_t nvec = (P + 3) / 4;
+  const f32x4* row = D + r * ld4;
+  double s = 0.0;
+  for (int64_t v = threadIdx.x; v < nvec; v += kBlock) {
+    const f32x4 q = masked(row[v] * A[v], lanes_valid(v, P));
+    s += static_cast<double>(q.x) * q.x + static_cast<double>(q.y) * q.y + static_cast<double>(q.z) * q.z +
+         static_cast<double>(q.w) * q.w;
+  }
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) {
+    const float f = static_cast<float>(sqrt(s)) / G[r];
+    out[r] = isfinite(f) ? f : 0.f;
+  }
+}
+
+// :274, :276-278  fpf = LRU_itr_lst / G_mat, NaN/inf -> 0.
+__global__ __launch_bounds__(kBlock) void fpf_index_lru_kernel(const float* __restrict__ lru,
+                                                               const float* __restrict__ G, int64_t n,
+                                                               float* __restrict__ out) {
+  const int64_t r = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (r >= n) return;
+  const float f = lru[r] / G[r];
+  out[r] = isfinite(f) ? f : 0.f;
+}
+
+unsigned col_blocks(int64_t P, int64_t cap) {
+  const int64_t nvec = (P + 3) / 4;
+  int64_t b = (nvec + kBlock - 1) / kBlock;
+  if (b > cap) b = cap;
+  return static_cast<unsigned>(b < 1 ? 1 : b);
+}
+
+int check_state(const void* diffs, int64_t n_rows, int64_t ld, int64_t P, const char* what) {
+  if (n_rows <= 0 || n_rows > INT32_MAX) return set_error(FEDAVG_EINVAL, "%s: bad n_rows %lld", what, (long long)n_rows);
+  if (P <= 0) return set_error(FEDAVG_EINVAL, "%s: P must be >= 1", what);
+  if (ld < P || (ld % 4) != 0)
+    return set_error(FEDAVG_EINVAL, "%s: need ld >= P and ld %% 4 == 0 (ld=%lld, P=%lld)", what, (long long)ld,
+                     (long long)P);
+  if (!diffs) return set_error(FEDAVG_EINVAL, "%s: null local_w_diffs", what);
+  if (!aligned16(diffs)) return set_error(FEDAVG_EALIGN, "%s: local_w_diffs must be 16-B aligned", what);
+  return FEDAVG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fedavg_fpf_set_rows_f32(float* diffs, int64_t n_rows, int64_t ld, const int64_t* row_idx, int64_t K,
+                            const float* rows, int64_t ld_rows, const float* last_w, int64_t P, void* stream) {
+  const char* what = "fedavg_fpf_set_rows_f32";
+  int rc = check_state(diffs, n_rows, ld, P, what);
+  if (rc) return rc;
+  if (K <= 0 || K > 65535) return set_error(FEDAVG_EINVAL, "%s: K must be in [1, 65535] (got %lld)", what, (long long)K);
+  if (!row_idx || !rows || !last_w) return set_error(FEDAVG_EINVAL, "%s: null buffer", what);
+  if (ld_rows < P || (ld_rows % 4) != 0) return set_error(FEDAVG_EINVAL, "%s: bad ld_rows", what);
+  if (!aligned16(rows) || !aligned16(last_w))
+    return set_error(FEDAVG_EALIGN, "%s: rows/last_w must be 16-B aligned", what);
+  hipLaunchKernelGGL(fpf_set_rows_kernel, dim3(col_blocks(P, 256), static_cast<unsigned>(K)), dim3(kBlock), 0,
+                     static_cast<hipStream_t>(stream), reinterpret_cast<f32x4*>(diffs), ld / 4, n_rows, row_idx,
+                     reinterpret_cast<const f32x4*>(rows), ld_rows / 4, reinterpret_cast<const f32x4*>(last_w), P);
+  return launch_status(what);
+}
+
+int64_t fedavg_fpf_workspace(int64_t P) {
+  if (P <= 0) return 0;
+  return col_blocks(P, kFpfMaxPartials);
+}
+
+int fedavg_fpf_end_round_f32(float* diffs, int64_t n_rows, int64_t ld, const uint8_t* keep_rows, float* a_mat,
+                             const float* w_glob, const float* last_w, int64_t P, float g2, double* workspace,
+                             int64_t workspace_elems, void* stream) {
+  const char* what = "fedavg_fpf_end_round_f32";
+  int rc = check_state(diffs, n_rows, ld, P, what);
+  if (rc) return rc;
+  if (!keep_rows || !a_mat || !w_glob || !last_w || !workspace) return set_error(FEDAVG_EINVAL, "%s: null buffer", what);
+  if (!aligned16(a_mat) || !aligned16(w_glob) || !aligned16(last_w))
+    return set_error(FEDAVG_EALIGN, "%s: A_mat/w_glob/last_w must be 16-B aligned", what);
+  const unsigned nparts = col_blocks(P, kFpfMaxPartials);
+  if (workspace_elems < nparts)
+    return set_error(FEDAVG_EINVAL, "%s: workspace needs %u doubles", what, nparts);
+  if (!(g2 != 0.f)) return set_error(FEDAVG_EINVAL, "%s: G2 must be nonzero", what);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(fpf_gdiff_partials_kernel, dim3(nparts), dim3(kBlock), 0, s,
+                     reinterpret_cast<const f32x4*>(w_glob), reinterpret_cast<const f32x4*>(last_w), P, workspace);
+  rc = launch_status(what);
+  if (rc) return rc;
+  const float c2 = static_cast<float>(1.0 - 1.0 / static_cast<double>(g2));  // (1 - 1/G2) as a Python float
+  const unsigned ry = static_cast<unsigned>((n_rows + kFpfRowsPerBlock - 1) / kFpfRowsPerBlock);
+  hipLaunchKernelGGL(fpf_end_round_kernel, dim3(col_blocks(P, 512), ry), dim3(kBlock), 0, s,
+                     reinterpret_cast<f32x4*>(diffs), ld / 4, n_rows, keep_rows, reinterpret_cast<f32x4*>(a_mat),
+                     reinterpret_cast<const f32x4*>(w_glob), reinterpret_cast<const f32x4*>(last_w), P, workspace,
+                     static_cast<int>(nparts), g2, c2);
+  return launch_status(what);
+}
+
+int fedavg_fpf_update_g(float* g_mat, float* itr_row, float* lru_itr, const uint8_t* selected, int64_t n_rows,
+                        float local_itr, int record, float g1, void* stream) {
+  const char* what = "fedavg_fpf_update_g";
+  if (n_rows <= 0) return set_error(FEDAVG_EINVAL, "%s: n_rows must be >= 1", what);
+  if (!g_mat || !itr_row || !selected) return set_error(FEDAVG_EINVAL, "%s: null buffer", what);
+  if (!(g1 != 0.f)) return set_error(FEDAVG_EINVAL, "%s: G1 must be nonzero", what);
+  const float c1 = static_cast<float>(1.0 - 1.0 / static_cast<double>(g1));
+  hipLaunchKernelGGL(fpf_update_g_kernel, dim3(static_cast<unsigned>((n_rows + kBlock - 1) / kBlock)), dim3(kBlock),
+                     0, static_cast<hipStream_t>(stream), g_mat, itr_row, lru_itr, selected, n_rows, local_itr,
+                     record ? 1 : 0, g1, c1);
+  return launch_status(what);
+}
+
+int fedavg_fpf_index_f32(const float* diffs, int64_t n_rows, int64_t ld, int64_t P, const float* a_mat,
+                         const float* g_mat, float* fpf, void* stream) {
+  const char* what = "fedavg_fpf_index_f32";
+  int rc = check_state(diffs, n_rows, ld, P, what);
+  if (rc) return rc;
+  if (!a_mat || !g_mat || !fpf) return set_error(FEDAVG_EINVAL, "%s: null buffer", what);
+  if (!aligned16(a_mat)) return set_error(FEDAVG_EALIGN, "%s: A_mat must be 16-B aligned", what);
+  hipLaunchKernelGGL(fpf_index_kernel, dim3(static_cast<unsigned>(n_rows)), dim3(kBlock), 0,
+                     static_cast<hipStream_t>(stream), reinterpret_cast<const f32x4*>(diffs), ld / 4, P,
+                     reinterpret_cast<const f32x4*>(a_mat), g_mat, fpf);
+  return launch_status(what);
+}
+
+int fedavg_fpf_index_lru(const float* lru_itr, const float* g_mat, int64_t n_rows, float* fpf, void* stream) {
+  const char* what = "fedavg_fpf_index_lru";
+  if (n_rows <= 0) return set_error(FEDAVG_EINVAL, "%s: n_rows must be >= 1", what);
+  if (!lru_itr || !g_mat || !fpf) return set_error(FEDAVG_EINVAL, "%s: null buffer", what);
+  hipLaunchKernelGGL(fpf_index_lru_kernel, dim3(static_cast<unsigned>((n_rows + kBlock - 1) / kBlock)), dim3(kBlock),
+                     0, static_cast<hipStream_t>(stream), lru_itr, g_mat, n_rows, fpf);
+  return launch_status(what);
+}
+
+}  // extern "C"

@@ -3,7 +3,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/${RUN_TAG:-r01h}; mkdir -p $OUT
 true
 echo gpu parity ok
-timeout -k 10 600 python scripts/bench_e2e.py --reps 5 > $OUT/e2e.jsonl 2> $OUT/e2e.err
+timeout -k 10 600 python bench.py --e2e --reps 5 > $OUT/e2e.jsonl 2> $OUT/e2e.err
 echo e2e done
 for cfg in "100 25000000 target" "100 6250000 chunk4" "500 11227812 resnet18gn" "37 3000001 odd" "1000 12500000 k1000" "100 600372 resnet56" "10 1206590 femnist"; do
   set -- $cfg

@@ -1,6 +1,6 @@
 """End-to-end rate of the drop-in: host state_dicts in, host state_dict out.
 
-    python scripts/bench_e2e.py [--configs mnist_lr,femnist_cnn,resnet56,target_flat] [--reps 5]
+    python bench.py --e2e [--configs mnist_lr,femnist_cnn,resnet56,target_flat] [--reps 5]
 
 The reference's aggregate starts and ends in host memory (client.py:96
 returns ``net.cpu().state_dict()``; fedavg_trainer.py:219 loads the result
@@ -26,12 +26,10 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
-sys.path.insert(0, str(ROOT / "oracle"))
 
 import numpy as np
 import torch
 
-import fedavg_oracle as O
 import mfl_amd
 
 
@@ -96,7 +94,7 @@ def fresh(counts, dicts):
     return [(counts[0], OrderedDict(dicts[0]))] + list(zip(counts[1:], dicts[1:]))
 
 
-def run(name, reps, train_ms=0.0):
+def run(name, reps, cpu_aggregate, cpu_distances, train_ms=0.0):
     K, shapes = CONFIGS[name]
     P = sum(math.prod(s) for _, s in shapes)
     counts, dicts = make_clients(K, shapes)
@@ -127,13 +125,13 @@ def run(name, reps, train_ms=0.0):
     for r in range(cpu_reps + 1):
         wl_ref = fresh(counts, dicts)
         t0 = time.perf_counter()
-        ref = O.aggregate_torch(wl_ref)
+        ref = cpu_aggregate(wl_ref)
         t = time.perf_counter() - t0
         if r:
             cpu_t.append(t)
     for r in range(min(cpu_reps, 2) + 1):
         t0 = time.perf_counter()
-        ref_norms = O.client_distances_torch(wl_ref, ref)
+        ref_norms = cpu_distances(wl_ref, ref)
         t = time.perf_counter() - t0
         if r:
             cpu_dist_t.append(t)
@@ -178,17 +176,19 @@ def run(name, reps, train_ms=0.0):
     }
 
 
-def main():
-    ap = argparse.ArgumentParser()
+def main(cpu_aggregate, cpu_distances, argv=None):
+    """Entry point for ``python bench.py --e2e ...``: bench.py hands in its CPU
+    baseline (the reference's torch loop and :291 norms, oracle/)."""
+    ap = argparse.ArgumentParser(prog="bench.py --e2e")
     ap.add_argument("--configs", default="mnist_lr,femnist_cnn,resnet56,target_flat")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--train-ms", type=float, default=5.0,
                     help="simulated per-client training time between streaming arrivals")
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
     torch.cuda.set_device(0)
     for name in args.configs.split(","):
-        print(json.dumps(run(name, args.reps, args.train_ms)), flush=True)
+        print(json.dumps(run(name, args.reps, cpu_aggregate, cpu_distances, args.train_ms)), flush=True)
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit("run as: python bench.py --e2e [--configs ...] [--reps N] [--train-ms MS]")

@@ -22,7 +22,7 @@ timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > "$OUT/bench.json" 2> "$OUT/b
 echo "[gpu_check] bench ok: $(cat "$OUT/bench.json")" | tee -a "$OUT/progress.log"
 
 if [[ "${E2E:-0}" == 1 ]]; then
-  timeout -k 10 600 python scripts/bench_e2e.py --reps 5 > "$OUT/e2e.jsonl" 2> "$OUT/e2e.err"
+  timeout -k 10 600 python bench.py --e2e --reps 5 > "$OUT/e2e.jsonl" 2> "$OUT/e2e.err"
   echo "[gpu_check] e2e ok" | tee -a "$OUT/progress.log"
 fi
 

@@ -1,0 +1,198 @@
+"""GPU parity of the FPF2 bookkeeping (fedavg_trainer.py:108-119, 210, 271-278, 314-327).
+
+* Against the reference itself: the rounds captured from the reference's own
+  ``train()`` loop (tests/golden/fpf, oracle/gen_golden_fpf.py) are replayed
+  through ``mfl_amd.FPFTracker`` + the GPU aggregate; every per-round FPF2 row
+  must match the reference's CSV row (zeros exactly, others to rtol 1e-5 --
+  the index is a norm, accumulated in fp64 here and in fp32 lanes by ATen).
+* Against the oracle on random rounds at the reference's real size
+  (client_num_in_total = 1000 vehicles, MNIST-LR P = 7850): ``local_w_diffs``,
+  ``G_mat``, ``local_itr_lst`` and ``LRU_itr_lst`` bit-identical; ``A_mat``
+  (one fp32 mean per round) to rtol 1e-5.
+"""
+import copy
+from collections import OrderedDict
+
+import numpy as np
+import pytest
+import torch
+
+import fedavg_oracle as O
+import fpf_oracle as FO
+import fpf_replay
+import mfl_amd
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda", 0)
+RTOL = 1e-5
+
+
+class _TrackerImpl:
+    def __init__(self, meta, init):
+        self.t = mfl_amd.FPFTracker(meta["client_num_in_total"], init, meta["comm_round"], device=DEV,
+                                    threshold=meta["threshold"])
+
+    def begin_round(self, last_w):
+        self.t.begin_round(last_w)
+
+    def record_client(self, c, w, last_w):
+        self.t.record_client(c, w)
+
+    def record_round(self, idx, w_locals, w_glob):
+        self.t.record_round(idx, w_locals, w_glob)
+
+    def aggregate(self, w_locals, model_state):
+        if not w_locals:
+            return copy.deepcopy(model_state)  # fedavg_trainer.py:442-443
+        return mfl_amd.aggregate(w_locals, device=DEV)
+
+    def fpf_index(self):
+        return self.t.fpf_index()
+
+    def end_round(self, t, idx, itr, w_glob, last_w):
+        self.t.end_round(t, idx, itr, w_glob)
+
+
+class _OracleImpl(_TrackerImpl):
+    def __init__(self, meta, init):
+        weight_size = sum(v.numel() for v in init.values())
+        self.o = FO.FPFOracle(meta["client_num_in_total"], weight_size, meta["comm_round"], meta["threshold"])
+
+    def begin_round(self, last_w):
+        pass
+
+    def record_client(self, c, w, last_w):
+        self.o.record_client(c, w, last_w)
+
+    def aggregate(self, w_locals, model_state):
+        if not w_locals:
+            return copy.deepcopy(model_state)
+        return O.aggregate_torch(w_locals)
+
+    def fpf_index(self):
+        return self.o.fpf_index()
+
+    def end_round(self, t, idx, itr, w_glob, last_w):
+        self.o.end_round(t, idx, itr, w_glob, last_w)
+
+
+def assert_fpf_rows(got, exp):
+    exp = np.asarray(exp, dtype=np.float64)
+    got = np.asarray(got, dtype=np.float64)
+    assert got.shape == exp.shape
+    assert np.array_equal(got == 0, exp == 0), "zero (scrubbed) positions differ"
+    np.testing.assert_allclose(got, exp, rtol=RTOL, atol=0)
+
+
+@pytest.mark.parametrize("after", [False, True], ids=["record_client", "record_round"])
+@pytest.mark.parametrize("name", fpf_replay.case_names())
+def test_fpf_tracker_matches_reference_loop(name, after):
+    case = fpf_replay.load_case(name)
+    impl = _TrackerImpl(case.meta, case.init)
+    got = fpf_replay.replay(case, impl, record_after_aggregate=after)
+    assert_fpf_rows(got, case.fpf)
+
+
+def _random_case(n_total, P, rounds, seed, threshold=FO.THRESHOLD_WEIGHT_SIZE, bn=False):
+    rng = np.random.default_rng(seed)
+    g = torch.Generator().manual_seed(seed)
+    init = OrderedDict(weight=torch.randn(P - 10, generator=g), bias=torch.randn(10, generator=g))
+    if bn:
+        init["num_batches_tracked"] = torch.tensor(5, dtype=torch.int64)
+        init["weight"] = init["weight"][:-1].clone()
+    meta = {"client_num_in_total": n_total, "comm_round": len(rounds), "threshold": threshold, "rounds": []}
+    states = []
+    for t, (K, itr) in enumerate(rounds):
+        idx = sorted(rng.choice(n_total, size=K, replace=False).tolist()) if K <= n_total else list(range(n_total))
+        if t == 2 and K >= 3:
+            idx[-1] = idx[0]  # a duplicate: the later client's row wins (sequential :210 writes)
+        rng.shuffle(idx)
+        meta["rounds"].append({"client_indexes": idx, "local_itr": itr,
+                               "sample_nums": rng.integers(1, 500, size=K).tolist()})
+        # client states are drawn around the initial model; the replay's last_w is the running average
+        round_states = []
+        for _ in range(K):
+            sd = OrderedDict()
+            for k, v in init.items():
+                sd[k] = (v + 1 if v.dtype == torch.int64
+                         else v + 0.05 * torch.randn(v.shape, generator=g) * (1 + t))
+            round_states.append(sd)
+        states.append(round_states)
+    return fpf_replay.FPFCase(meta, init, states, None)
+
+
+def _replay_both(case, after):
+    tr = _TrackerImpl(case.meta, case.init)
+    orc = _OracleImpl(case.meta, case.init)
+    rows_t = fpf_replay.replay(case, tr, record_after_aggregate=after)
+    rows_o = fpf_replay.replay(case, orc)
+    return tr.t, orc.o, rows_t, rows_o
+
+
+ROUNDS = [(20, 2), (35, 3), (12, 1), (40, 0), (1, 5), (64, 2)]
+
+
+@pytest.mark.parametrize("after", [False, True], ids=["record_client", "record_round"])
+def test_fpf_state_vs_oracle_reference_size(after):
+    """1000 vehicles x MNIST-LR (P = 7850), the reference's own FPF2 configuration."""
+    case = _random_case(1000, 7850, ROUNDS, seed=7)
+    t, o, rows_t, rows_o = _replay_both(case, after)
+    assert t.full and o.full
+    assert torch.equal(t.local_w_diffs.cpu(), o.local_w_diffs)  # bit-identical
+    assert torch.equal(t.G_mat.cpu(), o.G_mat)
+    assert torch.equal(t.local_itr_lst.cpu(), o.local_itr_lst)
+    a_t, a_o = t.A_mat.cpu().double().numpy(), o.A_mat.double().numpy()
+    np.testing.assert_allclose(a_t, a_o, rtol=RTOL, atol=RTOL * np.abs(a_o).max())
+    for r in range(len(ROUNDS)):
+        assert_fpf_rows(rows_t[r], rows_o[r])
+
+
+def test_fpf_state_vs_oracle_int_buffer_and_odd_p():
+    case = _random_case(37, 1013, ROUNDS, seed=11, bn=True)
+    t, o, rows_t, rows_o = _replay_both(case, True)
+    assert torch.equal(t.local_w_diffs.cpu(), o.local_w_diffs)
+    assert torch.equal(t.G_mat.cpu(), o.G_mat)
+    for r in range(len(ROUNDS)):
+        assert_fpf_rows(rows_t[r], rows_o[r])
+
+
+def test_fpf_lru_mode_exact():
+    case = _random_case(300, 2000, ROUNDS, seed=3, threshold=1000)
+    t, o, rows_t, rows_o = _replay_both(case, False)
+    assert not t.full and not o.full
+    assert torch.equal(t.LRU_itr_lst.cpu(), o.LRU_itr_lst)
+    assert torch.equal(t.G_mat.cpu(), o.G_mat)
+    assert np.array_equal(rows_t, rows_o)
+
+
+def test_fpf_near_threshold_many_blocks():
+    """P just under THRESHOLD_WEIGHT_SIZE: multi-block mean partials, 1000 rows."""
+    case = _random_case(1000, 99_990, [(50, 2), (100, 1), (30, 3)], seed=5)
+    t, o, rows_t, rows_o = _replay_both(case, True)
+    assert torch.equal(t.local_w_diffs.cpu(), o.local_w_diffs)
+    a_t, a_o = t.A_mat.cpu().double().numpy(), o.A_mat.double().numpy()
+    np.testing.assert_allclose(a_t, a_o, rtol=RTOL, atol=RTOL * np.abs(a_o).max())
+    for r in range(3):
+        assert_fpf_rows(rows_t[r], rows_o[r])
+
+
+def test_fpf_errors_like_reference():
+    init = OrderedDict(weight=torch.zeros(10, 5), bias=torch.zeros(10))
+    t = mfl_amd.FPFTracker(8, init, 3, device=DEV)
+    t.begin_round(init)
+    with pytest.raises(IndexError):
+        t.record_client(8, init)  # local_w_diffs[8] with 8 rows (:210)
+    t.record_client(-1, init)  # negative indexes wrap like torch's
+    with pytest.raises(IndexError):
+        t.end_round(3, [0], 1, init)  # local_itr_lst[3] with comm_round = 3 (:322)
+    with pytest.raises(IndexError):
+        t.end_round(0, [9], 1, init)
+    with pytest.raises(ValueError):
+        t.record_round([0], [(1, copy.deepcopy(init))], init)  # no device rows of this round
+    with pytest.raises(NotImplementedError):
+        mfl_amd.FPFTracker(8, OrderedDict(w=torch.zeros(3, dtype=torch.float64)), 3, device=DEV)
+    tb = mfl_amd.FPFTracker(8, OrderedDict(w=torch.zeros(3), m=torch.zeros(2, dtype=torch.bool)), 3, device=DEV)
+    tb.begin_round(OrderedDict(w=torch.zeros(3), m=torch.zeros(2, dtype=torch.bool)))
+    with pytest.raises(RuntimeError):
+        tb.record_client(0, OrderedDict(w=torch.ones(3), m=torch.ones(2, dtype=torch.bool)))

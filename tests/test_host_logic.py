@@ -230,3 +230,12 @@ def test_native_collect_falls_back_for_unusual_clients(case):
     else:
         with pytest.raises(err):
             table.collect([a, b])
+
+
+def test_fpf_tracker_without_gpu_fails_loudly():
+    import mfl_amd
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(mfl_amd.FedAvgLibraryError):
+        mfl_amd.FPFTracker(4, {"w": torch.zeros(3)}, 2)

@@ -109,3 +109,51 @@ def test_distance_with_bool_buffer_raises_like_reference():
     w_glob = O.aggregate_torch(w_locals)
     with pytest.raises(RuntimeError):
         O.client_distances_torch(w_locals, w_glob)
+
+
+# ---------------------------------------------------------------------------
+# FPF2 bookkeeping (fedavg_trainer.py:108-119, 210, 271-278, 314-327)
+import fpf_oracle as FO  # noqa: E402
+import fpf_replay  # noqa: E402
+
+FPF_CASES = fpf_replay.case_names()
+
+
+class _OracleImpl:
+    def __init__(self, case):
+        m = case.meta
+        self.o = FO.FPFOracle(m["client_num_in_total"], m["weight_size"], m["comm_round"], m["threshold"])
+
+    def begin_round(self, last_w):
+        pass
+
+    def record_client(self, c, w, last_w):
+        self.o.record_client(c, w, last_w)
+
+    def aggregate(self, w_locals, model_state):
+        if not w_locals:
+            return copy.deepcopy(model_state)  # fedavg_trainer.py:442-443
+        return O.aggregate_torch(w_locals)
+
+    def fpf_index(self):
+        return self.o.fpf_index()
+
+    def end_round(self, t, idx, itr, w_glob, last_w):
+        self.o.end_round(t, idx, itr, w_glob, last_w)
+
+
+def test_fpf_golden_present():
+    assert {"lr_full", "bn_full", "lr_lru"} <= set(FPF_CASES)
+
+
+@pytest.mark.parametrize("name", FPF_CASES)
+def test_fpf_oracle_matches_reference_loop(name):
+    """The restatement reproduces the reference train() loop's FPF CSV bit for bit."""
+    case = fpf_replay.load_case(name)
+    got = fpf_replay.replay(case, _OracleImpl(case))
+    assert got.shape == case.fpf.shape
+    assert np.array_equal(got.astype(np.float64), case.fpf)
+    assert case.meta["full"] == (name != "lr_lru")
+    if case.meta["full"]:
+        # empty round 6 -> A_mat NaN (0/0 at :319) -> every later index scrubbed to 0
+        assert np.count_nonzero(case.fpf[6]) > 0 and not np.any(case.fpf[7])
