@@ -128,11 +128,15 @@ def sampled_parity(red: ShardedReducer, weights, n_windows=6, width=2048):
     rng = np.random.default_rng(7)
     checked = 0
     for _ in range(n_windows):
-        lstart, _g, n = segs[int(rng.integers(0, len(segs)))]
+        lstart, gstart, n = segs[int(rng.integers(0, len(segs)))]
         w = min(width, n)
         s = lstart + int(rng.integers(0, n - w + 1))
         exp = O.reduce_f32(red.clients[:, s:s + w].cpu().numpy(), weights)
         got = red.local_out[s:s + w].cpu().numpy()
+        if red.host_out is not None:  # the copy the host consumer reads
+            g = gstart + (s - lstart)
+            if red.host_out[g:g + w].numpy().tobytes() != got.tobytes():
+                return {"ok": False, "columns_checked": checked, "bar": "host_out == device shard"}
         if got.tobytes() != exp.tobytes():
             return {"ok": False, "columns_checked": checked, "bar": "bit-exact vs oracle"}
         checked += w
@@ -152,6 +156,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--graph", action="store_true", help="N=1: replay each step from a captured hipGraph")
     ap.add_argument("--traffic-json", default="", help="PMC traffic summary (profiles/*.json) to attach")
+    ap.add_argument("--host-out", action="store_true",
+                    help="host consumer (SURVEY 8e): D2H each rank's shard into pinned host memory, no collective")
     args = ap.parse_args()
 
     world = env_int("WORLD_SIZE", 1)
@@ -175,10 +181,11 @@ def main():
     mfl_amd._lib.load()
 
     K, P_local, desc = WORKLOADS[args.workload]
-    chunks = args.chunks or (1 if world == 1 else 4)
+    chunks = args.chunks or (1 if world == 1 and not args.host_out else 4)
     P_total = P_local * world
+    host_out = torch.empty(P_total, dtype=torch.float32, pin_memory=True) if args.host_out else None
     # Each rank owns exactly P_local valid columns: plan over the global P.
-    red = ShardedReducer(K, P_total, chunks=chunks, device=dev, gather=not args.no_gather)
+    red = ShardedReducer(K, P_total, chunks=chunks, device=dev, gather=not args.no_gather, host_out=host_out)
     fill_synthetic(red.clients, rank)
     counts = sample_counts(K)
     weights = mfl_amd.sample_weights(counts)
@@ -317,8 +324,9 @@ def main():
                 "P_per_gpu": P_local,
                 "P_total": P_total,
                 "chunks": chunks,
-                "exchange": ("rccl all_gather_into_tensor, overlapped per chunk"
-                             if red.gather else "none (single GPU or --no-gather)"),
+                "exchange": ("rccl all_gather_into_tensor, overlapped per chunk" if red.gather else
+                             "none: each rank D2Hs its shard chunks into pinned host memory (host consumer)"
+                             if host_out is not None else "none (single GPU or --no-gather)"),
                 "parallelism": f"p-shard{world}",
                 "kernel_variant": {"unroll": tuned[0], "nt": tuned[1]} if tuned else "default",
                 "launch": "hipGraph replay" if args.graph else "eager (stream-ordered)",

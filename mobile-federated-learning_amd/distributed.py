@@ -105,11 +105,18 @@ class ShardedReducer:
 
     ``local_reduce`` is injectable so the sharding/gather logic can be tested
     with the ``gloo`` backend on CPU; the product default is the HIP kernel.
+
+    ``host_out`` (SURVEY §8e's alternative for a host consumer): a pinned
+    host tensor of >= P elements -- e.g. one mapping shared by all ranks of
+    the node.  Each rank then copies its finished chunks straight to their
+    global positions in it (D2H on a side stream, overlapped with the next
+    chunk's reduce) and no collective runs: the consumer of
+    ``fedavg_trainer.py:219`` is host memory anyway.
     """
 
     def __init__(self, K: int, P: int, *, chunks: int = 1, group=None, device=None,
                  dtype: torch.dtype = torch.float32, local_reduce: Optional[LocalReduce] = None,
-                 gather: bool = True):
+                 gather: bool = True, host_out: Optional[torch.Tensor] = None):
         self.group = group
         ws = dist.get_world_size(group) if dist.is_initialized() else 1
         rank = dist.get_rank(group) if dist.is_initialized() else 0
@@ -118,7 +125,20 @@ class ShardedReducer:
         self.dtype = dtype
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.local_reduce = local_reduce or _hip_local_reduce
+        self.host_out = host_out
+        if host_out is not None:
+            if host_out.device.type != "cpu" or host_out.dtype != dtype or host_out.numel() < P:
+                raise ValueError(f"host_out must be a host {dtype} tensor of >= {P} elements")
+            if self.device.type == "cuda" and not host_out.is_pinned():
+                raise ValueError("host_out must be pinned (async D2H)")
+            gather = False
         self.gather = gather and ws > 1
+        self._copy_stream = (torch.cuda.Stream(self.device)
+                             if host_out is not None and self.device.type == "cuda" else None)
+        # per chunk: (local start, global start, n) of its valid columns
+        S = self.plan.block
+        self._chunk_segments = [[(l, g, n) for l, g, n in self.plan.local_segments() if c * S <= l < (c + 1) * S]
+                                for c in range(self.plan.chunks)]
         self.clients = torch.empty((K, self.plan.local_cols), dtype=dtype, device=self.device)
         self.local_out = torch.empty(self.plan.local_cols, dtype=dtype, device=self.device)
         self.full = (torch.empty(self.plan.padded_P, dtype=dtype, device=self.device)
@@ -145,9 +165,26 @@ class ShardedReducer:
             if self.gather:
                 dst = self.full[c * plan.world_size * S:(c + 1) * plan.world_size * S]
                 works.append(dist.all_gather_into_tensor(dst, out_c, group=self.group, async_op=True))
+            elif self.host_out is not None:
+                self._to_host(c)
         for w in works:
             w.wait()
+        if self._copy_stream is not None:
+            self._copy_stream.synchronize()
+        if self.host_out is not None:
+            return self.host_out[:plan.P]
         return self.full[:plan.P] if self.gather else None
+
+    def _to_host(self, c: int) -> None:
+        segs = self._chunk_segments[c]
+        if self._copy_stream is None:  # CPU (gloo tests): plain copies
+            for l, g, n in segs:
+                self.host_out[g:g + n].copy_(self.local_out[l:l + n])
+            return
+        self._copy_stream.wait_stream(torch.cuda.current_stream(self.device))  # chunk c is reduced
+        with torch.cuda.stream(self._copy_stream):
+            for l, g, n in segs:
+                self.host_out[g:g + n].copy_(self.local_out[l:l + n], non_blocking=True)
 
     def local_model_columns(self):
         """(local_out views, global ranges) of the valid columns this rank reduced."""

@@ -78,3 +78,51 @@ def test_shard_plan_partitions_columns(P, ws, chunks):
             assert lstart % 64 == 0 and lstart + n <= plan.local_cols
             owned[gstart:gstart + n] += 1
     assert (owned == 1).all()
+
+
+def _worker_host_out(rank, ws, port, K, P, chunks, seed, q):
+    """SURVEY §8e host-consumer alternative: every rank D2Hs its shard into a
+    host output at global positions; no collective.  Ranks send their host
+    buffers back and the test merges them (in production one shared mapping)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        rng = np.random.default_rng(seed)
+        host = torch.from_numpy(rng.normal(0, 0.05, size=(K, P)).astype(np.float32))
+        n = rng.integers(1, 1000, size=K)
+        w = torch.tensor(np.array(O.sample_weights([int(v) for v in n]), np.float64).astype(np.float32))
+        host_out = torch.full((P,), float("nan"))
+        red = ShardedReducer(K, P, chunks=chunks, device="cpu", local_reduce=_torch_loop_reduce, host_out=host_out)
+        assert not red.gather
+        red.load_from_host(host)
+        got = red.step(w)
+        assert got.data_ptr() == host_out.data_ptr()
+        q.put((rank, host_out.numpy().copy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("ws,K,P,chunks", [(2, 5, 1001, 1), (3, 4, 4099, 3)])
+def test_sharded_reduce_host_out_matches_oracle(ws, K, P, chunks):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    seed = 23 + P
+    procs = [ctx.Process(target=_worker_host_out, args=(r, ws, port, K, P, chunks, seed, q)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    parts = dict(q.get(timeout=120) for _ in range(ws))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    merged = np.full(P, np.nan, dtype=np.float32)
+    for r in range(ws):
+        for _, g, n in plan_shards(P, ws, r, chunks).local_segments():
+            assert not np.isnan(parts[r][g:g + n]).any()
+            merged[g:g + n] = parts[r][g:g + n]
+    rng = np.random.default_rng(seed)
+    host = rng.normal(0, 0.05, size=(K, P)).astype(np.float32)
+    n = rng.integers(1, 1000, size=K)
+    expect = O.reduce_f32(host, O.sample_weights([int(v) for v in n]))
+    assert merged.tobytes() == expect.tobytes()

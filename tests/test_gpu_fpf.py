@@ -104,7 +104,8 @@ def _random_case(n_total, P, rounds, seed, threshold=FO.THRESHOLD_WEIGHT_SIZE, b
     meta = {"client_num_in_total": n_total, "comm_round": len(rounds), "threshold": threshold, "rounds": []}
     states = []
     for t, (K, itr) in enumerate(rounds):
-        idx = sorted(rng.choice(n_total, size=K, replace=False).tolist()) if K <= n_total else list(range(n_total))
+        K = min(K, n_total)
+        idx = sorted(rng.choice(n_total, size=K, replace=False).tolist())
         if t == 2 and K >= 3:
             idx[-1] = idx[0]  # a duplicate: the later client's row wins (sequential :210 writes)
         rng.shuffle(idx)

@@ -295,6 +295,23 @@ def test_sharded_reducer_single_rank_chunks():
     assert_bits(got, torch.from_numpy(exp))
 
 
+def test_sharded_reducer_host_out():
+    """SURVEY 8e host-consumer form: chunks D2H'd into pinned host memory, no collective."""
+    from mfl_amd.distributed import ShardedReducer
+    K, P = 9, 250_001
+    host = torch.randn((K, P)) * 0.05
+    w = _weights(K)
+    out = torch.full((P,), float("nan"), pin_memory=True)
+    red = ShardedReducer(K, P, chunks=4, device=DEV, host_out=out)
+    red.load_from_host(host)
+    for _ in range(2):  # second step rewrites the same host buffer
+        got = red.step(_w(w))
+        assert got.data_ptr() == out.data_ptr()
+        assert_bits(got.clone(), torch.from_numpy(O.reduce_f32(host.numpy(), w)))
+    with pytest.raises(ValueError):
+        ShardedReducer(K, P, device=DEV, host_out=torch.empty(P))  # not pinned
+
+
 def test_round_session_streaming_matches_golden():
     for name in ["mnist_lr_k100", "resnet_like_bn_k5", "int_dtypes_k3", "float64_key_k3", "bfloat16_key_k3"]:
         meta, w_locals, expected = load_case(name)
