@@ -36,7 +36,7 @@ import torch
 
 from . import _lib
 from .layout import KeyTable
-from .reduce import reduce_packed, weights_tensor
+from .reduce import weights_tensor
 
 __all__ = ["RoundSession"]
 
@@ -102,7 +102,7 @@ class RoundSession:
             raise ValueError("no clients added (the reference returns the global model then: use aggregate([]))")
         K = len(self.counts)
         acc_dict = w_locals[0][1] if w_locals is not None else OrderedDict()
-        from .aggregate import sample_weights
+        from .aggregate import reduce_and_fetch, sample_weights
 
         weights = sample_weights(self.counts)  # ZeroDivisionError like the reference
         outs = []
@@ -111,11 +111,11 @@ class RoundSession:
             self._compute.wait_stream(self._copy)
             for g in self.table.groups.values():
                 st = self._staging[g.dtype]
-                out_dev = reduce_packed(st.dev[:K], weights_tensor(weights, g.dtype, self.dev), g.P)
-                out_host = torch.empty(g.P, dtype=g.dtype, pin_memory=True)
-                out_host.copy_(out_dev, non_blocking=True)
+                out_dev, out_host = reduce_and_fetch(st.dev[:K], weights_tensor(weights, g.dtype, self.dev), g.P,
+                                                     self._copy)
                 outs.append((g, out_host))
                 dev_state[g.dtype] = (st.dev[:K], out_dev)
+            self._copy.synchronize()
             self._compute.synchronize()
         for g, out_host in outs:
             for name, t in self.table.unpack(g, out_host).items():

@@ -312,6 +312,33 @@ def test_sharded_reducer_host_out():
         ShardedReducer(K, P, device=DEV, host_out=torch.empty(P))  # not pinned
 
 
+@pytest.mark.parametrize("P", [4_194_304 + 3, 17_000_021])
+def test_aggregate_chunked_fetch_bit_exact(P):
+    """P >= 2 x D2H_CHUNK_MIN_COLS: the reduce runs in column chunks with the
+    D2H of chunk c overlapping the reduce of chunk c+1 (aggregate and session)."""
+    from collections import OrderedDict
+
+    K = 3
+    g = torch.Generator().manual_seed(P)
+    base = torch.randn(P, generator=g) * 0.05
+    dicts = [OrderedDict(a=(base[:1000] + 1e-3 * torch.randn(1000, generator=g)).reshape(10, 100),
+                         b=base[1000:] + 1e-3 * torch.randn(P - 1000, generator=g)) for _ in range(K)]
+    counts = [17, 400, 3]
+    w = O.sample_weights(counts)
+    flat = np.stack([torch.cat([d["a"].reshape(-1), d["b"]]).numpy() for d in dicts])
+    exp = torch.from_numpy(O.reduce_f32(flat, w))
+    agg = mfl_amd.DeviceAggregator(DEV)
+    wl = [(n, OrderedDict(d)) for n, d in zip(counts, dicts)]
+    out = agg.aggregate(wl)
+    assert_bits(torch.cat([out["a"].reshape(-1), out["b"]]), exp)
+    sess = agg.begin_round(dicts[0], K)
+    wl2 = [(n, OrderedDict(d)) for n, d in zip(counts, dicts)]
+    for n, d in wl2:
+        sess.add(n, d)
+    out2 = sess.finish(wl2)
+    assert_bits(torch.cat([out2["a"].reshape(-1), out2["b"]]), exp)
+
+
 def test_round_session_streaming_matches_golden():
     for name in ["mnist_lr_k100", "resnet_like_bn_k5", "int_dtypes_k3", "float64_key_k3", "bfloat16_key_k3"]:
         meta, w_locals, expected = load_case(name)
