@@ -107,26 +107,34 @@ D2H_CHUNK_MIN_COLS = 2 << 20
 D2H_MAX_CHUNKS = 8
 
 
-def reduce_and_fetch(devbuf: torch.Tensor, w_dev: torch.Tensor, P: int, copy_stream) -> Tuple[torch.Tensor,
-                                                                                             torch.Tensor]:
-    """Reduce ``devbuf`` [K, ld] on the current stream and copy the result to a
-    new pinned host buffer on ``copy_stream``, chunk by chunk.  Returns
-    ``(out_dev, out_host)``; the caller synchronizes ``copy_stream``."""
+def column_chunks(P: int) -> List[Tuple[int, int]]:
+    """Column ranges the averaged model is reduced and fetched in (256-B aligned starts)."""
+    n = max(1, min(D2H_MAX_CHUNKS, P // D2H_CHUNK_MIN_COLS))
+    step = -(-P // n)
+    step = -(-step // 64) * 64
+    return [(c0, min(P, c0 + step)) for c0 in range(0, P, step)] or [(0, 0)]
+
+
+def reduce_and_fetch(devbuf: torch.Tensor, w_dev: torch.Tensor, P: int, d2h_stream,
+                     ready: Optional[Sequence] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Reduce ``devbuf`` [K, ld] on the current stream in ``column_chunks(P)``
+    and copy each chunk to a new pinned host buffer on ``d2h_stream`` as soon
+    as it is reduced.  ``ready[c]`` (optional): an event after which chunk c's
+    input columns are in HBM -- the reduce of chunk c then waits only for
+    that, so the last client's H2D, the reduce and the D2H pipeline.
+    Returns ``(out_dev, out_host)``; the caller synchronizes ``d2h_stream``."""
     dev = devbuf.device
     compute = torch.cuda.current_stream(dev)
     out_dev = torch.empty(P, dtype=devbuf.dtype, device=dev)
     out_host = torch.empty(P, dtype=devbuf.dtype, pin_memory=True)
-    n = max(1, min(D2H_MAX_CHUNKS, P // D2H_CHUNK_MIN_COLS))
-    step = -(-P // n)
-    step = -(-step // 64) * 64  # 256-B aligned column offsets for the vector kernels
-    c0 = 0
-    while c0 < P:
-        c1 = min(P, c0 + step)
-        reduce_packed(devbuf[:, c0:c1] if P > step else devbuf, w_dev, c1 - c0, out_dev[c0:c1])
-        copy_stream.wait_stream(compute)
-        with torch.cuda.stream(copy_stream):
+    chunks = column_chunks(P)
+    for c, (c0, c1) in enumerate(chunks):
+        if ready is not None:
+            compute.wait_event(ready[c])
+        reduce_packed(devbuf[:, c0:c1] if len(chunks) > 1 else devbuf, w_dev, c1 - c0, out_dev[c0:c1])
+        d2h_stream.wait_stream(compute)
+        with torch.cuda.stream(d2h_stream):
             out_host[c0:c1].copy_(out_dev[c0:c1], non_blocking=True)
-        c0 = c1
     return out_dev, out_host
 
 
@@ -159,6 +167,7 @@ class DeviceAggregator:
         _lib.load()  # fail loudly and early if the HIP library is missing
         self._staging: Dict[torch.dtype, _Staging] = {}
         self._copy_stream = None
+        self._d2h_stream = None
         self.last_profile: Dict[str, float] = {}
         # device state of the last aggregate call (client rows + averaged model per
         # dtype group), reused by client_distances for the same round
@@ -188,6 +197,12 @@ class DeviceAggregator:
         if self._copy_stream is None:
             self._copy_stream = torch.cuda.Stream(self.device)
         return self._copy_stream
+
+    def _d2h_stream_for(self):
+        # its own stream: PCIe is full duplex, so result D2H runs beside pending H2D
+        if self._d2h_stream is None:
+            self._d2h_stream = torch.cuda.Stream(self.device)
+        return self._d2h_stream
 
     def _staging_for(self, dtype: torch.dtype, K: int, ld: int) -> _Staging:
         st = self._staging.get(dtype)
@@ -251,11 +266,12 @@ class DeviceAggregator:
             t1 = time.perf_counter()
             outs = []
             self._last = {"table": table, "K": K, "dev": {}}
+            d2h = self._d2h_stream_for()
             for g, devbuf, w_dev in staged:
-                out_dev, out_host = reduce_and_fetch(devbuf, w_dev, g.P, copy_s)
+                out_dev, out_host = reduce_and_fetch(devbuf, w_dev, g.P, d2h)
                 outs.append((g, out_host))
                 self._last["dev"][g.dtype] = (devbuf, out_dev)
-            copy_s.synchronize()
+            d2h.synchronize()
             compute.synchronize()
             t2 = time.perf_counter()
         for g, out_host in outs:

@@ -63,6 +63,12 @@ class RoundSession:
             self._copy.wait_stream(self._compute)
         self._staging = {g.dtype: aggregator._staging_for(g.dtype, max_clients, g.ld)
                          for g in self.table.groups.values()}
+        from .aggregate import column_chunks
+
+        # each row is uploaded in the column chunks finish() reduces in; the
+        # events of the latest add tell finish() when chunk c is complete
+        self._chunks = {g.dtype: column_chunks(g.P) for g in self.table.groups.values()}
+        self._ready = {}
         self.add_ms = 0.0
 
     def add(self, sample_num, state_dict: Mapping[str, torch.Tensor]) -> None:
@@ -79,8 +85,14 @@ class RoundSession:
             items = self.table.pack_items(g, ptrs, i, g.ld)
             _lib.check(self._lib.fedavg_pack_rows(items.ctypes.data, items.shape[0], st.host.data_ptr(),
                                                   st.host.element_size(), self._threads), "fedavg_pack_rows")
+            events = []
             with torch.cuda.stream(self._copy):
-                st.dev[i].copy_(st.host[i], non_blocking=True)
+                for c0, c1 in self._chunks[g.dtype]:
+                    st.dev[i, c0:c1].copy_(st.host[i, c0:c1], non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record(self._copy)
+                    events.append(ev)
+            self._ready[g.dtype] = events  # the copy stream is FIFO: covers earlier rows too
         self.counts.append(sample_num)
         self.dicts.append(state_dict)
         if keep:
@@ -108,15 +120,16 @@ class RoundSession:
         outs = []
         dev_state = {}
         with torch.cuda.device(self.dev):
-            self._compute.wait_stream(self._copy)
+            d2h = self.agg._d2h_stream_for()
             for g in self.table.groups.values():
                 st = self._staging[g.dtype]
                 out_dev, out_host = reduce_and_fetch(st.dev[:K], weights_tensor(weights, g.dtype, self.dev), g.P,
-                                                     self._copy)
+                                                     d2h, ready=self._ready[g.dtype])
                 outs.append((g, out_host))
                 dev_state[g.dtype] = (st.dev[:K], out_dev)
-            self._copy.synchronize()
+            d2h.synchronize()
             self._compute.synchronize()
+            self._compute.wait_stream(self._copy)  # nothing else may reuse the staging before its copies end
         for g, out_host in outs:
             for name, t in self.table.unpack(g, out_host).items():
                 acc_dict[name] = t
