@@ -64,6 +64,15 @@ int fedavg_reduce_f32_variant(const float* clients, int64_t K, int64_t P, int64_
 int fedavg_reduce_tiled_f32(const float* tiles, int64_t K, int64_t P, const float* weights,
                             float* out, int unroll, void* stream);
 
+/*
+ * Test hook: out[i] = in[i] (fp32 bit pattern) rounded to 16 bits by the
+ * production kernels' element rule -- mode 0: bf16, packed hardware RNE
+ * (v_cvt_pk_bf16_f32); 1: bf16, c10's integer round_to_nearest_even;
+ * 2: fp16, packed hardware (v_cvt_pk_f16_f32); 3: fp16, scalar
+ * v_cvt_f16_f32.  Lets the GPU tests compare the rules over all 2^32 inputs.
+ */
+int fedavg_probe_cvt16(const uint32_t* in, int64_t n, int mode, uint16_t* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

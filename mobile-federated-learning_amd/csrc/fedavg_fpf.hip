@@ -19,7 +19,7 @@
 namespace {
 using namespace fedavg_impl;
 
-constexpr int kFpfRowsPerBlock = 16;
+constexpr int kFpfRowsPerBlock = 4;
 constexpr int kFpfMaxPartials = 1024;
 
 __device__ __forceinline__ f32x4 masked(f32x4 v, int nv) {

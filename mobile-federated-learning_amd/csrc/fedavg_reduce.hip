@@ -204,6 +204,91 @@ struct OpF64 {
     const vec t = x * w;
     return acc + t;
   }
+  __device__ static vec finish(vec a) { return a; }
+};
+
+// Packed 16-bit rules: two elements per 32-bit word, fp32 math on pairs
+// (v_pk_mul_f32 / v_pk_add_f32) and gfx950's two-at-a-time round-to-nearest-
+// even conversions (v_cvt_pk_bf16_f32 / v_cvt_pk_f16_f32) -- about 5 VALU ops
+// per element and client instead of ~14 for the integer bf16 rounding, which
+// made the kernel ALU-bound.  For every non-NaN input the hardware rounding
+// equals c10's (checked over all 2^32 fp32 patterns, tests/test_gpu_parity.py
+// via fedavg_probe_cvt16); NaN is absorbing through the remaining mul/add
+// steps, so canonicalising NaN to c10's 0x7FC0 once at the store (bf16) gives
+// c10's bits for the whole reduction.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x2 opaque2(f32x2 v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
+struct BF16Pk {
+  __device__ static f32x2 unpack(unsigned int u) {
+    return f32x2{__uint_as_float(u << 16), __uint_as_float(u & 0xFFFF0000u)};
+  }
+  __device__ static unsigned int pack(f32x2 f) {
+    const bf16x2 b = __builtin_convertvector(f, bf16x2);
+    unsigned int u;
+    __builtin_memcpy(&u, &b, 4);
+    return u;
+  }
+  __device__ static unsigned short canon(unsigned short h) { return (h & 0x7FFFu) > 0x7F80u ? 0x7FC0u : h; }
+};
+
+struct F16Pk {
+  __device__ static f32x2 unpack(unsigned int u) {
+    f16x2 h;
+    __builtin_memcpy(&h, &u, 4);
+    return __builtin_convertvector(h, f32x2);
+  }
+  __device__ static unsigned int pack(f32x2 f) {
+    const f16x2 h = __builtin_convertvector(f, f16x2);
+    unsigned int u;
+    __builtin_memcpy(&u, &h, 4);
+    return u;
+  }
+  __device__ static unsigned short canon(unsigned short h) { return h; }  // NaN payloads are not specified
+};
+
+template <typename R>
+struct OpHalfPk {
+  using vec = u16x8;
+  using wt = float;
+  using elem = unsigned short;
+  static constexpr int kLanes = 8;
+  __device__ static vec first(vec x, wt w) {
+    u32x4 xu, r;
+    __builtin_memcpy(&xu, &x, 16);
+    const f32x2 w2{w, w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) r[j] = R::pack(opaque2(R::unpack(xu[j]) * w2));
+    vec o;
+    __builtin_memcpy(&o, &r, 16);
+    return o;
+  }
+  __device__ static vec step(vec acc, vec x, wt w) {
+    u32x4 xu, au;
+    __builtin_memcpy(&xu, &x, 16);
+    __builtin_memcpy(&au, &acc, 16);
+    const f32x2 w2{w, w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const unsigned int t = R::pack(opaque2(R::unpack(xu[j]) * w2));       // fl16(x*w)
+      au[j] = R::pack(opaque2(R::unpack(au[j]) + R::unpack(t)));             // fl16(acc + t)
+    }
+    vec o;
+    __builtin_memcpy(&o, &au, 16);
+    return o;
+  }
+  __device__ static vec finish(vec a) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] = R::canon(a[j]);
+    return a;
+  }
 };
 
 template <typename R>
@@ -223,6 +308,7 @@ struct OpHalf {
     for (int j = 0; j < 8; ++j) acc[j] = half_step<R>(acc[j], x[j], w, false);
     return acc;
   }
+  __device__ static vec finish(vec a) { return a; }
 };
 
 template <class Op, int U, int C, bool NT>
@@ -256,6 +342,7 @@ __device__ __forceinline__ void reduce_vec_group(typename Op::vec (&acc)[C], con
 template <class Op>
 __device__ __forceinline__ void store_vec(typename Op::elem* out, int64_t v, int64_t nvec, int tail,
                                           typename Op::vec a) {
+  a = Op::finish(a);
   typename Op::elem* o = out + v * Op::kLanes;
   if (tail == 0 || v != nvec - 1) {
     *reinterpret_cast<typename Op::vec*>(o) = a;
@@ -495,6 +582,25 @@ void launch_vec_nt(const Schedule& sc, const void* clients, int K, int64_t ld, i
   }
 }
 
+// Conversion probe (tests only): out[i] = the 16-bit rounding of the fp32
+// bit pattern in[i] by mode 0 = BF16Pk (hardware), 1 = c10 integer RNE,
+// 2 = F16Pk (hardware, packed), 3 = F16Rule (scalar v_cvt_f16_f32).
+__global__ __launch_bounds__(kBlock) void probe_cvt16_kernel(const unsigned int* __restrict__ in, int64_t n,
+                                                            int mode, unsigned short* __restrict__ out) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const float f = __uint_as_float(in[i]);
+  const f32x2 f2{f, 0.f};
+  unsigned short h;
+  switch (mode) {
+    case 0: h = static_cast<unsigned short>(BF16Pk::pack(opaque2(f2)) & 0xFFFFu); break;
+    case 1: h = BF16Rule::from_f32(opaque(f)); break;
+    case 2: h = static_cast<unsigned short>(F16Pk::pack(opaque2(f2)) & 0xFFFFu); break;
+    default: h = F16Rule::from_f32(opaque(f)); break;
+  }
+  out[i] = h;
+}
+
 // elem_bytes: 8 (fp64) or 2 (fp16/bf16).  The fp32 schedule is chosen for the
 // problem with the same 16-B slice count and byte footprint.
 template <class Op>
@@ -516,6 +622,15 @@ void launch_production_vec(const void* clients, int K, int64_t ld, int64_t P, co
 extern "C" {
 
 int fedavg_abi_version(void) { return 1; }
+
+int fedavg_probe_cvt16(const uint32_t* in, int64_t n, int mode, uint16_t* out, void* stream) {
+  if (n < 0 || !in || !out || mode < 0 || mode > 3)
+    return set_error(FEDAVG_EINVAL, "fedavg_probe_cvt16: bad arguments");
+  if (n == 0) return FEDAVG_OK;
+  hipLaunchKernelGGL(probe_cvt16_kernel, dim3(static_cast<unsigned>((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                     static_cast<hipStream_t>(stream), in, n, mode, out);
+  return launch_status("fedavg_probe_cvt16");
+}
 
 const char* fedavg_last_error(void) { return last_error_message(); }
 
@@ -595,9 +710,9 @@ static int reduce_half_entry(bool bf16, const uint16_t* clients, int64_t K, int6
   const bool vec = aligned16(clients) && aligned16(out) && (ld % 8) == 0;
   if (vec) {
     if (bf16)
-      launch_production_vec<OpHalf<BF16Rule>>(clients, static_cast<int>(K), ld, P, weights, out, s);
+      launch_production_vec<OpHalfPk<BF16Pk>>(clients, static_cast<int>(K), ld, P, weights, out, s);
     else
-      launch_production_vec<OpHalf<F16Rule>>(clients, static_cast<int>(K), ld, P, weights, out, s);
+      launch_production_vec<OpHalfPk<F16Pk>>(clients, static_cast<int>(K), ld, P, weights, out, s);
     return launch_status(what);
   }
   const int64_t items = P;

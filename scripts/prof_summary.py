@@ -1,6 +1,6 @@
 """Summarise rocprofv3 output of scripts/gpu_check.sh into profiles/.
 
-    python scripts/prof_summary.py gpurun_out/<tag> --round r01 --workload target --K 100 --P 25000000
+    python scripts/prof_summary.py gpurun_out/<tag> --round r01 --workload target --K 100 --P 25000000 --launches 4
 
 Reads (recursively) the ``*_kernel_stats.csv`` of the ``--kernel-trace
 --stats`` pass and the ``*_counter_collection.csv`` of the two separate PMC

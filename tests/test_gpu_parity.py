@@ -235,6 +235,59 @@ def test_reduce_half_exact(kind, K, P):
     assert_bits(out, exp, kind)
 
 
+@pytest.mark.parametrize("kind", ["float16", "bfloat16"])
+@pytest.mark.parametrize("K,P", [(7, 4099), (40, 70_001)])
+def test_reduce_half_adversarial_bit_patterns(kind, K, P):
+    """Random 16-bit patterns: subnormals, near-overflow, +-inf, NaNs of every
+    payload and sign.  Bit-exact vs the oracle; NaN positions must match, and
+    for bf16 every NaN is c10's canonical 0x7FC0 (the packed kernel
+    canonicalises at the store)."""
+    dt = torch.float16 if kind == "float16" else torch.bfloat16
+    rng = np.random.default_rng(P + K)
+    ld = (P + 63) // 64 * 64
+    bits = rng.integers(0, 1 << 16, size=(K, ld), dtype=np.uint16)
+    # keep most lanes finite so that not every column ends up NaN
+    expo_mask = np.uint16(0x7C00 if kind == "float16" else 0x7F80)
+    special = rng.random((K, ld)) < 0.9
+    bits[special & ((bits & expo_mask) == expo_mask)] ^= np.uint16(0x4000)
+    x = torch.from_numpy(bits.view(np.int16)).view(dt).to(DEV)
+    w = _weights(K)
+    out = mfl_amd.reduce_packed(x, _w(w), P)
+    xs = x[:, :P].cpu()
+    if kind == "float16":
+        exp = torch.from_numpy(O.reduce_half(xs.numpy(), w, kind))
+    else:
+        eb = O.reduce_half(xs.view(torch.int16).numpy(), w, kind)
+        exp = torch.from_numpy(eb.view(np.int16).copy()).view(torch.bfloat16)
+        got_bits = out.cpu().view(torch.int16).numpy().view(np.uint16)
+        nan = np.isnan(O.bf16_bits_to_f32(got_bits))
+        assert nan.any() and (got_bits[nan] == 0x7FC0).all()
+    assert_bits(out, exp, kind)
+
+
+def test_cvt16_hardware_rounding_equals_c10_all_fp32_inputs():
+    """The packed kernels round with v_cvt_pk_bf16_f32 / v_cvt_pk_f16_f32.
+    Over all 2^32 fp32 bit patterns: bf16 equals c10's integer
+    round_to_nearest_even and fp16 the scalar v_cvt_f16_f32, for every
+    non-NaN input (subnormals and overflow included); NaN stays NaN."""
+    lib = mfl_amd._lib.load()
+    n = 1 << 28
+    a = torch.empty(n, dtype=torch.int16, device=DEV)
+    b = torch.empty(n, dtype=torch.int16, device=DEV)
+    stream = torch.cuda.current_stream(DEV).cuda_stream
+    for chunk in range(16):
+        inp = torch.arange(chunk * n, (chunk + 1) * n, dtype=torch.int64, device=DEV).to(torch.int32)
+        nan_in = ((inp & 0x7F800000) == 0x7F800000) & ((inp & 0x7FFFFF) != 0)
+        for hw, ref, expo, mant in [(0, 1, 0x7F80, 0x7F), (2, 3, 0x7C00, 0x3FF)]:
+            mfl_amd._lib.check(lib.fedavg_probe_cvt16(inp.data_ptr(), n, hw, a.data_ptr(), stream), "probe")
+            mfl_amd._lib.check(lib.fedavg_probe_cvt16(inp.data_ptr(), n, ref, b.data_ptr(), stream), "probe")
+            same = (a == b) | nan_in
+            assert bool(same.all()), (chunk, hw, int((~same).sum()))
+            ai = a.to(torch.int32)
+            nan_out = ((ai & expo) == expo) & ((ai & mant) != 0)
+            assert bool((nan_out == nan_in).all()), (chunk, hw)
+
+
 @pytest.mark.parametrize("splits", [2, 4, 8])
 @pytest.mark.parametrize("K,P", [(3, 1000), (10, 7850), (100, 600_372), (500, 65_536)])
 def test_splitk_within_tolerance_and_deterministic(splits, K, P):
