@@ -152,6 +152,16 @@ int fedavg_fpf_index_lru(const float* lru_itr, const float* g_mat, int64_t n_row
                          void* stream);
 
 /*
+ * Zero-copy device -> pinned-host transfer of `bytes` bytes (the averaged
+ * model's D2H feeding fedavg_trainer.py:219): a kernel with a fixed grid of
+ * `blocks` workgroups (<= 0: 64) writes straight into the mapped pinned
+ * buffer, so a concurrent reduce keeps the other CUs (the runtime's D2H blit
+ * kernel spreads over the whole chip).  host_dst must be pinned host memory
+ * (checked with hipPointerGetAttributes); src and host_dst 16-B aligned.
+ */
+int fedavg_copy_to_host(const void* src, void* host_dst, int64_t bytes, int blocks, void* stream);
+
+/*
  * Host helper: weights[i] = (float)((double)n_i / (double)sum(n)) for integer
  * sample counts, exactly as Python's int/int true division followed by ATen's
  * double->float cast (fedavg_trainer.py:444-447,453).  Counts must be >= 0

@@ -31,6 +31,7 @@ of one freshly allocated host buffer (values and shapes are the reference's;
 from __future__ import annotations
 
 import copy
+import os
 import threading
 import time
 import weakref
@@ -105,6 +106,10 @@ def prepare(w_locals, model_global=None):
 # columns keep every launch a full-chip one; all schedules give the same bits.
 D2H_CHUNK_MIN_COLS = 2 << 20
 D2H_MAX_CHUNKS = 8
+# workgroups of the zero-copy D2H kernel (fedavg_copy_to_host); 0 = the
+# runtime's hipMemcpyAsync (a whole-chip blit kernel).  FEDAVG_D2H_BLOCKS
+# overrides it for measurements.
+D2H_BLOCKS = int(os.environ.get("FEDAVG_D2H_BLOCKS", "64"))
 
 
 def column_chunks(P: int) -> List[Tuple[int, int]]:
@@ -133,9 +138,19 @@ def reduce_and_fetch(devbuf: torch.Tensor, w_dev: torch.Tensor, P: int, d2h_stre
             compute.wait_event(ready[c])
         reduce_packed(devbuf[:, c0:c1] if len(chunks) > 1 else devbuf, w_dev, c1 - c0, out_dev[c0:c1])
         d2h_stream.wait_stream(compute)
-        with torch.cuda.stream(d2h_stream):
-            out_host[c0:c1].copy_(out_dev[c0:c1], non_blocking=True)
+        _fetch(out_dev[c0:c1], out_host[c0:c1], d2h_stream)
     return out_dev, out_host
+
+
+def _fetch(src: torch.Tensor, dst: torch.Tensor, stream) -> None:
+    """Device -> pinned host copy on ``stream`` (zero-copy kernel, small grid)."""
+    if D2H_BLOCKS <= 0:
+        with torch.cuda.stream(stream):
+            dst.copy_(src, non_blocking=True)
+        return
+    lib = _lib.load()
+    _lib.check(lib.fedavg_copy_to_host(src.data_ptr(), dst.data_ptr(), src.numel() * src.element_size(),
+                                       D2H_BLOCKS, stream.cuda_stream), "fedavg_copy_to_host")
 
 
 class _Staging:

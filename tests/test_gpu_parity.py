@@ -392,6 +392,28 @@ def test_aggregate_chunked_fetch_bit_exact(P):
     assert_bits(torch.cat([out2["a"].reshape(-1), out2["b"]]), exp)
 
 
+@pytest.mark.parametrize("nbytes", [16, 100, 4096 + 12, 50_000_016])
+def test_copy_to_host_zero_copy(nbytes):
+    lib = mfl_amd._lib.load()
+    src = torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device=DEV)
+    dst = torch.zeros(nbytes, dtype=torch.uint8, pin_memory=True)
+    s = torch.cuda.current_stream(DEV)
+    for blocks in (1, 64, 0):
+        dst.zero_()
+        mfl_amd._lib.check(lib.fedavg_copy_to_host(src.data_ptr(), dst.data_ptr(), nbytes, blocks, s.cuda_stream),
+                           "copy")
+        s.synchronize()
+        assert torch.equal(dst, src.cpu())
+
+
+def test_copy_to_host_rejects_pageable_memory():
+    lib = mfl_amd._lib.load()
+    src = torch.zeros(64, dtype=torch.uint8, device=DEV)
+    dst = torch.zeros(64, dtype=torch.uint8)  # pageable
+    rc = lib.fedavg_copy_to_host(src.data_ptr(), dst.data_ptr(), 64, 8, None)
+    assert rc == -10001
+
+
 def test_round_session_streaming_matches_golden():
     for name in ["mnist_lr_k100", "resnet_like_bn_k5", "int_dtypes_k3", "float64_key_k3", "bfloat16_key_k3"]:
         meta, w_locals, expected = load_case(name)
