@@ -181,7 +181,9 @@ def main():
     mfl_amd._lib.load()
 
     K, P_local, desc = WORKLOADS[args.workload]
-    chunks = args.chunks or (1 if world == 1 and not args.host_out else 4)
+    # N > 1: 8 chunks, so only 1/8 of the reduce is exposed before the first
+    # all-gather starts (the gather, not the reduce, is the longer of the two)
+    chunks = args.chunks or (1 if world == 1 and not args.host_out else 4 if args.host_out else 8)
     P_total = P_local * world
     host_out = torch.empty(P_total, dtype=torch.float32, pin_memory=True) if args.host_out else None
     # Each rank owns exactly P_local valid columns: plan over the global P.

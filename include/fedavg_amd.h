@@ -152,14 +152,28 @@ int fedavg_fpf_index_lru(const float* lru_itr, const float* g_mat, int64_t n_row
                          void* stream);
 
 /*
- * Zero-copy device -> pinned-host transfer of `bytes` bytes (the averaged
- * model's D2H feeding fedavg_trainer.py:219): a kernel with a fixed grid of
- * `blocks` workgroups (<= 0: 64) writes straight into the mapped pinned
- * buffer, so a concurrent reduce keeps the other CUs (the runtime's D2H blit
- * kernel spreads over the whole chip).  host_dst must be pinned host memory
- * (checked with hipPointerGetAttributes); src and host_dst 16-B aligned.
+ * Device -> pinned-host transfer of `bytes` bytes (the averaged model's D2H
+ * feeding fedavg_trainer.py:219).  blocks == 0: the runtime's DMA copy
+ * (hipMemcpyAsync; the production choice, fastest end to end).  blocks > 0:
+ * a zero-copy kernel with a fixed grid of `blocks` workgroups writing straight
+ * into the mapped pinned buffer, leaving the other CUs to a concurrent
+ * reduce.  host_dst must be pinned host memory (checked with
+ * hipPointerGetAttributes); src and host_dst 16-B aligned.
  */
 int fedavg_copy_to_host(const void* src, void* host_dst, int64_t bytes, int blocks, void* stream);
+
+/*
+ * Input distribution of the P-sharded reduce: one
+ * strided host->device DMA of `rows` rows of `width_bytes` each, from pinned
+ * host memory with row pitch `src_pitch_bytes` (the full [K, P] client
+ * buffer; host_src points at this rank's first column) into device rows of
+ * pitch `dst_pitch_bytes` (this rank's [K, ld] buffer).  Replaces, for one
+ * rank's columns, the per-client host tensors reaching the reduction
+ * (fedavg_trainer.py:199 -> :450-457).  host_src must be pinned (checked);
+ * stream-ordered and asynchronous.
+ */
+int fedavg_upload_shard(void* dst, int64_t dst_pitch_bytes, const void* host_src, int64_t src_pitch_bytes,
+                        int64_t width_bytes, int64_t rows, void* stream);
 
 /*
  * Host helper: weights[i] = (float)((double)n_i / (double)sum(n)) for integer

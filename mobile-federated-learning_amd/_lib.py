@@ -39,6 +39,7 @@ SIGNATURES = {
     "fedavg_fpf_index_lru": (_c_int, [_vp, _vp, _c_i64, _vp, _vp]),
     "fedavg_probe_cvt16": (_c_int, [_vp, _c_i64, _c_int, _vp, _vp]),
     "fedavg_copy_to_host": (_c_int, [_vp, _vp, _c_i64, _c_int, _vp]),
+    "fedavg_upload_shard": (_c_int, [_vp, _c_i64, _vp, _c_i64, _c_i64, _c_i64, _vp]),
     "fedavg_f32_schedule": (_c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp]),
     "fedavg_reduce_f32_tuned": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_int, _c_int, _vp]),
     "fedavg_reduce_f32_variant": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_int, _c_int, _c_int, _c_int,

@@ -106,10 +106,14 @@ def prepare(w_locals, model_global=None):
 # columns keep every launch a full-chip one; all schedules give the same bits.
 D2H_CHUNK_MIN_COLS = 2 << 20
 D2H_MAX_CHUNKS = 8
-# workgroups of the zero-copy D2H kernel (fedavg_copy_to_host); 0 = the
-# runtime's hipMemcpyAsync (a whole-chip blit kernel).  FEDAVG_D2H_BLOCKS
-# overrides it for measurements.
-D2H_BLOCKS = int(os.environ.get("FEDAVG_D2H_BLOCKS", "64"))
+# D2H engine of fedavg_copy_to_host: 0 = the runtime's DMA copy (production:
+# a streaming round's finish at K=100 x P=25M measured 2.67 ms vs 3.0-3.1 ms
+# for the 64-workgroup zero-copy kernel), > 0 = the zero-copy kernel with that
+# grid.  Both go through the C ABI rather than torch's copy_, so torch's
+# pinned-memory cache does not hold the output block behind a copy event (with
+# copy_ the first rounds re-allocated 100 MB of pinned memory: 8-10 ms
+# finishes).  FEDAVG_D2H_BLOCKS overrides it for measurements.
+D2H_BLOCKS = int(os.environ.get("FEDAVG_D2H_BLOCKS", "0"))
 
 
 def column_chunks(P: int) -> List[Tuple[int, int]]:
@@ -143,11 +147,7 @@ def reduce_and_fetch(devbuf: torch.Tensor, w_dev: torch.Tensor, P: int, d2h_stre
 
 
 def _fetch(src: torch.Tensor, dst: torch.Tensor, stream) -> None:
-    """Device -> pinned host copy on ``stream`` (zero-copy kernel, small grid)."""
-    if D2H_BLOCKS <= 0:
-        with torch.cuda.stream(stream):
-            dst.copy_(src, non_blocking=True)
-        return
+    """Device -> pinned host copy on ``stream`` (fedavg_copy_to_host, engine D2H_BLOCKS)."""
     lib = _lib.load()
     _lib.check(lib.fedavg_copy_to_host(src.data_ptr(), dst.data_ptr(), src.numel() * src.element_size(),
                                        D2H_BLOCKS, stream.cuda_stream), "fedavg_copy_to_host")

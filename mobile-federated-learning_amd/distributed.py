@@ -26,6 +26,7 @@ the kernel that produced the chunk).
 """
 from __future__ import annotations
 
+import contextlib
 from dataclasses import dataclass
 from typing import Callable, List, Optional, Sequence
 
@@ -34,7 +35,7 @@ import torch.distributed as dist
 
 from .reduce import ALIGN_ELEMS, reduce_packed
 
-__all__ = ["ShardPlan", "plan_shards", "ShardedReducer"]
+__all__ = ["ShardPlan", "plan_shards", "ShardedReducer", "upload_segments"]
 
 
 def _round_up(n: int, m: int) -> int:
@@ -86,6 +87,36 @@ def plan_shards(P: int, world_size: int, rank: int, chunks: int = 1, align: int 
         raise ValueError("bad shard plan arguments")
     block = max(_round_up(-(-P // (world_size * chunks)), align), align)
     return ShardPlan(P, world_size, rank, chunks, block)
+
+
+def upload_segments(dst: torch.Tensor, host: torch.Tensor, segs, stream: Optional[torch.cuda.Stream] = None) -> None:
+    """``dst[:, l:l+n] = host[:, g:g+n]`` for every ``(l, g, n)`` in ``segs``.
+
+    ``dst`` is a device ``[K, ld]`` buffer, ``host`` a host ``[K, >=P]`` one.
+    From pinned host memory with unit column stride every segment is one
+    strided DMA (``fedavg_upload_shard``: height K, src pitch = the host row);
+    otherwise torch's per-segment copy.  Asynchronous on ``stream`` (default:
+    the current stream) when pinned."""
+    K = dst.shape[0]
+    if dst.device.type == "cuda" and host.is_pinned() and host.stride(1) == 1 and dst.stride(1) == 1:
+        from . import _lib
+
+        lib = _lib.load()
+        es = host.element_size()
+        s = stream if stream is not None else torch.cuda.current_stream(dst.device)
+        dpitch = (dst.stride(0) if K > 1 else dst.shape[1]) * es
+        spitch = (host.stride(0) if K > 1 else host.shape[1]) * es
+        for lstart, gstart, n in segs:
+            if lstart + n > dst.shape[1] or gstart + n > host.shape[1]:
+                raise ValueError(f"segment ({lstart}, {gstart}, {n}) out of range")
+            rc = lib.fedavg_upload_shard(dst.data_ptr() + lstart * es, dpitch, host.data_ptr() + gstart * es, spitch,
+                                         n * es, K, s.cuda_stream)
+            _lib.check(rc, "fedavg_upload_shard")
+        return
+    ctx = torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
+    with ctx:
+        for lstart, gstart, n in segs:
+            dst[:, lstart:lstart + n].copy_(host[:, gstart:gstart + n], non_blocking=True)
 
 
 LocalReduce = Callable[[torch.Tensor, torch.Tensor, int, torch.Tensor], None]
@@ -145,13 +176,31 @@ class ShardedReducer:
                      if self.gather else None)
 
     # ------------------------------------------------------------------
-    def load_from_host(self, host_clients: torch.Tensor) -> None:
-        """Copy this rank's columns of a host ``[K, >=P]`` buffer (strided H2D)."""
-        if host_clients.shape[0] != self.K:
-            raise ValueError("host buffer has the wrong client count")
-        self.clients.zero_()
-        for lstart, gstart, n in self.plan.local_segments():
-            self.clients[:, lstart:lstart + n].copy_(host_clients[:, gstart:gstart + n], non_blocking=True)
+    def load_from_host(self, host_clients: torch.Tensor, stream: Optional[torch.cuda.Stream] = None) -> None:
+        """Copy this rank's columns of a host ``[K, >=P]`` buffer.
+
+        SURVEY.md section 8e's input distribution: from pinned host memory each
+        of this rank's column segments is ONE strided DMA (``fedavg_upload_shard``,
+        src pitch = the host row, height = K) straight into the device rows --
+        no host-side gather of the shard.  Padding columns are zeroed.
+        Asynchronous on ``stream`` (default: the current stream) when pinned.
+        """
+        if host_clients.dim() != 2 or host_clients.shape[0] != self.K:
+            raise ValueError("host buffer must be [K, >=P] with K = the reducer's client count")
+        if host_clients.shape[1] < self.plan.P or host_clients.dtype != self.dtype:
+            raise ValueError(f"host buffer must hold >= {self.plan.P} {self.dtype} columns")
+        segs = self.plan.local_segments()
+        self._zero_padding(segs)
+        upload_segments(self.clients, host_clients, segs, stream)
+
+    def _zero_padding(self, segs) -> None:
+        """Zero the local columns no global column maps to (tail of the plan)."""
+        covered = sorted((l, l + n) for l, _, n in segs)
+        pos = 0
+        for a, b in covered + [(self.plan.local_cols, self.plan.local_cols)]:
+            if a > pos:
+                self.clients[:, pos:a].zero_()
+            pos = max(pos, b)
 
     def step(self, weights: torch.Tensor) -> Optional[torch.Tensor]:
         """Reduce every local chunk; all-gather each as soon as it is ready."""

@@ -80,6 +80,20 @@ def test_splitk_bad_mode(lib):
     assert rc in (_lib.FEDAVG_EMODE, _lib.FEDAVG_EALIGN)
 
 
+@pytest.mark.parametrize("dpitch,spitch,width,rows", [(64, 64, 128, 2), (128, 32, 64, 2), (64, 64, 64, -1),
+                                                      (64, 64, -4, 2)])
+def test_upload_shard_rejects_bad_sizes_without_gpu(lib, dpitch, spitch, width, rows):
+    rc = lib.fedavg_upload_shard(None, dpitch, None, spitch, width, rows, None)
+    assert rc == _lib.FEDAVG_EINVAL
+    assert lib.fedavg_last_error().startswith(b"fedavg_upload_shard")
+
+
+def test_upload_shard_empty_is_noop_and_null_rejected(lib):
+    assert lib.fedavg_upload_shard(None, 64, None, 64, 0, 5, None) == 0
+    assert lib.fedavg_upload_shard(None, 64, None, 64, 64, 0, None) == 0
+    assert lib.fedavg_upload_shard(None, 64, None, 64, 64, 3, None) == _lib.FEDAVG_EINVAL
+
+
 def test_weights_helper_matches_python(lib):
     rng = np.random.default_rng(7)
     for K in (1, 2, 3, 10, 100, 1000):

@@ -365,6 +365,50 @@ def test_sharded_reducer_host_out():
         ShardedReducer(K, P, device=DEV, host_out=torch.empty(P))  # not pinned
 
 
+@pytest.mark.parametrize("ws,chunks", [(1, 3), (2, 1), (3, 4), (8, 8)])
+def test_upload_segments_strided_dma(ws, chunks):
+    """SURVEY 8e input distribution: every rank's column segments of a pinned
+    host [K, P] buffer land in its device rows via one strided DMA each."""
+    from mfl_amd.distributed import plan_shards, upload_segments
+    K, P = 7, 300_007
+    host = torch.randn((K, P)).pin_memory()
+    seen = torch.zeros(P, dtype=torch.int32)
+    for r in range(ws):
+        plan = plan_shards(P, ws, r, chunks)
+        dst = torch.full((K, plan.local_cols), float("nan"), device=DEV)
+        segs = plan.local_segments()
+        upload_segments(dst, host, segs)
+        torch.cuda.synchronize()
+        got = dst.cpu()
+        for l, g, n in segs:
+            assert torch.equal(got[:, l:l + n], host[:, g:g + n]), (r, l, g, n)
+            seen[g:g + n] += 1
+    assert bool((seen == 1).all())  # the ranks' segments partition the columns
+
+
+def test_upload_shard_rejects_pageable_source():
+    lib = mfl_amd._lib.load()
+    dst = torch.empty(64, device=DEV)
+    src = torch.zeros(64)  # pageable
+    assert lib.fedavg_upload_shard(dst.data_ptr(), 256, src.data_ptr(), 256, 256, 1, None) == -10001
+
+
+def test_sharded_reducer_load_from_pinned_host_zero_padding():
+    from mfl_amd.distributed import ShardedReducer
+    K, P = 10, 1_000_003
+    host = (torch.randn((K, P)) * 0.05).pin_memory()
+    w = _weights(K)
+    red = ShardedReducer(K, P, chunks=5, device=DEV)
+    red.clients.fill_(float("nan"))
+    red.load_from_host(host)
+    red.step(_w(w))
+    got = torch.cat([v for v, _ in red.local_model_columns()])
+    assert_bits(got, torch.from_numpy(O.reduce_f32(host.numpy(), w)))
+    valid = sum(n for _, _, n in red.plan.local_segments())
+    assert not torch.isnan(red.clients).any()  # padding columns were zeroed
+    assert valid == P
+
+
 @pytest.mark.parametrize("P", [4_194_304 + 3, 17_000_021])
 def test_aggregate_chunked_fetch_bit_exact(P):
     """P >= 2 x D2H_CHUNK_MIN_COLS: the reduce runs in column chunks with the
