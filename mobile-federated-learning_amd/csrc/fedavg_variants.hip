@@ -310,6 +310,52 @@ var_launcher pick_var(int unroll, int cols, int nt, int pipe) {
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// HBM read-ceiling probe (measurement only): how fast can this chip stream a
+// buffer with NO reduction structure?  The reduce's rate is judged against
+// this as well as against the 8 TB/s spec.  Each thread keeps 8 x 16-B loads
+// in flight and folds them into a register; a value-dependent store keeps
+// the loads alive without writing anything in practice.
+//   mode 0: grid-stride (thread v reads v, v + G*256, ...), nontemporal;
+//   mode 1: block-contiguous ranges (block b sweeps its own 1/G of the
+//           buffer, 32 KiB per block-step), nontemporal;
+//   mode 2: mode 1 with default-policy loads.
+// ---------------------------------------------------------------------------
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void probe_read_kernel(const f32x4* __restrict__ X, int64_t nvec,
+                                                            float* __restrict__ sink) {
+  constexpr int U = 8;
+  constexpr bool NT = MODE != 2;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (MODE == 0) {
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+    int64_t v = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    for (; v + (U - 1) * stride < nvec; v += U * stride) {
+      f32x4 xs[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) xs[u] = ld<NT>(X + v + u * stride);
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc += xs[u];
+    }
+    for (; v < nvec; v += stride) acc += ld<NT>(X + v);
+  } else {
+    const int64_t per = (nvec + gridDim.x - 1) / gridDim.x;
+    const int64_t b0 = static_cast<int64_t>(blockIdx.x) * per;
+    const int64_t b1 = (b0 + per) < nvec ? (b0 + per) : nvec;
+    int64_t v = b0 + threadIdx.x;
+    for (; v + (U - 1) * kBlock < b1; v += U * kBlock) {
+      f32x4 xs[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) xs[u] = ld<NT>(X + v + u * kBlock);
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc += xs[u];
+    }
+    for (; v < b1; v += kBlock) acc += ld<NT>(X + v);
+  }
+  if (acc.x + acc.y + acc.z + acc.w == 1234.5678f) sink[blockIdx.x] = acc.x;
+}
+
 }  // namespace
 
 extern "C" {
@@ -351,6 +397,27 @@ int fedavg_reduce_tiled_f32(const float* tiles, int64_t K, int64_t P, const floa
     case 8: hipLaunchKernelGGL((reduce_tiled_f32x4_kernel<8, false>), dim3(ntiles), dim3(kBlock), 0, s, X, k, P, weights, out); break;
     case 16: hipLaunchKernelGGL((reduce_tiled_f32x4_kernel<16, false>), dim3(ntiles), dim3(kBlock), 0, s, X, k, P, weights, out); break;
     default: return set_error(FEDAVG_EMODE, "%s: unsupported unroll %d", what, unroll);
+  }
+  return launch_status(what);
+}
+
+int fedavg_probe_read_f32x4(const float* buf, int64_t nvec, int mode, int blocks, int launches, float* sink,
+                            void* stream) {
+  const char* what = "fedavg_probe_read_f32x4";
+  if (nvec < 0 || blocks <= 0 || launches <= 0 || mode < 0 || mode > 2 || (nvec > 0 && (!buf || !sink)))
+    return set_error(FEDAVG_EINVAL, "%s: bad arguments", what);
+  if (nvec == 0) return FEDAVG_OK;
+  if (!aligned16(buf)) return set_error(FEDAVG_EALIGN, "%s: buffer must be 16-B aligned", what);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const f32x4* X = reinterpret_cast<const f32x4*>(buf);
+  const int64_t per = (nvec + launches - 1) / launches;
+  for (int64_t v0 = 0; v0 < nvec; v0 += per) {
+    const int64_t n = (nvec - v0) < per ? (nvec - v0) : per;
+    switch (mode) {
+      case 0: hipLaunchKernelGGL(probe_read_kernel<0>, dim3(blocks), dim3(kBlock), 0, s, X + v0, n, sink); break;
+      case 1: hipLaunchKernelGGL(probe_read_kernel<1>, dim3(blocks), dim3(kBlock), 0, s, X + v0, n, sink); break;
+      default: hipLaunchKernelGGL(probe_read_kernel<2>, dim3(blocks), dim3(kBlock), 0, s, X + v0, n, sink); break;
+    }
   }
   return launch_status(what);
 }
