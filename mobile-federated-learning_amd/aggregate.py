@@ -42,7 +42,7 @@ import torch
 
 from . import _lib
 from .layout import KeyTable
-from .reduce import client_sqdist, reduce_packed, weights_tensor
+from .reduce import client_sqdist, reduce_packed
 
 __all__ = [
     "sample_weights",
@@ -69,7 +69,7 @@ class _Prepared(tuple):
     """(acc_dict, KeyTable, state_dicts, weights, src_ptrs, keepalive) for a non-trivial call."""
 
 
-def prepare(w_locals, model_global=None):
+def prepare(w_locals, model_global=None, table_hint: Optional[KeyTable] = None):
     """Host-side part of ``aggregate``: the reference's early returns and errors.
 
     Returns either the final answer (empty ``w_locals`` -> copy of the global
@@ -78,6 +78,10 @@ def prepare(w_locals, model_global=None):
     Raises what the reference raises (``ZeroDivisionError`` on a zero sample
     total, ``KeyError`` on a missing key) and refuses inputs it would have
     broadcast (``ShapeMismatchError``).  Touches no GPU.
+
+    ``table_hint``: the key table of an earlier round, reused when client 0
+    has exactly its keys and every client matches it (a round's model
+    structure rarely changes); otherwise a fresh table is built from client 0.
     """
     if not w_locals:
         if model_global is None:
@@ -95,9 +99,23 @@ def prepare(w_locals, model_global=None):
             raise ValueError(
                 f"w_locals[{i}][1] is the same dict object as w_locals[0][1]; the reference would read "
                 "its own partial sums there (fedavg_trainer.py:199 deep-copies to avoid this)")
-    table = KeyTable(acc_dict)
-    ptrs, keepalive = table.collect(dicts)  # validates every client (KeyError / ShapeMismatchError / TypeError)
+    got = table_hint.try_collect(dicts) if table_hint is not None else None
+    if got is not None:
+        table = table_hint
+        ptrs, keepalive = got
+    else:
+        table = KeyTable(acc_dict)
+        ptrs, keepalive = table.collect(dicts)  # validates every client (KeyError / ShapeMismatchError / TypeError)
     return _Prepared((acc_dict, table, dicts, weights, ptrs, keepalive))
+
+
+def _trivial(w_locals, model_global=None):
+    """The reference's early answers (fedavg_trainer.py:442-447) without
+    building a key table: the empty list and state_dicts without keys.
+    Returns ``(True, answer)`` or ``(False, None)``."""
+    if not w_locals or len(w_locals[0][1]) == 0:
+        return True, prepare(w_locals, model_global)
+    return False, None
 
 
 # D2H pipelining of the averaged model: the reduce runs in column chunks and
@@ -154,12 +172,30 @@ def _fetch(src: torch.Tensor, dst: torch.Tensor, stream) -> None:
 
 
 class _Staging:
-    """Reusable pinned host rows + device buffer for one dtype group."""
+    """Reusable pinned host rows + device buffer for one dtype group, and the
+    group's weight vector (pinned + device) so a call uploads the weights with
+    its rows instead of allocating a pinned tensor per call."""
 
     def __init__(self, K: int, ld: int, dtype: torch.dtype, device: torch.device):
         self.K, self.ld, self.dtype = K, ld, dtype
         self.host = torch.empty((K, ld), dtype=dtype, pin_memory=True)
         self.dev = torch.empty((K, ld), dtype=dtype, device=device)
+        wdt = torch.float64 if dtype == torch.float64 else torch.float32
+        self.w_host = torch.empty(K, dtype=wdt, pin_memory=True)
+        self.w_dev = torch.empty(K, dtype=wdt, device=device)
+
+    def upload_weights(self, weights: Sequence[float], stream) -> torch.Tensor:
+        """``weights`` (the reference's Python doubles n_i / N) rounded once to
+        the group's weight dtype (round to nearest even: the cast ATen applies
+        to the scalar at fedavg_trainer.py:455) and copied on ``stream``.  The
+        caller synchronizes before the next call rewrites the pinned buffer."""
+        import numpy as np
+
+        K = len(weights)
+        self.w_host[:K].numpy()[:] = np.array([float(w) for w in weights], dtype=np.float64)
+        with torch.cuda.stream(stream):
+            self.w_dev[:K].copy_(self.w_host[:K], non_blocking=True)
+        return self.w_dev[:K]
 
 
 class DeviceAggregator:
@@ -188,6 +224,7 @@ class DeviceAggregator:
         # dtype group), reused by client_distances for the same round
         self._last: Dict[str, object] = {}
         self._session = None  # weakref to the open RoundSession, if any
+        self._table_hint: Optional[KeyTable] = None  # last round's key table (prepare reuses it)
 
     # ------------------------------------------------------------------
     def begin_round(self, template, max_clients: int):
@@ -228,10 +265,11 @@ class DeviceAggregator:
 
     def aggregate(self, w_locals, model_global=None):
         """``FedAvgTrainer.aggregate`` semantics; see the module docstring."""
-        prep = prepare(w_locals, model_global)
+        prep = prepare(w_locals, model_global, self._table_hint)
         if not isinstance(prep, _Prepared):
             return prep  # empty list / no keys: answered on the host like the reference
         self._check_no_open_session("aggregate")
+        self._table_hint = prep[1]
         acc_dict, table, dicts, weights, ptrs, keepalive = prep
         results = self._reduce_groups(table, ptrs, weights)
         del keepalive
@@ -250,9 +288,44 @@ class DeviceAggregator:
     # rows per H2D chunk: big enough to amortise a copy launch, small enough
     # that the first chunk's DMA starts while the host still packs the rest
     CHUNK_BYTES = 32 << 20
+    # fp32-only rounds whose rows are at most this many bytes run as ONE native
+    # call (fedavg_round_f32): pack, upload, reduce, fetch, wait -- no per-step
+    # Python/torch overhead, which is most of a tiny model's round.  Larger
+    # rounds take the pipelined path below (packing overlapped with H2D, the
+    # D2H overlapped with the reduce).  FEDAVG_SMALL_ROUND_BYTES overrides it.
+    SMALL_ROUND_BYTES = int(os.environ.get("FEDAVG_SMALL_ROUND_BYTES", str(4 << 20)))
+
+    def _reduce_small_round(self, table: KeyTable, ptrs, weights):
+        """One native call for a small fp32-only round (see SMALL_ROUND_BYTES)."""
+        import numpy as np
+
+        g = table.groups[torch.float32]
+        K, dev = ptrs.shape[0], self.device
+        lib = _lib.load()
+        t0 = time.perf_counter()
+        with torch.cuda.device(dev):
+            compute = torch.cuda.current_stream(dev)
+            if self._copy_stream is not None:
+                compute.wait_stream(self._copy_stream)  # earlier users of the staging are done
+            st = self._staging_for(g.dtype, K, g.ld)
+            items = table.pack_items(g, ptrs, 0, g.ld)
+            w64 = np.array([float(w) for w in weights], dtype=np.float64)
+            out_dev = torch.empty(g.P, dtype=torch.float32, device=dev)
+            out_host = torch.empty(g.P, dtype=torch.float32, pin_memory=True)
+            _lib.check(lib.fedavg_round_f32(items.ctypes.data, items.shape[0], st.host.data_ptr(), st.dev.data_ptr(),
+                                            K, g.P, g.ld, w64.ctypes.data, st.w_host.data_ptr(), st.w_dev.data_ptr(),
+                                            out_dev.data_ptr(), out_host.data_ptr(), max(1, torch.get_num_threads()),
+                                            compute.cuda_stream), "fedavg_round_f32")
+        self._last = {"table": table, "K": K, "dev": {torch.float32: (st.dev[:K], out_dev)}}
+        results = table.unpack(g, out_host)
+        self.last_profile = {"pack_issue_ms": 0.0, "h2d_kernel_d2h_ms": (time.perf_counter() - t0) * 1e3}
+        return results
 
     def _reduce_groups(self, table: KeyTable, ptrs, weights) -> "OrderedDict[str, torch.Tensor]":
         K = ptrs.shape[0]
+        if (len(table.groups) == 1 and torch.float32 in table.groups
+                and K * table.groups[torch.float32].ld * 4 <= self.SMALL_ROUND_BYTES):
+            return self._reduce_small_round(table, ptrs, weights)
         dev = self.device
         lib = _lib.load()
         threads = max(1, torch.get_num_threads())
@@ -275,7 +348,7 @@ class DeviceAggregator:
                                                     threads), "fedavg_pack_rows")
                     with torch.cuda.stream(copy_s):
                         devbuf[i0:i1].copy_(host[i0:i1], non_blocking=True)
-                w_dev = weights_tensor(weights, g.dtype, dev)
+                w_dev = st.upload_weights(weights, copy_s)
                 staged.append((g, devbuf, w_dev))
             compute.wait_stream(copy_s)
             t1 = time.perf_counter()
@@ -286,8 +359,9 @@ class DeviceAggregator:
                 out_dev, out_host = reduce_and_fetch(devbuf, w_dev, g.P, d2h)
                 outs.append((g, out_host))
                 self._last["dev"][g.dtype] = (devbuf, out_dev)
+            # the D2H stream waited on the compute stream after every chunk's
+            # reduce, so its completion covers the kernels too
             d2h.synchronize()
-            compute.synchronize()
             t2 = time.perf_counter()
         for g, out_host in outs:
             results.update(table.unpack(g, out_host))
@@ -390,9 +464,9 @@ def default_aggregator(device: Optional[torch.device] = None) -> DeviceAggregato
 
 def aggregate(w_locals, model_global=None, device: Optional[torch.device] = None):
     """Functional form of ``FedAvgTrainer.aggregate``."""
-    prep = prepare(w_locals, model_global)
-    if not isinstance(prep, _Prepared):
-        return prep
+    done, answer = _trivial(w_locals, model_global)
+    if done:
+        return answer  # answered on the host: no GPU needed
     return default_aggregator(device).aggregate(w_locals, model_global=model_global)
 
 

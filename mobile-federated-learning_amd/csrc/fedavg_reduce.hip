@@ -762,6 +762,48 @@ int fedavg_reduce_splitk_f32(const float* clients, int64_t K, int64_t P, int64_t
   return launch_status(what);
 }
 
+// A whole small round in ONE host call (the drop-in's path for models whose
+// K x ld rows fit in a few MB, e.g. the reference's own MNIST-LR config): pack
+// the clients' keys into the pinned rows (fedavg_pack_rows), round the
+// weights to fp32, upload rows and weights, reduce, fetch the averaged model
+// and wait -- all on `stream`.  The same steps through Python/torch cost ~100
+// us of host overhead per call; the reduction's bits are the same (same
+// kernel).  Buffers: host_rows/host_w/host_out pinned host memory; dev_rows
+// [K, ld], dev_w [K], dev_out [P] device memory (ld % 4 == 0, 16-B aligned).
+int fedavg_round_f32(const fedavg_pack_item* items, int64_t n_items, float* host_rows, float* dev_rows, int64_t K,
+                     int64_t P, int64_t ld, const double* weights, float* host_w, float* dev_w, float* dev_out,
+                     float* host_out, int n_threads, void* stream) {
+  const char* what = "fedavg_round_f32";
+  int rc = check_common(dev_rows, K, P, ld, dev_w, dev_out, what);
+  if (rc) return rc;
+  if (P == 0) return FEDAVG_OK;
+  if (!host_rows || !weights || !host_w || !host_out || (n_items > 0 && !items))
+    return set_error(FEDAVG_EINVAL, "%s: null buffer", what);
+  if (!aligned16(dev_rows) || !aligned16(dev_out) || (ld % 4) != 0 || !aligned4(dev_w))
+    return set_error(FEDAVG_EALIGN, "%s: needs 16-B aligned dev_rows/dev_out and ld %% 4 == 0", what);
+  rc = fedavg_pack_rows(items, n_items, host_rows, 4, n_threads);
+  if (rc) return set_error(rc, "%s: bad pack items", what);
+  for (int64_t i = 0; i < K; ++i) host_w[i] = static_cast<float>(weights[i]);  // ATen's scalar cast (:455)
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const size_t row_bytes = static_cast<size_t>(K) * static_cast<size_t>(ld) * sizeof(float);
+  hipError_t e = hipMemcpyAsync(dev_rows, host_rows, row_bytes, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(dev_w, host_w, static_cast<size_t>(K) * sizeof(float), hipMemcpyHostToDevice, s);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return set_error(-static_cast<int>(e), "%s: upload failed: %s", what, hipGetErrorString(e));
+  }
+  launch_production_f32(dev_rows, static_cast<int>(K), ld, P, dev_w, dev_out, s);
+  rc = launch_status(what);
+  if (rc) return rc;
+  e = hipMemcpyAsync(host_out, dev_out, static_cast<size_t>(P) * sizeof(float), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return set_error(-static_cast<int>(e), "%s: fetch failed: %s", what, hipGetErrorString(e));
+  }
+  return FEDAVG_OK;
+}
+
 int fedavg_weights_f32(const int64_t* sample_nums, int64_t K, float* weights) {
   if (K <= 0 || !sample_nums || !weights) return set_error(FEDAVG_EINVAL, "fedavg_weights_f32: bad arguments");
   int64_t total = 0;

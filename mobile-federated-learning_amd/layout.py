@@ -175,6 +175,19 @@ class KeyTable:
             ptrs[i] = [t.data_ptr() for t in ts]
         return ptrs, keepalive
 
+    def try_collect(self, state_dicts: Sequence[Mapping[str, torch.Tensor]]):
+        """:meth:`collect` for a table reused from an earlier round: the
+        ``(ptrs, keepalive)`` pair when client 0 has exactly this table's keys
+        in this order and every client holds them with the recorded shapes and
+        dtypes as contiguous host tensors (checked by the native walk), else
+        ``None`` -- never raises for a mismatch; the caller then builds a fresh
+        table from client 0."""
+        ext = _collect_ext()
+        if ext is None or not state_dicts or list(state_dicts[0].keys()) != self._names:
+            return None
+        got, _, _ = ext.collect(list(state_dicts), self._names, self._template)
+        return None if got is None else (got.numpy(), [])
+
     def pack_items(self, group: "Group", ptrs: np.ndarray, row0: int, ld: int) -> np.ndarray:
         """fedavg_pack_item rows [(src, numel, dst_offset, kind)] for clients
         ``row0 .. row0+len(ptrs)-1`` of ``group`` (dst offsets in elements from

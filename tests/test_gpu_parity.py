@@ -82,6 +82,24 @@ def test_dropin_repeated_rounds_reuse_staging():
             assert_bits(out[k], expected[k], name)
 
 
+@pytest.mark.parametrize("small_bytes", [0, 1 << 30])
+def test_small_round_native_path_and_pipelined_path_agree(small_bytes):
+    """fedavg_round_f32 (one native call) and the pipelined torch-stream path
+    give the reference's bits; both leave the round's rows in HBM for :291."""
+    for name in ["mnist_lr_k10", "mnist_lr_k100", "resnet_like_bn_k5", "int_dtypes_k3", "adversarial_k10",
+                 "flat_k10_p65"]:
+        meta, w_locals, expected = load_case(name)
+        agg = mfl_amd.DeviceAggregator(DEV)
+        agg.SMALL_ROUND_BYTES = small_bytes
+        out = agg.aggregate(w_locals)
+        for k, exp in expected.items():
+            assert_bits(out[k], exp, f"{name}/{k} small_bytes={small_bytes}")
+        has_bool = any(t.dtype == torch.bool for _, sd in w_locals[1:] for t in sd.values())
+        if torch.float32 in agg._last.get("dev", {}) and not has_bool:  # :291 raises on bool buffers
+            norms = agg.client_distances(w_locals, out)
+            assert norms.shape == (len(w_locals),) and norms[0] == 0.0
+
+
 def test_dropin_femnist_cnn_shape():
     # FEMNIST + CNN_DropOut (P = 1,206,590; 8 keys), K = 10
     shapes = [("conv2d_1.weight", (32, 1, 3, 3)), ("conv2d_1.bias", (32,)), ("conv2d_2.weight", (64, 32, 3, 3)),

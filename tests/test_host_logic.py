@@ -232,6 +232,50 @@ def test_native_collect_falls_back_for_unusual_clients(case):
             table.collect([a, b])
 
 
+def test_prepare_reuses_table_hint_only_when_client0_matches():
+    """DeviceAggregator reuses the previous round's KeyTable (prepare's
+    table_hint) only when client 0 has exactly its keys, in order, with the
+    same shapes and dtypes; otherwise it builds a fresh table, and a bad later
+    client still raises the reference's exception."""
+    from mfl_amd.layout import _collect_ext
+    a = OrderedDict(w=torch.ones(2, 3), b=torch.zeros(2))
+    b = OrderedDict(w=torch.ones(2, 3) * 2, b=torch.ones(2))
+    table = prepare([(1, a), (2, b)])[1]
+    p = prepare([(1, OrderedDict(a)), (2, b)], table_hint=table)
+    assert (p[1] is table) == (_collect_ext() is not None)
+    assert (p[4] == prepare([(1, OrderedDict(a)), (2, b)])[4]).all()
+    cases = [
+        OrderedDict(w=torch.ones(3, 3), b=torch.zeros(2)),                      # other shape
+        OrderedDict(w=torch.ones(2, 3), b=torch.zeros(2), c=torch.ones(1)),     # extra key in client 0
+        OrderedDict(b=torch.zeros(2), w=torch.ones(2, 3)),                      # other key order
+        OrderedDict(w=torch.ones(2, 3, dtype=torch.float64), b=torch.zeros(2)),  # other dtype
+    ]
+    for c in cases:
+        other = OrderedDict((k, v.clone()) for k, v in c.items())
+        p = prepare([(1, c), (2, other)], table_hint=table)
+        assert p[1] is not table
+        assert [e.name for e in p[1].entries] == list(c.keys())
+        assert [e.shape for e in p[1].entries] == [tuple(v.shape) for v in c.values()]
+    with pytest.raises(KeyError):
+        prepare([(1, OrderedDict(a)), (2, OrderedDict(w=torch.ones(2, 3)))], table_hint=table)
+    with pytest.raises(mfl_amd.ShapeMismatchError):
+        prepare([(1, OrderedDict(a)), (2, OrderedDict(w=torch.ones(3, 2), b=torch.ones(2)))], table_hint=table)
+
+
+def test_functional_aggregate_trivial_cases_need_no_gpu():
+    class M:
+        def cpu(self):
+            return self
+
+        def state_dict(self):
+            return OrderedDict(w=torch.arange(3.0))
+
+    out = mfl_amd.aggregate([], model_global=M())
+    assert torch.equal(out["w"], torch.arange(3.0))
+    empty = OrderedDict()
+    assert mfl_amd.aggregate([(1, empty), (2, OrderedDict())]) is empty
+
+
 def test_fpf_tracker_without_gpu_fails_loudly():
     import mfl_amd
 
