@@ -213,11 +213,13 @@ int fedavg_pack_rows(const fedavg_pack_item* items, int64_t n_items, void* dst_b
  * round's fp32 rows are a few MB, e.g. the reference's MNIST-LR config):
  * fedavg_pack_rows(items -> host_rows), host_w[i] = (float)weights[i] (the
  * reference's Python-double weights n_i / N, fedavg_trainer.py:453, rounded as
- * ATen rounds the scalar at :455), H2D of rows and weights, the exact fp32
- * reduce (same kernels and bits as fedavg_reduce_f32), D2H of the averaged
- * model into host_out, then waits for `stream`.  host_rows [K, ld], host_w
+ * ATen rounds the scalar at :455), then ONE kernel that reads the rows and
+ * weights from pinned memory, copies them to dev_rows / dev_w (kept for the
+ * round's later passes), reduces in the reference's order (the bits of
+ * fedavg_reduce_f32) and writes the averaged model to dev_out and host_out;
+ * then waits for `stream`.  host_rows [K, ld], host_w
  * [K], host_out [P]: pinned host memory; dev_rows [K, ld], dev_w [K], dev_out
- * [P]: device memory; ld % 4 == 0, dev_rows / dev_out 16-B aligned.
+ * [P]: device memory; ld % 4 == 0, rows/out buffers 16-B aligned.
  * Synchronous: on return host_out holds the result.
  */
 int fedavg_round_f32(const fedavg_pack_item* items, int64_t n_items, float* host_rows, float* dev_rows, int64_t K,

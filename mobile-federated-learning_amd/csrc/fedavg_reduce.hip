@@ -451,6 +451,52 @@ __global__ __launch_bounds__(64 * SPLITS) void reduce_splitk_f32x4_kernel(
 //     back-to-back rounds when loaded with the default policy (there U = 16,
 //     C = 4 was fastest: 89% vs 81% for C = 1).
 // ---------------------------------------------------------------------------
+
+// ---------------------------------------------------------------------------
+// Small-round kernel (fedavg_round_f32 for rounds of a few MB): ONE launch
+// instead of H2D + reduce + D2H.  It reads the packed client rows straight
+// from pinned host memory (zero-copy over PCIe), keeps a copy of them in HBM
+// for the round's later passes (the :291 distances, FPF :210), reduces in the
+// reference's order -- acc = x0*w0, acc = acc + xk*wk, one rounding each, the
+// same bits as every other exact kernel -- and writes the averaged model to
+// HBM and to pinned host memory.  A tiny round is latency-bound: three
+// stream operations (two DMA engine hand-offs) cost more than the bytes.
+// ---------------------------------------------------------------------------
+template <int U>
+__global__ __launch_bounds__(kBlock) void round_small_f32x4_kernel(
+    const f32x4* __restrict__ Xh, f32x4* __restrict__ Xd, int K, int64_t ld4, int64_t nvec, int tail,
+    const float* __restrict__ Wh, float* __restrict__ Wd, float* __restrict__ out_d, float* __restrict__ out_h) {
+  if (blockIdx.x == 0)
+    for (int k = threadIdx.x; k < K; k += kBlock) Wd[k] = Wh[k];
+  const int64_t v = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (v >= nvec) return;
+  const f32x4* col = Xh + v;
+  f32x4* dcol = Xd + v;
+  f32x4 x0 = col[0];
+  dcol[0] = x0;
+  f32x4 acc = x0 * Wh[0];  // fedavg_trainer.py:455 (i == 0)
+  int k = 1;
+  for (; k + U <= K; k += U) {
+    f32x4 xs[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) xs[u] = col[static_cast<int64_t>(k + u) * ld4];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      dcol[static_cast<int64_t>(k + u) * ld4] = xs[u];
+      const f32x4 term = xs[u] * Wh[k + u];
+      acc = acc + term;  // fedavg_trainer.py:457
+    }
+  }
+  for (; k < K; ++k) {
+    const f32x4 x = col[static_cast<int64_t>(k) * ld4];
+    dcol[static_cast<int64_t>(k) * ld4] = x;
+    const f32x4 term = x * Wh[k];
+    acc = acc + term;
+  }
+  store_slice(out_d, v, nvec, tail, acc);
+  store_slice(out_h, v, nvec, tail, acc);
+}
+
 struct Schedule {
   int unroll, cols, nt, blocks_per_launch;
 };
@@ -765,11 +811,12 @@ int fedavg_reduce_splitk_f32(const float* clients, int64_t K, int64_t P, int64_t
 // A whole small round in ONE host call (the drop-in's path for models whose
 // K x ld rows fit in a few MB, e.g. the reference's own MNIST-LR config): pack
 // the clients' keys into the pinned rows (fedavg_pack_rows), round the
-// weights to fp32, upload rows and weights, reduce, fetch the averaged model
-// and wait -- all on `stream`.  The same steps through Python/torch cost ~100
-// us of host overhead per call; the reduction's bits are the same (same
-// kernel).  Buffers: host_rows/host_w/host_out pinned host memory; dev_rows
-// [K, ld], dev_w [K], dev_out [P] device memory (ld % 4 == 0, 16-B aligned).
+// weights to fp32, then one launch of round_small_f32x4_kernel (rows read
+// from pinned memory and kept in HBM, reduce, result to HBM and to pinned
+// memory) and wait.  The same steps through Python/torch cost ~100 us of host
+// overhead per call.  Buffers: host_rows/host_w/host_out pinned host memory;
+// dev_rows [K, ld], dev_w [K], dev_out [P] device memory (ld % 4 == 0,
+// 16-B aligned).
 int fedavg_round_f32(const fedavg_pack_item* items, int64_t n_items, float* host_rows, float* dev_rows, int64_t K,
                      int64_t P, int64_t ld, const double* weights, float* host_w, float* dev_w, float* dev_out,
                      float* host_out, int n_threads, void* stream) {
@@ -785,21 +832,18 @@ int fedavg_round_f32(const fedavg_pack_item* items, int64_t n_items, float* host
   if (rc) return set_error(rc, "%s: bad pack items", what);
   for (int64_t i = 0; i < K; ++i) host_w[i] = static_cast<float>(weights[i]);  // ATen's scalar cast (:455)
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const size_t row_bytes = static_cast<size_t>(K) * static_cast<size_t>(ld) * sizeof(float);
-  hipError_t e = hipMemcpyAsync(dev_rows, host_rows, row_bytes, hipMemcpyHostToDevice, s);
-  if (e == hipSuccess) e = hipMemcpyAsync(dev_w, host_w, static_cast<size_t>(K) * sizeof(float), hipMemcpyHostToDevice, s);
-  if (e != hipSuccess) {
-    (void)hipGetLastError();
-    return set_error(-static_cast<int>(e), "%s: upload failed: %s", what, hipGetErrorString(e));
-  }
-  launch_production_f32(dev_rows, static_cast<int>(K), ld, P, dev_w, dev_out, s);
+  if (!aligned16(host_rows) || !aligned16(host_out) || !aligned4(host_w))
+    return set_error(FEDAVG_EALIGN, "%s: host_rows/host_out must be 16-B aligned", what);
+  const int64_t nvec = (P + 3) / 4;
+  hipLaunchKernelGGL(round_small_f32x4_kernel<16>, dim3(grid_for(nvec, kBlock)), dim3(kBlock), 0, s,
+                     reinterpret_cast<const f32x4*>(host_rows), reinterpret_cast<f32x4*>(dev_rows),
+                     static_cast<int>(K), ld / 4, nvec, static_cast<int>(P & 3), host_w, dev_w, dev_out, host_out);
   rc = launch_status(what);
   if (rc) return rc;
-  e = hipMemcpyAsync(host_out, dev_out, static_cast<size_t>(P) * sizeof(float), hipMemcpyDeviceToHost, s);
-  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  const hipError_t e = hipStreamSynchronize(s);
   if (e != hipSuccess) {
     (void)hipGetLastError();
-    return set_error(-static_cast<int>(e), "%s: fetch failed: %s", what, hipGetErrorString(e));
+    return set_error(-static_cast<int>(e), "%s: %s", what, hipGetErrorString(e));
   }
   return FEDAVG_OK;
 }
