@@ -602,20 +602,26 @@ void launch_vec_split(const void* clients, int K, int64_t ld, int64_t P, const v
   }
 }
 
+// fp16/bf16 schedule from the fp32 one for the same bytes per row.  Each 16-B
+// vector unpacks into 8 fp32 lanes of work, so the deep fp32 batches are cut
+// to stay spill-free -- except the large-P key: there the packed kernel wants
+// the fp32 kernel's 32 x 16-B loads in flight per thread as U8 x C4 (158
+// VGPRs), not U2 x C8 (16 loads): 6,543 vs 5,896 GB/s at K=100 x P=25M bf16
+// and 6,641 vs 6,595 at K=500 x P=11.2M (profiles/sweeps/r01_half_*.jsonl).
+inline int half_key(int key) {
+  switch (key) {
+    case 408: return 804;
+    case 804: case 1604: return 404;
+    case 1601: return 801;
+    default: return key;
+  }
+}
+
 template <class Op, bool NT>
 void launch_vec_nt(const Schedule& sc, const void* clients, int K, int64_t ld, int64_t P, const void* W, void* out,
                    hipStream_t s) {
   int key = sc.unroll * 100 + sc.cols;
-  if constexpr (Op::kLanes == 8) {
-    // fp16/bf16 unpack every 16-B vector into 8 fp32 lanes of work: halve the
-    // rows per batch so the schedule stays spill-free (same bytes per block-step)
-    switch (key) {
-      case 408: key = 208; break;
-      case 804: case 1604: key = 404; break;
-      case 1601: key = 801; break;
-      default: break;
-    }
-  }
+  if constexpr (Op::kLanes == 8) key = half_key(key);
   switch (key) {
     case 408: launch_vec_split<Op, 4, 8, NT>(clients, K, ld, P, W, out, sc.blocks_per_launch, s); break;
     case 208: launch_vec_split<Op, 2, 8, NT>(clients, K, ld, P, W, out, sc.blocks_per_launch, s); break;
@@ -658,6 +664,28 @@ void launch_production_vec(const void* clients, int K, int64_t ld, int64_t P, co
     launch_vec_nt<Op, true>(sc, clients, K, ld, P, W, out, s);
   else
     launch_vec_nt<Op, false>(sc, clients, K, ld, P, W, out, s);
+}
+
+// Benchmarking hook (fedavg_reduce_half_variant): the packed fp16/bf16 kernel
+// with an explicit (rows per batch U, 16-B slices per thread C) schedule,
+// nontemporal loads and round-split at max_blocks blocks per launch.
+template <class Op>
+bool launch_half_variant(int U, int C, const void* clients, int K, int64_t ld, int64_t P, const void* W, void* out,
+                         int bpl, hipStream_t s) {
+  switch (U * 100 + C) {
+    case 208: launch_vec_split<Op, 2, 8, true>(clients, K, ld, P, W, out, bpl, s); return true;
+    case 408: launch_vec_split<Op, 4, 8, true>(clients, K, ld, P, W, out, bpl, s); return true;
+    case 108: launch_vec_split<Op, 1, 8, true>(clients, K, ld, P, W, out, bpl, s); return true;
+    case 404: launch_vec_split<Op, 4, 4, true>(clients, K, ld, P, W, out, bpl, s); return true;
+    case 204: launch_vec_split<Op, 2, 4, true>(clients, K, ld, P, W, out, bpl, s); return true;
+    case 804: launch_vec_split<Op, 8, 4, true>(clients, K, ld, P, W, out, bpl, s); return true;
+    case 802: launch_vec_split<Op, 8, 2, true>(clients, K, ld, P, W, out, bpl, s); return true;
+    case 402: launch_vec_split<Op, 4, 2, true>(clients, K, ld, P, W, out, bpl, s); return true;
+    case 116: launch_vec_split<Op, 1, 16, true>(clients, K, ld, P, W, out, bpl, s); return true;
+    case 216: launch_vec_split<Op, 2, 16, true>(clients, K, ld, P, W, out, bpl, s); return true;
+    case 1601: launch_vec_split<Op, 16, 1, true>(clients, K, ld, P, W, out, bpl, s); return true;
+    default: return false;
+  }
 }
 
 }  // namespace
@@ -782,6 +810,39 @@ int fedavg_reduce_f16(const uint16_t* clients, int64_t K, int64_t P, int64_t ld,
 int fedavg_reduce_bf16(const uint16_t* clients, int64_t K, int64_t P, int64_t ld, const float* weights,
                        uint16_t* out, void* stream) {
   return reduce_half_entry(true, clients, K, P, ld, weights, out, stream, "fedavg_reduce_bf16");
+}
+
+int fedavg_reduce_half_variant(int bf16, const uint16_t* clients, int64_t K, int64_t P, int64_t ld,
+                               const float* weights, uint16_t* out, int unroll, int cols, int max_blocks,
+                               void* stream) {
+  const char* what = "fedavg_reduce_half_variant";
+  int rc = check_common(clients, K, P, ld, weights, out, what);
+  if (rc) return rc;
+  if (P == 0) return FEDAVG_OK;
+  if (!aligned16(clients) || !aligned16(out) || (ld % 8) != 0)
+    return set_error(FEDAVG_EALIGN, "%s: needs 16-B aligned clients/out and ld %% 8 == 0", what);
+  const int bpl = max_blocks > 0 ? max_blocks : (1 << 30);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const bool ok = bf16 ? launch_half_variant<OpHalfPk<BF16Pk>>(unroll, cols, clients, static_cast<int>(K), ld, P,
+                                                               weights, out, bpl, s)
+                       : launch_half_variant<OpHalfPk<F16Pk>>(unroll, cols, clients, static_cast<int>(K), ld, P,
+                                                              weights, out, bpl, s);
+  if (!ok) return set_error(FEDAVG_EMODE, "%s: unsupported unroll=%d cols=%d", what, unroll, cols);
+  return launch_status(what);
+}
+
+int fedavg_half_schedule(int64_t K, int64_t P, int* unroll, int* cols, int* nontemporal, int* launches) {
+  if (K <= 0 || P < 0) return set_error(FEDAVG_EINVAL, "fedavg_half_schedule: bad sizes");
+  const Schedule sc = choose_schedule(K, P * 2 / 4);  // the fp32 problem with the same bytes per row
+  const int key = half_key(sc.unroll * 100 + sc.cols);
+  const int64_t nvec = (P + 7) / 8;
+  const int64_t span = static_cast<int64_t>(kBlock) * (key % 100);
+  const int64_t blocks = (nvec + span - 1) / span;
+  if (unroll) *unroll = key / 100;
+  if (cols) *cols = key % 100;
+  if (nontemporal) *nontemporal = sc.nt;
+  if (launches) *launches = static_cast<int>((blocks + sc.blocks_per_launch - 1) / sc.blocks_per_launch);
+  return FEDAVG_OK;
 }
 
 int fedavg_reduce_splitk_f32(const float* clients, int64_t K, int64_t P, int64_t ld, const float* weights,
