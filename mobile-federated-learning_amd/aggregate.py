@@ -287,7 +287,7 @@ class DeviceAggregator:
 
     # rows per H2D chunk: big enough to amortise a copy launch, small enough
     # that the first chunk's DMA starts while the host still packs the rest
-    CHUNK_BYTES = 32 << 20
+    CHUNK_BYTES = int(os.environ.get("FEDAVG_CHUNK_BYTES", str(32 << 20)))
     # fp32-only rounds whose rows are at most this many bytes run as ONE native
     # call (fedavg_round_f32): pack, upload, reduce, fetch, wait -- no per-step
     # Python/torch overhead, which is most of a tiny model's round.  Larger
