@@ -225,6 +225,8 @@ class DeviceAggregator:
         self._last: Dict[str, object] = {}
         self._session = None  # weakref to the open RoundSession, if any
         self._table_hint: Optional[KeyTable] = None  # last round's key table (prepare reuses it)
+        # one round at a time per aggregator: the staging buffers are shared
+        self._lock = threading.Lock()
 
     # ------------------------------------------------------------------
     def begin_round(self, template, max_clients: int):
@@ -271,8 +273,10 @@ class DeviceAggregator:
         self._check_no_open_session("aggregate")
         self._table_hint = prep[1]
         acc_dict, table, dicts, weights, ptrs, keepalive = prep
-        results = self._reduce_groups(table, ptrs, weights)
+        with self._lock:
+            results = self._reduce_groups(table, ptrs, weights)
         del keepalive
+        table.forget_tensors()  # retained as the next round's hint and in _last: keep no host tensors
         # weak references: the round's dicts are the caller's (the reference drops
         # them at the next round); a dead or replaced dict simply misses the cache
         try:

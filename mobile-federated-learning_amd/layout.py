@@ -175,6 +175,15 @@ class KeyTable:
             ptrs[i] = [t.data_ptr() for t in ts]
         return ptrs, keepalive
 
+    def forget_tensors(self) -> "KeyTable":
+        """Replace the template tensors (client 0's, kept for the native walk's
+        shape/dtype checks) by meta tensors of the same shapes and dtypes, so a
+        table retained across rounds does not keep a round's host tensors
+        alive.  Idempotent; returns self."""
+        if self._template and self._template[0].device.type != "meta":
+            self._template = [torch.empty(e.shape, dtype=e.src_dtype, device="meta") for e in self.entries]
+        return self
+
     def try_collect(self, state_dicts: Sequence[Mapping[str, torch.Tensor]]):
         """:meth:`collect` for a table reused from an earlier round: the
         ``(ptrs, keepalive)`` pair when client 0 has exactly this table's keys

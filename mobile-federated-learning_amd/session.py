@@ -134,6 +134,7 @@ class RoundSession:
             for name, t in self.table.unpack(g, out_host).items():
                 acc_dict[name] = t
         self._keepalive.clear()
+        self.table.forget_tensors()
         # leave the round's device rows + averaged model for client_distances (:291)
         try:
             self.agg._last = {"table": self.table, "K": K, "dev": dev_state,
