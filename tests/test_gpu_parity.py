@@ -383,12 +383,12 @@ def test_sharded_reducer_host_out():
         ShardedReducer(K, P, device=DEV, host_out=torch.empty(P))  # not pinned
 
 
-@pytest.mark.parametrize("ws,chunks", [(1, 3), (2, 1), (3, 4), (8, 8)])
-def test_upload_segments_strided_dma(ws, chunks):
+@pytest.mark.parametrize("ws,chunks,K", [(1, 3, 7), (2, 1, 7), (3, 4, 7), (8, 8, 7), (3, 2, 1)])
+def test_upload_segments_strided_dma(ws, chunks, K):
     """SURVEY 8e input distribution: every rank's column segments of a pinned
     host [K, P] buffer land in its device rows via one strided DMA each."""
     from mfl_amd.distributed import plan_shards, upload_segments
-    K, P = 7, 300_007
+    P = 300_007
     host = torch.randn((K, P)).pin_memory()
     seen = torch.zeros(P, dtype=torch.int32)
     for r in range(ws):
