@@ -73,6 +73,41 @@ int fedavg_reduce_tiled_f32(const float* tiles, int64_t K, int64_t P, const floa
  */
 int fedavg_probe_cvt16(const uint32_t* in, int64_t n, int mode, uint16_t* out, void* stream);
 
+/*
+ * Packed fp16 (bf16 = 0) / bf16 (bf16 = 1) exact kernel with an explicit
+ * schedule: unroll rows per batch x cols 16-B slices (8 halves) per thread,
+ * (U, C) in {(1,8), (2,8), (4,8), (2,4), (4,4), (8,4), (4,2), (8,2), (1,16),
+ * (2,16), (16,1)}; nontemporal loads; round-split launches of <= max_blocks
+ * blocks (0 = one launch).  Same bits as fedavg_reduce_f16 / _bf16.
+ * fedavg_half_schedule reports the production choice for [K, P].
+ */
+int fedavg_reduce_half_variant(int bf16, const uint16_t* clients, int64_t K, int64_t P, int64_t ld,
+                               const float* weights, uint16_t* out, int unroll, int cols, int max_blocks,
+                               void* stream);
+int fedavg_half_schedule(int64_t K, int64_t P, int* unroll, int* cols, int* nontemporal, int* launches);
+
+/*
+ * Distance pass (fedavg_client_sqdist_f32) with an explicit schedule: unroll
+ * client rows per batch x cols 16-B slices per thread ((4,4), (8,4), (4,8),
+ * (2,8)), round-split launches of <= max_blocks blocks (0 = one launch).
+ * workspace: fedavg_client_sqdist_workspace(K, P) doubles covers every
+ * variant.  Per-wave partials differ with the schedule, so the fp64 sums may
+ * differ in their last bits between variants (each one is deterministic).
+ */
+int fedavg_client_sqdist_variant(const float* clients, int64_t K, int64_t P, int64_t ld, const float* glob,
+                                 double* workspace, int64_t workspace_elems, double* sumsq, int unroll, int cols,
+                                 int max_blocks, void* stream);
+
+/*
+ * HBM read-ceiling probe (measurement only): stream `nvec` 16-B vectors of a
+ * device buffer with no reduction structure, in `launches` equal launches of
+ * `blocks` workgroups each.  mode 0: grid-stride, nontemporal; 1: one
+ * contiguous range per block, nontemporal; 2: as 1 with default-policy loads.
+ * `sink` needs `blocks` floats (written only on an impossible value match).
+ */
+int fedavg_probe_read_f32x4(const float* buf, int64_t nvec, int mode, int blocks, int launches, float* sink,
+                            void* stream);
+
 #ifdef __cplusplus
 }
 #endif

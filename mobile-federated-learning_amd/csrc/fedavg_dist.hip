@@ -15,12 +15,15 @@ using namespace fedavg_impl;
 // accurate value it approximates.  HBM-read bound like the reduce: 4K+4 B per
 // element.  Thread = C 16-B column slices (slice j at base + tid + 256j).
 // ---------------------------------------------------------------------------
-constexpr int kDistCols = 4;
-constexpr int kDistRows = 4;
-
-__device__ __forceinline__ double sq4(f32x4 d) {
-  return static_cast<double>(d.x) * d.x + static_cast<double>(d.y) * d.y + static_cast<double>(d.z) * d.z +
-         static_cast<double>(d.w) * d.w;
+// acc + the exact squares of d's four lanes, in fp64 with fused multiply-adds
+// (this pass is tolerance-pinned, not bit-pinned: a fused square-add rounds
+// once, so it is closer to the exact sum, and it halves the fp64 work)
+__device__ __forceinline__ double sq4_add(double acc, f32x4 d) {
+  const double x = d.x, y = d.y, z = d.z, w = d.w;
+  acc = __builtin_fma(x, x, acc);
+  acc = __builtin_fma(y, y, acc);
+  acc = __builtin_fma(z, z, acc);
+  return __builtin_fma(w, w, acc);
 }
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -29,12 +32,15 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
+// Block b of a launch covers C*256 column slices starting at slice
+// b*C*256 of that launch's window; its waves write partials at global wave
+// index wave_base + b*4 + wave.  U client rows are loaded per batch.
+template <int U, int C>
 __global__ __launch_bounds__(kBlock) void client_sqdist_f32x4_kernel(
     const f32x4* __restrict__ X, int K, int64_t ld4, int64_t nvec, int tail, const f32x4* __restrict__ G,
-    double* __restrict__ partials, int64_t nwaves) {
-  constexpr int C = kDistCols;
+    double* __restrict__ partials, int64_t nwaves, int64_t wave_base) {
   const int lane = threadIdx.x & 63;
-  const int64_t wave_id = static_cast<int64_t>(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
+  const int64_t wave_id = wave_base + static_cast<int64_t>(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
   const int64_t base = static_cast<int64_t>(blockIdx.x) * kBlock * C + threadIdx.x;
   f32x4 g[C];
   int nv[C];  // valid elements of slice j (0..4): padding lanes never contribute
@@ -47,17 +53,16 @@ __global__ __launch_bounds__(kBlock) void client_sqdist_f32x4_kernel(
     nv[j] = !valid[j] ? 0 : (tail != 0 && v == nvec - 1 ? tail : 4);
   }
   const f32x4* col = X + base;
-  int k = 0;
-  for (; k < K; k += kDistRows) {
-    const int rows = (K - k) < kDistRows ? (K - k) : kDistRows;
-    f32x4 xs[kDistRows][C];
+  for (int k = 0; k < K; k += U) {
+    const int rows = (K - k) < U ? (K - k) : U;
+    f32x4 xs[U][C];
 #pragma unroll
-    for (int u = 0; u < kDistRows; ++u)
+    for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int j = 0; j < C; ++j)
         xs[u][j] = (u < rows && valid[j]) ? ld<true>(col + static_cast<int64_t>(k + u) * ld4 + j * kBlock) : g[j];
 #pragma unroll
-    for (int u = 0; u < kDistRows; ++u) {
+    for (int u = 0; u < U; ++u) {
       if (u >= rows) break;
       double acc = 0.0;
 #pragma unroll
@@ -69,7 +74,7 @@ __global__ __launch_bounds__(kBlock) void client_sqdist_f32x4_kernel(
           d.z = nv[j] > 2 ? d.z : 0.f;
           d.w = 0.f;
         }
-        acc += sq4(d);
+        acc = sq4_add(acc, d);
       }
       acc = wave_sum(acc);
       if (lane == 0) partials[static_cast<int64_t>(k + u) * nwaves + wave_id] = acc;
@@ -93,10 +98,39 @@ __global__ __launch_bounds__(kBlock) void client_sqdist_finalize_kernel(const do
   if (threadIdx.x == 0) out[k] = red[0];
 }
 
-int64_t sqdist_waves(int64_t P) {
+// Production schedule of the distance pass: 32 x 16-B loads in flight per
+// thread (U4 x C8, as the reduce) in one launch; scripts/dist_variants.py
+// (profiles/sweeps/r01_dist_*.jsonl) measured round-split launches within 1 %
+// of it and the first version (U4 x C4) 6 % behind.
+constexpr int kDistCols = 8;
+constexpr int kDistRows = 4;
+constexpr int kDistBlocksPerLaunch = 0;  // one launch: measured 1 % ahead of round-split here
+
+int64_t sqdist_waves_for(int64_t P, int cols) {
   const int64_t nvec = (P + 3) / 4;
-  const int64_t blocks = (nvec + kBlock * kDistCols - 1) / (kBlock * kDistCols);
+  const int64_t blocks = (nvec + kBlock * cols - 1) / (kBlock * cols);
   return blocks * (kBlock / 64);
+}
+
+template <int U, int C>
+void launch_sqdist(const float* clients, int K, int64_t ld, int64_t P, const float* glob, double* partials,
+                   int64_t nwaves, int max_blocks, hipStream_t s) {
+  const int64_t nvec = (P + 3) / 4;
+  const int64_t span = static_cast<int64_t>(kBlock) * C;
+  const int64_t blocks = (nvec + span - 1) / span;
+  const int64_t bpl = max_blocks > 0 ? max_blocks : blocks;
+  const int64_t nl = (blocks + bpl - 1) / bpl;
+  const int64_t per_blocks = (blocks + nl - 1) / nl;  // equal launches, whole blocks each
+  const f32x4* X = reinterpret_cast<const f32x4*>(clients);
+  const f32x4* Gv = reinterpret_cast<const f32x4*>(glob);
+  for (int64_t b0 = 0; b0 < blocks; b0 += per_blocks) {
+    const int64_t nb = (blocks - b0) < per_blocks ? (blocks - b0) : per_blocks;
+    const int64_t v0 = b0 * span;
+    const int64_t n = (nvec - v0) < nb * span ? (nvec - v0) : nb * span;
+    const int tail = (v0 + n == nvec) ? static_cast<int>(P & 3) : 0;
+    hipLaunchKernelGGL((client_sqdist_f32x4_kernel<U, C>), dim3(static_cast<unsigned>(nb)), dim3(kBlock), 0, s,
+                       X + v0, K, ld / 4, n, tail, Gv + v0, partials, nwaves, b0 * (kBlock / 64));
+  }
 }
 
 }  // namespace
@@ -105,25 +139,37 @@ extern "C" {
 
 int64_t fedavg_client_sqdist_workspace(int64_t K, int64_t P) {
   if (K <= 0 || P <= 0) return 0;
-  return K * sqdist_waves(P);
+  return K * sqdist_waves_for(P, 4);  // enough for every variant (cols = 4 has the most waves)
 }
 
 int fedavg_client_sqdist_f32(const float* clients, int64_t K, int64_t P, int64_t ld, const float* glob,
                              double* workspace, int64_t workspace_elems, double* sumsq, void* stream) {
+  return fedavg_client_sqdist_variant(clients, K, P, ld, glob, workspace, workspace_elems, sumsq, kDistRows,
+                                      kDistCols, kDistBlocksPerLaunch, stream);
+}
+
+int fedavg_client_sqdist_variant(const float* clients, int64_t K, int64_t P, int64_t ld, const float* glob,
+                                 double* workspace, int64_t workspace_elems, double* sumsq, int unroll, int cols,
+                                 int max_blocks, void* stream) {
   const char* what = "fedavg_client_sqdist_f32";
   int rc = check_common(clients, K, P, ld, glob, sumsq, what);
   if (rc) return rc;
   if (P == 0) return set_error(FEDAVG_EINVAL, "%s: P must be >= 1", what);
   if (!aligned16(clients) || !aligned16(glob) || (ld % 4) != 0)
     return set_error(FEDAVG_EALIGN, "%s: needs 16-B aligned clients/glob and ld %% 4 == 0", what);
-  const int64_t nwaves = sqdist_waves(P);
+  if (cols != 4 && cols != 8) return set_error(FEDAVG_EMODE, "%s: cols must be 4 or 8", what);
+  const int64_t nwaves = sqdist_waves_for(P, cols);
   if (!workspace || workspace_elems < K * nwaves)
     return set_error(FEDAVG_EINVAL, "%s: workspace needs %lld doubles", what, (long long)(K * nwaves));
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const int64_t nvec = (P + 3) / 4;
-  hipLaunchKernelGGL(client_sqdist_f32x4_kernel, dim3(static_cast<unsigned>(nwaves / (kBlock / 64))), dim3(kBlock),
-                     0, s, reinterpret_cast<const f32x4*>(clients), static_cast<int>(K), ld / 4, nvec,
-                     static_cast<int>(P & 3), reinterpret_cast<const f32x4*>(glob), workspace, nwaves);
+  const int k = static_cast<int>(K);
+  switch (unroll * 100 + cols) {
+    case 404: launch_sqdist<4, 4>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    case 804: launch_sqdist<8, 4>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    case 408: launch_sqdist<4, 8>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    case 208: launch_sqdist<2, 8>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    default: return set_error(FEDAVG_EMODE, "%s: unsupported unroll=%d cols=%d", what, unroll, cols);
+  }
   rc = launch_status(what);
   if (rc) return rc;
   hipLaunchKernelGGL(client_sqdist_finalize_kernel, dim3(static_cast<unsigned>(K)), dim3(kBlock), 0, s, workspace,

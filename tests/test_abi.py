@@ -45,6 +45,17 @@ def test_library_exports_every_declared_symbol(lib):
         assert name in _lib.SIGNATURES, f"{name} declared but not typed in _lib.SIGNATURES"
 
 
+def test_every_exported_entry_point_is_declared(lib):
+    """The reverse direction: no fedavg_* symbol of the .so is missing from
+    include/*.h (the C ABI is exactly what the headers declare)."""
+    import subprocess
+    nm = subprocess.run(["nm", "-D", "--defined-only", str(_lib.library_path())], capture_output=True, text=True,
+                        check=True).stdout
+    exported = sorted({ln.split()[-1] for ln in nm.splitlines() if ln.split() and ln.split()[-1].startswith("fedavg_")})
+    declared = set(declared_functions())
+    assert exported and [n for n in exported if n not in declared] == []
+
+
 def test_library_is_gfx950_code_object():
     data = _lib.library_path().read_bytes()
     assert b"gfx950" in data
