@@ -303,9 +303,17 @@ def main():
         if Path(tj).exists():
             try:
                 tr = json.loads(Path(tj).read_text())
-                roofline["traffic"] = tr.get("hbm_bytes_per_launch")
-                roofline["traffic_source"] = os.path.relpath(tj, ROOT)
-            except (ValueError, OSError):
+                src = os.path.relpath(tj, ROOT)
+                if tr.get("algorithmic_bytes_per_launch") == roofline["bytes_per_launch"]:
+                    roofline["traffic"] = tr.get("hbm_bytes_per_launch")
+                    roofline["traffic_source"] = src
+                elif tr.get("traffic_over_algorithmic"):
+                    # other launch geometry (e.g. N > 1: 8 chunks per rank): the PMC
+                    # traffic/algorithmic ratio of the same kernel, applied to this launch
+                    ratio = float(tr["traffic_over_algorithmic"])
+                    roofline["traffic"] = int(round(ratio * roofline["bytes_per_launch"]))
+                    roofline["traffic_source"] = f"{src} (PMC ratio {ratio} x this launch's algorithmic bytes)"
+            except (ValueError, OSError, KeyError):
                 pass
         out = {
             "metric": METRIC,
