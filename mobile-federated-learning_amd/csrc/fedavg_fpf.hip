@@ -7,8 +7,9 @@
 // operation (no FMA: the library is built with -ffp-contract=off), so
 // local_w_diffs, G_mat, local_itr_lst and LRU_itr_lst are bit-identical.  The
 // two reductions -- global_w_diff.mean() (:319) and the row norms (:272) --
-// accumulate in fp64 in a fixed order and round once; the reference's fp32
-// reductions are within their own rounding error of that value.
+// accumulate in fp64 in a fixed order and round once (the norm's squares with
+// explicit fp64 fused multiply-adds); the reference's fp32 reductions are
+// within their own rounding error of that value.
 //
 // Padding lanes (columns P..ld) never contribute: every load past P is
 // replaced by a select, so whatever the padding holds cannot leak in.
@@ -143,18 +144,38 @@ __global__ __launch_bounds__(kBlock) void fpf_update_g_kernel(float* __restrict_
 // :272, :276-278  fpf[r] = norm(local_w_diffs[r] * A_mat) / G_mat[r], NaN/inf -> 0.
 // One block per row; products rounded to fp32 like the reference's
 // `local_w_diffs * A_mat`, squares and sum in fp64, one rounding at the end.
+__device__ __forceinline__ double sq4_add(double acc, f32x4 q) {
+  const double x = q.x, y = q.y, z = q.z, w = q.w;  // exact squares, one rounding per fused add
+  acc = __builtin_fma(x, x, acc);
+  acc = __builtin_fma(y, y, acc);
+  acc = __builtin_fma(z, z, acc);
+  return __builtin_fma(w, w, acc);
+}
+
+// The row is streamed with 8 x 16-B nontemporal loads in flight per thread
+// (one block per row: 256 threads x 8 = 32 KiB per block-step); A_mat is
+// re-read by every row, so its loads keep the default cache policy.
 __global__ __launch_bounds__(kBlock) void fpf_index_kernel(const f32x4* __restrict__ D, int64_t ld4, int64_t P,
                                                            const f32x4* __restrict__ A, const float* __restrict__ G,
                                                            float* __restrict__ out) {
+  constexpr int U = 8;
   __shared__ double red[kBlock / 64];
   const int64_t r = blockIdx.x;
   const int64_t nvec = (P + 3) / 4;
   const f32x4* row = D + r * ld4;
   double s = 0.0;
-  for (int64_t v = threadIdx.x; v < nvec; v += kBlock) {
-    const f32x4 q = masked(row[v] * A[v], lanes_valid(v, P));
-    s += static_cast<double>(q.x) * q.x + static_cast<double>(q.y) * q.y + static_cast<double>(q.z) * q.z +
-         static_cast<double>(q.w) * q.w;
+  for (int64_t v = threadIdx.x; v < nvec; v += U * kBlock) {
+    // a full batch of U loads per thread, the last one predicated: every
+    // thread keeps U loads in flight even when the row is short (P = 7,850)
+    f32x4 d[U], a[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool in = v + u * kBlock < nvec;
+      d[u] = in ? ld<true>(row + v + u * kBlock) : f32x4{0.f, 0.f, 0.f, 0.f};
+      a[u] = in ? A[v + u * kBlock] : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) s = sq4_add(s, masked(d[u] * a[u], lanes_valid(v + u * kBlock, P)));
   }
   s = block_sum(s, red);
   if (threadIdx.x == 0) {
