@@ -143,6 +143,40 @@ def sampled_parity(red: ShardedReducer, weights, n_windows=6, width=2048):
     return {"ok": True, "columns_checked": checked, "bar": "bit-exact vs oracle (sampled windows)"}
 
 
+def overlap_diagnostics(red: ShardedReducer, w_dev, steps: int, step_elapsed: float, reps: int = 5) -> dict:
+    """N > 1, after the timed region (not part of `value`): the reduce alone
+    and the all-gather alone, each timed like a step (barrier + sync on both
+    sides, max over ranks), so the JSON line shows how much of the exchange
+    the chunked pipeline hides.  overlap = (reduce + gather - step) /
+    min(reduce, gather): 1 = fully hidden, 0 = serialised."""
+    def timed(fn):
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t = torch.tensor([(time.perf_counter() - t0) / reps], dtype=torch.float64, device=red.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item()) * 1e3
+
+    gather = red.gather
+    red.gather = False
+    try:
+        reduce_ms = timed(lambda: red.step(w_dev))
+    finally:
+        red.gather = gather
+    gather_ms = timed(red.gather_only)
+    step_ms = step_elapsed / steps * 1e3
+    return {"reduce_only_ms": round(reduce_ms, 4), "gather_only_ms": round(gather_ms, 4), "step_ms": round(step_ms, 4),
+            "overlap": round((reduce_ms + gather_ms - step_ms) / max(min(reduce_ms, gather_ms), 1e-9), 3),
+            "gather_bytes_in_per_rank": int(red.plan.padded_P - red.plan.local_cols) * 4,
+            "note": "after the timed region; not part of value"}
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
@@ -181,9 +215,11 @@ def main():
     mfl_amd._lib.load()
 
     K, P_local, desc = WORKLOADS[args.workload]
-    # N > 1: 8 chunks, so only 1/8 of the reduce is exposed before the first
-    # all-gather starts (the gather, not the reduce, is the longer of the two)
-    chunks = args.chunks or (1 if world == 1 and not args.host_out else 4 if args.host_out else 8)
+    # N > 1: 4 chunks.  scripts/overlap_probe.py: a
+    # collective-sized kernel hardly runs beside a reduce launch, so chunking
+    # hides ~25 % of the shorter leg, and 8 chunks' smaller launches cost the
+    # reduce more (1.55 vs 1.48 ms) than they hide
+    chunks = args.chunks or (1 if world == 1 and not args.host_out else 4)
     P_total = P_local * world
     host_out = torch.empty(P_total, dtype=torch.float32, pin_memory=True) if args.host_out else None
     # Each rank owns exactly P_local valid columns: plan over the global P.
@@ -268,6 +304,10 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed_max, kernel_ms_max = float(t[0]), float(t[1])
 
+    diagnostics = None
+    if world > 1 and red.gather:
+        diagnostics = overlap_diagnostics(red, w_dev, args.steps, elapsed_max)
+
     parity = sampled_parity(red, weights)
     if world > 1:
         ok = torch.tensor([1.0 if parity["ok"] else 0.0], device=dev)
@@ -344,6 +384,8 @@ def main():
             "roofline": roofline,
             "parity": parity,
         }
+        if diagnostics is not None:
+            out["diagnostics"] = diagnostics
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(P_local)
         print(json.dumps(out), flush=True)

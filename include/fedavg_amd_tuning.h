@@ -108,6 +108,19 @@ int fedavg_client_sqdist_variant(const float* clients, int64_t K, int64_t P, int
 int fedavg_probe_read_f32x4(const float* buf, int64_t nvec, int mode, int blocks, int launches, float* sink,
                             void* stream);
 
+/*
+ * Co-scheduling probes (measurement only).  fedavg_probe_busy_copy: copy
+ * `bytes` with `blocks` workgroups of a kernel holding ~240 VGPRs per wave, a
+ * stand-in for a collective's kernel (RCCL's generic kernel on gfx950 holds
+ * 261 VGPR + 17 AGPR).  fedavg_stream_create_masked: a non-blocking stream
+ * whose kernels may use all CUs but the last `reserve_cus` (hip CU mask), or,
+ * with reserve_cus == 0, a stream of the given priority; destroy it with
+ * fedavg_stream_destroy.
+ */
+int fedavg_probe_busy_copy(const void* src, void* dst, int64_t bytes, int blocks, void* stream);
+int fedavg_stream_create_masked(int reserve_cus, int priority, void** stream);
+int fedavg_stream_destroy(void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -356,6 +356,33 @@ __global__ __launch_bounds__(kBlock) void probe_read_kernel(const f32x4* __restr
   if (acc.x + acc.y + acc.z + acc.w == 1234.5678f) sink[blockIdx.x] = acc.x;
 }
 
+// ---------------------------------------------------------------------------
+// Co-scheduling probe (measurement only): a stand-in for a collective's
+// kernel -- few workgroups, each wave holding ~260 VGPRs like RCCL's generic
+// kernel on gfx950 (261 VGPR + 17 AGPR per its code-object metadata) -- that
+// copies a buffer.  Run next to the reduce it shows whether such a kernel
+// finds room on the CUs while a reduce launch holds them.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock, 1) void probe_busy_copy_kernel(const f32x4* __restrict__ src,
+                                                                   f32x4* __restrict__ dst, int64_t nvec) {
+  constexpr int R = 36;  // float4 registers per thread: ~294 VGPRs per wave, as RCCL's kernel
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+  for (int64_t v0 = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; v0 < nvec; v0 += stride * R) {
+    f32x4 r[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int64_t v = v0 + i * stride;
+      r[i] = v < nvec ? ld<true>(src + v) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int64_t v = v0 + i * stride;
+      if (v < nvec) dst[v] = r[i];
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -420,6 +447,50 @@ int fedavg_probe_read_f32x4(const float* buf, int64_t nvec, int mode, int blocks
     }
   }
   return launch_status(what);
+}
+
+int fedavg_probe_busy_copy(const void* src, void* dst, int64_t bytes, int blocks, void* stream) {
+  const char* what = "fedavg_probe_busy_copy";
+  if (bytes < 0 || blocks <= 0 || (bytes > 0 && (!src || !dst))) return set_error(FEDAVG_EINVAL, "%s: bad arguments", what);
+  if (bytes == 0) return FEDAVG_OK;
+  if (!aligned16(src) || !aligned16(dst) || (bytes % 16) != 0)
+    return set_error(FEDAVG_EALIGN, "%s: 16-B aligned buffers and sizes only", what);
+  hipLaunchKernelGGL(probe_busy_copy_kernel, dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0,
+                     static_cast<hipStream_t>(stream), static_cast<const f32x4*>(src), static_cast<f32x4*>(dst),
+                     bytes / 16);
+  return launch_status(what);
+}
+
+int fedavg_stream_create_masked(int reserve_cus, int priority, void** stream) {
+  const char* what = "fedavg_stream_create_masked";
+  if (!stream || reserve_cus < 0) return set_error(FEDAVG_EINVAL, "%s: bad arguments", what);
+  hipStream_t s = nullptr;
+  hipError_t e;
+  if (reserve_cus == 0) {
+    e = hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority);
+  } else {
+    const int cus = cu_count();
+    if (reserve_cus >= cus) return set_error(FEDAVG_EINVAL, "%s: cannot reserve %d of %d CUs", what, reserve_cus, cus);
+    uint32_t mask[16] = {0};
+    const int nwords = (cus + 31) / 32 > 16 ? 16 : (cus + 31) / 32;
+    for (int c = 0; c < cus - reserve_cus && c < 512; ++c) mask[c / 32] |= 1u << (c % 32);
+    e = hipExtStreamCreateWithCUMask(&s, static_cast<uint32_t>(nwords), mask);
+  }
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return set_error(-static_cast<int>(e), "%s: %s", what, hipGetErrorString(e));
+  }
+  *stream = s;
+  return FEDAVG_OK;
+}
+
+int fedavg_stream_destroy(void* stream) {
+  const hipError_t e = hipStreamDestroy(static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return set_error(-static_cast<int>(e), "fedavg_stream_destroy: %s", hipGetErrorString(e));
+  }
+  return FEDAVG_OK;
 }
 
 }  // extern "C"

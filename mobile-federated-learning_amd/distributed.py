@@ -224,6 +224,18 @@ class ShardedReducer:
             return self.host_out[:plan.P]
         return self.full[:plan.P] if self.gather else None
 
+    def gather_only(self) -> None:
+        """The exchange step alone: all-gather every chunk of ``local_out``
+        (diagnostics: bench.py times it next to the full step)."""
+        if not self.gather:
+            return
+        plan, S = self.plan, self.plan.block
+        works = [dist.all_gather_into_tensor(self.full[c * plan.world_size * S:(c + 1) * plan.world_size * S],
+                                             self.local_out[c * S:(c + 1) * S], group=self.group, async_op=True)
+                 for c in range(plan.chunks)]
+        for w in works:
+            w.wait()
+
     def _to_host(self, c: int) -> None:
         segs = self._chunk_segments[c]
         if self._copy_stream is None:  # CPU (gloo tests): plain copies

@@ -47,6 +47,9 @@ def _worker(rank, ws, port, K, P, chunks, seed, q):
         full = red.step(w)
         expect = O.reduce_f32(host.numpy(), O.sample_weights([int(v) for v in n]))
         ok = full.numpy().tobytes() == expect.tobytes()
+        red.full.zero_()
+        red.gather_only()  # the exchange step alone reassembles the same model
+        ok = ok and red.full[:P].numpy().tobytes() == expect.tobytes()
         q.put((rank, ok, red.plan.valid_local_cols()))
     finally:
         dist.destroy_process_group()
