@@ -202,11 +202,21 @@ class KeyTable:
         ``row0 .. row0+len(ptrs)-1`` of ``group`` (dst offsets in elements from
         the start of the [K, ld] staging buffer)."""
         nc, nk = ptrs.shape[0], len(group.keys)
-        items = np.empty((nc, nk, 4), dtype=np.int64)
-        items[:, :, 0] = ptrs[:, group.key_index]
-        items[:, :, 1] = group.numel
-        items[:, :, 2] = (np.arange(row0, row0 + nc, dtype=np.int64) * ld)[:, None] + group.offset[None, :]
-        items[:, :, 3] = group.kind
+        # the numel / offset / kind columns depend only on the table and the row
+        # range: built once per (row0, rows, ld); only the addresses change per
+        # call.  The array is reused by the next call with the same range, so
+        # it must be consumed (the packer does, synchronously) before then.
+        cache = group.__dict__.setdefault("_items_cache", {})
+        items = cache.get((row0, nc, ld))
+        if items is None:
+            items = np.empty((nc, nk, 4), dtype=np.int64)
+            items[:, :, 1] = group.numel
+            items[:, :, 2] = (np.arange(row0, row0 + nc, dtype=np.int64) * ld)[:, None] + group.offset[None, :]
+            items[:, :, 3] = group.kind
+            if len(cache) >= 256:  # bounded: a session adds one row range per client
+                cache.clear()
+            cache[(row0, nc, ld)] = items
+        np.take(ptrs, group.key_index, axis=1, out=items[:, :, 0])
         return items.reshape(nc * nk, 4)
 
     @property
