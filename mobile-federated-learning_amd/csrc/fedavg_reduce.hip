@@ -501,28 +501,33 @@ struct Schedule {
   int unroll, cols, nt, blocks_per_launch;
 };
 
-constexpr int kBlocksPerLaunch = 768;
+// Round-split launches hold 3 blocks per CU (768 on the 256-CU MI355X); the
+// CU count is read from the device, so a partitioned GPU (fewer CUs per
+// device) keeps one resident round per launch.
+constexpr int kBlocksPerCU = 3;
+inline int blocks_per_launch() { return kBlocksPerCU * cu_count(); }
 
 Schedule choose_schedule(int64_t K, int64_t P) {
   const int64_t nvec = (P + 3) / 4;
-  Schedule sc{8, 1, 1, kBlocksPerLaunch};
+  Schedule sc{8, 1, 1, blocks_per_launch()};
+  const int64_t full = 2 * static_cast<int64_t>(cu_count());  // blocks for a full-chip launch (512 on MI355X)
   if (K <= 4) {
     // a block's work is tiny (K rows): one launch, many short blocks; round
     // splitting would only add launch boundaries (K=2..3 sweeps: +14-22 %)
     sc.cols = 1;
     sc.blocks_per_launch = 1 << 30;
-  } else if (nvec >= int64_t(512) * kBlock * 8) {
+  } else if (nvec >= full * kBlock * 8) {
     sc.unroll = 4, sc.cols = 8;
-  } else if (nvec >= int64_t(512) * kBlock * 4) {
+  } else if (nvec >= full * kBlock * 4) {
     sc.cols = 4;
-  } else if (nvec >= int64_t(512) * kBlock * 2) {
+  } else if (nvec >= full * kBlock * 2) {
     sc.cols = 2;
   } else {
     // short rows: few blocks, so each thread's client chain is the critical
     // path; deeper batches (16 rows) cut its round trips (+11-12 %), and with
     // many clients 4 slices per thread keep 64 loads in flight
     sc.unroll = 16;
-    sc.cols = (K >= 500 && nvec >= int64_t(128) * kBlock * 4) ? 4 : 1;
+    sc.cols = (K >= 500 && nvec >= full / 4 * kBlock * 4) ? 4 : 1;
   }
   const double bytes = 4.0 * static_cast<double>(K) * static_cast<double>(P);
   if (K > 4 && bytes > 64.0 * (1 << 20) && bytes <= 240.0 * (1 << 20)) {
