@@ -153,6 +153,31 @@ def test_reduce_f32_exact_large(K, P):
     assert_bits(out, torch.from_numpy(exp), f"K={K} P={P}")
 
 
+def _schedule_boundary_cases():
+    """(K, P) on both sides of every production-schedule switch: the slice
+    count per thread steps at 2 x CUs x 256 threads x {2, 4, 8} float4
+    columns, the Infinity-Cache band spans 64-240 MiB of client rows, and
+    K <= 4 takes the single-launch path."""
+    full = 2 * torch.cuda.get_device_properties(DEV).multi_processor_count
+    cases = []
+    for c in (2, 4, 8):
+        t = full * 256 * c * 4  # elements at the switch
+        cases += [(5, t - 4), (5, t - 1), (5, t), (5, t + 3)]
+    mib = 1 << 20
+    cases += [(20, 64 * mib // 80 - 3), (20, 64 * mib // 80 + 5), (20, 240 * mib // 80 - 1), (20, 240 * mib // 80 + 7)]
+    cases += [(4, 1_000_003), (5, 1_000_003), (1, 65), (2, 7)]
+    return cases
+
+
+def test_schedule_switch_boundaries_bit_exact():
+    for K, P in _schedule_boundary_cases():
+        x = _clients(K, P, seed=K * 7 + P)
+        w = _weights(K, seed=P)
+        out = mfl_amd.reduce_packed(x, _w(w), P)
+        exp = O.reduce_f32(x[:, :P].cpu().numpy(), w)
+        assert_bits(out, torch.from_numpy(exp), f"K={K} P={P} schedule={mfl_amd._lib.f32_schedule(K, P)}")
+
+
 @pytest.mark.parametrize("unroll", [4, 8, 16])
 @pytest.mark.parametrize("nt", [0, 1])
 def test_tuned_variants_bit_identical(unroll, nt):
