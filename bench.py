@@ -215,11 +215,11 @@ def main():
     mfl_amd._lib.load()
 
     K, P_local, desc = WORKLOADS[args.workload]
-    # N > 1: 4 chunks.  scripts/overlap_probe.py: a
-    # collective-sized kernel hardly runs beside a reduce launch, so chunking
-    # hides ~25 % of the shorter leg, and 8 chunks' smaller launches cost the
-    # reduce more (1.55 vs 1.48 ms) than they hide
-    chunks = args.chunks or (1 if world == 1 and not args.host_out else 4)
+    # N > 1: 8 chunks.  scripts/overlap_probe.py: with a
+    # stand-in for RCCL's kernel that stays resident like an xGMI-bound
+    # all-gather, 8 chunks hide 82-87 % of the shorter leg (4 chunks: 52-70 %)
+    # for gathers of 1.0-3.0 ms per step
+    chunks = args.chunks or (1 if world == 1 and not args.host_out else 4 if args.host_out else 8)
     P_total = P_local * world
     host_out = torch.empty(P_total, dtype=torch.float32, pin_memory=True) if args.host_out else None
     # Each rank owns exactly P_local valid columns: plan over the global P.

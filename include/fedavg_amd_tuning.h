@@ -110,14 +110,15 @@ int fedavg_probe_read_f32x4(const float* buf, int64_t nvec, int mode, int blocks
 
 /*
  * Co-scheduling probes (measurement only).  fedavg_probe_busy_copy: copy
- * `bytes` with `blocks` workgroups of a kernel holding ~240 VGPRs per wave, a
- * stand-in for a collective's kernel (RCCL's generic kernel on gfx950 holds
- * 261 VGPR + 17 AGPR).  fedavg_stream_create_masked: a non-blocking stream
+ * `bytes` with `blocks` workgroups of a kernel holding ~294 registers per
+ * wave, then keep every wave resident until hold_us microseconds after it
+ * started -- a stand-in for a collective's kernel (RCCL's generic kernel on
+ * gfx950 holds 261 VGPR + 17 AGPR; bound by xGMI, it stays resident).  fedavg_stream_create_masked: a non-blocking stream
  * whose kernels may use all CUs but the last `reserve_cus` (hip CU mask), or,
  * with reserve_cus == 0, a stream of the given priority; destroy it with
  * fedavg_stream_destroy.
  */
-int fedavg_probe_busy_copy(const void* src, void* dst, int64_t bytes, int blocks, void* stream);
+int fedavg_probe_busy_copy(const void* src, void* dst, int64_t bytes, int blocks, int hold_us, void* stream);
 int fedavg_stream_create_masked(int reserve_cus, int priority, void** stream);
 int fedavg_stream_destroy(void* stream);
 

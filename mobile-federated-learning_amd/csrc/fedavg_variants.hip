@@ -360,11 +360,15 @@ __global__ __launch_bounds__(kBlock) void probe_read_kernel(const f32x4* __restr
 // Co-scheduling probe (measurement only): a stand-in for a collective's
 // kernel -- few workgroups, each wave holding ~260 VGPRs like RCCL's generic
 // kernel on gfx950 (261 VGPR + 17 AGPR per its code-object metadata) -- that
-// copies a buffer.  Run next to the reduce it shows whether such a kernel
-// finds room on the CUs while a reduce launch holds them.
+// copies a buffer and then, optionally, stays resident for hold_us
+// microseconds (a collective bound by xGMI rather than HBM spends most of its
+// time resident and waiting).  Run next to the reduce it shows whether such a
+// kernel finds room on the CUs while a reduce launch holds them.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock, 1) void probe_busy_copy_kernel(const f32x4* __restrict__ src,
-                                                                   f32x4* __restrict__ dst, int64_t nvec) {
+                                                                   f32x4* __restrict__ dst, int64_t nvec,
+                                                                   uint64_t hold_ticks) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz constant clock
   constexpr int R = 36;  // float4 registers per thread: ~294 VGPRs per wave, as RCCL's kernel
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
   for (int64_t v0 = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; v0 < nvec; v0 += stride * R) {
@@ -381,6 +385,7 @@ __global__ __launch_bounds__(kBlock, 1) void probe_busy_copy_kernel(const f32x4*
       if (v < nvec) dst[v] = r[i];
     }
   }
+  while (__builtin_amdgcn_s_memrealtime() - t0 < hold_ticks) __builtin_amdgcn_s_sleep(32);
 }
 
 }  // namespace
@@ -449,15 +454,15 @@ int fedavg_probe_read_f32x4(const float* buf, int64_t nvec, int mode, int blocks
   return launch_status(what);
 }
 
-int fedavg_probe_busy_copy(const void* src, void* dst, int64_t bytes, int blocks, void* stream) {
+int fedavg_probe_busy_copy(const void* src, void* dst, int64_t bytes, int blocks, int hold_us, void* stream) {
   const char* what = "fedavg_probe_busy_copy";
-  if (bytes < 0 || blocks <= 0 || (bytes > 0 && (!src || !dst))) return set_error(FEDAVG_EINVAL, "%s: bad arguments", what);
-  if (bytes == 0) return FEDAVG_OK;
+  if (bytes < 0 || blocks <= 0 || hold_us < 0 || (bytes > 0 && (!src || !dst)))
+    return set_error(FEDAVG_EINVAL, "%s: bad arguments", what);
   if (!aligned16(src) || !aligned16(dst) || (bytes % 16) != 0)
     return set_error(FEDAVG_EALIGN, "%s: 16-B aligned buffers and sizes only", what);
   hipLaunchKernelGGL(probe_busy_copy_kernel, dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0,
                      static_cast<hipStream_t>(stream), static_cast<const f32x4*>(src), static_cast<f32x4*>(dst),
-                     bytes / 16);
+                     bytes / 16, static_cast<uint64_t>(hold_us) * 100u);
   return launch_status(what);
 }
 

@@ -1,13 +1,17 @@
 """Does a collective-sized kernel find CUs while the reduce runs?  (1 GPU)
 
     python scripts/overlap_probe.py [--K 100] [--cols 25000000] [--reps 8]
+                                    [--hold-us 0] [--copy-frac 1.0]
 
 Mimics one rank of the N=8 P-sharded step on a single MI355X: the exact
 reduce over C column chunks on the compute stream and, after each chunk, a
 stand-in for RCCL's all-gather kernel on a side stream ordered after that
 chunk's reduce.  The stand-in (fedavg_probe_busy_copy) holds ~294 registers
 per wave like RCCL's generic kernel on gfx950 (261 VGPR + 17 AGPR in its code
-object) and copies the 7/8 x chunk bytes one rank receives at N = 8.  A wave
+object) and copies the 7/8 x chunk bytes one rank receives at N = 8 (times
+--copy-frac), then stays resident until --hold-us / C microseconds after it
+started: with a small copy fraction and a hold it behaves like a collective
+bound by xGMI rather than HBM (resident, waiting, light on HBM).  A wave
 that size fits on a SIMD only next to <= 218 registers of other waves, so
 whether it can run beside the reduce depends on the reduce's registers per
 wave x waves per SIMD.
@@ -38,6 +42,10 @@ def main():
     ap.add_argument("--cols", type=int, default=25_000_000)
     ap.add_argument("--reps", type=int, default=8)
     ap.add_argument("--copy-blocks", default="32,64")
+    ap.add_argument("--hold-us", type=int, default=0, help="per step, split over the chunks")
+    ap.add_argument("--copy-frac", type=float, default=1.0)
+    ap.add_argument("--chunk-list", default="4,8")
+    ap.add_argument("--production-only", action="store_true")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -62,7 +70,7 @@ def main():
 
     def step(C, tuned, side, legs, copy_blocks):
         S = cols // C
-        cbytes = 7 * S * 4
+        cbytes = int(7 * S * 4 * args.copy_frac) // 16 * 16
         for c in range(C):
             with torch.cuda.stream(comp):
                 if "r" in legs:
@@ -72,17 +80,19 @@ def main():
             if "c" in legs:
                 side.wait_event(ev)
                 mfl_amd._lib.check(lib.fedavg_probe_busy_copy(src.data_ptr(), dst.data_ptr(), cbytes, copy_blocks,
-                                                              side.cuda_stream), "copy")
+                                                              args.hold_us // C, side.cuda_stream), "copy")
         torch.cuda.current_stream().wait_stream(comp)
         torch.cuda.current_stream().wait_stream(side)
 
     configs = []
-    for C in (4, 8):
+    for C in [int(c) for c in args.chunk_list.split(",")]:
         S = cols // C
         prod = mfl_amd._lib.f32_schedule(K, S)
         scheds = [("production U%d C%d mb768" % (prod["unroll"], prod["cols"]), None),
                   ("U2 C4 mb512", (2, 1, 4, 4, 512)), ("U2 C4 mb768", (2, 1, 4, 4, 768)),
                   ("U2 C8 mb768", (2, 1, 8, 4, 768)), ("U4 C4 mb512", (4, 1, 4, 4, 512))]
+        if args.production_only:
+            scheds = scheds[:1]
         for sname, tuned in scheds:
             configs.append((C, sname, tuned))
     rows = []
@@ -105,7 +115,8 @@ def main():
             assert torch.equal(out, ref), "reduce result changed"
             r = {k: round(float(np.median(v)), 4) for k, v in res.items()}
             serial = r["reduce_only"] + r["copy_only"]
-            row = {"chunks": C, "schedule": sname, "copy_blocks": cb, **r,
+            row = {"chunks": C, "schedule": sname, "copy_blocks": cb, "hold_us": args.hold_us,
+                   "copy_frac": args.copy_frac, **r,
                    "hidden_frac": round((serial - r["overlap"]) / min(r["reduce_only"], r["copy_only"]), 3),
                    "hidden_frac_hiprio": round((serial - r["overlap_hiprio"]) / min(r["reduce_only"], r["copy_only"]), 3)}
             rows.append(row)
