@@ -56,7 +56,36 @@ static py::tuple collect(py::list dicts, py::list names, py::list templ) {
   return py::make_tuple(ptrs, -1, -1);
 }
 
+// unpack(flat, offsets, shapes) -> [views]: view j is flat[offsets[j] :
+// offsets[j] + numel(shapes[j])] shaped shapes[j] -- the averaged model's keys
+// as views of the one host buffer the reduction wrote (the Python loop costs
+// ~3.6 us per key: 1.3 ms for resnet56's 350 keys every round).
+static py::list unpack(const at::Tensor& flat, py::list offsets, py::list shapes) {
+  const Py_ssize_t N = PyList_GET_SIZE(offsets.ptr());
+  if (PyList_GET_SIZE(shapes.ptr()) != N) throw std::invalid_argument("offsets/shapes length mismatch");
+  if (flat.dim() != 1 || !flat.is_contiguous()) throw std::invalid_argument("flat must be a contiguous 1-D tensor");
+  py::list out(N);
+  std::vector<int64_t> size, stride;
+  for (Py_ssize_t j = 0; j < N; ++j) {
+    const int64_t off = PyLong_AsLongLong(PyList_GET_ITEM(offsets.ptr(), j));
+    PyObject* shp = PyList_GET_ITEM(shapes.ptr(), j);
+    const Py_ssize_t nd = PyTuple_GET_SIZE(shp);
+    size.resize(nd);
+    stride.resize(nd);
+    int64_t numel = 1;
+    for (Py_ssize_t d = nd - 1; d >= 0; --d) {
+      size[d] = PyLong_AsLongLong(PyTuple_GET_ITEM(shp, d));
+      stride[d] = numel;
+      numel *= size[d];
+    }
+    if (off < 0 || off + numel > flat.numel()) throw std::out_of_range("unpack: key range outside the buffer");
+    out[j] = flat.as_strided(size, stride, flat.storage_offset() + off);
+  }
+  return out;
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "native state_dict walk for mfl_amd (host metadata only)";
   m.def("collect", &collect, "validate clients against client 0 and gather data pointers");
+  m.def("unpack", &unpack, "views of a flat buffer shaped like the key table's keys");
 }

@@ -258,6 +258,15 @@ class KeyTable:
 
     def unpack(self, group: Group, flat: torch.Tensor) -> "OrderedDict[str, torch.Tensor]":
         """Views of ``flat`` [>=P] shaped as the group's keys (result dtype)."""
+        ext = _collect_ext()
+        if ext is not None and hasattr(ext, "unpack") and flat.dim() == 1 and flat.is_contiguous():
+            meta = group.__dict__.get("_unpack_meta")
+            if meta is None:
+                meta = ([e.name for e in group.keys], [int(e.offset) for e in group.keys],
+                        [tuple(int(d) for d in e.shape) for e in group.keys])
+                group._unpack_meta = meta
+            names, offsets, shapes = meta
+            return OrderedDict(zip(names, ext.unpack(flat, offsets, shapes)))
         out = OrderedDict()
         for e in group.keys:
             out[e.name] = flat[e.offset:e.offset + e.numel].view(e.shape)
