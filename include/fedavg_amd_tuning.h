@@ -99,6 +99,20 @@ int fedavg_client_sqdist_variant(const float* clients, int64_t K, int64_t P, int
                                  int max_blocks, void* stream);
 
 /*
+ * The FPF2 index (:272) as a column-window pass (measurement only): blocks
+ * cover (column window x row group) and leave one fp64 partial per (row,
+ * wave) in `workspace` (fedavg_fpf_index_workspace(n_rows, P) doubles), summed
+ * per row in a fixed order.  unroll rows per batch x cols 16-B slices per
+ * thread ((4,1), (8,1), (16,1), (8,2), (4,4), (8,4), (4,8)); row_groups
+ * blocks along the rows (0 = about 3 blocks per CU).  Measured slower than
+ * the production one-block-per-row fedavg_fpf_index_f32.
+ */
+int64_t fedavg_fpf_index_workspace(int64_t n_rows, int64_t P);
+int fedavg_fpf_index_variant(const float* diffs, int64_t n_rows, int64_t ld, int64_t P, const float* a_mat,
+                             const float* g_mat, float* fpf, double* workspace, int64_t workspace_elems, int unroll,
+                             int cols, int row_groups, void* stream);
+
+/*
  * HBM read-ceiling probe (measurement only): stream `nvec` 16-B vectors of a
  * device buffer with no reduction structure, in `launches` equal launches of
  * `blocks` workgroups each.  mode 0: grid-stride, nontemporal; 1: one

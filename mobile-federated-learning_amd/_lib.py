@@ -39,6 +39,9 @@ SIGNATURES = {
     "fedavg_fpf_update_g": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_float, _c_int, _c_float, _vp]),
     "fedavg_fpf_index_f32": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _vp]),
     "fedavg_fpf_index_lru": (_c_int, [_vp, _vp, _c_i64, _vp, _vp]),
+    "fedavg_fpf_index_workspace": (_c_i64, [_c_i64, _c_i64]),
+    "fedavg_fpf_index_variant": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _c_i64, _c_int, _c_int,
+                                          _c_int, _vp]),
     "fedavg_probe_cvt16": (_c_int, [_vp, _c_i64, _c_int, _vp, _vp]),
     "fedavg_copy_to_host": (_c_int, [_vp, _vp, _c_i64, _c_int, _vp]),
     "fedavg_upload_shard": (_c_int, [_vp, _c_i64, _vp, _c_i64, _c_i64, _c_i64, _vp]),

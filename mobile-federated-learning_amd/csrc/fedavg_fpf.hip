@@ -184,6 +184,90 @@ __global__ __launch_bounds__(kBlock) void fpf_index_kernel(const f32x4* __restri
   }
 }
 
+// :272 as a column-window pass (the reduce's access pattern).  Block
+// (bx, by) covers C*256 column slices of rows [by*R, (by+1)*R) and walks
+// those rows U at a time, so the blocks of a row group read one compact window
+// of the same few rows together; each wave leaves one fp64 partial per row:
+// partials[row][bx*4 + wave].  fpf_index_finalize_kernel then sums a row's
+// partials in a fixed order (deterministic) and applies :272/:276-278.
+template <int U, int C>
+__global__ __launch_bounds__(kBlock) void fpf_index_partials_kernel(const f32x4* __restrict__ D, int64_t ld4,
+                                                                    int64_t n_rows, int64_t P, int64_t rows_per_group,
+                                                                    const f32x4* __restrict__ A,
+                                                                    double* __restrict__ partials, int64_t nwc) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nvec = (P + 3) / 4;
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * kBlock * C + threadIdx.x;
+  const int64_t wave_col = static_cast<int64_t>(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
+  f32x4 a[C];
+  int nv[C];
+#pragma unroll
+  for (int j = 0; j < C; ++j) {
+    const int64_t v = base + static_cast<int64_t>(j) * kBlock;
+    nv[j] = v < nvec ? lanes_valid(v, P) : 0;
+    a[j] = nv[j] > 0 ? A[v] : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const int64_t r0 = static_cast<int64_t>(blockIdx.y) * rows_per_group;
+  const int64_t r1 = (r0 + rows_per_group) < n_rows ? (r0 + rows_per_group) : n_rows;
+  for (int64_t r = r0; r < r1; r += U) {
+    f32x4 d[U][C];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < C; ++j)
+        d[u][j] = (r + u < r1 && nv[j] > 0) ? ld<true>(D + (r + u) * ld4 + base + j * kBlock)
+                                            : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (r + u >= r1) break;
+      double acc = 0.0;
+#pragma unroll
+      for (int j = 0; j < C; ++j) acc = sq4_add(acc, masked(d[u][j] * a[j], nv[j]));
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+      if (lane == 0) partials[(r + u) * nwc + wave_col] = acc;
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void fpf_index_finalize_kernel(const double* __restrict__ partials, int64_t nwc,
+                                                                    int64_t n_rows, const float* __restrict__ G,
+                                                                    float* __restrict__ out) {
+  const int64_t r = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (r >= n_rows) return;
+  double s = 0.0;
+  for (int64_t w = 0; w < nwc; ++w) s += partials[r * nwc + w];
+  const float f = static_cast<float>(sqrt(s)) / G[r];
+  out[r] = isfinite(f) ? f : 0.f;
+}
+
+int64_t index_col_blocks(int64_t P, int cols) {
+  const int64_t nvec = (P + 3) / 4;
+  return (nvec + static_cast<int64_t>(kBlock) * cols - 1) / (static_cast<int64_t>(kBlock) * cols);
+}
+
+// Row groups so that one launch holds about 3 blocks per CU.
+int64_t index_row_groups(int64_t n_rows, int64_t col_blocks) {
+  int64_t g = (3 * static_cast<int64_t>(cu_count()) + col_blocks - 1) / col_blocks;
+  if (g < 1) g = 1;
+  if (g > n_rows) g = n_rows;
+  return g;
+}
+
+template <int U, int C>
+void launch_index_windows(const float* diffs, int64_t n_rows, int64_t ld, int64_t P, const float* a_mat,
+                          const float* g_mat, float* fpf, double* ws, int64_t groups, hipStream_t s) {
+  const int64_t cb = index_col_blocks(P, C);
+  const int64_t nwc = cb * (kBlock / 64);
+  const int64_t rpg = (n_rows + groups - 1) / groups;
+  const int64_t gy = (n_rows + rpg - 1) / rpg;
+  hipLaunchKernelGGL((fpf_index_partials_kernel<U, C>), dim3(static_cast<unsigned>(cb), static_cast<unsigned>(gy)),
+                     dim3(kBlock), 0, s, reinterpret_cast<const f32x4*>(diffs), ld / 4, n_rows, P, rpg,
+                     reinterpret_cast<const f32x4*>(a_mat), ws, nwc);
+  hipLaunchKernelGGL(fpf_index_finalize_kernel, dim3(static_cast<unsigned>((n_rows + kBlock - 1) / kBlock)),
+                     dim3(kBlock), 0, s, ws, nwc, n_rows, g_mat, fpf);
+}
+
 // :274, :276-278  fpf = LRU_itr_lst / G_mat, NaN/inf -> 0.
 __global__ __launch_bounds__(kBlock) void fpf_index_lru_kernel(const float* __restrict__ lru,
                                                                const float* __restrict__ G, int64_t n,
@@ -287,6 +371,38 @@ int fedavg_fpf_index_f32(const float* diffs, int64_t n_rows, int64_t ld, int64_t
   hipLaunchKernelGGL(fpf_index_kernel, dim3(static_cast<unsigned>(n_rows)), dim3(kBlock), 0,
                      static_cast<hipStream_t>(stream), reinterpret_cast<const f32x4*>(diffs), ld / 4, P,
                      reinterpret_cast<const f32x4*>(a_mat), g_mat, fpf);
+  return launch_status(what);
+}
+
+int64_t fedavg_fpf_index_workspace(int64_t n_rows, int64_t P) {
+  if (n_rows <= 0 || P <= 0) return 0;
+  return n_rows * index_col_blocks(P, 1) * (kBlock / 64);  // enough for every column width
+}
+
+int fedavg_fpf_index_variant(const float* diffs, int64_t n_rows, int64_t ld, int64_t P, const float* a_mat,
+                             const float* g_mat, float* fpf, double* workspace, int64_t workspace_elems, int unroll,
+                             int cols, int row_groups, void* stream) {
+  const char* what = "fedavg_fpf_index_variant";
+  int rc = check_state(diffs, n_rows, ld, P, what);
+  if (rc) return rc;
+  if (!a_mat || !g_mat || !fpf || !workspace) return set_error(FEDAVG_EINVAL, "%s: null buffer", what);
+  if (!aligned16(a_mat)) return set_error(FEDAVG_EALIGN, "%s: A_mat must be 16-B aligned", what);
+  if (cols != 1 && cols != 2 && cols != 4 && cols != 8) return set_error(FEDAVG_EMODE, "%s: cols must be 1, 2, 4 or 8", what);
+  const int64_t need = n_rows * index_col_blocks(P, cols) * (kBlock / 64);
+  if (workspace_elems < need) return set_error(FEDAVG_EINVAL, "%s: workspace needs %lld doubles", what, (long long)need);
+  const int64_t groups = row_groups > 0 ? (row_groups < n_rows ? row_groups : n_rows)
+                                        : index_row_groups(n_rows, index_col_blocks(P, cols));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  switch (unroll * 100 + cols) {
+    case 401: launch_index_windows<4, 1>(diffs, n_rows, ld, P, a_mat, g_mat, fpf, workspace, groups, s); break;
+    case 801: launch_index_windows<8, 1>(diffs, n_rows, ld, P, a_mat, g_mat, fpf, workspace, groups, s); break;
+    case 1601: launch_index_windows<16, 1>(diffs, n_rows, ld, P, a_mat, g_mat, fpf, workspace, groups, s); break;
+    case 802: launch_index_windows<8, 2>(diffs, n_rows, ld, P, a_mat, g_mat, fpf, workspace, groups, s); break;
+    case 404: launch_index_windows<4, 4>(diffs, n_rows, ld, P, a_mat, g_mat, fpf, workspace, groups, s); break;
+    case 804: launch_index_windows<8, 4>(diffs, n_rows, ld, P, a_mat, g_mat, fpf, workspace, groups, s); break;
+    case 408: launch_index_windows<4, 8>(diffs, n_rows, ld, P, a_mat, g_mat, fpf, workspace, groups, s); break;
+    default: return set_error(FEDAVG_EMODE, "%s: unsupported unroll=%d cols=%d", what, unroll, cols);
+  }
   return launch_status(what);
 }
 
