@@ -169,6 +169,29 @@ def _schedule_boundary_cases():
     return cases
 
 
+def test_random_shapes_strides_and_offsets_bit_exact():
+    """60 seeded random problems: K in [1, 300], P in [1, 300K], row stride
+    ld >= P with NaN in the padding (it must never leak into a result), the
+    buffer start at a 4/8/12-byte offset now and then (scalar path), and an
+    output written into a larger NaN-filled buffer (nothing outside [0, P))."""
+    rng = np.random.default_rng(2024)
+    for case in range(60):
+        K = int(rng.integers(1, 301))
+        P = int(rng.integers(1, 300_001)) if case % 3 else int(rng.integers(1, 5000))
+        pad = int(rng.choice([0, 1, 3, 4, 60, 64, 1000]))
+        off = int(rng.choice([0, 0, 0, 1, 2, 3]))
+        ld = P + pad + off
+        store = torch.full((K * ld + 8,), float("nan"), device=DEV)
+        x = store[off:off + K * ld].view(K, ld)
+        x[:, :P] = torch.randn((K, P), device=DEV, generator=torch.Generator(device=DEV).manual_seed(case)) * 0.05
+        w = _weights(K, seed=case)
+        big = torch.full((P + 16,), float("nan"), device=DEV)
+        out = mfl_amd.reduce_packed(x, _w(w), P, out=big[4:4 + P])
+        exp = O.reduce_f32(x[:, :P].cpu().numpy(), w)
+        assert_bits(out, torch.from_numpy(exp), f"case {case}: K={K} P={P} ld={ld} off={off}")
+        assert torch.isnan(big[:4]).all() and torch.isnan(big[4 + P:]).all(), f"case {case}: wrote outside out"
+
+
 def test_schedule_switch_boundaries_bit_exact():
     for K, P in _schedule_boundary_cases():
         x = _clients(K, P, seed=K * 7 + P)
