@@ -169,6 +169,44 @@ def _schedule_boundary_cases():
     return cases
 
 
+def test_dropin_random_state_dicts_bit_exact():
+    """30 seeded random rounds through the drop-in: 1-40 clients, 1-12 keys of
+    random shapes (0-d to 4-d), fp32 with int64 / int32 / bool buffers and
+    now and then an fp64, fp16 or bf16 key, sample counts 1..10^6; one
+    aggregator across rounds (staging reuse, key-table reuse and rebuild)."""
+    import copy
+    from collections import OrderedDict
+    rng = np.random.default_rng(77)
+    agg = mfl_amd.DeviceAggregator(DEV)
+    extra = [torch.float64, torch.float16, torch.bfloat16]
+    for case in range(30):
+        K = int(rng.integers(1, 41))
+        keys = []
+        for j in range(int(rng.integers(1, 13))):
+            shape = tuple(int(d) for d in rng.integers(1, 40, size=int(rng.integers(0, 5))))
+            r = rng.random()
+            dt = (torch.float32 if r < 0.7 else torch.int64 if r < 0.8 else torch.int32 if r < 0.85
+                  else torch.bool if r < 0.9 else extra[int(rng.integers(0, 3))])
+            keys.append((f"k{j}", shape, dt))
+        g = torch.Generator().manual_seed(case)
+        w_locals = []
+        for i in range(K):
+            sd = OrderedDict()
+            for name, shape, dt in keys:
+                if dt == torch.bool:
+                    sd[name] = torch.rand(shape, generator=g) > 0.5
+                elif not dt.is_floating_point:
+                    sd[name] = torch.randint(-1000, 1000, shape, generator=g).to(dt)
+                else:
+                    sd[name] = (torch.randn(shape, generator=g) * 0.05).to(dt)
+            w_locals.append((int(rng.integers(1, 10**6)), sd))
+        ref = O.aggregate_torch(copy.deepcopy(w_locals))
+        out = agg.aggregate(w_locals)
+        assert out is w_locals[0][1]
+        for k in ref:
+            assert_bits(out[k], ref[k], f"case {case} key {k}")
+
+
 def test_random_shapes_strides_and_offsets_bit_exact():
     """60 seeded random problems: K in [1, 300], P in [1, 300K], row stride
     ld >= P with NaN in the padding (it must never leak into a result), the
