@@ -125,12 +125,10 @@ def _trivial(w_locals, model_global=None):
 D2H_CHUNK_MIN_COLS = 2 << 20
 D2H_MAX_CHUNKS = 8
 # D2H engine of fedavg_copy_to_host: 0 = the runtime's DMA copy (production:
-# a streaming round's finish at K=100 x P=25M measured 2.67 ms vs 3.0-3.1 ms
-# for the 64-workgroup zero-copy kernel), > 0 = the zero-copy kernel with that
-# grid.  Both go through the C ABI rather than torch's copy_, so torch's
-# pinned-memory cache does not hold the output block behind a copy event (with
-# copy_ the first rounds re-allocated 100 MB of pinned memory: 8-10 ms
-# finishes).  FEDAVG_D2H_BLOCKS overrides it for measurements.
+# a streaming round's finish at K=100 x P=25M measured 2.67 ms in steady state
+# vs 3.0-3.1 ms for the 64-workgroup zero-copy kernel),
+# > 0 = the zero-copy kernel with that grid.  FEDAVG_D2H_BLOCKS overrides it
+# for measurements.
 D2H_BLOCKS = int(os.environ.get("FEDAVG_D2H_BLOCKS", "0"))
 
 
