@@ -200,6 +200,7 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus > 1 needs torch.distributed.run (one process per GPU)")
+        raise SystemExit(f"--gpus {args.gpus} does not match WORLD_SIZE={world} (one process per GPU)")
     # Rehearsal knobs (a 1-GPU box): FEDAVG_DIST_BACKEND=gloo and
     # FEDAVG_SAME_DEVICE=1 run N ranks on cuda:0.  The driver's runs use the
     # defaults: RCCL ("nccl") with one GPU per rank.
