@@ -383,6 +383,9 @@ def main():
                 "launch": "hipGraph replay" if args.graph else "eager (stream-ordered)",
             },
             "roofline": roofline,
+            # the whole step against the node's HBM-read roofline (N x 8 TB/s):
+            # north_star's "fraction of the HBM-read roofline" at N GPUs
+            "step_frac_of_node_hbm": round(value / (world * HBM_PEAK_GBS), 4),
             "parity": parity,
         }
         if diagnostics is not None:
