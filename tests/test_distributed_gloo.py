@@ -71,7 +71,8 @@ def test_sharded_reduce_allgather_matches_oracle(ws, K, P, chunks):
     assert sum(n for _, _, n in results) == P  # every column owned exactly once
 
 
-@pytest.mark.parametrize("P,ws,chunks", [(1, 2, 1), (100, 8, 1), (25_000_000, 8, 4), (11_227_812, 8, 2), (7850, 3, 5)])
+@pytest.mark.parametrize("P,ws,chunks", [(1, 2, 1), (100, 8, 1), (25_000_000, 8, 4), (11_227_812, 8, 2), (7850, 3, 5),
+                                          (200_000_000, 8, 8), (50_000_000, 2, 8), (100_000_000, 4, 8)])
 def test_shard_plan_partitions_columns(P, ws, chunks):
     owned = np.zeros(P, dtype=np.int32)
     for r in range(ws):
