@@ -70,6 +70,12 @@ class RoundSession:
         self._chunks = {g.dtype: column_chunks(g.P) for g in self.table.groups.values()}
         self._ready = {}
         self.add_ms = 0.0
+        # a round whose fp32 rows fit in SMALL_ROUND_BYTES finishes in ONE
+        # native call (fedavg_round_f32 over the rows add() already packed):
+        # its kernel reads them from pinned memory, so add() skips the H2D
+        groups = self.table.groups
+        self._small = (len(groups) == 1 and torch.float32 in groups
+                       and max_clients * groups[torch.float32].ld * 4 <= aggregator.SMALL_ROUND_BYTES)
 
     def add(self, sample_num, state_dict: Mapping[str, torch.Tensor]) -> None:
         """Validate, pack and start uploading one client's row (fedavg_trainer.py:199)."""
@@ -85,6 +91,8 @@ class RoundSession:
             items = self.table.pack_items(g, ptrs, i, g.ld)
             _lib.check(self._lib.fedavg_pack_rows(items.ctypes.data, items.shape[0], st.host.data_ptr(),
                                                   st.host.element_size(), self._threads), "fedavg_pack_rows")
+            if self._small:
+                continue
             events = []
             with torch.cuda.stream(self._copy):
                 for c0, c1 in self._chunks[g.dtype]:
@@ -117,6 +125,8 @@ class RoundSession:
         from .aggregate import reduce_and_fetch, sample_weights
 
         weights = sample_weights(self.counts)  # ZeroDivisionError like the reference
+        if self._small:
+            return self._finish_small(K, weights, acc_dict)
         outs = []
         dev_state = {}
         with torch.cuda.device(self.dev):
@@ -133,6 +143,28 @@ class RoundSession:
         for g, out_host in outs:
             for name, t in self.table.unpack(g, out_host).items():
                 acc_dict[name] = t
+        return self._close(K, dev_state, acc_dict)
+
+    def _finish_small(self, K, weights, acc_dict):
+        """Rows already packed by add(): weights, one kernel, result copy, in one native call."""
+        import numpy as np
+
+        g = self.table.groups[torch.float32]
+        st = self._staging[torch.float32]
+        w64 = np.array([float(w) for w in weights], dtype=np.float64)
+        with torch.cuda.device(self.dev):
+            self._compute.wait_stream(self._copy)  # earlier users of the device staging are done
+            out_dev = torch.empty(g.P, dtype=torch.float32, device=self.dev)
+            out_host = torch.empty(g.P, dtype=torch.float32, pin_memory=True)
+            _lib.check(self._lib.fedavg_round_f32(None, 0, st.host.data_ptr(), st.dev.data_ptr(), K, g.P, g.ld,
+                                                  w64.ctypes.data, st.w_host.data_ptr(), st.w_dev.data_ptr(),
+                                                  out_dev.data_ptr(), out_host.data_ptr(), self._threads,
+                                                  self._compute.cuda_stream), "fedavg_round_f32")
+        for name, t in self.table.unpack(g, out_host).items():
+            acc_dict[name] = t
+        return self._close(K, {torch.float32: (st.dev[:K], out_dev)}, acc_dict)
+
+    def _close(self, K, dev_state, acc_dict):
         self._keepalive.clear()
         self.table.forget_tensors()
         # leave the round's device rows + averaged model for client_distances (:291)

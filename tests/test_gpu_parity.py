@@ -562,17 +562,27 @@ def test_copy_to_host_rejects_pageable_memory():
     assert rc == -10001
 
 
-def test_round_session_streaming_matches_golden():
-    for name in ["mnist_lr_k100", "resnet_like_bn_k5", "int_dtypes_k3", "float64_key_k3", "bfloat16_key_k3"]:
+@pytest.mark.parametrize("small_bytes", [None, 0])  # one-call finish for small fp32 rounds / chunked path
+def test_round_session_streaming_matches_golden(small_bytes):
+    small_seen = 0
+    for name in ["mnist_lr_k100", "mnist_lr_k10", "resnet_like_bn_k5", "int_dtypes_k3", "float64_key_k3",
+                 "bfloat16_key_k3", "flat_k10_p65", "single_client_k1", "ieee_specials_k4", "subnormal_products_k3",
+                 "adversarial_k10", "float_counts_k4"]:
         meta, w_locals, expected = load_case(name)
         agg = mfl_amd.DeviceAggregator(DEV)
+        if small_bytes is not None:
+            agg.SMALL_ROUND_BYTES = small_bytes
         sess = agg.begin_round(w_locals[0][1], len(w_locals) + 3)
+        groups = sess.table.groups
+        assert sess._small == (small_bytes is None and list(groups) == [torch.float32])
+        small_seen += sess._small
         for n, sd in w_locals:
             sess.add(n, sd)
         out = sess.finish(w_locals)
         assert out is w_locals[0][1]
         for k, exp in expected.items():
             assert_bits(out[k], exp, f"{name}/{k}")
+    assert small_seen >= (4 if small_bytes is None else 0)
 
 
 def test_round_session_checks_w_locals():
