@@ -226,6 +226,22 @@ int fedavg_round_f32(const fedavg_pack_item* items, int64_t n_items, float* host
                      int64_t P, int64_t ld, const double* weights, float* host_w, float* dev_w, float* dev_out,
                      float* host_out, int n_threads, void* stream);
 
+/*
+ * Device-resident clients: the reference's aggregate (fedavg_trainer.py:441-458)
+ * reduces whatever device its state_dicts live on; when the clients' tensors
+ * are already in HBM (client.py:96 without the .cpu()), this packs them into
+ * the [K, ld] rows with ONE kernel instead of a host walk.  Same item list and
+ * conversions as fedavg_pack_rows, but every item's src must be device memory
+ * of the current device and dst_base is the device staging buffer.  The item
+ * table and a chunk prefix sum are written to host_ws (pinned) and copied to
+ * dev_ws (device) on `stream`, both of fedavg_pack_rows_device_workspace(n_items)
+ * bytes, 16-B aligned; host_ws must not be rewritten until `stream` has passed
+ * this call.  Stream-ordered and asynchronous.  Returns 0 or a negative code.
+ */
+int64_t fedavg_pack_rows_device_workspace(int64_t n_items);
+int fedavg_pack_rows_device(const fedavg_pack_item* items, int64_t n_items, void* dst_base, int64_t elem_size,
+                            void* host_ws, void* dev_ws, int64_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -176,23 +176,33 @@ class _Staging:
 
     def __init__(self, K: int, ld: int, dtype: torch.dtype, device: torch.device):
         self.K, self.ld, self.dtype = K, ld, dtype
-        self.host = torch.empty((K, ld), dtype=dtype, pin_memory=True)
+        self._host = None  # pinned rows, allocated on first use (device-resident clients never need them)
         self.dev = torch.empty((K, ld), dtype=dtype, device=device)
         wdt = torch.float64 if dtype == torch.float64 else torch.float32
         self.w_host = torch.empty(K, dtype=wdt, pin_memory=True)
         self.w_dev = torch.empty(K, dtype=wdt, device=device)
+        self._w_done = torch.cuda.Event()  # the last weight copy has read w_host
+
+    @property
+    def host(self) -> torch.Tensor:
+        if self._host is None:
+            self._host = torch.empty((self.K, self.ld), dtype=self.dtype, pin_memory=True)
+        return self._host
 
     def upload_weights(self, weights: Sequence[float], stream) -> torch.Tensor:
         """``weights`` (the reference's Python doubles n_i / N) rounded once to
         the group's weight dtype (round to nearest even: the cast ATen applies
-        to the scalar at fedavg_trainer.py:455) and copied on ``stream``.  The
-        caller synchronizes before the next call rewrites the pinned buffer."""
+        to the scalar at fedavg_trainer.py:455) and copied on ``stream``.
+        Waits for the previous call's copy before rewriting the pinned buffer
+        (a device-resident round returns without synchronizing)."""
         import numpy as np
 
         K = len(weights)
+        self._w_done.synchronize()
         self.w_host[:K].numpy()[:] = np.array([float(w) for w in weights], dtype=np.float64)
         with torch.cuda.stream(stream):
             self.w_dev[:K].copy_(self.w_host[:K], non_blocking=True)
+        self._w_done.record(stream)
         return self.w_dev[:K]
 
 
@@ -223,6 +233,7 @@ class DeviceAggregator:
         self._last: Dict[str, object] = {}
         self._session = None  # weakref to the open RoundSession, if any
         self._table_hint: Optional[KeyTable] = None  # last round's key table (prepare reuses it)
+        self._pack_ws = None  # (pinned, device, event) item table of fedavg_pack_rows_device
         # one round at a time per aggregator: the staging buffers are shared
         self._lock = threading.Lock()
 
@@ -271,8 +282,12 @@ class DeviceAggregator:
         self._check_no_open_session("aggregate")
         self._table_hint = prep[1]
         acc_dict, table, dicts, weights, ptrs, keepalive = prep
+        on_device = self._client_device(table, dicts).type == "cuda"
         with self._lock:
-            results = self._reduce_groups(table, ptrs, weights)
+            if on_device:
+                results = self._reduce_groups_device(table, ptrs, weights)
+            else:
+                results = self._reduce_groups(table, ptrs, weights)
         del keepalive
         table.forget_tensors()  # retained as the next round's hint and in _last: keep no host tensors
         # weak references: the round's dicts are the caller's (the reference drops
@@ -286,6 +301,55 @@ class DeviceAggregator:
         for e in table.entries:
             acc_dict[e.name] = results[e.name]
         return acc_dict
+
+    def _client_device(self, table: KeyTable, dicts) -> torch.device:
+        dev = table.client_device(dicts)
+        if dev.type == "cuda" and dev != self.device:
+            raise ValueError(f"the clients' tensors are on {dev}; this aggregator runs on {self.device}")
+        return dev
+
+    def _pack_on_device(self, table: KeyTable, g, ptrs, row0: int, dst: torch.Tensor, stream) -> None:
+        """Rows ``row0 ..`` of ``dst`` [K, ld] from device-resident clients
+        ``ptrs``: one fedavg_pack_rows_device launch on ``stream``."""
+        lib = _lib.load()
+        items = table.pack_items(g, ptrs, row0, g.ld)
+        n = items.shape[0]
+        need = lib.fedavg_pack_rows_device_workspace(n)
+        ws = self._pack_ws
+        if ws is not None:
+            ws[2].synchronize()  # the previous pack has consumed its item table
+        if ws is None or ws[0].numel() < need:
+            cap = max(need, 1 << 16)
+            ws = (torch.empty(cap, dtype=torch.uint8, pin_memory=True),
+                  torch.empty(cap, dtype=torch.uint8, device=self.device), torch.cuda.Event())
+            self._pack_ws = ws
+        _lib.check(lib.fedavg_pack_rows_device(items.ctypes.data, n, dst.data_ptr(), dst.element_size(),
+                                               ws[0].data_ptr(), ws[1].data_ptr(), ws[0].numel(),
+                                               stream.cuda_stream), "fedavg_pack_rows_device")
+        ws[2].record(stream)
+
+    def _reduce_groups_device(self, table: KeyTable, ptrs, weights) -> "OrderedDict[str, torch.Tensor]":
+        """Device-resident clients: pack in HBM, reduce, and return the averaged
+        model as device tensors on the current stream (no host round trip, no
+        synchronization: like the reference's torch ops on device tensors)."""
+        K, dev = ptrs.shape[0], self.device
+        t0 = time.perf_counter()
+        results: "OrderedDict[str, torch.Tensor]" = OrderedDict()
+        with torch.cuda.device(dev):
+            compute = torch.cuda.current_stream(dev)
+            if self._copy_stream is not None:
+                compute.wait_stream(self._copy_stream)  # earlier users of the staging are done
+            self._last = {"table": table, "K": K, "dev": {}}
+            for g in table.groups.values():
+                st = self._staging_for(g.dtype, K, g.ld)
+                self._pack_on_device(table, g, ptrs, 0, st.dev, compute)
+                w_dev = st.upload_weights(weights, compute)
+                out_dev = torch.empty(g.P, dtype=g.dtype, device=dev)
+                reduce_packed(st.dev[:K], w_dev, g.P, out_dev)
+                self._last["dev"][g.dtype] = (st.dev[:K], out_dev)
+                results.update(table.unpack(g, out_dev))
+        self.last_profile = {"pack_issue_ms": (time.perf_counter() - t0) * 1e3, "h2d_kernel_d2h_ms": 0.0}
+        return results
 
     # rows per H2D chunk: big enough to amortise a copy launch, small enough
     # that the first chunk's DMA starts while the host still packs the rest
@@ -427,10 +491,18 @@ class DeviceAggregator:
         g = table.groups[torch.float32]
         K = len(w_locals)
         rows = [sd if sd is not w_glob else template for _, sd in w_locals]  # aliased rows are overridden
-        ptrs, keep = table.collect(rows)
+        cdev = self._client_device(table, rows)
+        ptrs, keep = table.collect(rows, cdev)
         gtable = KeyTable(w_glob)
-        gptrs, gkeep = gtable.collect([w_glob])
+        gptrs, gkeep = gtable.collect([w_glob], cdev)  # w - w_glob needs one device (TypeError otherwise)
         gg = gtable.groups[torch.float32]
+        if cdev.type == "cuda":
+            dev = torch.empty((K + 1, g.ld), dtype=torch.float32, device=self.device)
+            stream = torch.cuda.current_stream(self.device)
+            self._pack_on_device(table, g, ptrs, 0, dev, stream)
+            self._pack_on_device(gtable, gg, gptrs, K, dev, stream)
+            del keep, gkeep
+            return dev[:K], dev[K], g.P
         lib = _lib.load()
         host = torch.empty((K + 1, g.ld), dtype=torch.float32, pin_memory=True)
         items = table.pack_items(g, ptrs, 0, g.ld)
@@ -469,6 +541,10 @@ def aggregate(w_locals, model_global=None, device: Optional[torch.device] = None
     done, answer = _trivial(w_locals, model_global)
     if done:
         return answer  # answered on the host: no GPU needed
+    if device is None:  # device-resident clients are reduced on their own device
+        first = next(iter(w_locals[0][1].values()))
+        if isinstance(first, torch.Tensor) and first.is_cuda:
+            device = first.device
     return default_aggregator(device).aggregate(w_locals, model_global=model_global)
 
 

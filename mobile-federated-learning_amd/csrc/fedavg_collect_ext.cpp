@@ -6,9 +6,10 @@
 // 0.75 us per tensor (26 ms for resnet56 x 100 clients, 35,000 tensors); here
 // the dict lookups and tensor metadata are read through the torch C++ API.
 //
-// collect(dicts, names, template) -> (ptrs[K, N] int64, bad_client, bad_key)
+// collect(dicts, names, template, device_index=-1) -> (ptrs[K, N] int64, bad_client, bad_key)
 //   template[j] is client 0's tensor for names[j].  A client tensor passes
-//   when it has the template's sizes and dtype and is a contiguous CPU tensor.
+//   when it has the template's sizes and dtype and is contiguous, on the host
+//   (device_index -1) or on HIP device `device_index` (device-resident clients).
 //   On the first one that does not (or a missing key), the scan stops and
 //   returns its (client, key) index so the Python layer can raise the
 //   reference's exception or take its general path; otherwise (-1, -1).
@@ -19,7 +20,7 @@
 
 namespace py = pybind11;
 
-static py::tuple collect(py::list dicts, py::list names, py::list templ) {
+static py::tuple collect(py::list dicts, py::list names, py::list templ, int64_t device_index) {
   const Py_ssize_t K = PyList_GET_SIZE(dicts.ptr());
   const Py_ssize_t N = PyList_GET_SIZE(names.ptr());
   if (PyList_GET_SIZE(templ.ptr()) != N) throw std::invalid_argument("template/names length mismatch");
@@ -45,7 +46,8 @@ static py::tuple collect(py::list dicts, py::list names, py::list templ) {
       bool ok = THPVariable_Check(t);
       if (ok) {
         const at::Tensor& ten = THPVariable_Unpack(t);
-        ok = ten.scalar_type() == dtypes[j] && ten.sizes() == c10::IntArrayRef(sizes[j]) && ten.is_cpu() &&
+        const bool where = device_index < 0 ? ten.is_cpu() : (ten.is_cuda() && ten.get_device() == device_index);
+        ok = ten.scalar_type() == dtypes[j] && ten.sizes() == c10::IntArrayRef(sizes[j]) && where &&
              ten.is_contiguous();
         if (ok) out[i * N + j] = reinterpret_cast<int64_t>(ten.data_ptr());
       }
@@ -86,6 +88,7 @@ static py::list unpack(const at::Tensor& flat, py::list offsets, py::list shapes
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "native state_dict walk for mfl_amd (host metadata only)";
-  m.def("collect", &collect, "validate clients against client 0 and gather data pointers");
+  m.def("collect", &collect, "validate clients against client 0 and gather data pointers", py::arg("dicts"),
+        py::arg("names"), py::arg("templ"), py::arg("device_index") = -1);
   m.def("unpack", &unpack, "views of a flat buffer shaped like the key table's keys");
 }

@@ -1,0 +1,241 @@
+// fedavg_pack.hip -- packing DEVICE-resident client state_dicts into the
+// [K, ld] client-major rows the reduction streams.
+//
+// The reference's clients return host state_dicts (client.py:96,
+// `net.cpu().state_dict()`), but its aggregate (fedavg_trainer.py:441-458) is
+// device-agnostic: with the clients' tensors left in HBM (the client trained
+// on this GPU and the caller skipped the .cpu()) it reduces them where they
+// lie.  The host packer (fedavg_host.cpp) cannot read HBM, and one device copy
+// per key costs a launch each (35,000 for resnet56 x 100 clients), so this is
+// the same item list as fedavg_pack_rows executed by ONE kernel.  Like the
+// host packer it balances ELEMENTS, not items: wave w takes elements
+// [w*kPackChunk, (w+1)*kPackChunk) of the items laid end to end (a prefix sum
+// of numel built on the host and shipped with the items), finds its first
+// item with a 64-way search across its lanes (a few probe rounds instead of a
+// 15-level binary search for 35,000 items) and walks the items it overlaps.
+// Waves, not workgroups, are the walkers: a model of many small keys
+// (resnet56: 350 keys, most under 1,000 elements) is bound by the latency of
+// each item's metadata load and copy, so more independent walkers finish it
+// sooner.
+// Raw copies move 16-B vectors: the destination is aligned by a short byte
+// head, the source is then read with dword-aligned global_load_dwordx4 (fp32
+// and fp64 always; fp16/bf16 when source and destination agree mod 4 bytes,
+// element by element otherwise).  Integer/bool sources are converted to fp32
+// element by element with static_cast, as the host packer and ATen's
+// promotion of `int_tensor * python_float` do (fedavg_trainer.py:455); raw
+// items are copied as bit patterns (NaN payloads kept).  HBM-bound: per
+// element, the source bytes read + elem_size bytes written.
+#include "common.hpp"
+
+namespace {
+using namespace fedavg_impl;
+
+constexpr int kPackThreads = 256;                                    // 4 waves per workgroup
+constexpr int kWave = 64;
+constexpr int kPackPer = 16;                                         // scalar loads in flight per lane
+constexpr int kPackVecPer = 8;                                       // 16-B loads in flight per lane
+constexpr int64_t kPackStep = static_cast<int64_t>(kWave) * kPackPer;  // elements per scalar pass
+constexpr int64_t kPackChunk = 4096;                                 // elements per wave
+constexpr int64_t kPackBlockElems = kPackChunk * (kPackThreads / kWave);
+
+enum : int64_t { kRaw = 0, kI64 = 1, kI32 = 2, kI16 = 3, kI8 = 4, kU8 = 5, kBool = 6 };
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef u32x4 u32x4_a4 __attribute__((aligned(4)));  // dword-aligned 16-B source vector
+
+struct Bits {
+  template <typename T>
+  __device__ T operator()(T v) const { return v; }
+};
+struct ToF32 {
+  template <typename T>
+  __device__ float operator()(T v) const { return static_cast<float>(v); }
+};
+struct BoolToF32 {
+  __device__ float operator()(uint8_t v) const { return v ? 1.0f : 0.0f; }
+};
+
+__device__ __forceinline__ int lane_id() { return static_cast<int>(threadIdx.x & (kWave - 1)); }
+
+// n elements src -> dst, converted by op, by one wave
+template <typename S, typename D, typename Op>
+__device__ __forceinline__ void pack_span(const S* __restrict__ src, D* __restrict__ dst, int64_t n, Op op) {
+  const int lane = lane_id();
+  for (int64_t base = 0; base < n; base += kPackStep) {
+    S v[kPackPer];
+#pragma unroll
+    for (int j = 0; j < kPackPer; ++j) {
+      const int64_t e = base + lane + j * kWave;
+      if (e < n) v[j] = __builtin_nontemporal_load(src + e);
+    }
+#pragma unroll
+    for (int j = 0; j < kPackPer; ++j) {
+      const int64_t e = base + lane + j * kWave;
+      if (e < n) dst[e] = op(v[j]);
+    }
+  }
+}
+
+// nb raw bytes src -> dst (elements of es bytes), by one wave
+__device__ __forceinline__ void copy_raw(const char* __restrict__ s, char* __restrict__ d, int64_t nb, int es) {
+  const uintptr_t da = reinterpret_cast<uintptr_t>(d);
+  if (((reinterpret_cast<uintptr_t>(s) - da) & 3u) != 0) {  // cannot be dword-aligned together
+    if (es == 2)
+      pack_span(reinterpret_cast<const uint16_t*>(s), reinterpret_cast<uint16_t*>(d), nb / 2, Bits{});
+    else if (es == 4)
+      pack_span(reinterpret_cast<const uint32_t*>(s), reinterpret_cast<uint32_t*>(d), nb / 4, Bits{});
+    else
+      pack_span(reinterpret_cast<const uint64_t*>(s), reinterpret_cast<uint64_t*>(d), nb / 8, Bits{});
+    return;
+  }
+  int64_t head = static_cast<int64_t>((16u - (da & 15u)) & 15u);
+  if (head > nb) head = nb;
+  const int64_t n16 = (nb - head) >> 4;
+  const int64_t tail0 = head + (n16 << 4);
+  const int lane = lane_id();
+  if (lane < head) d[lane] = s[lane];
+  if (lane < nb - tail0) d[tail0 + lane] = s[tail0 + lane];
+  const u32x4_a4* vs = reinterpret_cast<const u32x4_a4*>(s + head);
+  u32x4* vd = reinterpret_cast<u32x4*>(d + head);
+  for (int64_t base = 0; base < n16; base += static_cast<int64_t>(kWave) * kPackVecPer) {
+    u32x4 v[kPackVecPer];
+#pragma unroll
+    for (int j = 0; j < kPackVecPer; ++j) {
+      const int64_t e = base + lane + j * kWave;
+      if (e < n16) v[j] = __builtin_nontemporal_load(vs + e);
+    }
+#pragma unroll
+    for (int j = 0; j < kPackVecPer; ++j) {
+      const int64_t e = base + lane + j * kWave;
+      if (e < n16) __builtin_nontemporal_store(v[j], vd + e);
+    }
+  }
+}
+
+// the largest i < n_items with start[i] <= g (start nondecreasing, start[0] =
+// 0 <= g): 64 probes per round across the wave, ballot, keep the last hit
+__device__ __forceinline__ int64_t find_item(const int64_t* __restrict__ start, int64_t n_items, int64_t g) {
+  const int lane = lane_id();
+  int64_t lo = 0, hi = n_items;
+  while (hi - lo > 1) {
+    const int64_t step = (hi - lo + 63) / 64;
+    const int64_t idx = lo + lane * step;
+    const bool hit = idx < hi && start[idx] <= g;
+    const unsigned long long m = __ballot(hit);
+    const int last = 63 - __clzll(m);
+    lo += last * step;
+    hi = hi < lo + step ? hi : lo + step;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(kPackThreads) void pack_rows_device_kernel(const fedavg_pack_item* __restrict__ items,
+                                                                        const int64_t* __restrict__ start,
+                                                                        int64_t n_items, int64_t total,
+                                                                        char* __restrict__ dst_base, int es) {
+  const int64_t g0 = static_cast<int64_t>(blockIdx.x) * kPackBlockElems + (threadIdx.x / kWave) * kPackChunk;
+  if (g0 >= total) return;  // a wave past the end of the last workgroup's range
+  const int64_t g1 = total - g0 < kPackChunk ? total : g0 + kPackChunk;
+  for (int64_t i = find_item(start, n_items, g0); i < n_items; ++i) {
+    const int64_t s0 = start[i];
+    if (s0 >= g1) break;
+    const fedavg_pack_item it = items[i];
+    const int64_t a = (g0 > s0 ? g0 : s0) - s0;
+    const int64_t z = (g1 < s0 + it.numel ? g1 : s0 + it.numel) - s0;
+    if (z <= a) continue;
+    const char* src = reinterpret_cast<const char*>(it.src);
+    float* dstf = reinterpret_cast<float*>(dst_base) + it.dst_offset + a;
+    switch (it.kind) {
+      case kRaw: copy_raw(src + a * es, dst_base + (it.dst_offset + a) * es, (z - a) * es, es); break;
+      case kI64: pack_span(reinterpret_cast<const int64_t*>(src) + a, dstf, z - a, ToF32{}); break;
+      case kI32: pack_span(reinterpret_cast<const int32_t*>(src) + a, dstf, z - a, ToF32{}); break;
+      case kI16: pack_span(reinterpret_cast<const int16_t*>(src) + a, dstf, z - a, ToF32{}); break;
+      case kI8: pack_span(reinterpret_cast<const int8_t*>(src) + a, dstf, z - a, ToF32{}); break;
+      case kU8: pack_span(reinterpret_cast<const uint8_t*>(src) + a, dstf, z - a, ToF32{}); break;
+      case kBool: pack_span(reinterpret_cast<const uint8_t*>(src) + a, dstf, z - a, BoolToF32{}); break;
+      default: break;  // rejected on the host
+    }
+  }
+}
+
+bool device_memory(const void* p) {
+  hipPointerAttribute_t attr;
+  if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return attr.type == hipMemoryTypeDevice;
+}
+
+int64_t items_bytes(int64_t n_items) { return n_items * static_cast<int64_t>(sizeof(fedavg_pack_item)); }
+
+}  // namespace
+
+extern "C" {
+
+int64_t fedavg_pack_rows_device_workspace(int64_t n_items) {
+  if (n_items < 0) return -1;
+  return items_bytes(n_items) + (n_items + 1) * static_cast<int64_t>(sizeof(int64_t));
+}
+
+int fedavg_pack_rows_device(const fedavg_pack_item* items, int64_t n_items, void* dst_base, int64_t elem_size,
+                            void* host_ws, void* dev_ws, int64_t ws_bytes, void* stream) {
+  const char* what = "fedavg_pack_rows_device";
+  if (n_items < 0 || (n_items > 0 && (!items || !dst_base || !host_ws || !dev_ws)) ||
+      (elem_size != 2 && elem_size != 4 && elem_size != 8))
+    return set_error(FEDAVG_EINVAL, "%s: bad arguments", what);
+  if (n_items == 0) return FEDAVG_OK;
+  if (ws_bytes < fedavg_pack_rows_device_workspace(n_items))
+    return set_error(FEDAVG_EINVAL, "%s: workspace needs %lld bytes", what,
+                     (long long)fedavg_pack_rows_device_workspace(n_items));
+  if (!aligned16(host_ws) || !aligned16(dev_ws) || !aligned16(dst_base))
+    return set_error(FEDAVG_EALIGN, "%s: dst_base and the workspaces must be 16-B aligned", what);
+  if (!device_memory(dst_base) || !device_memory(dev_ws))
+    return set_error(FEDAVG_EINVAL, "%s: dst_base and dev_ws must be device memory", what);
+  hipPointerAttribute_t attr;
+  if (hipPointerGetAttributes(&attr, host_ws) != hipSuccess || attr.type != hipMemoryTypeHost) {
+    (void)hipGetLastError();
+    return set_error(FEDAVG_EINVAL, "%s: host_ws is not pinned host memory", what);
+  }
+  auto* h_items = static_cast<fedavg_pack_item*>(host_ws);
+  auto* h_start = reinterpret_cast<int64_t*>(static_cast<char*>(host_ws) + items_bytes(n_items));
+  int64_t total = 0;
+  const void* first_src = nullptr;
+  const void* last_src = nullptr;
+  for (int64_t i = 0; i < n_items; ++i) {
+    const fedavg_pack_item& it = items[i];
+    if (it.numel < 0 || it.dst_offset < 0 || it.kind < kRaw || it.kind > kBool || (it.numel > 0 && !it.src) ||
+        (it.kind != kRaw && elem_size != 4))
+      return set_error(FEDAVG_EINVAL, "%s: bad item %lld", what, (long long)i);
+    h_items[i] = it;
+    h_start[i] = total;
+    total += it.numel;
+    if (it.numel > 0) {
+      if (!first_src) first_src = reinterpret_cast<const void*>(it.src);
+      last_src = reinterpret_cast<const void*>(it.src);
+    }
+  }
+  h_start[n_items] = total;
+  if (total == 0) return FEDAVG_OK;
+  const int64_t blocks = (total + kPackBlockElems - 1) / kPackBlockElems;
+  if (blocks > INT32_MAX) return set_error(FEDAVG_EINVAL, "%s: %lld elements exceed one launch", what, (long long)total);
+  // the sources must live in HBM: a host address would fault the kernel
+  // (spot check of the first and last source; the Python layer checks every
+  // tensor's device)
+  if (!device_memory(first_src) || !device_memory(last_src))
+    return set_error(FEDAVG_EINVAL, "%s: item sources must be device memory", what);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const hipError_t e = hipMemcpyAsync(dev_ws, host_ws, static_cast<size_t>(fedavg_pack_rows_device_workspace(n_items)),
+                                      hipMemcpyHostToDevice, s);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return set_error(-static_cast<int>(e), "%s: hipMemcpyAsync failed: %s", what, hipGetErrorString(e));
+  }
+  const auto* d_items = static_cast<const fedavg_pack_item*>(dev_ws);
+  const auto* d_start = reinterpret_cast<const int64_t*>(static_cast<const char*>(dev_ws) + items_bytes(n_items));
+  hipLaunchKernelGGL(pack_rows_device_kernel, dim3(static_cast<unsigned>(blocks)), dim3(kPackThreads), 0, s, d_items,
+                     d_start, n_items, total, static_cast<char*>(dst_base), static_cast<int>(elem_size));
+  return launch_status(what);
+}
+
+}  // extern "C"

@@ -23,7 +23,7 @@ from __future__ import annotations
 
 from collections import OrderedDict
 from dataclasses import dataclass, field
-from typing import Dict, List, Mapping, Sequence, Tuple
+from typing import Dict, List, Mapping, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -140,24 +140,43 @@ class KeyTable:
             g.kind = np.array([0 if e.src_dtype == g.dtype else _PACK_KIND[e.src_dtype] for e in g.keys],
                               dtype=np.int64)
 
-    def collect(self, state_dicts: Sequence[Mapping[str, torch.Tensor]]):
+    def client_device(self, state_dicts: Sequence[Mapping[str, torch.Tensor]]) -> torch.device:
+        """Where the clients' tensors live, read from client 0's first key:
+        the host (client.py:96 returns ``net.cpu().state_dict()``) or one HIP
+        device (clients left in HBM).  :meth:`collect` then requires every
+        tensor of every client to be there."""
+        if not state_dicts or not self._names:
+            return torch.device("cpu")
+        t = state_dicts[0][self._names[0]]  # KeyError, as in the reference
+        if not isinstance(t, torch.Tensor):
+            raise TypeError(f"state_dict entry {self._names[0]!r} is not a tensor")
+        if t.device.type not in ("cpu", "cuda"):
+            raise TypeError(f"state_dict tensors on {t.device} are not supported (host or HIP device only)")
+        return t.device
+
+    def collect(self, state_dicts: Sequence[Mapping[str, torch.Tensor]], device: Optional[torch.device] = None):
         """Validate every client against client 0 and gather source addresses.
 
         Returns ``(ptrs, keepalive)``: ``ptrs`` is an int64 ``[K, n_keys]``
-        array of host data pointers in table order; ``keepalive`` holds
-        contiguous copies made for non-contiguous sources.  Raises like
-        :meth:`validate`.  One list comprehension per attribute per client keeps
-        the per-key Python cost to a few hundred ns.
+        array of data pointers in table order, all on ``device`` (default:
+        :meth:`client_device`); ``keepalive`` holds contiguous copies made for
+        non-contiguous sources.  Raises like :meth:`validate`, and
+        ``TypeError`` for a tensor on another device.  One list comprehension
+        per attribute per client keeps the per-key Python cost to a few
+        hundred ns.
         """
         names, shapes, dtypes = self._names, self._shapes, self._dtypes
+        if device is None:
+            device = self.client_device(state_dicts)
+        dev_index = -1 if device.type == "cpu" else device.index
         ext = _collect_ext()
         if ext is not None:
-            got, bad_i, _bad_j = ext.collect(list(state_dicts), names, self._template)
+            got, bad_i, _bad_j = ext.collect(list(state_dicts), names, self._template, dev_index)
             if got is not None:
                 return got.numpy(), []
             # something unusual at client bad_i (missing key, other shape/dtype,
-            # non-contiguous or non-CPU tensor): the general path below raises
-            # the reference's exception or handles it
+            # non-contiguous tensor or one on another device): the general
+            # path below raises the reference's exception or handles it
         ptrs = np.empty((len(state_dicts), len(names)), dtype=np.int64)
         keepalive = []
         for i, sd in enumerate(state_dicts):
@@ -165,10 +184,9 @@ class KeyTable:
             if [t.shape for t in ts] != shapes or [t.dtype for t in ts] != dtypes:
                 self.validate([sd], first_index=i)
                 raise AssertionError("unreachable")  # validate raised
-            if not all([t.is_cpu for t in ts]):
-                raise TypeError(f"client {i}: state_dict tensors must be host (CPU) tensors, as client.py:96 "
-                                "returns them (net.cpu().state_dict()); use reduce_packed/reduce_tensors for "
-                                "device-resident updates")
+            if not all([t.device == device for t in ts]):
+                raise TypeError(f"client {i}: every state_dict tensor must be on {device}, like client 0's first "
+                                "key (host tensors as client.py:96 returns them, or all on one HIP device)")
             if not all([t.is_contiguous() for t in ts]):
                 ts = [t if t.is_contiguous() else t.contiguous() for t in ts]
                 keepalive.append(ts)
@@ -188,13 +206,15 @@ class KeyTable:
         """:meth:`collect` for a table reused from an earlier round: the
         ``(ptrs, keepalive)`` pair when client 0 has exactly this table's keys
         in this order and every client holds them with the recorded shapes and
-        dtypes as contiguous host tensors (checked by the native walk), else
+        dtypes as contiguous tensors on one device (checked by the native walk), else
         ``None`` -- never raises for a mismatch; the caller then builds a fresh
         table from client 0."""
         ext = _collect_ext()
         if ext is None or not state_dicts or list(state_dicts[0].keys()) != self._names:
             return None
-        got, _, _ = ext.collect(list(state_dicts), self._names, self._template)
+        device = self.client_device(state_dicts)
+        got, _, _ = ext.collect(list(state_dicts), self._names, self._template,
+                                -1 if device.type == "cpu" else device.index)
         return None if got is None else (got.numpy(), [])
 
     def pack_items(self, group: "Group", ptrs: np.ndarray, row0: int, ld: int) -> np.ndarray:

@@ -69,6 +69,7 @@ class RoundSession:
         # events of the latest add tell finish() when chunk c is complete
         self._chunks = {g.dtype: column_chunks(g.P) for g in self.table.groups.values()}
         self._ready = {}
+        self._client_dev = None
         self.add_ms = 0.0
         # a round whose fp32 rows fit in SMALL_ROUND_BYTES finishes in ONE
         # native call (fedavg_round_f32 over the rows add() already packed):
@@ -85,7 +86,27 @@ class RoundSession:
         if i >= self.max_clients:
             raise ValueError(f"more than max_clients={self.max_clients} clients added")
         t0 = time.perf_counter()
-        ptrs, keep = self.table.collect([state_dict])
+        if self._client_dev is None:  # fixed by the first client: host or this aggregator's device
+            self._client_dev = self.agg._client_device(self.table, [state_dict])
+            if self._client_dev.type == "cuda":
+                self._small = False
+        ptrs, keep = self.table.collect([state_dict], self._client_dev)
+        if self._client_dev.type == "cuda":
+            # device-resident client: one packing kernel on the copy stream,
+            # after the work that produced the client's tensors
+            self._copy.wait_stream(torch.cuda.current_stream(self.dev))
+            for g in self.table.groups.values():
+                self.agg._pack_on_device(self.table, g, ptrs, i, self._staging[g.dtype].dev, self._copy)
+        else:
+            self._add_host(i, ptrs)
+        self.counts.append(sample_num)
+        self.dicts.append(state_dict)
+        if keep:
+            self._keepalive.append(keep)
+        self.add_ms += (time.perf_counter() - t0) * 1e3
+
+    def _add_host(self, i, ptrs):
+        """Pack host client ``i`` into its pinned row and start its H2D (unless the round is small)."""
         for g in self.table.groups.values():
             st = self._staging[g.dtype]
             items = self.table.pack_items(g, ptrs, i, g.ld)
@@ -101,11 +122,6 @@ class RoundSession:
                     ev.record(self._copy)
                     events.append(ev)
             self._ready[g.dtype] = events  # the copy stream is FIFO: covers earlier rows too
-        self.counts.append(sample_num)
-        self.dicts.append(state_dict)
-        if keep:
-            self._keepalive.append(keep)
-        self.add_ms += (time.perf_counter() - t0) * 1e3
 
     def finish(self, w_locals=None):
         """Reduce the added clients; ``aggregate``'s contract (fedavg_trainer.py:441-458)."""
@@ -127,6 +143,8 @@ class RoundSession:
         weights = sample_weights(self.counts)  # ZeroDivisionError like the reference
         if self._small:
             return self._finish_small(K, weights, acc_dict)
+        if self._client_dev.type == "cuda":
+            return self._finish_device(K, weights, acc_dict)
         outs = []
         dev_state = {}
         with torch.cuda.device(self.dev):
@@ -163,6 +181,24 @@ class RoundSession:
         for name, t in self.table.unpack(g, out_host).items():
             acc_dict[name] = t
         return self._close(K, {torch.float32: (st.dev[:K], out_dev)}, acc_dict)
+
+    def _finish_device(self, K, weights, acc_dict):
+        """Device-resident clients: the averaged model stays in HBM (device
+        tensors, ordered on the current stream, no host round trip)."""
+        from .reduce import reduce_packed
+
+        dev_state = {}
+        with torch.cuda.device(self.dev):
+            self._compute.wait_stream(self._copy)  # every client's packing kernel
+            for g in self.table.groups.values():
+                st = self._staging[g.dtype]
+                w_dev = st.upload_weights(weights, self._compute)
+                out_dev = torch.empty(g.P, dtype=g.dtype, device=self.dev)
+                reduce_packed(st.dev[:K], w_dev, g.P, out_dev)
+                dev_state[g.dtype] = (st.dev[:K], out_dev)
+                for name, t in self.table.unpack(g, out_dev).items():
+                    acc_dict[name] = t
+        return self._close(K, dev_state, acc_dict)
 
     def _close(self, K, dev_state, acc_dict):
         self._keepalive.clear()

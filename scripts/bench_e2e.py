@@ -12,7 +12,9 @@ two agree bit for bit.  It also times the streaming form (RoundSession):
 clients added one by one as they would arrive from the round loop (with a
 simulated per-client training time, --train-ms, between arrivals), and the
 time from the last arrival to the averaged model (the part left on the
-round's critical path).  One JSON line per config.
+round's critical path).  Last, the same rounds with the clients' tensors
+already on the GPU (device in, device out; see tests/test_gpu_device_clients.py).
+One JSON line per config.
 """
 from __future__ import annotations
 
@@ -155,6 +157,41 @@ def run(name, reps, cpu_aggregate, cpu_distances, train_ms=0.0):
             add_ms.append(sess.add_ms)
     same_stream = all(torch.equal(sout[k].reshape(-1).view(torch.int32), out[k].reshape(-1).view(torch.int32))
                       for k in out)
+    # device-resident clients (client.py:96 without the .cpu()): state_dicts
+    # already in HBM, averaged model returned in HBM -- one packing kernel,
+    # the weights, the reduce; timed to the device result being complete
+    dev = torch.device("cuda", 0)
+    ddicts = [OrderedDict((k, v.to(dev)) for k, v in sd.items()) for sd in dicts]
+    dev_t, dcrit = [], []
+    for r in range(reps + 1):
+        wl = fresh(counts, ddicts)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        dout = agg.aggregate(wl)
+        torch.cuda.synchronize()
+        t = time.perf_counter() - t0
+        if r:
+            dev_t.append(t)
+    same_dev = all(torch.equal(dout[k].cpu().reshape(-1).view(torch.int32), out[k].reshape(-1).view(torch.int32))
+                   for k in out)
+    for r in range(reps + 1):
+        wl = fresh(counts, ddicts)
+        torch.cuda.synchronize()
+        sess = agg.begin_round(wl[0][1], K)
+        for n, sd in wl:
+            if train_ms:
+                time.sleep(train_ms / 1e3)
+            sess.add(n, sd)
+        t0 = time.perf_counter()
+        dsout = sess.finish(wl)
+        torch.cuda.synchronize()
+        t = time.perf_counter() - t0
+        if r:
+            dcrit.append(t)
+    same_dev = same_dev and all(torch.equal(dsout[k].cpu().reshape(-1).view(torch.int32),
+                                            out[k].reshape(-1).view(torch.int32)) for k in out)
+    del ddicts, wl, dout, dsout
+    gd = float(np.median(dev_t))
     same = all(torch.equal(out[k].reshape(-1).view(torch.int32), ref[k].reshape(-1).view(torch.int32)) for k in ref)
     g, c = float(np.median(gpu_t)), float(np.median(cpu_t))
     return {
@@ -170,6 +207,9 @@ def run(name, reps, cpu_aggregate, cpu_distances, train_ms=0.0):
         "stream_add_ms_total_median": round(float(np.median(add_ms)), 3),
         "stream_bit_exact": bool(same_stream),
         "stream_train_ms_per_client": train_ms,
+        "device_clients_ms_median": round(gd * 1e3, 3), "device_clients_GBps": round(alg / gd / 1e9, 2),
+        "device_clients_stream_finish_ms_median": round(float(np.median(dcrit)) * 1e3, 3),
+        "device_clients_bit_exact": bool(same_dev),
         "dist_ms_median": round(float(np.median(dist_t)) * 1e3, 3) if dist_t else None,
         "cpu_dist_ms_median": round(float(np.median(cpu_dist_t)) * 1e3, 3),
         "dist_max_rel_vs_cpu_ref": dist_rel,

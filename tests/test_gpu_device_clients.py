@@ -1,0 +1,245 @@
+"""Device-resident clients: state_dicts whose tensors already live in HBM.
+
+The reference's ``aggregate`` (fedavg_trainer.py:441-458) runs its torch ops
+on whatever device the clients' tensors are on; client.py:96 moves them to the
+host (``net.cpu().state_dict()``), and a GPU-side deployment drops that copy.
+Then the drop-in packs the rows with one kernel (``fedavg_pack_rows_device``)
+and returns device tensors.  Parity bar as everywhere: bit-exact against the
+reference's golden vectors and the torch oracle; the packing kernel is checked
+byte for byte against the host packer (``fedavg_pack_rows``).
+"""
+import copy
+from collections import OrderedDict
+
+import numpy as np
+import pytest
+import torch
+
+import fedavg_oracle as O
+import mfl_amd
+from golden_io import case_names, load_case
+from test_gpu_parity import assert_bits
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda", 0)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu(gpu_available):
+    mfl_amd._lib.load()
+    torch.cuda.set_device(DEV)
+    yield
+
+
+def _to_dev(w_locals):
+    return [(n, OrderedDict((k, v.to(DEV)) for k, v in sd.items())) for n, sd in w_locals]
+
+
+_CASES = [c for c in case_names() if c not in ("empty_w_locals", "no_keys_k2")]
+
+
+@pytest.mark.parametrize("name", _CASES)
+def test_device_clients_match_reference_golden(name):
+    _, w_locals, expected = load_case(name)
+    dl = _to_dev(w_locals)
+    first = dl[0][1]
+    others = [dict(sd) for _, sd in dl[1:]]
+    out = mfl_amd.aggregate(dl)  # the device is taken from the clients' tensors
+    assert out is first
+    assert list(out.keys()) == list(expected.keys())
+    for k, exp in expected.items():
+        assert out[k].device == DEV
+        assert_bits(out[k], exp, f"{name}/{k}")
+    for d, (_, sd) in zip(others, dl[1:]):
+        assert all(d[k] is sd[k] for k in d)
+
+
+@pytest.mark.parametrize("name", ["mnist_lr_k100", "resnet_like_bn_k5", "int_dtypes_k3", "float64_key_k3",
+                                  "bfloat16_key_k3", "float16_key_k3", "ieee_specials_k4", "single_client_k1",
+                                  "int64_nbt_example"])
+def test_device_clients_streaming_session(name):
+    _, w_locals, expected = load_case(name)
+    dl = _to_dev(w_locals)
+    agg = mfl_amd.DeviceAggregator(DEV)
+    sess = agg.begin_round(dl[0][1], len(dl) + 2)
+    for n, sd in dl:
+        sess.add(n, sd)
+    out = sess.finish(dl)
+    assert out is dl[0][1]
+    for k, exp in expected.items():
+        assert out[k].device == DEV
+        assert_bits(out[k], exp, f"{name}/{k}")
+
+
+def test_device_clients_random_rounds_bit_exact():
+    """20 seeded random rounds (1-40 clients, 1-12 keys of random shapes and
+    dtypes incl. int64/int32/int16/int8/uint8/bool buffers and fp64/fp16/bf16
+    keys) through one aggregator, device in, device out, against the torch
+    oracle on the host copies."""
+    rng = np.random.default_rng(91)
+    agg = mfl_amd.DeviceAggregator(DEV)
+    extra = [torch.float64, torch.float16, torch.bfloat16, torch.int16, torch.int8, torch.uint8]
+    for case in range(20):
+        K = int(rng.integers(1, 41))
+        keys = []
+        for j in range(int(rng.integers(1, 13))):
+            shape = tuple(int(d) for d in rng.integers(1, 40, size=int(rng.integers(0, 5))))
+            r = rng.random()
+            dt = (torch.float32 if r < 0.6 else torch.int64 if r < 0.7 else torch.int32 if r < 0.75
+                  else torch.bool if r < 0.8 else extra[int(rng.integers(0, len(extra)))])
+            keys.append((f"k{j}", shape, dt))
+        g = torch.Generator().manual_seed(1000 + case)
+        w_locals = []
+        for i in range(K):
+            sd = OrderedDict()
+            for name, shape, dt in keys:
+                if dt == torch.bool:
+                    sd[name] = torch.rand(shape, generator=g) > 0.5
+                elif dt == torch.uint8:
+                    sd[name] = torch.randint(0, 256, shape, generator=g).to(dt)
+                elif not dt.is_floating_point:
+                    sd[name] = torch.randint(-100, 100, shape, generator=g).to(dt)
+                else:
+                    sd[name] = (torch.randn(shape, generator=g) * 0.05).to(dt)
+            w_locals.append((int(rng.integers(1, 10**6)), sd))
+        ref = O.aggregate_torch(copy.deepcopy(w_locals))
+        out = agg.aggregate(_to_dev(w_locals))
+        for k in ref:
+            assert out[k].device == DEV
+            assert_bits(out[k], ref[k], f"case {case} key {k}")
+
+
+def test_pack_kernel_matches_host_packer():
+    """fedavg_pack_rows_device vs fedavg_pack_rows on the same item list:
+    every kind, empty items, items spanning many 16K-element chunks, odd
+    offsets; compared byte for byte (padding included)."""
+    lib = mfl_amd._lib.load()
+    g = torch.Generator().manual_seed(5)
+    kinds = {0: torch.float32, 1: torch.int64, 2: torch.int32, 3: torch.int16, 4: torch.int8, 5: torch.uint8,
+             6: torch.bool}
+    sizes = [0, 1, 3, 63, 64, 65, 16_383, 16_384, 16_385, 100_003, 1_000_000, 7]
+    srcs_h, items = [], []
+    off = 5
+    for j, n in enumerate(sizes):
+        kind = j % 7
+        dt = kinds[kind]
+        if dt == torch.bool:
+            t = torch.rand(n, generator=g) > 0.5
+        elif dt == torch.float32:
+            t = torch.randn(n, generator=g)
+        elif dt == torch.uint8:
+            t = torch.randint(0, 256, (n,), generator=g).to(dt)
+        else:
+            t = torch.randint(-(2**31), 2**31 - 1, (n,), generator=g).to(dt)
+            if dt == torch.int64:
+                t = t * 4099 + 3  # beyond 2^24: the int64 -> fp32 rounding matters
+        srcs_h.append(t)
+        items.append((kind, off, n))
+        off += n + (j % 3)
+    total = off + 11
+    srcs_d = [t.to(DEV) for t in srcs_h]
+    it_h = np.array([[t.data_ptr(), n, o, k] for t, (k, o, n) in zip(srcs_h, items)], dtype=np.int64)
+    it_d = np.array([[t.data_ptr(), n, o, k] for t, (k, o, n) in zip(srcs_d, items)], dtype=np.int64)
+    host = torch.full((total,), -7.0, dtype=torch.float32)
+    mfl_amd._lib.check(lib.fedavg_pack_rows(it_h.ctypes.data, len(items), host.data_ptr(), 4, 4), "pack")
+    dev = torch.full((total,), -7.0, dtype=torch.float32, device=DEV)
+    need = lib.fedavg_pack_rows_device_workspace(len(items))
+    ws_h = torch.empty(need, dtype=torch.uint8, pin_memory=True)
+    ws_d = torch.empty(need, dtype=torch.uint8, device=DEV)
+    s = torch.cuda.current_stream(DEV)
+    mfl_amd._lib.check(lib.fedavg_pack_rows_device(it_d.ctypes.data, len(items), dev.data_ptr(), 4, ws_h.data_ptr(),
+                                                   ws_d.data_ptr(), need, s.cuda_stream), "pack_device")
+    s.synchronize()
+    assert dev.cpu().view(torch.int32).numpy().tobytes() == host.view(torch.int32).numpy().tobytes()
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float16, torch.bfloat16])
+def test_pack_kernel_raw_other_widths(dtype):
+    lib = mfl_amd._lib.load()
+    esize = torch.empty(0, dtype=dtype).element_size()
+    g = torch.Generator().manual_seed(esize)
+    srcs = [(torch.randn(n, generator=g) * 3).to(dtype).to(DEV) for n in (1, 40_000, 16_384 * 4 + 1, 0, 9)]
+    off, rows = 3, []
+    for t in srcs:
+        rows.append([t.data_ptr(), t.numel(), off, 0])
+        off += t.numel() + 1
+    it = np.array(rows, dtype=np.int64)
+    dev = torch.zeros(off + 2, dtype=dtype, device=DEV)
+    need = lib.fedavg_pack_rows_device_workspace(len(rows))
+    ws_h = torch.empty(need, dtype=torch.uint8, pin_memory=True)
+    ws_d = torch.empty(need, dtype=torch.uint8, device=DEV)
+    mfl_amd._lib.check(lib.fedavg_pack_rows_device(it.ctypes.data, len(rows), dev.data_ptr(), esize, ws_h.data_ptr(),
+                                                   ws_d.data_ptr(), need, None), "pack_device")
+    torch.cuda.synchronize()
+    exp = torch.zeros(off + 2, dtype=dtype)
+    for t, r in zip(srcs, rows):
+        exp[r[2]:r[2] + r[1]] = t.cpu()
+    assert torch.equal(dev.cpu().view(torch.uint8), exp.view(torch.uint8))
+
+
+def test_pack_kernel_rejects_host_sources_and_bad_items():
+    lib = mfl_amd._lib.load()
+    host_src = torch.ones(100)
+    dev = torch.zeros(200, device=DEV)
+    need = lib.fedavg_pack_rows_device_workspace(1)
+    ws_h = torch.empty(need, dtype=torch.uint8, pin_memory=True)
+    ws_d = torch.empty(need, dtype=torch.uint8, device=DEV)
+    it = np.array([[host_src.data_ptr(), 100, 0, 0]], dtype=np.int64)
+    rc = lib.fedavg_pack_rows_device(it.ctypes.data, 1, dev.data_ptr(), 4, ws_h.data_ptr(), ws_d.data_ptr(), need, None)
+    assert rc == -10001  # a host source would fault the kernel: refused before launch
+    d_src = torch.ones(100, device=DEV)
+    bad = np.array([[d_src.data_ptr(), 100, 0, 9]], dtype=np.int64)  # unknown kind
+    rc = lib.fedavg_pack_rows_device(bad.ctypes.data, 1, dev.data_ptr(), 4, ws_h.data_ptr(), ws_d.data_ptr(), need, None)
+    assert rc == -10001
+    pageable = torch.empty(need, dtype=torch.uint8)
+    ok = np.array([[d_src.data_ptr(), 100, 0, 0]], dtype=np.int64)
+    rc = lib.fedavg_pack_rows_device(ok.ctypes.data, 1, dev.data_ptr(), 4, pageable.data_ptr(), ws_d.data_ptr(), need,
+                                     None)
+    assert rc == -10001
+    rc = lib.fedavg_pack_rows_device(ok.ctypes.data, 1, dev.data_ptr(), 4, ws_h.data_ptr(), ws_d.data_ptr(), need - 1,
+                                     None)
+    assert rc == -10001
+    torch.cuda.synchronize()
+    assert float(dev.sum()) == 0.0  # nothing was launched
+
+
+def test_mixed_devices_rejected():
+    _, w_locals, _ = load_case("mnist_lr_k10")
+    dl = _to_dev(w_locals)
+    dl[3] = w_locals[3]  # one client left on the host
+    with pytest.raises(TypeError):
+        mfl_amd.DeviceAggregator(DEV).aggregate(dl)
+    dl = _to_dev(w_locals)
+    dl[0][1]["linear.bias"] = dl[0][1]["linear.bias"].cpu()  # one key of client 0 on the host
+    with pytest.raises(TypeError):
+        mfl_amd.DeviceAggregator(DEV).aggregate(dl)
+
+
+def test_device_clients_distances_cached_and_uncached():
+    _, w_locals, _ = load_case("mnist_lr_k100")
+    ref_locals = copy.deepcopy(w_locals)
+    ref_glob = O.aggregate_torch(ref_locals)
+    exact = O.client_distances_exact(ref_locals, ref_glob)
+    dl = _to_dev(w_locals)
+    agg = mfl_amd.DeviceAggregator(DEV)
+    w_glob = agg.aggregate(dl)
+    norms = agg.client_distances(dl, w_glob)  # rows left in HBM by the aggregate
+    assert norms[0] == 0.0
+    assert np.all(np.abs(norms - exact) <= np.spacing(exact.astype(np.float32)).astype(np.float64))
+    again = mfl_amd.DeviceAggregator(DEV).client_distances(dl, w_glob)  # packed on the device afresh
+    assert np.array_equal(again, norms)
+    host_glob = OrderedDict((k, v.cpu()) for k, v in w_glob.items())
+    with pytest.raises(TypeError):  # w - w_glob across devices
+        mfl_amd.DeviceAggregator(DEV).client_distances(dl[1:], host_glob)
+
+
+def test_device_and_host_rounds_alternate_on_one_aggregator():
+    _, w_locals, expected = load_case("resnet_like_bn_k5")
+    agg = mfl_amd.DeviceAggregator(DEV)
+    for r in range(3):
+        _, wl, _ = load_case("resnet_like_bn_k5")
+        out = agg.aggregate(_to_dev(wl) if r % 2 == 0 else wl)
+        for k, exp in expected.items():
+            assert out[k].device.type == ("cuda" if r % 2 == 0 else "cpu")
+            assert_bits(out[k], exp, f"round {r} {k}")
