@@ -27,6 +27,14 @@ Deliberate tightening: differing shapes or dtypes for one key raise
 Representation difference: the returned tensors of one dtype group are views
 of one freshly allocated host buffer (values and shapes are the reference's;
 ``load_state_dict`` at fedavg_trainer.py:219 copies them out).
+
+Device-resident clients: when the clients' tensors are all on this GPU (a
+deployment that drops client.py:96's ``.cpu()``), the reference's device-
+agnostic loop would compute on the GPU and return GPU tensors; so does the
+drop-in: one packing kernel (``fedavg_pack_rows_device``) gathers the keys into
+the HBM rows, the same reduce runs, and the result comes back as views of a
+device buffer, ordered on the current stream without a host synchronization.
+Clients split between host and device raise ``TypeError``.
 """
 from __future__ import annotations
 

@@ -283,3 +283,26 @@ def test_fpf_tracker_without_gpu_fails_loudly():
         pytest.skip("GPU present")
     with pytest.raises(mfl_amd.FedAvgLibraryError):
         mfl_amd.FPFTracker(4, {"w": torch.zeros(3)}, 2)
+
+
+def test_client_device_and_mixed_device_rejection():
+    """Where the clients live is read from client 0's first key; collect then
+    requires every tensor of every client there (host clients, or all on one
+    HIP device -- checked here with meta tensors standing in for a device)."""
+    _, w_locals, _ = load_case("mnist_lr_k10")
+    dicts = [sd for _, sd in w_locals]
+    table = KeyTable(dicts[0])
+    assert table.client_device(dicts) == torch.device("cpu")
+    ptrs, _ = table.collect(dicts)
+    assert ptrs.shape == (10, 2)
+    mixed = [OrderedDict(sd) for sd in dicts]
+    mixed[4]["linear.bias"] = mixed[4]["linear.bias"].to("meta")
+    with pytest.raises(TypeError, match="client 4"):
+        table.collect(mixed)
+    with pytest.raises(TypeError):
+        prepare([(n, sd) for (n, _), sd in zip(w_locals, mixed)])
+    meta0 = [OrderedDict((k, v.to("meta")) for k, v in dicts[0].items())] + dicts[1:]
+    with pytest.raises(TypeError, match="not supported"):
+        KeyTable(meta0[0]).client_device(meta0)
+    # a retained table never accepts clients on another device than it was asked for
+    assert table.try_collect(mixed) is None
