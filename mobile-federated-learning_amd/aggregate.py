@@ -382,6 +382,7 @@ class DeviceAggregator:
             if self._copy_stream is not None:
                 compute.wait_stream(self._copy_stream)  # earlier users of the staging are done
             st = self._staging_for(g.dtype, K, g.ld)
+            st._w_done.synchronize()  # the native call rewrites w_host: an async device round may still read it
             items = table.pack_items(g, ptrs, 0, g.ld)
             w64 = np.array([float(w) for w in weights], dtype=np.float64)
             out_dev = torch.empty(g.P, dtype=torch.float32, device=dev)

@@ -172,6 +172,7 @@ class RoundSession:
         w64 = np.array([float(w) for w in weights], dtype=np.float64)
         with torch.cuda.device(self.dev):
             self._compute.wait_stream(self._copy)  # earlier users of the device staging are done
+            st._w_done.synchronize()  # the native call rewrites w_host: an async device round may still read it
             out_dev = torch.empty(g.P, dtype=torch.float32, device=self.dev)
             out_host = torch.empty(g.P, dtype=torch.float32, pin_memory=True)
             _lib.check(self._lib.fedavg_round_f32(None, 0, st.host.data_ptr(), st.dev.data_ptr(), K, g.P, g.ld,

@@ -234,12 +234,22 @@ def test_device_clients_distances_cached_and_uncached():
         mfl_amd.DeviceAggregator(DEV).client_distances(dl[1:], host_glob)
 
 
-def test_device_and_host_rounds_alternate_on_one_aggregator():
-    _, w_locals, expected = load_case("resnet_like_bn_k5")
+@pytest.mark.parametrize("name", ["resnet_like_bn_k5", "mnist_lr_k10"])  # pipelined / one-call host rounds
+def test_device_and_host_rounds_alternate_on_one_aggregator(name):
+    """A device round returns before its kernels ran; the host round right
+    after it (no synchronization in between) must not disturb it through the
+    shared staging (weights, rows), and both must be exact."""
+    _, _, expected = load_case(name)
     agg = mfl_amd.DeviceAggregator(DEV)
-    for r in range(3):
-        _, wl, _ = load_case("resnet_like_bn_k5")
-        out = agg.aggregate(_to_dev(wl) if r % 2 == 0 else wl)
-        for k, exp in expected.items():
+    outs = []
+    for r in range(4):
+        _, wl, _ = load_case(name)
+        if r % 2 == 0:  # different weights each round: a stale weight vector would show
+            wl = [(n * (r + 1) if i == 0 else n, sd) for i, (n, sd) in enumerate(wl)]
+        outs.append((r, copy.deepcopy(wl) if r % 2 == 0 else None, agg.aggregate(_to_dev(wl) if r % 2 == 0 else wl)))
+    torch.cuda.synchronize()
+    for r, ref_in, out in outs:
+        exp = O.aggregate_torch(ref_in) if ref_in is not None else expected
+        for k in exp:
             assert out[k].device.type == ("cuda" if r % 2 == 0 else "cpu")
-            assert_bits(out[k], exp, f"round {r} {k}")
+            assert_bits(out[k], exp[k], f"{name} round {r} {k}")
