@@ -137,10 +137,25 @@ class FPFTracker:
             raise IndexError(f"index {r} is out of bounds for dimension 0 with size {self.n}")
         return r + self.n if r < 0 else r
 
+    def _aggregator(self):
+        if self._agg is not None:
+            return self._agg
+        from .aggregate import default_aggregator
+
+        return default_aggregator(self.device)
+
     def _upload(self, table: KeyTable, sd: Mapping[str, torch.Tensor], dst: torch.Tensor) -> None:
-        """Pack one state_dict into the pinned row and copy it to ``dst`` [ld]."""
-        ptrs, keep = table.collect([sd])
+        """Pack one state_dict into the pinned row and copy it to ``dst`` [ld]
+        (a state_dict already on this GPU is packed in HBM by one kernel)."""
+        agg = self._aggregator()
+        where = agg._client_device(table, [sd])  # ValueError for another GPU
+        ptrs, keep = table.collect([sd], where)
         g = table.groups[torch.float32]
+        if where.type == "cuda":
+            with torch.cuda.device(self.device):
+                agg._pack_on_device(table, g, ptrs, 0, dst, torch.cuda.current_stream(self.device))
+            del keep
+            return
         items = table.pack_items(g, ptrs, 0, self.ld)
         with torch.cuda.device(self.device):
             torch.cuda.current_stream(self.device).synchronize()  # the pinned row is free again
@@ -215,12 +230,7 @@ class FPFTracker:
         if not idx:
             return
         self._check_bool()
-        agg = self._agg
-        if agg is None:
-            from .aggregate import default_aggregator
-
-            agg = default_aggregator(self.device)
-        last = agg._last
+        last = self._aggregator()._last
         refs = last.get("refs")
         ok = (refs is not None and last["acc"]() is w_glob and len(refs) == len(w_locals)
               and all(r() is sd for r, (_, sd) in zip(refs, w_locals))
@@ -282,12 +292,7 @@ class FPFTracker:
         self._have_last_w = False
 
     def _glob_on_device(self, w_glob) -> torch.Tensor:
-        agg = self._agg
-        if agg is None:
-            from .aggregate import default_aggregator
-
-            agg = default_aggregator(self.device)
-        last = agg._last
+        last = self._aggregator()._last
         acc = last.get("acc")
         if (acc is not None and acc() is w_glob and set(last.get("dev", {})) == {torch.float32}
                 and [(e.name, e.numel) for e in last["table"].entries]

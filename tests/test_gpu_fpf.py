@@ -54,6 +54,36 @@ class _TrackerImpl:
         self.t.end_round(t, idx, itr, w_glob)
 
 
+class _DeviceTrackerImpl(_TrackerImpl):
+    """The same loop with every state_dict on the GPU (client.py:96 without
+    the .cpu()): last_w, the clients and the aggregate's result."""
+
+    def __init__(self, meta, init):
+        super().__init__(meta, init)
+        self._dev = {}
+
+    def _d(self, sd):
+        if id(sd) not in self._dev:  # keeps sd alive, so the id is not reused
+            self._dev[id(sd)] = (sd, OrderedDict((k, v.to(DEV)) for k, v in sd.items()))
+        return self._dev[id(sd)][1]
+
+    def begin_round(self, last_w):
+        self.t.begin_round(self._d(last_w))
+
+    def record_client(self, c, w, last_w):
+        self.t.record_client(c, self._d(w))
+
+    def record_round(self, idx, w_locals, w_glob):
+        self.t.record_round(idx, [(n, self._d(sd)) for n, sd in w_locals], w_glob)
+
+    def aggregate(self, w_locals, model_state):
+        if not w_locals:
+            return self._d(copy.deepcopy(model_state))
+        out = mfl_amd.aggregate([(n, self._d(sd)) for n, sd in w_locals])
+        assert all(v.device == DEV for v in out.values())
+        return out
+
+
 class _OracleImpl(_TrackerImpl):
     def __init__(self, meta, init):
         weight_size = sum(v.numel() for v in init.values())
@@ -92,6 +122,16 @@ def test_fpf_tracker_matches_reference_loop(name, after):
     impl = _TrackerImpl(case.meta, case.init)
     got = fpf_replay.replay(case, impl, record_after_aggregate=after)
     assert_fpf_rows(got, case.fpf)
+
+
+@pytest.mark.parametrize("after", [False, True], ids=["record_client", "record_round"])
+@pytest.mark.parametrize("name", fpf_replay.case_names())
+def test_fpf_tracker_device_resident_clients(name, after):
+    case = fpf_replay.load_case(name)
+    got = fpf_replay.replay(case, _DeviceTrackerImpl(case.meta, case.init), record_after_aggregate=after)
+    assert_fpf_rows(got, case.fpf)
+    host = fpf_replay.replay(case, _TrackerImpl(case.meta, case.init), record_after_aggregate=after)
+    assert np.array_equal(got.view(np.uint32), host.view(np.uint32))  # same bits as the host-client loop
 
 
 def _random_case(n_total, P, rounds, seed, threshold=FO.THRESHOLD_WEIGHT_SIZE, bn=False):
