@@ -119,6 +119,12 @@ int fedavg_fpf_index_variant(const float* diffs, int64_t n_rows, int64_t ld, int
  * contiguous range per block, nontemporal; 2: as 1 with default-policy loads.
  * `sink` needs `blocks` floats (written only on an impossible value match).
  */
+/* The production U4 x C8 nt reduce with an XCD-aware workgroup order (XCD x
+ * takes one contiguous run of column slices); same round-split launches, same
+ * bits.  Measurement only. */
+int fedavg_reduce_f32_xcd(const float* clients, int64_t K, int64_t P, int64_t ld, const float* weights, float* out,
+                          int max_blocks, void* stream);
+
 int fedavg_probe_read_f32x4(const float* buf, int64_t nvec, int mode, int blocks, int launches, float* sink,
                             void* stream);
 

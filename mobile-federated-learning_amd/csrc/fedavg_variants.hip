@@ -388,6 +388,59 @@ __global__ __launch_bounds__(kBlock, 1) void probe_busy_copy_kernel(const f32x4*
   while (__builtin_amdgcn_s_memrealtime() - t0 < hold_ticks) __builtin_amdgcn_s_sleep(32);
 }
 
+// XCD-aware block order (measurement only).  The dispatcher hands workgroup i
+// of a launch to XCD i % 8, so in launch order neighbouring 32-KiB column
+// slices of a row sit on different XCDs (and L2s).  This variant renumbers
+// the workgroups so XCD x works on one contiguous run of slices: logical
+// block = start(x) + i / 8, a bijection for any grid size.  The reduce has no
+// reuse across blocks, so this tests whether HBM/Infinity-Fabric locality of
+// each XCD's stream matters for a pure read stream.
+template <int U, int C, bool NT>
+__global__ __launch_bounds__(kBlock) void reduce_f32x4_xcd_kernel(const f32x4* __restrict__ X, int K, int64_t ld4,
+                                                                  int64_t nvec, int tail, const float* __restrict__ W,
+                                                                  float* __restrict__ out) {
+  constexpr int kXcds = 8;
+  const int64_t G = gridDim.x, i = blockIdx.x;
+  const int64_t q = G / kXcds, r = G % kXcds, x = i % kXcds;
+  const int64_t b = x * q + (x < r ? x : r) + i / kXcds;
+  const int64_t span = static_cast<int64_t>(kBlock) * C;
+  const int64_t base = b * span;
+  if (base >= nvec) return;
+  if (base + span <= nvec) {
+    f32x4 acc[C];
+    reduce_full_group<U, C, NT, false>(acc, X + base + threadIdx.x, K, ld4, W);
+#pragma unroll
+    for (int j = 0; j < C; ++j) store_slice(out, base + threadIdx.x + j * kBlock, nvec, tail, acc[j]);
+  } else {
+    for (int j = 0; j < C; ++j) {
+      const int64_t v = base + threadIdx.x + j * kBlock;
+      if (v >= nvec) break;
+      f32x4 acc[1];
+      reduce_full_group<U, 1, NT, false>(acc, X + v, K, ld4, W);
+      store_slice(out, v, nvec, tail, acc[0]);
+    }
+  }
+}
+
+// launch_split's equal round-split launches, with the XCD-aware order
+template <int U, int C, bool NT>
+void launch_split_xcd(const float* clients, int K, int64_t ld, int64_t P, const float* W, float* out, int max_blocks,
+                      hipStream_t s) {
+  const int64_t nvec = (P + 3) / 4;
+  const int64_t span = static_cast<int64_t>(kBlock) * C;
+  const int64_t resident = max_blocks > 0 ? max_blocks : resident_blocks(reduce_f32x4_xcd_kernel<U, C, NT>);
+  const int64_t blocks = (nvec + span - 1) / span;
+  const int64_t nl = (blocks + resident - 1) / resident;
+  const int64_t per = ((nvec + nl - 1) / nl + span - 1) / span * span;
+  const f32x4* X = reinterpret_cast<const f32x4*>(clients);
+  for (int64_t v0 = 0; v0 < nvec; v0 += per) {
+    const int64_t n = (nvec - v0) < per ? (nvec - v0) : per;
+    const int tail = (v0 + n == nvec) ? static_cast<int>(P & 3) : 0;
+    hipLaunchKernelGGL((reduce_f32x4_xcd_kernel<U, C, NT>), dim3(static_cast<unsigned>((n + span - 1) / span)),
+                       dim3(kBlock), 0, s, X + v0, K, ld / 4, n, tail, W, out + v0 * 4);
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -496,6 +549,18 @@ int fedavg_stream_destroy(void* stream) {
     return set_error(-static_cast<int>(e), "fedavg_stream_destroy: %s", hipGetErrorString(e));
   }
   return FEDAVG_OK;
+}
+
+int fedavg_reduce_f32_xcd(const float* clients, int64_t K, int64_t P, int64_t ld, const float* weights, float* out,
+                          int max_blocks, void* stream) {
+  const char* what = "fedavg_reduce_f32_xcd";
+  if (K <= 0 || P <= 0 || ld < P || !clients || !weights || !out || K > INT32_MAX)
+    return set_error(FEDAVG_EINVAL, "%s: bad arguments", what);
+  if (!aligned16(clients) || !aligned16(out) || (ld % 4) != 0)
+    return set_error(FEDAVG_EALIGN, "%s: needs 16-B aligned clients/out and ld %% 4 == 0", what);
+  launch_split_xcd<4, 8, true>(clients, static_cast<int>(K), ld, P, weights, out, max_blocks,
+                               static_cast<hipStream_t>(stream));
+  return launch_status(what);
 }
 
 }  // extern "C"
