@@ -70,6 +70,8 @@ class RoundSession:
         self._chunks = {g.dtype: column_chunks(g.P) for g in self.table.groups.values()}
         self._ready = {}
         self._client_dev = None
+        self._out_host = {}
+        self.finish_profile = {}
         self.add_ms = 0.0
         # a round whose fp32 rows fit in SMALL_ROUND_BYTES finishes in ONE
         # native call (fedavg_round_f32 over the rows add() already packed):
@@ -90,6 +92,12 @@ class RoundSession:
             self._client_dev = self.agg._client_device(self.table, [state_dict])
             if self._client_dev.type == "cuda":
                 self._small = False
+            elif not self._small:
+                # the result's pinned buffers, allocated while clients still
+                # train instead of inside finish(): a fresh 100 MB pinned
+                # allocation costs 5.6-8.6 ms
+                self._out_host = {g.dtype: torch.empty(g.P, dtype=g.dtype, pin_memory=True)
+                                  for g in self.table.groups.values()}
         ptrs, keep = self.table.collect([state_dict], self._client_dev)
         if self._client_dev.type == "cuda":
             # device-resident client: one packing kernel on the copy stream,
@@ -147,20 +155,27 @@ class RoundSession:
             return self._finish_device(K, weights, acc_dict)
         outs = []
         dev_state = {}
+        t0 = time.perf_counter()
         with torch.cuda.device(self.dev):
             d2h = self.agg._d2h_stream_for()
             for g in self.table.groups.values():
                 st = self._staging[g.dtype]
                 out_dev, out_host = reduce_and_fetch(st.dev[:K], weights_tensor(weights, g.dtype, self.dev), g.P,
-                                                     d2h, ready=self._ready[g.dtype])
+                                                     d2h, ready=self._ready[g.dtype],
+                                                     out_host=self._out_host.get(g.dtype))
                 outs.append((g, out_host))
                 dev_state[g.dtype] = (st.dev[:K], out_dev)
+            t1 = time.perf_counter()
             d2h.synchronize()
             self._compute.synchronize()
             self._compute.wait_stream(self._copy)  # nothing else may reuse the staging before its copies end
+        t2 = time.perf_counter()
         for g, out_host in outs:
             for name, t in self.table.unpack(g, out_host).items():
                 acc_dict[name] = t
+        # host-side phases of the finish (ms): issuing weights/reduce/D2H, waiting for them, unpacking
+        self.finish_profile = {"issue_ms": (t1 - t0) * 1e3, "wait_ms": (t2 - t1) * 1e3,
+                               "unpack_ms": (time.perf_counter() - t2) * 1e3}
         return self._close(K, dev_state, acc_dict)
 
     def _finish_small(self, K, weights, acc_dict):

@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--P", type=int, default=25_000_000)
     ap.add_argument("--train-ms", type=float, default=5.0)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--keep-results", action="store_true",
+                    help="keep every round's result alive (each round then copies into a never-used pinned buffer)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -39,6 +41,7 @@ def main():
     dicts = [OrderedDict(w=base + 1e-3 * torch.randn(args.P, generator=g)) for _ in range(args.K)]
     counts = list(np.random.default_rng(1).integers(1, 1000, size=args.K))
     agg = mfl_amd.DeviceAggregator(dev)
+    kept = []
     for r in range(args.rounds):
         wl = [(int(n), OrderedDict(d)) for n, d in zip(counts, dicts)]
         torch.cuda.synchronize()
@@ -50,11 +53,15 @@ def main():
             sess.add(n, sd)
             add_ns.append((t0, time.perf_counter_ns()))
         t0 = time.perf_counter_ns()
-        sess.finish(wl)
+        out = sess.finish(wl)
         t1 = time.perf_counter_ns()
+        if args.keep_results:
+            kept.append(out)
         print(json.dumps({"round": r, "last_add_start_ns": add_ns[-1][0], "last_add_end_ns": add_ns[-1][1],
                           "last_add_ms": (add_ns[-1][1] - add_ns[-1][0]) / 1e6,
-                          "finish_start_ns": t0, "finish_end_ns": t1, "finish_ms": (t1 - t0) / 1e6}), flush=True)
+                          "finish_start_ns": t0, "finish_end_ns": t1, "finish_ms": (t1 - t0) / 1e6,
+                          "finish_phases_ms": {k: round(v, 3) for k, v in sess.finish_profile.items()}}),
+              flush=True)
 
 
 if __name__ == "__main__":
