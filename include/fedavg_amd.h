@@ -242,6 +242,30 @@ int64_t fedavg_pack_rows_device_workspace(int64_t n_items);
 int fedavg_pack_rows_device(const fedavg_pack_item* items, int64_t n_items, void* dst_base, int64_t elem_size,
                             void* host_ws, void* dev_ws, int64_t ws_bytes, void* stream);
 
+/*
+ * Zero-copy aggregation of device-resident clients (no [K, ld] rows): the fp32
+ * group of the model as a key table -- key_numel / key_offset (element offset
+ * in `out` / `glob`) / key_kind (fedavg_pack_item kinds: 0 fp32, 1..6 integer
+ * and bool sources promoted to fp32) -- and client_ptrs [K][n_keys], the
+ * device address of client k's tensor for key j (fp32 sources 4-B aligned).
+ * fedavg_reduce_segments_f32 writes the averaged fp32 group into `out` [P]
+ * with the bits of fedavg_reduce_f32 on the packed rows (fedavg_trainer.py:
+ * 450-457); fedavg_client_sqdist_segments_f32 is fedavg_client_sqdist_f32 on
+ * the same tables (:291; partials: fedavg_segments_partials doubles).  The
+ * tables are staged through host_ws (pinned) into dev_ws (device), both
+ * fedavg_segments_workspace(K, n_keys) bytes; host_ws must not be rewritten
+ * until `stream` has passed the call.  Stream-ordered, asynchronous.
+ */
+int64_t fedavg_segments_workspace(int64_t K, int64_t n_keys);
+int64_t fedavg_segments_partials(const int64_t* key_numel, int64_t n_keys, int64_t K);
+int fedavg_reduce_segments_f32(const int64_t* client_ptrs, const int64_t* key_numel, const int64_t* key_offset,
+                               const int64_t* key_kind, int64_t n_keys, int64_t K, const float* weights, float* out,
+                               void* host_ws, void* dev_ws, int64_t ws_bytes, void* stream);
+int fedavg_client_sqdist_segments_f32(const int64_t* client_ptrs, const int64_t* key_numel, const int64_t* key_offset,
+                                      const int64_t* key_kind, int64_t n_keys, int64_t K, const float* glob,
+                                      double* partials, int64_t partial_elems, double* sumsq, void* host_ws,
+                                      void* dev_ws, int64_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -31,9 +31,11 @@ of one freshly allocated host buffer (values and shapes are the reference's;
 Device-resident clients: when the clients' tensors are all on this GPU (a
 deployment that drops client.py:96's ``.cpu()``), the reference's device-
 agnostic loop would compute on the GPU and return GPU tensors; so does the
-drop-in: one packing kernel (``fedavg_pack_rows_device``) gathers the keys into
-the HBM rows, the same reduce runs, and the result comes back as views of a
-device buffer, ordered on the current stream without a host synchronization.
+drop-in: the fp32 keys are reduced straight from the clients' own tensors
+(``fedavg_reduce_segments_f32``, a pointer-table kernel, no packing; other
+dtype groups are packed into rows by ``fedavg_pack_rows_device`` first), and
+the result comes back as views of a device buffer, ordered on the current
+stream without a host synchronization.
 Clients split between host and device raise ``TypeError``.
 """
 from __future__ import annotations
@@ -182,27 +184,17 @@ def _fetch(src: torch.Tensor, dst: torch.Tensor, stream) -> None:
                                        D2H_BLOCKS, stream.cuda_stream), "fedavg_copy_to_host")
 
 
-class _Staging:
-    """Reusable pinned host rows + device buffer for one dtype group, and the
-    group's weight vector (pinned + device) so a call uploads the weights with
-    its rows instead of allocating a pinned tensor per call."""
+class _Weights:
+    """A pinned + device weight vector reused across calls (no pinned
+    allocation per call)."""
 
-    def __init__(self, K: int, ld: int, dtype: torch.dtype, device: torch.device):
-        self.K, self.ld, self.dtype = K, ld, dtype
-        self._host = None  # pinned rows, allocated on first use (device-resident clients never need them)
-        self.dev = torch.empty((K, ld), dtype=dtype, device=device)
-        wdt = torch.float64 if dtype == torch.float64 else torch.float32
+    def __init__(self, K: int, wdt: torch.dtype, device: torch.device):
+        self.K = K
         self.w_host = torch.empty(K, dtype=wdt, pin_memory=True)
         self.w_dev = torch.empty(K, dtype=wdt, device=device)
         self._w_done = torch.cuda.Event()  # the last weight copy has read w_host
 
-    @property
-    def host(self) -> torch.Tensor:
-        if self._host is None:
-            self._host = torch.empty((self.K, self.ld), dtype=self.dtype, pin_memory=True)
-        return self._host
-
-    def upload_weights(self, weights: Sequence[float], stream) -> torch.Tensor:
+    def upload(self, weights: Sequence[float], stream) -> torch.Tensor:
         """``weights`` (the reference's Python doubles n_i / N) rounded once to
         the group's weight dtype (round to nearest even: the cast ATen applies
         to the scalar at fedavg_trainer.py:455) and copied on ``stream``.
@@ -217,6 +209,27 @@ class _Staging:
             self.w_dev[:K].copy_(self.w_host[:K], non_blocking=True)
         self._w_done.record(stream)
         return self.w_dev[:K]
+
+
+class _Staging(_Weights):
+    """Reusable pinned host rows + device buffer for one dtype group, and the
+    group's weight vector (pinned + device) so a call uploads the weights with
+    its rows instead of allocating a pinned tensor per call."""
+
+    def __init__(self, K: int, ld: int, dtype: torch.dtype, device: torch.device):
+        super().__init__(K, torch.float64 if dtype == torch.float64 else torch.float32, device)
+        self.ld, self.dtype = ld, dtype
+        self._host = None  # pinned rows, allocated on first use (device-resident clients never need them)
+        self.dev = torch.empty((K, ld), dtype=dtype, device=device)
+
+    @property
+    def host(self) -> torch.Tensor:
+        if self._host is None:
+            self._host = torch.empty((self.K, self.ld), dtype=self.dtype, pin_memory=True)
+        return self._host
+
+    def upload_weights(self, weights: Sequence[float], stream) -> torch.Tensor:
+        return self.upload(weights, stream)
 
 
 class DeviceAggregator:
@@ -246,7 +259,9 @@ class DeviceAggregator:
         self._last: Dict[str, object] = {}
         self._session = None  # weakref to the open RoundSession, if any
         self._table_hint: Optional[KeyTable] = None  # last round's key table (prepare reuses it)
-        self._pack_ws = None  # (pinned, device, event) item table of fedavg_pack_rows_device
+        self._table_ws = None  # (pinned, device) staging of the device kernels' tables
+        self._table_ws_done = None  # event: the last staged table has been copied and used
+        self._seg_weights = None  # weights of the zero-copy (segments) reduce
         # one round at a time per aggregator: the staging buffers are shared
         self._lock = threading.Lock()
 
@@ -310,6 +325,10 @@ class DeviceAggregator:
             self._last["acc"] = weakref.ref(acc_dict)
         except TypeError:  # plain dicts cannot be weakly referenced: no reuse
             self._last.pop("dev", None)
+        if self._last.get("segments"):
+            # client 0's own tensors: its dict is about to hold the average
+            # (:449), and the rows of a zero-copy round are packed on demand
+            self._last["seg_keep0"] = OrderedDict((e.name, acc_dict[e.name]) for e in table.entries)
         # replace values in place, keeping client 0's key order (fedavg_trainer.py:450-457)
         for e in table.entries:
             acc_dict[e.name] = results[e.name]
@@ -327,24 +346,108 @@ class DeviceAggregator:
         lib = _lib.load()
         items = table.pack_items(g, ptrs, row0, g.ld)
         n = items.shape[0]
-        need = lib.fedavg_pack_rows_device_workspace(n)
-        ws = self._pack_ws
-        if ws is not None:
-            ws[2].synchronize()  # the previous pack has consumed its item table
+        host_ws, dev_ws = self._stage_ws(lib.fedavg_pack_rows_device_workspace(n))
+        _lib.check(lib.fedavg_pack_rows_device(items.ctypes.data, n, dst.data_ptr(), dst.element_size(),
+                                               host_ws.data_ptr(), dev_ws.data_ptr(), host_ws.numel(),
+                                               stream.cuda_stream), "fedavg_pack_rows_device")
+        self._table_ws_done.record(stream)
+
+    def _stage_ws(self, need: int):
+        """The (pinned, device) table workspace, at least ``need`` bytes, once
+        the previous user has consumed it; the caller records
+        ``_table_ws_done`` on its stream after its call."""
+        if self._table_ws_done is None:
+            self._table_ws_done = torch.cuda.Event()
+        self._table_ws_done.synchronize()
+        ws = self._table_ws
         if ws is None or ws[0].numel() < need:
             cap = max(need, 1 << 16)
             ws = (torch.empty(cap, dtype=torch.uint8, pin_memory=True),
-                  torch.empty(cap, dtype=torch.uint8, device=self.device), torch.cuda.Event())
-            self._pack_ws = ws
-        _lib.check(lib.fedavg_pack_rows_device(items.ctypes.data, n, dst.data_ptr(), dst.element_size(),
-                                               ws[0].data_ptr(), ws[1].data_ptr(), ws[0].numel(),
-                                               stream.cuda_stream), "fedavg_pack_rows_device")
-        ws[2].record(stream)
+                  torch.empty(cap, dtype=torch.uint8, device=self.device))
+            self._table_ws = ws
+        return ws
+
+    # device-resident fp32 groups are reduced straight from the clients'
+    # tensors (fedavg_reduce_segments_f32: 4 B per element instead of the
+    # rows' 12); FEDAVG_DEVICE_ROWS=1 packs rows first as the streaming path does
+    DEVICE_SEGMENTS = os.environ.get("FEDAVG_DEVICE_ROWS", "0") != "1"
+
+    @staticmethod
+    def _segment_tables(g, ptrs):
+        import numpy as np
+
+        return (np.ascontiguousarray(ptrs[:, g.key_index]), np.ascontiguousarray(g.numel),
+                np.ascontiguousarray(g.offset), np.ascontiguousarray(g.kind))
+
+    def _reduce_segments(self, g, ptrs, weights, stream) -> torch.Tensor:
+        """The fp32 group reduced from the clients' own tensors (zero-copy)."""
+        lib = _lib.load()
+        K = ptrs.shape[0]
+        cptrs, numel, offset, kind = self._segment_tables(g, ptrs)
+        w = self._seg_weights
+        if w is None or w.K < K:
+            w = self._seg_weights = _Weights(K, torch.float32, self.device)
+        w_dev = w.upload(weights, stream)
+        out_dev = torch.empty(g.P, dtype=torch.float32, device=self.device)
+        host_ws, dev_ws = self._stage_ws(lib.fedavg_segments_workspace(K, len(numel)))
+        _lib.check(lib.fedavg_reduce_segments_f32(cptrs.ctypes.data, numel.ctypes.data, offset.ctypes.data,
+                                                  kind.ctypes.data, len(numel), K, w_dev.data_ptr(),
+                                                  out_dev.data_ptr(), host_ws.data_ptr(), dev_ws.data_ptr(),
+                                                  host_ws.numel(), stream.cuda_stream), "fedavg_reduce_segments_f32")
+        self._table_ws_done.record(stream)
+        return out_dev
+
+    def _sqdist_segments(self, table: KeyTable, dicts, glob: torch.Tensor) -> torch.Tensor:
+        """:291 sums of squares straight from device-resident clients' tensors."""
+        lib = _lib.load()
+        g = table.groups[torch.float32]
+        ptrs, keep = table.collect(dicts, self.device)
+        K = len(dicts)
+        cptrs, numel, offset, kind = self._segment_tables(g, ptrs)
+        stream = torch.cuda.current_stream(self.device)
+        partials = torch.empty(max(1, lib.fedavg_segments_partials(numel.ctypes.data, len(numel), K)),
+                               dtype=torch.float64, device=self.device)
+        sumsq = torch.empty(K, dtype=torch.float64, device=self.device)
+        host_ws, dev_ws = self._stage_ws(lib.fedavg_segments_workspace(K, len(numel)))
+        _lib.check(lib.fedavg_client_sqdist_segments_f32(cptrs.ctypes.data, numel.ctypes.data, offset.ctypes.data,
+                                                         kind.ctypes.data, len(numel), K, glob.data_ptr(),
+                                                         partials.data_ptr(), partials.numel(), sumsq.data_ptr(),
+                                                         host_ws.data_ptr(), dev_ws.data_ptr(), host_ws.numel(),
+                                                         stream.cuda_stream), "fedavg_client_sqdist_segments_f32")
+        self._table_ws_done.record(stream)
+        del keep
+        return sumsq
+
+    def materialize_rows(self):
+        """The last round's client rows in HBM (``[K, ld]``), packing them on
+        demand after a zero-copy round: client 0 from its original tensors
+        (its dict now holds the average, :449), the others from their dicts.
+        Returns the rows or None when the last round left none."""
+        last = self._last
+        if "seg_keep0" not in last:
+            dev = last.get("dev", {}).get(torch.float32)
+            return None if dev is None else dev[0]
+        refs = last.get("refs")
+        dicts = [last["seg_keep0"]] + [r() for r in refs[1:]] if refs is not None else [None]
+        if any(d is None for d in dicts):
+            return None
+        table, K = last["table"], last["K"]
+        g = table.groups[torch.float32]
+        st = self._staging_for(torch.float32, K, g.ld)
+        ptrs, keep = table.collect(dicts, self.device)
+        with torch.cuda.device(self.device):
+            self._pack_on_device(table, g, ptrs, 0, st.dev, torch.cuda.current_stream(self.device))
+        del keep
+        last["dev"][torch.float32] = (st.dev[:K], last["dev"][torch.float32][1])
+        del last["seg_keep0"]
+        return st.dev[:K]
 
     def _reduce_groups_device(self, table: KeyTable, ptrs, weights) -> "OrderedDict[str, torch.Tensor]":
-        """Device-resident clients: pack in HBM, reduce, and return the averaged
-        model as device tensors on the current stream (no host round trip, no
-        synchronization: like the reference's torch ops on device tensors)."""
+        """Device-resident clients: the fp32 group reduced straight from the
+        clients' tensors (zero-copy), other groups packed in HBM and reduced;
+        the averaged model returned as device tensors on the current stream
+        (no host round trip, no synchronization: like the reference's torch
+        ops on device tensors)."""
         K, dev = ptrs.shape[0], self.device
         t0 = time.perf_counter()
         results: "OrderedDict[str, torch.Tensor]" = OrderedDict()
@@ -354,12 +457,17 @@ class DeviceAggregator:
                 compute.wait_stream(self._copy_stream)  # earlier users of the staging are done
             self._last = {"table": table, "K": K, "dev": {}}
             for g in table.groups.values():
-                st = self._staging_for(g.dtype, K, g.ld)
-                self._pack_on_device(table, g, ptrs, 0, st.dev, compute)
-                w_dev = st.upload_weights(weights, compute)
-                out_dev = torch.empty(g.P, dtype=g.dtype, device=dev)
-                reduce_packed(st.dev[:K], w_dev, g.P, out_dev)
-                self._last["dev"][g.dtype] = (st.dev[:K], out_dev)
+                if g.dtype == torch.float32 and self.DEVICE_SEGMENTS:
+                    out_dev = self._reduce_segments(g, ptrs, weights, compute)
+                    self._last["dev"][g.dtype] = (None, out_dev)  # no rows: see materialize_rows
+                    self._last["segments"] = True
+                else:
+                    st = self._staging_for(g.dtype, K, g.ld)
+                    self._pack_on_device(table, g, ptrs, 0, st.dev, compute)
+                    w_dev = st.upload_weights(weights, compute)
+                    out_dev = torch.empty(g.P, dtype=g.dtype, device=dev)
+                    reduce_packed(st.dev[:K], w_dev, g.P, out_dev)
+                    self._last["dev"][g.dtype] = (st.dev[:K], out_dev)
                 results.update(table.unpack(g, out_dev))
         self.last_profile = {"pack_issue_ms": (time.perf_counter() - t0) * 1e3, "h2d_kernel_d2h_ms": 0.0}
         return results
@@ -481,13 +589,21 @@ class DeviceAggregator:
         if has_bool and any(sd is not w_glob for _, sd in w_locals):
             raise RuntimeError("Subtraction, the `-` operator, with a bool tensor is not supported "
                                "(fedavg_trainer.py:291 on a state_dict with bool buffers)")
-        if cached:
-            devbuf, out_dev = last["dev"][torch.float32]
-            P = last["table"].groups[torch.float32].P
-        else:
-            devbuf, out_dev, P = self._upload_for_distances(w_locals, w_glob)
         with torch.cuda.device(self.device):
-            sumsq = client_sqdist(devbuf, out_dev, P).cpu().numpy()
+            if cached:
+                devbuf, out_dev = last["dev"][torch.float32]
+                P = last["table"].groups[torch.float32].P
+                if devbuf is None:  # zero-copy round: read the clients' tensors where they lie
+                    # the dict aliased to w_glob (client 0, :449) holds the average
+                    # now; its own tensors stand in (its norm is overridden below)
+                    dicts = [last["seg_keep0"] if sd is w_glob else sd for _, sd in w_locals]
+                    sumsq_dev = self._sqdist_segments(last["table"], dicts, out_dev)
+                else:
+                    sumsq_dev = client_sqdist(devbuf, out_dev, P)
+            else:
+                devbuf, out_dev, P = self._upload_for_distances(w_locals, w_glob)
+                sumsq_dev = client_sqdist(devbuf, out_dev, P)
+            sumsq = sumsq_dev.cpu().numpy()
             glob_finite = bool(torch.isfinite(out_dev[:P]).all())
         norms = np.sqrt(sumsq).astype(np.float32).astype(np.float64)
         for i, (_, sd) in enumerate(w_locals):

@@ -24,7 +24,8 @@ REPO_DIR = PKG_DIR.parent
 CSRC_DIR = PKG_DIR / "csrc"
 # translation units of libfedavg_amd.so, compiled in parallel then linked
 HIP_SOURCES = [CSRC_DIR / "fedavg_reduce.hip", CSRC_DIR / "fedavg_variants.hip", CSRC_DIR / "fedavg_dist.hip",
-               CSRC_DIR / "fedavg_fpf.hip", CSRC_DIR / "fedavg_xfer.hip", CSRC_DIR / "fedavg_pack.hip"]
+               CSRC_DIR / "fedavg_fpf.hip", CSRC_DIR / "fedavg_xfer.hip", CSRC_DIR / "fedavg_pack.hip",
+               CSRC_DIR / "fedavg_segments.hip"]
 CSRC_HOST = CSRC_DIR / "fedavg_host.cpp"
 CSRC_COMMON = CSRC_DIR / "common.hpp"
 CSRC_COLLECT = CSRC_DIR / "fedavg_collect_ext.cpp"

@@ -1,0 +1,438 @@
+// fedavg_segments.hip -- zero-copy aggregation of DEVICE-resident clients.
+//
+// When the clients' state_dicts are already in HBM (client.py:96 without the
+// .cpu()), the reduction (fedavg_trainer.py:450-457) and the :291 distance
+// pass can read every client's tensors where they lie instead of packing them
+// into [K, ld] rows first: packing moves 8 B per element (read + write) before
+// the reduce reads 4 B again, so a round costs 12 B per element through rows
+// and 4 B here.  The model's fp32 group is described by a key table
+// (numel, output offset, source kind) and a pointer table [n_keys][K] (client
+// k's address of key j).  Each key is cut into units of kSegSpan columns; a
+// workgroup reduces one unit over all K clients with the production schedule
+// (U4 client rows per batch, C8 16-B column slices per thread), reading each
+// client through its pointer with dword-aligned global_load_dwordx4 (client
+// tensors need only fp32 alignment), in the reference's client order with
+// separately rounded products and sums -- the bits of fedavg_reduce_f32 on
+// the packed rows.  Integer/bool keys (num_batches_tracked, ...) are converted
+// to fp32 per element with static_cast, as the packers do.  Units are issued
+// key-major in round-split launches of 3 x CUs workgroups, so a launch streams
+// one compact window of every client's tensors, like the row-major reduce.
+#include "common.hpp"
+
+namespace {
+using namespace fedavg_impl;
+
+typedef f32x4 f32x4_a4 __attribute__((aligned(4)));  // dword-aligned 16-B vector (client tensors, outputs)
+
+constexpr int kSegU = 4;
+constexpr int kSegC = 8;
+constexpr int64_t kSegSpan = static_cast<int64_t>(kBlock) * kSegC * 4;  // columns per unit
+constexpr int kSegBlocksPerCU = 3;
+
+enum : int64_t { kRaw = 0, kI64 = 1, kI32 = 2, kI16 = 3, kI8 = 4, kU8 = 5, kBool = 6 };
+
+struct SegKey {
+  int64_t numel, out_offset, kind, unit_start;
+};
+
+// the key owning unit u: the largest j with keys[j].unit_start <= u (keys
+// without units share their successor's start and lose the tie); 64 probes
+// per round across the wave
+__device__ __forceinline__ int64_t find_key(const SegKey* __restrict__ keys, int64_t n_keys, int64_t u) {
+  const int lane = static_cast<int>(threadIdx.x & 63u);
+  int64_t lo = 0, hi = n_keys;
+  while (hi - lo > 1) {
+    const int64_t step = (hi - lo + 63) / 64;
+    const int64_t idx = lo + lane * step;
+    const bool hit = idx < hi && keys[idx].unit_start <= u;
+    const unsigned long long m = __ballot(hit);
+    lo += (63 - __clzll(m)) * step;
+    hi = hi < lo + step ? hi : lo + step;
+  }
+  return lo;
+}
+
+// Client addresses come from the pointer table as integers, so the compiler
+// cannot infer their address space and would emit flat loads (which also
+// count against lgkmcnt and stall the scalar pointer-table loads): every
+// client access goes through an explicit global (address_space 1) pointer.
+template <typename T>
+using gptr = __attribute__((address_space(1))) const T*;
+
+template <typename T>
+__device__ __forceinline__ gptr<T> to_global(const void* p) {
+  return (gptr<T>)(reinterpret_cast<uintptr_t>(p));
+}
+
+__device__ __forceinline__ f32x4 ldu(const float* p) { return __builtin_nontemporal_load(to_global<f32x4_a4>(p)); }
+
+// elements [col, col + 4) of a unit with n columns: a full 16-B vector, or
+// the valid head of one (the rest 0)
+__device__ __forceinline__ f32x4 load_slice(const float* p, int64_t col, int64_t n) {
+  if (col + 4 <= n) return ldu(p + col);
+  const gptr<float> q = to_global<float>(p);
+  f32x4 v{0.f, 0.f, 0.f, 0.f};
+  if (col < n) v.x = q[col];
+  if (col + 1 < n) v.y = q[col + 1];
+  if (col + 2 < n) v.z = q[col + 2];
+  return v;
+}
+
+__device__ __forceinline__ void store_slice_u(float* o, int64_t col, int64_t n, f32x4 a) {
+  if (col + 4 <= n) {
+    *reinterpret_cast<f32x4_a4*>(o + col) = a;
+  } else if (col < n) {
+    o[col] = a.x;
+    if (col + 1 < n) o[col + 1] = a.y;
+    if (col + 2 < n) o[col + 2] = a.z;
+  }
+}
+
+__device__ __forceinline__ float load_cvt(const void* base, int64_t kind, int64_t e) {
+  switch (kind) {
+    case kI64: return static_cast<float>(to_global<int64_t>(base)[e]);
+    case kI32: return static_cast<float>(to_global<int32_t>(base)[e]);
+    case kI16: return static_cast<float>(to_global<int16_t>(base)[e]);
+    case kI8: return static_cast<float>(to_global<int8_t>(base)[e]);
+    case kU8: return static_cast<float>(to_global<uint8_t>(base)[e]);
+    case kBool: return to_global<uint8_t>(base)[e] ? 1.0f : 0.0f;
+    default: return to_global<float>(base)[e];
+  }
+}
+
+// one unit of an fp32 key: FULL units (all kSegSpan columns) take the
+// unconditional 16-B path with U rows per batch; the last unit of a key
+// masks its tail slice element by element
+template <int U, int C, bool FULL>
+__device__ __forceinline__ void reduce_raw_unit(const int64_t* __restrict__ P, int K, int64_t c0, int64_t n,
+                                                const float* __restrict__ W, float* __restrict__ o) {
+  f32x4 acc[C];
+  const float w0 = W[0];
+  const float* x0 = reinterpret_cast<const float*>(P[0]) + c0;
+#pragma unroll
+  for (int s = 0; s < C; ++s) {
+    const int64_t col = 4 * (threadIdx.x + s * kBlock);
+    acc[s] = (FULL ? ldu(x0 + col) : load_slice(x0, col, n)) * w0;  // :455, i == 0
+  }
+  const int nb = (K - 1) / U;
+  int k = 1;
+  // the next batch's client addresses are loaded one batch ahead, so the
+  // pointer-table latency overlaps the current batch's data loads
+  int64_t nxt[U];
+#pragma unroll
+  for (int r = 0; r < U; ++r) nxt[r] = nb > 0 ? P[1 + r] : 0;
+  for (int b = 0; b < nb; ++b, k += U) {
+    int64_t cur[U];
+#pragma unroll
+    for (int r = 0; r < U; ++r) cur[r] = nxt[r];
+    if (b + 1 < nb) {
+#pragma unroll
+      for (int r = 0; r < U; ++r) nxt[r] = P[k + U + r];
+    }
+    f32x4 xs[U][C];
+#pragma unroll
+    for (int r = 0; r < U; ++r) {
+      const float* xr = reinterpret_cast<const float*>(cur[r]) + c0;
+#pragma unroll
+      for (int s = 0; s < C; ++s) {
+        const int64_t col = 4 * (threadIdx.x + s * kBlock);
+        xs[r][s] = FULL ? ldu(xr + col) : load_slice(xr, col, n);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < U; ++r) {
+      const float w = W[k + r];
+#pragma unroll
+      for (int s = 0; s < C; ++s) {
+        const f32x4 term = xs[r][s] * w;  // :455 product, then the :457 sum, in client order
+        acc[s] = acc[s] + term;
+      }
+    }
+  }
+  for (; k < K; ++k) {
+    const float* xr = reinterpret_cast<const float*>(P[k]) + c0;
+    const float w = W[k];
+#pragma unroll
+    for (int s = 0; s < C; ++s) {
+      const int64_t col = 4 * (threadIdx.x + s * kBlock);
+      const f32x4 term = (FULL ? ldu(xr + col) : load_slice(xr, col, n)) * w;
+      acc[s] = acc[s] + term;
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < C; ++s) {
+    const int64_t col = 4 * (threadIdx.x + s * kBlock);
+    if (FULL)
+      *reinterpret_cast<f32x4_a4*>(o + col) = acc[s];
+    else
+      store_slice_u(o, col, n, acc[s]);
+  }
+}
+
+template <int U, int C>
+__global__ __launch_bounds__(kBlock) void reduce_segments_f32_kernel(const SegKey* __restrict__ keys,
+                                                                     const int64_t* __restrict__ ptrs, int64_t n_keys,
+                                                                     int64_t unit0, int K, const float* __restrict__ W,
+                                                                     float* __restrict__ out) {
+  const int64_t u = unit0 + blockIdx.x;
+  const int64_t j = find_key(keys, n_keys, u);
+  const SegKey key = keys[j];
+  const int64_t c0 = (u - key.unit_start) * kSegSpan;
+  const int64_t n = key.numel - c0 < kSegSpan ? key.numel - c0 : kSegSpan;
+  const int64_t* P = ptrs + j * K;
+  float* o = out + key.out_offset + c0;
+  if (key.kind == kRaw) {
+    if (n == kSegSpan)
+      reduce_raw_unit<U, C, true>(P, K, c0, n, W, o);
+    else
+      reduce_raw_unit<1, C, false>(P, K, c0, n, W, o);
+    return;
+  }
+  // integer / bool key: element by element, converted like the packers
+  constexpr int kPer = 4 * C;
+  float acc[kPer];
+  const float w0 = W[0];
+  const void* x0 = reinterpret_cast<const void*>(P[0]);
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    const int64_t e = threadIdx.x + static_cast<int64_t>(i) * kBlock;
+    acc[i] = e < n ? load_cvt(x0, key.kind, c0 + e) * w0 : 0.f;
+  }
+  for (int k = 1; k < K; ++k) {
+    const void* xk = reinterpret_cast<const void*>(P[k]);
+    const float w = W[k];
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int64_t e = threadIdx.x + static_cast<int64_t>(i) * kBlock;
+      if (e < n) {
+        const float term = load_cvt(xk, key.kind, c0 + e) * w;
+        acc[i] = acc[i] + term;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    const int64_t e = threadIdx.x + static_cast<int64_t>(i) * kBlock;
+    if (e < n) o[e] = acc[i];
+  }
+}
+
+__device__ __forceinline__ double sq4_add(double acc, f32x4 d) {
+  const double x = d.x, y = d.y, z = d.z, w = d.w;
+  acc = __builtin_fma(x, x, acc);
+  acc = __builtin_fma(y, y, acc);
+  acc = __builtin_fma(z, z, acc);
+  return __builtin_fma(w, w, acc);
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// :291 on the same units: per client, sum over the unit's columns of
+// fl32(x - g)^2 in fp64 (fused square-adds, as client_sqdist_f32x4_kernel),
+// one partial per wave: partials[k][unit * 4 + wave].  Lanes past the unit's
+// end contribute exactly 0 (x and g both read as 0 there).
+template <int C>
+__global__ __launch_bounds__(kBlock) void sqdist_segments_f32_kernel(const SegKey* __restrict__ keys,
+                                                                     const int64_t* __restrict__ ptrs, int64_t n_keys,
+                                                                     int64_t unit0, int K, const float* __restrict__ G,
+                                                                     double* __restrict__ partials, int64_t nparts) {
+  const int64_t u = unit0 + blockIdx.x;
+  const int64_t j = find_key(keys, n_keys, u);
+  const SegKey key = keys[j];
+  const int64_t c0 = (u - key.unit_start) * kSegSpan;
+  const int64_t n = key.numel - c0 < kSegSpan ? key.numel - c0 : kSegSpan;
+  const int64_t* P = ptrs + j * K;
+  const float* g = G + key.out_offset + c0;
+  const int64_t part = u * (kBlock / 64) + (threadIdx.x >> 6);
+  const int lane = static_cast<int>(threadIdx.x & 63u);
+  if (key.kind == kRaw) {
+    f32x4 gv[C];
+#pragma unroll
+    for (int s = 0; s < C; ++s) gv[s] = load_slice(g, 4 * (threadIdx.x + s * kBlock), n);
+    for (int k = 0; k < K; ++k) {
+      const float* xk = reinterpret_cast<const float*>(P[k]) + c0;
+      double acc = 0.0;
+#pragma unroll
+      for (int s = 0; s < C; ++s) acc = sq4_add(acc, load_slice(xk, 4 * (threadIdx.x + s * kBlock), n) - gv[s]);
+      acc = wave_sum(acc);
+      if (lane == 0) partials[static_cast<int64_t>(k) * nparts + part] = acc;
+    }
+    return;
+  }
+  constexpr int kPer = 4 * C;
+  for (int k = 0; k < K; ++k) {
+    const void* xk = reinterpret_cast<const void*>(P[k]);
+    double acc = 0.0;
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int64_t e = threadIdx.x + static_cast<int64_t>(i) * kBlock;
+      if (e < n) {
+        const double d = static_cast<double>(load_cvt(xk, key.kind, c0 + e) - g[e]);  // fp32 difference
+        acc = __builtin_fma(d, d, acc);
+      }
+    }
+    acc = wave_sum(acc);
+    if (lane == 0) partials[static_cast<int64_t>(k) * nparts + part] = acc;
+  }
+}
+
+// sumsq[k] = sum of partials[k][*] in a fixed order (one workgroup per client)
+__global__ __launch_bounds__(kBlock) void segments_finalize_kernel(const double* __restrict__ partials, int64_t nparts,
+                                                                   double* __restrict__ sumsq) {
+  __shared__ double red[kBlock];
+  const int64_t k = blockIdx.x;
+  double s = 0.0;
+  for (int64_t w = threadIdx.x; w < nparts; w += kBlock) s += partials[k * nparts + w];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = kBlock / 2; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) sumsq[k] = red[0];
+}
+
+bool device_memory(const void* p) {
+  hipPointerAttribute_t attr;
+  if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return attr.type == hipMemoryTypeDevice;
+}
+
+int64_t units_of(const int64_t* numel, int64_t n_keys) {
+  int64_t units = 0;
+  for (int64_t j = 0; j < n_keys; ++j) units += (numel[j] + kSegSpan - 1) / kSegSpan;
+  return units;
+}
+
+// Validate the tables, write the device tables into host_ws, copy them to
+// dev_ws on `s`.  Returns the unit count (> 0), 0 for an empty model, or a
+// negative error code.
+int64_t stage_tables(const char* what, const int64_t* client_ptrs, const int64_t* numel, const int64_t* offset,
+                     const int64_t* kind, int64_t n_keys, int64_t K, void* host_ws, void* dev_ws, int64_t ws_bytes,
+                     hipStream_t s) {
+  if (n_keys <= 0 || K <= 0 || K > INT32_MAX || !client_ptrs || !numel || !offset || !kind || !host_ws || !dev_ws)
+    return set_error(FEDAVG_EINVAL, "%s: bad arguments", what);
+  if (ws_bytes < fedavg_segments_workspace(K, n_keys))
+    return set_error(FEDAVG_EINVAL, "%s: workspace needs %lld bytes", what,
+                     (long long)fedavg_segments_workspace(K, n_keys));
+  if (!aligned16(host_ws) || !aligned16(dev_ws)) return set_error(FEDAVG_EALIGN, "%s: workspaces must be 16-B aligned", what);
+  hipPointerAttribute_t attr;
+  if (hipPointerGetAttributes(&attr, host_ws) != hipSuccess || attr.type != hipMemoryTypeHost) {
+    (void)hipGetLastError();
+    return set_error(FEDAVG_EINVAL, "%s: host_ws is not pinned host memory", what);
+  }
+  if (!device_memory(dev_ws)) return set_error(FEDAVG_EINVAL, "%s: dev_ws must be device memory", what);
+  auto* hk = static_cast<SegKey*>(host_ws);
+  auto* hp = reinterpret_cast<int64_t*>(static_cast<char*>(host_ws) + n_keys * static_cast<int64_t>(sizeof(SegKey)));
+  int64_t units = 0;
+  const void* first_src = nullptr;
+  const void* last_src = nullptr;
+  for (int64_t j = 0; j < n_keys; ++j) {
+    if (numel[j] < 0 || offset[j] < 0 || kind[j] < kRaw || kind[j] > kBool)
+      return set_error(FEDAVG_EINVAL, "%s: bad key %lld", what, (long long)j);
+    hk[j] = SegKey{numel[j], offset[j], kind[j], units};
+    units += (numel[j] + kSegSpan - 1) / kSegSpan;
+    for (int64_t k = 0; k < K; ++k) {
+      const int64_t p = client_ptrs[k * n_keys + j];
+      if (numel[j] > 0) {
+        if (p == 0 || (kind[j] == kRaw && (p & 3) != 0))
+          return set_error(FEDAVG_EINVAL, "%s: client %lld key %lld: null or misaligned source", what, (long long)k,
+                           (long long)j);
+        if (!first_src) first_src = reinterpret_cast<const void*>(p);
+        last_src = reinterpret_cast<const void*>(p);
+      }
+      hp[j * K + k] = p;
+    }
+  }
+  if (units == 0) return 0;
+  // a host address would fault the kernels: spot check of the first and last
+  // source (the Python layer checks every tensor's device)
+  if (!device_memory(first_src) || !device_memory(last_src))
+    return set_error(FEDAVG_EINVAL, "%s: client sources must be device memory", what);
+  const hipError_t e = hipMemcpyAsync(dev_ws, host_ws, static_cast<size_t>(fedavg_segments_workspace(K, n_keys)),
+                                      hipMemcpyHostToDevice, s);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return set_error(-static_cast<int>(e), "%s: hipMemcpyAsync failed: %s", what, hipGetErrorString(e));
+  }
+  return units;
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t fedavg_segments_workspace(int64_t K, int64_t n_keys) {
+  if (K <= 0 || n_keys <= 0) return 0;
+  return n_keys * static_cast<int64_t>(sizeof(SegKey)) + n_keys * K * static_cast<int64_t>(sizeof(int64_t));
+}
+
+int64_t fedavg_segments_partials(const int64_t* key_numel, int64_t n_keys, int64_t K) {
+  if (!key_numel || n_keys <= 0 || K <= 0) return 0;
+  return K * units_of(key_numel, n_keys) * (kBlock / 64);
+}
+
+int fedavg_reduce_segments_f32(const int64_t* client_ptrs, const int64_t* key_numel, const int64_t* key_offset,
+                               const int64_t* key_kind, int64_t n_keys, int64_t K, const float* weights, float* out,
+                               void* host_ws, void* dev_ws, int64_t ws_bytes, void* stream) {
+  const char* what = "fedavg_reduce_segments_f32";
+  if (!weights || !out) return set_error(FEDAVG_EINVAL, "%s: null weights/out", what);
+  if (!device_memory(out)) return set_error(FEDAVG_EINVAL, "%s: out must be device memory", what);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t units = stage_tables(what, client_ptrs, key_numel, key_offset, key_kind, n_keys, K, host_ws, dev_ws,
+                                     ws_bytes, s);
+  if (units <= 0) return static_cast<int>(units);
+  const auto* keys = static_cast<const SegKey*>(dev_ws);
+  const auto* ptrs = reinterpret_cast<const int64_t*>(static_cast<const char*>(dev_ws) +
+                                                      n_keys * static_cast<int64_t>(sizeof(SegKey)));
+  // round-split: equal launches of at most 3 x CUs workgroups (the reduce's schedule)
+  const int64_t cap = static_cast<int64_t>(kSegBlocksPerCU) * cu_count();
+  const int64_t nl = (units + cap - 1) / cap;
+  const int64_t per = (units + nl - 1) / nl;
+  for (int64_t u0 = 0; u0 < units; u0 += per) {
+    const int64_t nb = units - u0 < per ? units - u0 : per;
+    hipLaunchKernelGGL((reduce_segments_f32_kernel<kSegU, kSegC>), dim3(static_cast<unsigned>(nb)), dim3(kBlock), 0,
+                       s, keys, ptrs, n_keys, u0, static_cast<int>(K), weights, out);
+  }
+  return launch_status(what);
+}
+
+int fedavg_client_sqdist_segments_f32(const int64_t* client_ptrs, const int64_t* key_numel, const int64_t* key_offset,
+                                      const int64_t* key_kind, int64_t n_keys, int64_t K, const float* glob,
+                                      double* partials, int64_t partial_elems, double* sumsq, void* host_ws,
+                                      void* dev_ws, int64_t ws_bytes, void* stream) {
+  const char* what = "fedavg_client_sqdist_segments_f32";
+  if (!glob || !partials || !sumsq) return set_error(FEDAVG_EINVAL, "%s: null glob/partials/sumsq", what);
+  if (!device_memory(glob) || !device_memory(partials) || !device_memory(sumsq))
+    return set_error(FEDAVG_EINVAL, "%s: glob, partials and sumsq must be device memory", what);
+  const int64_t need = fedavg_segments_partials(key_numel, n_keys, K);
+  if (partial_elems < need) return set_error(FEDAVG_EINVAL, "%s: partials need %lld doubles", what, (long long)need);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t units = stage_tables(what, client_ptrs, key_numel, key_offset, key_kind, n_keys, K, host_ws, dev_ws,
+                                     ws_bytes, s);
+  if (units < 0) return static_cast<int>(units);
+  if (units == 0) {
+    const hipError_t e = hipMemsetAsync(sumsq, 0, static_cast<size_t>(K) * sizeof(double), s);
+    return e == hipSuccess ? FEDAVG_OK : set_error(-static_cast<int>(e), "%s: hipMemsetAsync failed", what);
+  }
+  const auto* keys = static_cast<const SegKey*>(dev_ws);
+  const auto* ptrs = reinterpret_cast<const int64_t*>(static_cast<const char*>(dev_ws) +
+                                                      n_keys * static_cast<int64_t>(sizeof(SegKey)));
+  const int64_t nparts = units * (kBlock / 64);
+  hipLaunchKernelGGL((sqdist_segments_f32_kernel<kSegC>), dim3(static_cast<unsigned>(units)), dim3(kBlock), 0, s, keys,
+                     ptrs, n_keys, int64_t(0), static_cast<int>(K), glob, partials, nparts);
+  int rc = launch_status(what);
+  if (rc) return rc;
+  hipLaunchKernelGGL(segments_finalize_kernel, dim3(static_cast<unsigned>(K)), dim3(kBlock), 0, s, partials, nparts,
+                     sumsq);
+  return launch_status(what);
+}
+
+}  // extern "C"

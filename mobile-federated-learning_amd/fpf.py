@@ -240,7 +240,9 @@ class FPFTracker:
         if not ok:
             raise ValueError("record_round needs the device rows of the aggregate that produced w_glob; "
                              "call record_client(client_idx, w) before aggregate instead")
-        devbuf, _ = last["dev"][torch.float32]
+        devbuf = self._aggregator().materialize_rows()  # packed on demand after a zero-copy round
+        if devbuf is None:
+            raise ValueError("record_round: the round's client dicts are gone; call record_client before aggregate")
         self._set_rows(devbuf, devbuf.stride(0), idx)
 
     def fpf_index(self) -> np.ndarray:

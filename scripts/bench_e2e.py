@@ -162,7 +162,7 @@ def run(name, reps, cpu_aggregate, cpu_distances, train_ms=0.0):
     # the weights, the reduce; timed to the device result being complete
     dev = torch.device("cuda", 0)
     ddicts = [OrderedDict((k, v.to(dev)) for k, v in sd.items()) for sd in dicts]
-    dev_t, dcrit = [], []
+    dev_t, dcrit, ddist_t = [], [], []
     for r in range(reps + 1):
         wl = fresh(counts, ddicts)
         torch.cuda.synchronize()
@@ -172,6 +172,12 @@ def run(name, reps, cpu_aggregate, cpu_distances, train_ms=0.0):
         t = time.perf_counter() - t0
         if r:
             dev_t.append(t)
+        if not has_bool:  # :291 right after, on the clients' own tensors
+            t0 = time.perf_counter()
+            dnorms = agg.client_distances(wl, dout)
+            t = time.perf_counter() - t0
+            if r:
+                ddist_t.append(t)
     same_dev = all(torch.equal(dout[k].cpu().reshape(-1).view(torch.int32), out[k].reshape(-1).view(torch.int32))
                    for k in out)
     for r in range(reps + 1):
@@ -210,6 +216,9 @@ def run(name, reps, cpu_aggregate, cpu_distances, train_ms=0.0):
         "device_clients_ms_median": round(gd * 1e3, 3), "device_clients_GBps": round(alg / gd / 1e9, 2),
         "device_clients_stream_finish_ms_median": round(float(np.median(dcrit)) * 1e3, 3),
         "device_clients_bit_exact": bool(same_dev),
+        "device_clients_dist_ms_median": round(float(np.median(ddist_t)) * 1e3, 3) if ddist_t else None,
+        "device_clients_dist_max_rel_vs_host": (float(np.max(np.abs(dnorms - norms) / np.maximum(np.abs(norms), 1e-30)))
+                                                if ddist_t and dist_t else None),
         "dist_ms_median": round(float(np.median(dist_t)) * 1e3, 3) if dist_t else None,
         "cpu_dist_ms_median": round(float(np.median(cpu_dist_t)) * 1e3, 3),
         "dist_max_rel_vs_cpu_ref": dist_rel,

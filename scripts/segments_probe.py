@@ -1,0 +1,91 @@
+"""Zero-copy (segments) reduce vs the row reduce, on the same bytes.
+
+    python scripts/segments_probe.py [--K 100 --P 25000000] [--rounds 4] [--reps 8]
+
+Three variants, interleaved in one process, all bit-identical:
+  rows         production reduce on one [K, ld] buffer (fedavg_reduce_f32),
+  seg-rows     fedavg_reduce_segments_f32 with the pointers set to the rows of
+               that same buffer (one key of P elements per client),
+  seg-tensors  fedavg_reduce_segments_f32 on K separately allocated client
+               tensors (the device-resident drop-in's case).
+Separates the kernel's own cost from where the clients' memory lies.  One
+JSON line per variant: median ms per call (HIP events) and GB/s.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+import numpy as np
+import torch
+
+import mfl_amd
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--K", type=int, default=100)
+    ap.add_argument("--P", type=int, default=25_000_000)
+    ap.add_argument("--rounds", type=int, default=4)
+    ap.add_argument("--reps", type=int, default=8)
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    lib = mfl_amd._lib.load()
+    K, P = args.K, args.P
+    ld = (P + 63) // 64 * 64
+    rows = torch.empty((K, ld), device=dev)
+    g = torch.Generator(device=dev).manual_seed(3)
+    tensors = []
+    for k in range(K):
+        t = torch.randn(P, generator=g, device=dev) * 0.05
+        rows[k, :P].copy_(t)
+        tensors.append(t)
+    w = mfl_amd.weights_tensor(mfl_amd.sample_weights(list(range(1, K + 1))), torch.float32, dev)
+    outs = {n: torch.empty(P, device=dev) for n in ("rows", "seg-rows", "seg-tensors")}
+    meta = [np.array([v], dtype=np.int64) for v in (P, 0, 0)]
+    ptr_rows = np.array([[rows[k].data_ptr()] for k in range(K)], dtype=np.int64)
+    ptr_tens = np.array([[t.data_ptr()] for t in tensors], dtype=np.int64)
+    need = lib.fedavg_segments_workspace(K, 1)
+    ws = {n: (torch.empty(need, dtype=torch.uint8, pin_memory=True), torch.empty(need, dtype=torch.uint8, device=dev))
+          for n in ("seg-rows", "seg-tensors")}
+    stream = torch.cuda.current_stream(dev)
+
+    def run(n):
+        if n == "rows":
+            mfl_amd.reduce_packed(rows, w, P, outs[n])
+            return
+        ptrs = ptr_rows if n == "seg-rows" else ptr_tens
+        h, d = ws[n]
+        mfl_amd._lib.check(lib.fedavg_reduce_segments_f32(ptrs.ctypes.data, meta[0].ctypes.data, meta[1].ctypes.data,
+                                                          meta[2].ctypes.data, 1, K, w.data_ptr(), outs[n].data_ptr(),
+                                                          h.data_ptr(), d.data_ptr(), need, stream.cuda_stream), n)
+
+    for n in outs:
+        run(n)
+    torch.cuda.synchronize()
+    same = all(torch.equal(outs[n].view(torch.int32), outs["rows"].view(torch.int32)) for n in outs)
+    times = {n: [] for n in outs}
+    for _ in range(args.rounds):
+        for n in outs:
+            for _ in range(args.reps):
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                run(n)
+                e.record()
+                times[n].append((s, e))
+            torch.cuda.synchronize()  # the pinned table of the next call
+    alg = 4 * K * P + 4 * P + 4 * K
+    for n in outs:
+        ms = float(np.median([s.elapsed_time(e) for s, e in times[n]]))
+        print(json.dumps({"variant": n, "K": K, "P": P, "ms_median": round(ms, 4), "GBps": round(alg / ms / 1e6, 1),
+                          "bit_identical": bool(same)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

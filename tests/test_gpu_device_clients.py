@@ -39,12 +39,14 @@ def _to_dev(w_locals):
 _CASES = [c for c in case_names() if c not in ("empty_w_locals", "no_keys_k2")]
 
 
+@pytest.mark.parametrize("rows", [False, True], ids=["zero_copy", "rows"])
 @pytest.mark.parametrize("name", _CASES)
-def test_device_clients_match_reference_golden(name):
+def test_device_clients_match_reference_golden(name, rows, monkeypatch):
     _, w_locals, expected = load_case(name)
     dl = _to_dev(w_locals)
     first = dl[0][1]
     others = [dict(sd) for _, sd in dl[1:]]
+    monkeypatch.setattr(mfl_amd.DeviceAggregator, "DEVICE_SEGMENTS", not rows)
     out = mfl_amd.aggregate(dl)  # the device is taken from the clients' tensors
     assert out is first
     assert list(out.keys()) == list(expected.keys())
@@ -253,3 +255,110 @@ def test_device_and_host_rounds_alternate_on_one_aggregator(name):
         for k in exp:
             assert out[k].device.type == ("cuda" if r % 2 == 0 else "cpu")
             assert_bits(out[k], exp[k], f"{name} round {r} {k}")
+
+
+def _segment_case(K, specs, seed, offset_base=3):
+    """K clients whose keys are views into one flat device buffer per client at
+    odd fp32 offsets (4-B aligned, not 16-B), of the given (shape, dtype)."""
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    dicts = []
+    for i in range(K):
+        sizes = [int(np.prod(shape)) for shape, _ in specs]
+        flat = torch.empty(sum(sizes) + 4 * len(specs) + offset_base, device=DEV)
+        sd, off = OrderedDict(), offset_base + i % 3
+        for j, ((shape, dt), n) in enumerate(zip(specs, sizes)):
+            if dt == torch.float32:
+                sd[f"k{j}"] = (torch.randn(n, generator=g, device=DEV) * 0.05).view(shape)
+                flat[off:off + n] = sd[f"k{j}"].reshape(-1)
+                sd[f"k{j}"] = flat[off:off + n].view(shape)
+                off += n + 1
+            elif dt == torch.bool:
+                sd[f"k{j}"] = torch.rand(shape, generator=g, device=DEV) > 0.5
+            else:
+                sd[f"k{j}"] = torch.randint(-3000, 3000, shape, generator=g, device=DEV).to(dt)
+        dicts.append(sd)
+    counts = [int(c) for c in np.random.default_rng(seed).integers(1, 1000, size=K)]
+    return [(n, sd) for n, sd in zip(counts, dicts)]
+
+
+_SEG_SPECS = [((8192,), torch.float32), ((8191,), torch.float32), ((8193,), torch.float32), ((0,), torch.float32),
+              ((3, 5), torch.float32), ((), torch.int64), ((7,), torch.int32), ((1,), torch.float32),
+              ((40_001,), torch.float32), ((5, 2), torch.bool), ((16_384 * 3 + 2,), torch.float32)]
+
+
+@pytest.mark.parametrize("K", [1, 2, 5, 33])
+def test_segments_reduce_bit_identical_to_rows(K):
+    """Zero-copy reduce (fedavg_reduce_segments_f32, views at odd offsets,
+    key tails around the 8,192-column unit, integer/bool keys) against the
+    packed-rows reduce of the same clients and the torch oracle."""
+    wl = _segment_case(K, _SEG_SPECS, seed=K)
+    ref = O.aggregate_torch([(n, OrderedDict((k, v.cpu()) for k, v in sd.items())) for n, sd in wl])
+    seg = mfl_amd.DeviceAggregator(DEV)
+    rows = mfl_amd.DeviceAggregator(DEV)
+    rows.DEVICE_SEGMENTS = False
+    out_seg = seg.aggregate([(n, OrderedDict(sd)) for n, sd in wl])
+    assert seg._last["dev"][torch.float32][0] is None  # no rows were packed
+    out_rows = rows.aggregate([(n, OrderedDict(sd)) for n, sd in wl])
+    for k in ref:
+        assert_bits(out_seg[k], ref[k], f"segments K={K} {k}")
+        assert_bits(out_rows[k], out_seg[k].cpu(), f"rows vs segments K={K} {k}")
+
+
+def test_segments_distances_match_rows_path():
+    wl = _segment_case(9, [s for s in _SEG_SPECS if s[1] != torch.bool], seed=11)
+    seg = mfl_amd.DeviceAggregator(DEV)
+    rows = mfl_amd.DeviceAggregator(DEV)
+    rows.DEVICE_SEGMENTS = False
+    wa = [(n, OrderedDict(sd)) for n, sd in wl]
+    wb = [(n, OrderedDict(sd)) for n, sd in wl]
+    ga, gb = seg.aggregate(wa), rows.aggregate(wb)
+    na = seg.client_distances(wa, ga)  # zero-copy sums of squares
+    nb = rows.client_distances(wb, gb)  # packed rows
+    ref_locals = [(n, OrderedDict((k, v.cpu()) for k, v in sd.items())) for n, sd in wl]
+    ref_glob = O.aggregate_torch(copy.deepcopy(ref_locals))
+    ref_locals[0] = (ref_locals[0][0], ref_glob)
+    exact = O.client_distances_exact(ref_locals, ref_glob)
+    assert na[0] == 0.0 and nb[0] == 0.0
+    assert np.all(np.abs(na - exact) <= np.spacing(exact.astype(np.float32)).astype(np.float64))
+    assert np.all(np.abs(na - nb) <= np.spacing(exact.astype(np.float32)).astype(np.float64))
+
+
+def test_segments_rows_materialized_for_fpf_record_round():
+    """After a zero-copy round the rows are packed on demand (client 0 from its
+    own tensors, not the average its dict now holds)."""
+    _, w_locals, _ = load_case("mnist_lr_k10")
+    dl = _to_dev(w_locals)
+    client0 = OrderedDict((k, v.clone()) for k, v in dl[0][1].items())
+    agg = mfl_amd.DeviceAggregator(DEV)
+    agg.aggregate(dl)
+    rows = agg.materialize_rows()
+    assert rows is not None and rows.shape[0] == 10
+    P = sum(v.numel() for v in client0.values())
+    exp0 = torch.cat([v.reshape(-1) for v in client0.values()])
+    exp3 = torch.cat([v.reshape(-1) for v in dl[3][1].values()])
+    assert torch.equal(rows[0, :P], exp0) and torch.equal(rows[3, :P], exp3)
+    assert agg.materialize_rows() is rows or torch.equal(agg.materialize_rows(), rows)
+
+
+def test_segments_rejects_host_sources():
+    lib = mfl_amd._lib.load()
+    host = torch.ones(100)
+    out = torch.zeros(100, device=DEV)
+    w = torch.ones(1, device=DEV)
+    need = lib.fedavg_segments_workspace(1, 1)
+    ws_h = torch.empty(need, dtype=torch.uint8, pin_memory=True)
+    ws_d = torch.empty(need, dtype=torch.uint8, device=DEV)
+    ptrs = np.array([[host.data_ptr()]], dtype=np.int64)
+    meta = [np.array([v], dtype=np.int64) for v in (100, 0, 0)]
+    rc = lib.fedavg_reduce_segments_f32(ptrs.ctypes.data, meta[0].ctypes.data, meta[1].ctypes.data,
+                                        meta[2].ctypes.data, 1, 1, w.data_ptr(), out.data_ptr(), ws_h.data_ptr(),
+                                        ws_d.data_ptr(), need, None)
+    assert rc == -10001
+    dsrc = torch.ones(101, device=DEV)
+    odd = np.array([[dsrc.data_ptr() + 2]], dtype=np.int64)  # not fp32-aligned
+    rc = lib.fedavg_reduce_segments_f32(odd.ctypes.data, meta[0].ctypes.data, meta[1].ctypes.data,
+                                        meta[2].ctypes.data, 1, 1, w.data_ptr(), out.data_ptr(), ws_h.data_ptr(),
+                                        ws_d.data_ptr(), need, None)
+    assert rc == -10001
+    torch.cuda.synchronize()
+    assert float(out.sum()) == 0.0
