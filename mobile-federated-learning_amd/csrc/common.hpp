@@ -53,6 +53,45 @@ int check_common(const void* clients, int64_t K, int64_t P, int64_t ld, const vo
 __host__ __device__ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 __host__ __device__ inline bool aligned4(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 3u) == 0; }
 
+// hipPointerGetAttributes: is p device memory / pinned host memory of the
+// runtime (host-side checks before a kernel dereferences caller addresses)
+inline bool is_device_memory(const void* p) {
+  hipPointerAttribute_t attr;
+  if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return attr.type == hipMemoryTypeDevice;
+}
+
+inline bool is_pinned_host_memory(const void* p) {
+  hipPointerAttribute_t attr;
+  if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return attr.type == hipMemoryTypeHost;
+}
+
+// The largest i in [0, n) with start(i) <= g, for a nondecreasing start()
+// with start(0) <= g: 64 probes per round across the wave, ballot, keep the
+// last hit (a few rounds instead of a binary search's ~15 dependent loads for
+// tables of tens of thousands of entries).  Every lane returns the same i.
+template <typename Start>
+__device__ __forceinline__ int64_t wave_search_last_le(Start start, int64_t n, int64_t g) {
+  const int lane = static_cast<int>(threadIdx.x & 63u);
+  int64_t lo = 0, hi = n;
+  while (hi - lo > 1) {
+    const int64_t step = (hi - lo + 63) / 64;
+    const int64_t idx = lo + lane * step;
+    const bool hit = idx < hi && start(idx) <= g;
+    const unsigned long long m = __ballot(hit);
+    lo += (63 - __clzll(m)) * step;
+    hi = hi < lo + step ? hi : lo + step;
+  }
+  return lo;
+}
+
 inline unsigned grid_for(int64_t items, int per_block) {
   return static_cast<unsigned>((items + per_block - 1) / per_block);
 }

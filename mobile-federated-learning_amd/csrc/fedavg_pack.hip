@@ -112,23 +112,6 @@ __device__ __forceinline__ void copy_raw(const char* __restrict__ s, char* __res
   }
 }
 
-// the largest i < n_items with start[i] <= g (start nondecreasing, start[0] =
-// 0 <= g): 64 probes per round across the wave, ballot, keep the last hit
-__device__ __forceinline__ int64_t find_item(const int64_t* __restrict__ start, int64_t n_items, int64_t g) {
-  const int lane = lane_id();
-  int64_t lo = 0, hi = n_items;
-  while (hi - lo > 1) {
-    const int64_t step = (hi - lo + 63) / 64;
-    const int64_t idx = lo + lane * step;
-    const bool hit = idx < hi && start[idx] <= g;
-    const unsigned long long m = __ballot(hit);
-    const int last = 63 - __clzll(m);
-    lo += last * step;
-    hi = hi < lo + step ? hi : lo + step;
-  }
-  return lo;
-}
-
 __global__ __launch_bounds__(kPackThreads) void pack_rows_device_kernel(const fedavg_pack_item* __restrict__ items,
                                                                         const int64_t* __restrict__ start,
                                                                         int64_t n_items, int64_t total,
@@ -136,7 +119,7 @@ __global__ __launch_bounds__(kPackThreads) void pack_rows_device_kernel(const fe
   const int64_t g0 = static_cast<int64_t>(blockIdx.x) * kPackBlockElems + (threadIdx.x / kWave) * kPackChunk;
   if (g0 >= total) return;  // a wave past the end of the last workgroup's range
   const int64_t g1 = total - g0 < kPackChunk ? total : g0 + kPackChunk;
-  for (int64_t i = find_item(start, n_items, g0); i < n_items; ++i) {
+  for (int64_t i = wave_search_last_le([&](int64_t x) { return start[x]; }, n_items, g0); i < n_items; ++i) {
     const int64_t s0 = start[i];
     if (s0 >= g1) break;
     const fedavg_pack_item it = items[i];
@@ -156,15 +139,6 @@ __global__ __launch_bounds__(kPackThreads) void pack_rows_device_kernel(const fe
       default: break;  // rejected on the host
     }
   }
-}
-
-bool device_memory(const void* p) {
-  hipPointerAttribute_t attr;
-  if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
-    (void)hipGetLastError();
-    return false;
-  }
-  return attr.type == hipMemoryTypeDevice;
 }
 
 int64_t items_bytes(int64_t n_items) { return n_items * static_cast<int64_t>(sizeof(fedavg_pack_item)); }
@@ -190,13 +164,9 @@ int fedavg_pack_rows_device(const fedavg_pack_item* items, int64_t n_items, void
                      (long long)fedavg_pack_rows_device_workspace(n_items));
   if (!aligned16(host_ws) || !aligned16(dev_ws) || !aligned16(dst_base))
     return set_error(FEDAVG_EALIGN, "%s: dst_base and the workspaces must be 16-B aligned", what);
-  if (!device_memory(dst_base) || !device_memory(dev_ws))
+  if (!is_device_memory(dst_base) || !is_device_memory(dev_ws))
     return set_error(FEDAVG_EINVAL, "%s: dst_base and dev_ws must be device memory", what);
-  hipPointerAttribute_t attr;
-  if (hipPointerGetAttributes(&attr, host_ws) != hipSuccess || attr.type != hipMemoryTypeHost) {
-    (void)hipGetLastError();
-    return set_error(FEDAVG_EINVAL, "%s: host_ws is not pinned host memory", what);
-  }
+  if (!is_pinned_host_memory(host_ws)) return set_error(FEDAVG_EINVAL, "%s: host_ws is not pinned host memory", what);
   auto* h_items = static_cast<fedavg_pack_item*>(host_ws);
   auto* h_start = reinterpret_cast<int64_t*>(static_cast<char*>(host_ws) + items_bytes(n_items));
   int64_t total = 0;
@@ -222,7 +192,7 @@ int fedavg_pack_rows_device(const fedavg_pack_item* items, int64_t n_items, void
   // the sources must live in HBM: a host address would fault the kernel
   // (spot check of the first and last source; the Python layer checks every
   // tensor's device)
-  if (!device_memory(first_src) || !device_memory(last_src))
+  if (!is_device_memory(first_src) || !is_device_memory(last_src))
     return set_error(FEDAVG_EINVAL, "%s: item sources must be device memory", what);
   hipStream_t s = static_cast<hipStream_t>(stream);
   const hipError_t e = hipMemcpyAsync(dev_ws, host_ws, static_cast<size_t>(fedavg_pack_rows_device_workspace(n_items)),

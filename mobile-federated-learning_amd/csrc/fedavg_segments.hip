@@ -35,21 +35,10 @@ struct SegKey {
   int64_t numel, out_offset, kind, unit_start;
 };
 
-// the key owning unit u: the largest j with keys[j].unit_start <= u (keys
-// without units share their successor's start and lose the tie); 64 probes
-// per round across the wave
+// the key owning unit u (keys without units share their successor's start
+// and lose the tie)
 __device__ __forceinline__ int64_t find_key(const SegKey* __restrict__ keys, int64_t n_keys, int64_t u) {
-  const int lane = static_cast<int>(threadIdx.x & 63u);
-  int64_t lo = 0, hi = n_keys;
-  while (hi - lo > 1) {
-    const int64_t step = (hi - lo + 63) / 64;
-    const int64_t idx = lo + lane * step;
-    const bool hit = idx < hi && keys[idx].unit_start <= u;
-    const unsigned long long m = __ballot(hit);
-    lo += (63 - __clzll(m)) * step;
-    hi = hi < lo + step ? hi : lo + step;
-  }
-  return lo;
+  return wave_search_last_le([&](int64_t x) { return keys[x].unit_start; }, n_keys, u);
 }
 
 // Client addresses come from the pointer table as integers, so the compiler
@@ -296,15 +285,6 @@ __global__ __launch_bounds__(kBlock) void segments_finalize_kernel(const double*
   if (threadIdx.x == 0) sumsq[k] = red[0];
 }
 
-bool device_memory(const void* p) {
-  hipPointerAttribute_t attr;
-  if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
-    (void)hipGetLastError();
-    return false;
-  }
-  return attr.type == hipMemoryTypeDevice;
-}
-
 int64_t units_of(const int64_t* numel, int64_t n_keys) {
   int64_t units = 0;
   for (int64_t j = 0; j < n_keys; ++j) units += (numel[j] + kSegSpan - 1) / kSegSpan;
@@ -323,12 +303,8 @@ int64_t stage_tables(const char* what, const int64_t* client_ptrs, const int64_t
     return set_error(FEDAVG_EINVAL, "%s: workspace needs %lld bytes", what,
                      (long long)fedavg_segments_workspace(K, n_keys));
   if (!aligned16(host_ws) || !aligned16(dev_ws)) return set_error(FEDAVG_EALIGN, "%s: workspaces must be 16-B aligned", what);
-  hipPointerAttribute_t attr;
-  if (hipPointerGetAttributes(&attr, host_ws) != hipSuccess || attr.type != hipMemoryTypeHost) {
-    (void)hipGetLastError();
-    return set_error(FEDAVG_EINVAL, "%s: host_ws is not pinned host memory", what);
-  }
-  if (!device_memory(dev_ws)) return set_error(FEDAVG_EINVAL, "%s: dev_ws must be device memory", what);
+  if (!is_pinned_host_memory(host_ws)) return set_error(FEDAVG_EINVAL, "%s: host_ws is not pinned host memory", what);
+  if (!is_device_memory(dev_ws)) return set_error(FEDAVG_EINVAL, "%s: dev_ws must be device memory", what);
   auto* hk = static_cast<SegKey*>(host_ws);
   auto* hp = reinterpret_cast<int64_t*>(static_cast<char*>(host_ws) + n_keys * static_cast<int64_t>(sizeof(SegKey)));
   int64_t units = 0;
@@ -354,7 +330,7 @@ int64_t stage_tables(const char* what, const int64_t* client_ptrs, const int64_t
   if (units == 0) return 0;
   // a host address would fault the kernels: spot check of the first and last
   // source (the Python layer checks every tensor's device)
-  if (!device_memory(first_src) || !device_memory(last_src))
+  if (!is_device_memory(first_src) || !is_device_memory(last_src))
     return set_error(FEDAVG_EINVAL, "%s: client sources must be device memory", what);
   const hipError_t e = hipMemcpyAsync(dev_ws, host_ws, static_cast<size_t>(fedavg_segments_workspace(K, n_keys)),
                                       hipMemcpyHostToDevice, s);
@@ -384,7 +360,7 @@ int fedavg_reduce_segments_f32(const int64_t* client_ptrs, const int64_t* key_nu
                                void* host_ws, void* dev_ws, int64_t ws_bytes, void* stream) {
   const char* what = "fedavg_reduce_segments_f32";
   if (!weights || !out) return set_error(FEDAVG_EINVAL, "%s: null weights/out", what);
-  if (!device_memory(out)) return set_error(FEDAVG_EINVAL, "%s: out must be device memory", what);
+  if (!is_device_memory(out)) return set_error(FEDAVG_EINVAL, "%s: out must be device memory", what);
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int64_t units = stage_tables(what, client_ptrs, key_numel, key_offset, key_kind, n_keys, K, host_ws, dev_ws,
                                      ws_bytes, s);
@@ -410,7 +386,7 @@ int fedavg_client_sqdist_segments_f32(const int64_t* client_ptrs, const int64_t*
                                       void* dev_ws, int64_t ws_bytes, void* stream) {
   const char* what = "fedavg_client_sqdist_segments_f32";
   if (!glob || !partials || !sumsq) return set_error(FEDAVG_EINVAL, "%s: null glob/partials/sumsq", what);
-  if (!device_memory(glob) || !device_memory(partials) || !device_memory(sumsq))
+  if (!is_device_memory(glob) || !is_device_memory(partials) || !is_device_memory(sumsq))
     return set_error(FEDAVG_EINVAL, "%s: glob, partials and sumsq must be device memory", what);
   const int64_t need = fedavg_segments_partials(key_numel, n_keys, K);
   if (partial_elems < need) return set_error(FEDAVG_EINVAL, "%s: partials need %lld doubles", what, (long long)need);

@@ -36,11 +36,7 @@ int fedavg_copy_to_host(const void* src, void* host_dst, int64_t bytes, int bloc
   if (!aligned16(src) || !aligned16(host_dst))
     return set_error(FEDAVG_EALIGN, "%s: src and host_dst must be 16-B aligned", what);
   // only pinned (registered) host memory is reachable from the device
-  hipPointerAttribute_t attr;
-  if (hipPointerGetAttributes(&attr, host_dst) != hipSuccess || attr.type != hipMemoryTypeHost) {
-    (void)hipGetLastError();
-    return set_error(FEDAVG_EINVAL, "%s: host_dst is not pinned host memory", what);
-  }
+  if (!is_pinned_host_memory(host_dst)) return set_error(FEDAVG_EINVAL, "%s: host_dst is not pinned host memory", what);
   if (blocks < 0) return set_error(FEDAVG_EINVAL, "%s: blocks must be >= 0", what);
   if (blocks == 0) {
     const hipError_t e = hipMemcpyAsync(host_dst, src, static_cast<size_t>(bytes), hipMemcpyDeviceToHost,
@@ -76,11 +72,7 @@ int fedavg_upload_shard(void* dst, int64_t dst_pitch_bytes, const void* host_src
   if (rows == 0 || width_bytes == 0) return FEDAVG_OK;
   if (!dst || !host_src) return set_error(FEDAVG_EINVAL, "%s: null buffer", what);
   // async only from pinned memory; a pageable source would silently serialise
-  hipPointerAttribute_t attr;
-  if (hipPointerGetAttributes(&attr, host_src) != hipSuccess || attr.type != hipMemoryTypeHost) {
-    (void)hipGetLastError();
-    return set_error(FEDAVG_EINVAL, "%s: host_src is not pinned host memory", what);
-  }
+  if (!is_pinned_host_memory(host_src)) return set_error(FEDAVG_EINVAL, "%s: host_src is not pinned host memory", what);
   const hipError_t e = hipMemcpy2DAsync(dst, static_cast<size_t>(dst_pitch_bytes), host_src,
                                         static_cast<size_t>(src_pitch_bytes), static_cast<size_t>(width_bytes),
                                         static_cast<size_t>(rows), hipMemcpyHostToDevice,
