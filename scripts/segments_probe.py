@@ -7,7 +7,8 @@ Three variants, interleaved in one process, all bit-identical:
   seg-rows     fedavg_reduce_segments_f32 with the pointers set to the rows of
                that same buffer (one key of P elements per client),
   seg-tensors  fedavg_reduce_segments_f32 on K separately allocated client
-               tensors (the device-resident drop-in's case).
+               tensors (the device-resident drop-in's case),
+  *-pow2-pitch the first two on rows at a power-of-two pitch (128 MiB).
 Separates the kernel's own cost from where the clients' memory lies.  One
 JSON line per variant: median ms per call (HIP events) and GB/s.
 """
@@ -47,20 +48,33 @@ def main():
         rows[k, :P].copy_(t)
         tensors.append(t)
     w = mfl_amd.weights_tensor(mfl_amd.sample_weights(list(range(1, K + 1))), torch.float32, dev)
-    outs = {n: torch.empty(P, device=dev) for n in ("rows", "seg-rows", "seg-tensors")}
+    # rows of one buffer at a power-of-two pitch (128 MiB for P=25M): do
+    # congruent client starts alone cost the separate tensors their rate?
+    ld2 = 1 << max(0, (P - 1).bit_length())
+    rows2 = torch.empty((K, ld2), device=dev)
+    rows2[:, :P].copy_(rows[:, :P])
+    outs = {n: torch.empty(P, device=dev) for n in ("rows", "rows-pow2-pitch", "seg-rows", "seg-pow2-pitch",
+                                                    "seg-tensors")}
     meta = [np.array([v], dtype=np.int64) for v in (P, 0, 0)]
     ptr_rows = np.array([[rows[k].data_ptr()] for k in range(K)], dtype=np.int64)
     ptr_tens = np.array([[t.data_ptr()] for t in tensors], dtype=np.int64)
+    ptr_pow2 = np.array([[rows2[k].data_ptr()] for k in range(K)], dtype=np.int64)
+    starts = [int(t.data_ptr()) for t in tensors]
+    print(json.dumps({"tensor_start_alignment_log2": [min(31, (a & -a).bit_length() - 1) for a in starts[:8]],
+                      "pitch_bytes_rows": ld * 4, "pitch_bytes_pow2": ld2 * 4}), flush=True)
     need = lib.fedavg_segments_workspace(K, 1)
     ws = {n: (torch.empty(need, dtype=torch.uint8, pin_memory=True), torch.empty(need, dtype=torch.uint8, device=dev))
-          for n in ("seg-rows", "seg-tensors")}
+          for n in ("seg-rows", "seg-pow2-pitch", "seg-tensors")}
     stream = torch.cuda.current_stream(dev)
 
     def run(n):
         if n == "rows":
             mfl_amd.reduce_packed(rows, w, P, outs[n])
             return
-        ptrs = ptr_rows if n == "seg-rows" else ptr_tens
+        if n == "rows-pow2-pitch":
+            mfl_amd.reduce_packed(rows2, w, P, outs[n])
+            return
+        ptrs = {"seg-rows": ptr_rows, "seg-pow2-pitch": ptr_pow2, "seg-tensors": ptr_tens}[n]
         h, d = ws[n]
         mfl_amd._lib.check(lib.fedavg_reduce_segments_f32(ptrs.ctypes.data, meta[0].ctypes.data, meta[1].ctypes.data,
                                                           meta[2].ctypes.data, 1, K, w.data_ptr(), outs[n].data_ptr(),
