@@ -125,6 +125,19 @@ int fedavg_fpf_index_variant(const float* diffs, int64_t n_rows, int64_t ld, int
 int fedavg_reduce_f32_xcd(const float* clients, int64_t K, int64_t P, int64_t ld, const float* weights, float* out,
                           int max_blocks, void* stream);
 
+/*
+ * Zero-copy device-client reduce (fedavg_reduce_segments_f32, same tables and
+ * workspaces) with an explicit schedule: unroll client pointers per load
+ * batch x cols 16-B slices per thread, (U, C) in {(4,8) production, (8,4),
+ * (2,8), (4,4), (8,2), (16,2), (2,16), (1,16)}; units of 1,024 x cols
+ * columns; round-split launches of <= blocks_per_cu x CUs workgroups
+ * (0 = one launch).  Same bits as the production call.
+ */
+int fedavg_reduce_segments_f32_variant(const int64_t* client_ptrs, const int64_t* key_numel, const int64_t* key_offset,
+                                       const int64_t* key_kind, int64_t n_keys, int64_t K, const float* weights,
+                                       float* out, void* host_ws, void* dev_ws, int64_t ws_bytes, int unroll, int cols,
+                                       int blocks_per_cu, void* stream);
+
 int fedavg_probe_read_f32x4(const float* buf, int64_t nvec, int mode, int blocks, int launches, float* sink,
                             void* stream);
 

@@ -10,8 +10,9 @@
 // k's address of key j).  Each key is cut into units of kSegSpan columns; a
 // workgroup reduces one unit over all K clients with the production schedule
 // (U4 client rows per batch, C8 16-B column slices per thread), reading each
-// client through its pointer with dword-aligned global_load_dwordx4 (client
-// tensors need only fp32 alignment), in the reference's client order with
+// client through its pointer with dword-aligned 16-B loads (client tensors
+// need only fp32 alignment; full units through a buffer descriptor per
+// client, tails through global pointers), in the reference's client order with
 // separately rounded products and sums -- the bits of fedavg_reduce_f32 on
 // the packed rows.  Integer/bool keys (num_batches_tracked, ...) are converted
 // to fp32 per element with static_cast, as the packers do.  Units are issued
@@ -28,6 +29,7 @@ constexpr int kSegU = 4;
 constexpr int kSegC = 8;
 constexpr int64_t kSegSpan = static_cast<int64_t>(kBlock) * kSegC * 4;  // columns per unit
 constexpr int kSegBlocksPerCU = 3;
+constexpr int64_t kSegSpanMaxBytes = static_cast<int64_t>(kBlock) * 16 * 16;  // widest unit (C = 16), bytes
 
 enum : int64_t { kRaw = 0, kI64 = 1, kI32 = 2, kI16 = 3, kI8 = 4, kU8 = 5, kBool = 6 };
 
@@ -54,6 +56,27 @@ __device__ __forceinline__ gptr<T> to_global(const void* p) {
 }
 
 __device__ __forceinline__ f32x4 ldu(const float* p) { return __builtin_nontemporal_load(to_global<f32x4_a4>(p)); }
+
+// Full units read through a buffer descriptor per client: the wave-uniform
+// base (client pointer + unit start) goes to SGPRs via readfirstlane and each
+// lane's slice is a 32-bit voffset shared by every client, so a load costs no
+// 64-bit VGPR address (with plain global pointers the compiler hoists the
+// loop-invariant part into one 64-bit VGPR pair per (client, slice) load,
+// which caps the loads it keeps in flight).  aux 2 = nt, as ldu().
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t unit_rsrc(const float* unit_base) {
+  const uint64_t a = reinterpret_cast<uint64_t>(unit_base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32));
+  void* p = reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(p, 0, static_cast<int>(kSegSpanMaxBytes), 0x00020000);
+}
+
+__device__ __forceinline__ f32x4 ldb(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(byte_off), 0, 2);
+  return __builtin_bit_cast(f32x4, v);
+}
 
 // elements [col, col + 4) of a unit with n columns: a full 16-B vector, or
 // the valid head of one (the rest 0)
@@ -96,12 +119,15 @@ template <int U, int C, bool FULL>
 __device__ __forceinline__ void reduce_raw_unit(const int64_t* __restrict__ P, int K, int64_t c0, int64_t n,
                                                 const float* __restrict__ W, float* __restrict__ o) {
   f32x4 acc[C];
+  uint32_t off[C];  // byte offsets of this lane's slices inside the unit
+#pragma unroll
+  for (int s = 0; s < C; ++s) off[s] = 16u * (threadIdx.x + s * kBlock);
   const float w0 = W[0];
   const float* x0 = reinterpret_cast<const float*>(P[0]) + c0;
 #pragma unroll
   for (int s = 0; s < C; ++s) {
     const int64_t col = 4 * (threadIdx.x + s * kBlock);
-    acc[s] = (FULL ? ldu(x0 + col) : load_slice(x0, col, n)) * w0;  // :455, i == 0
+    acc[s] = (FULL ? ldb(unit_rsrc(x0), off[s]) : load_slice(x0, col, n)) * w0;  // :455, i == 0
   }
   const int nb = (K - 1) / U;
   int k = 1;
@@ -122,10 +148,13 @@ __device__ __forceinline__ void reduce_raw_unit(const int64_t* __restrict__ P, i
 #pragma unroll
     for (int r = 0; r < U; ++r) {
       const float* xr = reinterpret_cast<const float*>(cur[r]) + c0;
+      if constexpr (FULL) {
+        const __amdgpu_buffer_rsrc_t rr = unit_rsrc(xr);
 #pragma unroll
-      for (int s = 0; s < C; ++s) {
-        const int64_t col = 4 * (threadIdx.x + s * kBlock);
-        xs[r][s] = FULL ? ldu(xr + col) : load_slice(xr, col, n);
+        for (int s = 0; s < C; ++s) xs[r][s] = ldb(rr, off[s]);
+      } else {
+#pragma unroll
+        for (int s = 0; s < C; ++s) xs[r][s] = load_slice(xr, 4 * (threadIdx.x + s * kBlock), n);
       }
     }
 #pragma unroll
@@ -144,7 +173,7 @@ __device__ __forceinline__ void reduce_raw_unit(const int64_t* __restrict__ P, i
 #pragma unroll
     for (int s = 0; s < C; ++s) {
       const int64_t col = 4 * (threadIdx.x + s * kBlock);
-      const f32x4 term = (FULL ? ldu(xr + col) : load_slice(xr, col, n)) * w;
+      const f32x4 term = (FULL ? ldb(unit_rsrc(xr), off[s]) : load_slice(xr, col, n)) * w;
       acc[s] = acc[s] + term;
     }
   }
@@ -163,15 +192,16 @@ __global__ __launch_bounds__(kBlock) void reduce_segments_f32_kernel(const SegKe
                                                                      const int64_t* __restrict__ ptrs, int64_t n_keys,
                                                                      int64_t unit0, int K, const float* __restrict__ W,
                                                                      float* __restrict__ out) {
+  constexpr int64_t span = static_cast<int64_t>(kBlock) * C * 4;  // columns per unit
   const int64_t u = unit0 + blockIdx.x;
   const int64_t j = find_key(keys, n_keys, u);
   const SegKey key = keys[j];
-  const int64_t c0 = (u - key.unit_start) * kSegSpan;
-  const int64_t n = key.numel - c0 < kSegSpan ? key.numel - c0 : kSegSpan;
+  const int64_t c0 = (u - key.unit_start) * span;
+  const int64_t n = key.numel - c0 < span ? key.numel - c0 : span;
   const int64_t* P = ptrs + j * K;
   float* o = out + key.out_offset + c0;
   if (key.kind == kRaw) {
-    if (n == kSegSpan)
+    if (n == span)
       reduce_raw_unit<U, C, true>(P, K, c0, n, W, o);
     else
       reduce_raw_unit<1, C, false>(P, K, c0, n, W, o);
@@ -285,9 +315,9 @@ __global__ __launch_bounds__(kBlock) void segments_finalize_kernel(const double*
   if (threadIdx.x == 0) sumsq[k] = red[0];
 }
 
-int64_t units_of(const int64_t* numel, int64_t n_keys) {
+int64_t units_of(const int64_t* numel, int64_t n_keys, int64_t span = kSegSpan) {
   int64_t units = 0;
-  for (int64_t j = 0; j < n_keys; ++j) units += (numel[j] + kSegSpan - 1) / kSegSpan;
+  for (int64_t j = 0; j < n_keys; ++j) units += (numel[j] + span - 1) / span;
   return units;
 }
 
@@ -296,7 +326,7 @@ int64_t units_of(const int64_t* numel, int64_t n_keys) {
 // negative error code.
 int64_t stage_tables(const char* what, const int64_t* client_ptrs, const int64_t* numel, const int64_t* offset,
                      const int64_t* kind, int64_t n_keys, int64_t K, void* host_ws, void* dev_ws, int64_t ws_bytes,
-                     hipStream_t s) {
+                     hipStream_t s, int64_t span = kSegSpan) {
   if (n_keys <= 0 || K <= 0 || K > INT32_MAX || !client_ptrs || !numel || !offset || !kind || !host_ws || !dev_ws)
     return set_error(FEDAVG_EINVAL, "%s: bad arguments", what);
   if (ws_bytes < fedavg_segments_workspace(K, n_keys))
@@ -314,7 +344,7 @@ int64_t stage_tables(const char* what, const int64_t* client_ptrs, const int64_t
     if (numel[j] < 0 || offset[j] < 0 || kind[j] < kRaw || kind[j] > kBool)
       return set_error(FEDAVG_EINVAL, "%s: bad key %lld", what, (long long)j);
     hk[j] = SegKey{numel[j], offset[j], kind[j], units};
-    units += (numel[j] + kSegSpan - 1) / kSegSpan;
+    units += (numel[j] + span - 1) / span;
     for (int64_t k = 0; k < K; ++k) {
       const int64_t p = client_ptrs[k * n_keys + j];
       if (numel[j] > 0) {
@@ -339,6 +369,21 @@ int64_t stage_tables(const char* what, const int64_t* client_ptrs, const int64_t
     return set_error(-static_cast<int>(e), "%s: hipMemcpyAsync failed: %s", what, hipGetErrorString(e));
   }
   return units;
+}
+
+// round-split: equal launches of at most `cap` workgroups (production: 3 x
+// CUs, the reduce's schedule); cap <= 0 = one launch
+template <int U, int C>
+void launch_reduce_segments(const SegKey* keys, const int64_t* ptrs, int64_t n_keys, int64_t units, int64_t K,
+                            const float* weights, float* out, int64_t cap, hipStream_t s) {
+  if (cap <= 0) cap = units;
+  const int64_t nl = (units + cap - 1) / cap;
+  const int64_t per = (units + nl - 1) / nl;
+  for (int64_t u0 = 0; u0 < units; u0 += per) {
+    const int64_t nb = units - u0 < per ? units - u0 : per;
+    hipLaunchKernelGGL((reduce_segments_f32_kernel<U, C>), dim3(static_cast<unsigned>(nb)), dim3(kBlock), 0, s, keys,
+                       ptrs, n_keys, u0, static_cast<int>(K), weights, out);
+  }
 }
 
 }  // namespace
@@ -368,15 +413,8 @@ int fedavg_reduce_segments_f32(const int64_t* client_ptrs, const int64_t* key_nu
   const auto* keys = static_cast<const SegKey*>(dev_ws);
   const auto* ptrs = reinterpret_cast<const int64_t*>(static_cast<const char*>(dev_ws) +
                                                       n_keys * static_cast<int64_t>(sizeof(SegKey)));
-  // round-split: equal launches of at most 3 x CUs workgroups (the reduce's schedule)
-  const int64_t cap = static_cast<int64_t>(kSegBlocksPerCU) * cu_count();
-  const int64_t nl = (units + cap - 1) / cap;
-  const int64_t per = (units + nl - 1) / nl;
-  for (int64_t u0 = 0; u0 < units; u0 += per) {
-    const int64_t nb = units - u0 < per ? units - u0 : per;
-    hipLaunchKernelGGL((reduce_segments_f32_kernel<kSegU, kSegC>), dim3(static_cast<unsigned>(nb)), dim3(kBlock), 0,
-                       s, keys, ptrs, n_keys, u0, static_cast<int>(K), weights, out);
-  }
+  launch_reduce_segments<kSegU, kSegC>(keys, ptrs, n_keys, units, K, weights, out,
+                                       static_cast<int64_t>(kSegBlocksPerCU) * cu_count(), s);
   return launch_status(what);
 }
 
@@ -408,6 +446,41 @@ int fedavg_client_sqdist_segments_f32(const int64_t* client_ptrs, const int64_t*
   if (rc) return rc;
   hipLaunchKernelGGL(segments_finalize_kernel, dim3(static_cast<unsigned>(K)), dim3(kBlock), 0, s, partials, nparts,
                      sumsq);
+  return launch_status(what);
+}
+
+// tuning hook (fedavg_amd_tuning.h): the zero-copy reduce with an explicit
+// (U, C) schedule -- units of 1,024 x C columns -- and launch size; same bits
+int fedavg_reduce_segments_f32_variant(const int64_t* client_ptrs, const int64_t* key_numel, const int64_t* key_offset,
+                                       const int64_t* key_kind, int64_t n_keys, int64_t K, const float* weights,
+                                       float* out, void* host_ws, void* dev_ws, int64_t ws_bytes, int unroll, int cols,
+                                       int blocks_per_cu, void* stream) {
+  const char* what = "fedavg_reduce_segments_f32_variant";
+  if (!weights || !out) return set_error(FEDAVG_EINVAL, "%s: null weights/out", what);
+  if (!is_device_memory(out)) return set_error(FEDAVG_EINVAL, "%s: out must be device memory", what);
+  const int uc = unroll * 100 + cols;
+  if (uc != 408 && uc != 804 && uc != 208 && uc != 404 && uc != 802 && uc != 1602 && uc != 216 && uc != 116)
+    return set_error(FEDAVG_EMODE, "%s: unsupported (unroll, cols) = (%d, %d)", what, unroll, cols);
+  if (blocks_per_cu < 0) return set_error(FEDAVG_EINVAL, "%s: blocks_per_cu < 0", what);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t span = static_cast<int64_t>(kBlock) * cols * 4;
+  const int64_t units = stage_tables(what, client_ptrs, key_numel, key_offset, key_kind, n_keys, K, host_ws, dev_ws,
+                                     ws_bytes, s, span);
+  if (units <= 0) return static_cast<int>(units);
+  const auto* keys = static_cast<const SegKey*>(dev_ws);
+  const auto* ptrs = reinterpret_cast<const int64_t*>(static_cast<const char*>(dev_ws) +
+                                                      n_keys * static_cast<int64_t>(sizeof(SegKey)));
+  const int64_t cap = static_cast<int64_t>(blocks_per_cu) * cu_count();
+  switch (uc) {
+    case 408: launch_reduce_segments<4, 8>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;
+    case 804: launch_reduce_segments<8, 4>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;
+    case 208: launch_reduce_segments<2, 8>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;
+    case 404: launch_reduce_segments<4, 4>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;
+    case 802: launch_reduce_segments<8, 2>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;
+    case 1602: launch_reduce_segments<16, 2>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;
+    case 216: launch_reduce_segments<2, 16>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;
+    default: launch_reduce_segments<1, 16>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;
+  }
   return launch_status(what);
 }
 

@@ -1,6 +1,6 @@
 """Zero-copy (segments) reduce vs the row reduce, on the same bytes.
 
-    python scripts/segments_probe.py [--K 100 --P 25000000] [--rounds 4] [--reps 8]
+    python scripts/segments_probe.py [--K 100 --P 25000000] [--rounds 4] [--reps 8] [--sweep]
 
 Three variants, interleaved in one process, all bit-identical:
   rows         production reduce on one [K, ld] buffer (fedavg_reduce_f32),
@@ -34,6 +34,9 @@ def main():
     ap.add_argument("--P", type=int, default=25_000_000)
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--reps", type=int, default=8)
+    ap.add_argument("--sweep", action="store_true",
+                    help="also time fedavg_reduce_segments_f32_variant schedules (U, C, blocks per CU) on the "
+                         "separate tensors and on the rows")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -53,8 +56,12 @@ def main():
     ld2 = 1 << max(0, (P - 1).bit_length())
     rows2 = torch.empty((K, ld2), device=dev)
     rows2[:, :P].copy_(rows[:, :P])
-    outs = {n: torch.empty(P, device=dev) for n in ("rows", "rows-pow2-pitch", "seg-rows", "seg-pow2-pitch",
-                                                    "seg-tensors")}
+    names = ["rows", "rows-pow2-pitch", "seg-rows", "seg-pow2-pitch", "seg-tensors"]
+    sched = [(4, 8, 3), (4, 8, 0), (4, 8, 2), (4, 8, 4), (4, 8, 6), (8, 4, 3), (8, 4, 6), (2, 8, 3), (2, 8, 6),
+             (4, 4, 3), (4, 4, 6), (8, 2, 6), (16, 2, 3), (2, 16, 3), (1, 16, 3), (1, 16, 6)]
+    if args.sweep:
+        names += [f"var-{src}-U{u}C{c}b{b}" for src in ("tensors", "rows") for u, c, b in sched]
+    outs = {n: torch.empty(P, device=dev) for n in names}
     meta = [np.array([v], dtype=np.int64) for v in (P, 0, 0)]
     ptr_rows = np.array([[rows[k].data_ptr()] for k in range(K)], dtype=np.int64)
     ptr_tens = np.array([[t.data_ptr()] for t in tensors], dtype=np.int64)
@@ -64,7 +71,7 @@ def main():
                       "pitch_bytes_rows": ld * 4, "pitch_bytes_pow2": ld2 * 4}), flush=True)
     need = lib.fedavg_segments_workspace(K, 1)
     ws = {n: (torch.empty(need, dtype=torch.uint8, pin_memory=True), torch.empty(need, dtype=torch.uint8, device=dev))
-          for n in ("seg-rows", "seg-pow2-pitch", "seg-tensors")}
+          for n in names if n.startswith(("seg-", "var-"))}
     stream = torch.cuda.current_stream(dev)
 
     def run(n):
@@ -74,8 +81,17 @@ def main():
         if n == "rows-pow2-pitch":
             mfl_amd.reduce_packed(rows2, w, P, outs[n])
             return
-        ptrs = {"seg-rows": ptr_rows, "seg-pow2-pitch": ptr_pow2, "seg-tensors": ptr_tens}[n]
         h, d = ws[n]
+        if n.startswith("var-"):
+            _, src, uc = n.split("-")
+            u, rest = uc[1:].split("C")
+            c, b = rest.split("b")
+            ptrs = ptr_tens if src == "tensors" else ptr_rows
+            mfl_amd._lib.check(lib.fedavg_reduce_segments_f32_variant(
+                ptrs.ctypes.data, meta[0].ctypes.data, meta[1].ctypes.data, meta[2].ctypes.data, 1, K, w.data_ptr(),
+                outs[n].data_ptr(), h.data_ptr(), d.data_ptr(), need, int(u), int(c), int(b), stream.cuda_stream), n)
+            return
+        ptrs = {"seg-rows": ptr_rows, "seg-pow2-pitch": ptr_pow2, "seg-tensors": ptr_tens}[n]
         mfl_amd._lib.check(lib.fedavg_reduce_segments_f32(ptrs.ctypes.data, meta[0].ctypes.data, meta[1].ctypes.data,
                                                           meta[2].ctypes.data, 1, K, w.data_ptr(), outs[n].data_ptr(),
                                                           h.data_ptr(), d.data_ptr(), need, stream.cuda_stream), n)
@@ -83,7 +99,7 @@ def main():
     for n in outs:
         run(n)
     torch.cuda.synchronize()
-    same = all(torch.equal(outs[n].view(torch.int32), outs["rows"].view(torch.int32)) for n in outs)
+    same = {n: bool(torch.equal(outs[n].view(torch.int32), outs["rows"].view(torch.int32))) for n in outs}
     times = {n: [] for n in outs}
     for _ in range(args.rounds):
         for n in outs:
@@ -98,7 +114,7 @@ def main():
     for n in outs:
         ms = float(np.median([s.elapsed_time(e) for s, e in times[n]]))
         print(json.dumps({"variant": n, "K": K, "P": P, "ms_median": round(ms, 4), "GBps": round(alg / ms / 1e6, 1),
-                          "bit_identical": bool(same)}), flush=True)
+                          "bit_identical": same[n]}), flush=True)
 
 
 if __name__ == "__main__":

@@ -362,3 +362,45 @@ def test_segments_rejects_host_sources():
     assert rc == -10001
     torch.cuda.synchronize()
     assert float(out.sum()) == 0.0
+
+
+_SEG_VARIANTS = [(4, 8, 3), (4, 8, 0), (8, 4, 3), (2, 8, 6), (4, 4, 3), (8, 2, 6), (16, 2, 3), (2, 16, 3), (1, 16, 1)]
+
+
+@pytest.mark.parametrize("K", [1, 6, 19])
+def test_segments_variants_bit_identical(K):
+    """Every schedule of the tuning hook fedavg_reduce_segments_f32_variant
+    (units of 1,024 x C columns, so the key tails fall differently) gives the
+    production zero-copy reduce's bits, integer/bool keys included."""
+    kinds = {torch.float32: 0, torch.int64: 1, torch.int32: 2, torch.bool: 6}
+    wl = _segment_case(K, _SEG_SPECS, seed=100 + K)
+    keys = list(wl[0][1].keys())
+    numel = np.array([wl[0][1][k].numel() for k in keys], dtype=np.int64)
+    offset = np.concatenate([[0], np.cumsum(numel)[:-1]]).astype(np.int64)
+    kind = np.array([kinds[wl[0][1][k].dtype] for k in keys], dtype=np.int64)
+    ptrs = np.array([[sd[k].data_ptr() for k in keys] for _, sd in wl], dtype=np.int64)
+    w = mfl_amd.weights_tensor(mfl_amd.sample_weights([n for n, _ in wl]), torch.float32, DEV)
+    lib = mfl_amd._lib.load()
+    need = lib.fedavg_segments_workspace(K, len(keys))
+    P = int(numel.sum())
+    args = (ptrs.ctypes.data, numel.ctypes.data, offset.ctypes.data, kind.ctypes.data, len(keys), K, w.data_ptr())
+    ref = torch.full((P,), float("nan"), device=DEV)
+    ws = [(torch.empty(need, dtype=torch.uint8, pin_memory=True), torch.empty(need, dtype=torch.uint8, device=DEV))
+          for _ in range(len(_SEG_VARIANTS) + 1)]
+    mfl_amd._lib.check(lib.fedavg_reduce_segments_f32(*args, ref.data_ptr(), ws[0][0].data_ptr(),
+                                                      ws[0][1].data_ptr(), need, None), "production")
+    outs = []
+    for i, (u, c, b) in enumerate(_SEG_VARIANTS):
+        out = torch.full((P,), float("nan"), device=DEV)
+        mfl_amd._lib.check(lib.fedavg_reduce_segments_f32_variant(*args, out.data_ptr(), ws[i + 1][0].data_ptr(),
+                                                                  ws[i + 1][1].data_ptr(), need, u, c, b, None),
+                           f"U{u}C{c}b{b}")
+        outs.append(out)
+    torch.cuda.synchronize()
+    exp = O.aggregate_torch([(n, OrderedDict((k, v.cpu()) for k, v in sd.items())) for n, sd in wl])
+    assert_bits(ref.cpu(), torch.cat([exp[k].reshape(-1).float() for k in keys]), f"production K={K}")
+    for (u, c, b), out in zip(_SEG_VARIANTS, outs):
+        assert torch.equal(out.view(torch.int32), ref.view(torch.int32)), f"U{u}C{c}b{b} K={K}"
+    bad = lib.fedavg_reduce_segments_f32_variant(*args, ref.data_ptr(), ws[0][0].data_ptr(), ws[0][1].data_ptr(),
+                                                 need, 3, 8, 3, None)
+    assert bad == -10003
