@@ -324,7 +324,8 @@ def main():
         bytes_call = algorithmic_bytes(K, S)
         achieved = bytes_call / (kernel_ms_max * 1e-3) / 1e9
         if sched:
-            kname = (f"reduce_f32x4_var_kernel<U={sched['unroll']},C={sched['cols']},nt={sched['nontemporal']}> "
+            kern = "reduce_f32x4_buf_kernel" if sched["cols"] == 16 else "reduce_f32x4_var_kernel"
+            kname = (f"{kern}<U={sched['unroll']},C={sched['cols']},nt={sched['nontemporal']}> "
                      f"(exact, sequential client order; round-split x{launches_per_call})")
         else:
             kname = f"tuned variant {tuned}"

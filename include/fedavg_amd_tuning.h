@@ -138,6 +138,13 @@ int fedavg_reduce_segments_f32_variant(const int64_t* client_ptrs, const int64_t
                                        float* out, void* host_ws, void* dev_ws, int64_t ws_bytes, int unroll, int cols,
                                        int blocks_per_cu, void* stream);
 
+/* The exact fp32 row reduce through buffer descriptors (one per client row
+ * and column group, base in SGPRs, 32-bit lane offsets) in launch_split's
+ * round-split schedule; (unroll, cols) in {(4,8), (8,4), (4,4), (2,8),
+ * (2,16), (1,16), (8,8), (4,16)}; max_blocks 0 = resident blocks.  Same bits. */
+int fedavg_reduce_f32_buf(const float* clients, int64_t K, int64_t P, int64_t ld, const float* weights, float* out,
+                          int unroll, int cols, int max_blocks, void* stream);
+
 int fedavg_probe_read_f32x4(const float* buf, int64_t nvec, int mode, int blocks, int launches, float* sink,
                             void* stream);
 

@@ -32,6 +32,7 @@ SIGNATURES = {
     "fedavg_segments_workspace": (_c_i64, [_c_i64, _c_i64]),
     "fedavg_segments_partials": (_c_i64, [_vp, _c_i64, _c_i64]),
     "fedavg_reduce_segments_f32": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _c_i64, _vp]),
+    "fedavg_reduce_f32_buf": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_int, _c_int, _c_int, _vp]),
     "fedavg_reduce_segments_f32_variant": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _c_i64,
                                                     _c_int, _c_int, _c_int, _vp]),
     "fedavg_client_sqdist_segments_f32": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_i64, _vp, _vp, _c_i64, _vp, _vp,

@@ -333,4 +333,97 @@ void launch_split(const float* clients, int K, int64_t ld, int64_t P, const floa
   }
 }
 
+// Row reduce through buffer descriptors: a full column group reads client
+// row k through one descriptor whose base (row k + the group's first column)
+// is wave-uniform and sits in SGPRs (readfirstlane), with the lane's slice as
+// a 32-bit voffset shared by every row -- no 64-bit VGPR address per (row,
+// slice) load.  aux 2 = nt.  Same per-element order as reduce_full_group, so
+// the same bits; the ragged last group takes reduce_full_group's global path.
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* base, int bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo), 0, bytes,
+                                           0x00020000);
+}
+
+__device__ __forceinline__ f32x4 ld_rsrc_nt(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(byte_off), 0, 2));
+}
+
+template <int U, int C>
+__global__ __launch_bounds__(kBlock) void reduce_f32x4_buf_kernel(const f32x4* __restrict__ X, int K, int64_t ld4,
+                                                                  int64_t nvec, int tail, const float* __restrict__ W,
+                                                                  float* __restrict__ out) {
+  constexpr int64_t span = static_cast<int64_t>(kBlock) * C;  // float4 columns per group
+  constexpr int bytes = static_cast<int>(span * 16);
+  uint32_t off[C];
+#pragma unroll
+  for (int j = 0; j < C; ++j) off[j] = 16u * (threadIdx.x + j * kBlock);
+  for (int64_t base = static_cast<int64_t>(blockIdx.x) * span; base < nvec;
+       base += static_cast<int64_t>(gridDim.x) * span) {
+    if (base + span <= nvec) {
+      f32x4 acc[C];
+      const float w0 = W[0];
+      {
+        const __amdgpu_buffer_rsrc_t r0 = uniform_rsrc(X + base, bytes);
+#pragma unroll
+        for (int j = 0; j < C; ++j) acc[j] = ld_rsrc_nt(r0, off[j]) * w0;
+      }
+      const int nb = (K - 1) / U;
+      int k = 1;
+      for (int b = 0; b < nb; ++b, k += U) {
+        f32x4 xs[U][C];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const __amdgpu_buffer_rsrc_t r = uniform_rsrc(X + static_cast<int64_t>(k + u) * ld4 + base, bytes);
+#pragma unroll
+          for (int j = 0; j < C; ++j) xs[u][j] = ld_rsrc_nt(r, off[j]);
+        }
+        consume_batch<U, C>(acc, xs, W, k);
+      }
+      for (; k < K; ++k) {
+        const __amdgpu_buffer_rsrc_t r = uniform_rsrc(X + static_cast<int64_t>(k) * ld4 + base, bytes);
+        const float w = W[k];
+#pragma unroll
+        for (int j = 0; j < C; ++j) {
+          const f32x4 term = ld_rsrc_nt(r, off[j]) * w;
+          acc[j] = acc[j] + term;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < C; ++j) store_slice(out, base + threadIdx.x + j * kBlock, nvec, tail, acc[j]);
+    } else {
+      for (int j = 0; j < C; ++j) {
+        const int64_t v = base + threadIdx.x + j * kBlock;
+        if (v >= nvec) break;
+        f32x4 acc[1];
+        reduce_full_group<U, 1, true, false>(acc, X + v, K, ld4, W);
+        store_slice(out, v, nvec, tail, acc[0]);
+      }
+    }
+  }
+}
+
+// launch_split's round-split schedule with the buffer-descriptor kernel
+template <int U, int C>
+void launch_split_buf(const float* clients, int K, int64_t ld, int64_t P, const float* W, float* out, int max_blocks,
+                      hipStream_t s) {
+  const int64_t nvec = (P + 3) / 4;
+  const int64_t span = static_cast<int64_t>(kBlock) * C;
+  const int64_t resident = max_blocks > 0 ? max_blocks : resident_blocks(reduce_f32x4_buf_kernel<U, C>);
+  const int64_t blocks = (nvec + span - 1) / span;
+  const int64_t nl = (blocks + resident - 1) / resident;
+  const int64_t per = ((nvec + nl - 1) / nl + span - 1) / span * span;
+  const f32x4* X = reinterpret_cast<const f32x4*>(clients);
+  for (int64_t v0 = 0; v0 < nvec; v0 += per) {
+    const int64_t n = (nvec - v0) < per ? (nvec - v0) : per;
+    const int tail = (v0 + n == nvec) ? static_cast<int>(P & 3) : 0;
+    hipLaunchKernelGGL((reduce_f32x4_buf_kernel<U, C>), dim3(static_cast<unsigned>((n + span - 1) / span)),
+                       dim3(kBlock), 0, s, X + v0, K, ld / 4, n, tail, W, out + v0 * 4);
+  }
+}
+
 }  // namespace fedavg_impl

@@ -540,13 +540,31 @@ Schedule choose_schedule(int64_t K, int64_t P) {
   return sc;
 }
 
+// The fp32 kernel's own refinement (the fp64/fp16/bf16 paths keep
+// choose_schedule): rows long enough to fill a whole round-split launch with
+// 16-slice groups take U2 x C16 through per-row buffer descriptors
+// (reduce_f32x4_buf_kernel, 32-bit lane offsets shared by every row):
+// 7.09-7.13 vs 6.96-7.01 TB/s at K=100 x 25M, interleaved
+// (scripts/buf_probe.py, profiles/r01_buf_probe*.jsonl); below that width
+// the 16-slice groups leave the launch short of blocks (4.4 TB/s at K=500 x 5M).
+Schedule choose_f32_schedule(int64_t K, int64_t P) {
+  Schedule sc = choose_schedule(K, P);
+  const int64_t nvec = (P + 3) / 4;
+  if (sc.nt && sc.unroll == 4 && sc.cols == 8 && nvec >= static_cast<int64_t>(sc.blocks_per_launch) * kBlock * 16) {
+    sc.unroll = 2;
+    sc.cols = 16;
+  }
+  return sc;
+}
+
 void launch_production_f32(const float* clients, int K, int64_t ld, int64_t P, const float* W, float* out,
                            hipStream_t s) {
-  const Schedule sc = choose_schedule(K, P);
+  const Schedule sc = choose_f32_schedule(K, P);
   const int bpl = sc.blocks_per_launch;
   const int key = sc.unroll * 100 + sc.cols;
   if (sc.nt) {
     switch (key) {
+      case 216: launch_split_buf<2, 16>(clients, K, ld, P, W, out, bpl, s); return;
       case 408: launch_split<4, 8, true>(clients, K, ld, P, W, out, bpl, s); return;
       case 804: launch_split<8, 4, true>(clients, K, ld, P, W, out, bpl, s); return;
       case 802: launch_split<8, 2, true>(clients, K, ld, P, W, out, bpl, s); return;
@@ -728,7 +746,7 @@ int fedavg_reduce_f32(const float* clients, int64_t K, int64_t P, int64_t ld, co
 
 int fedavg_f32_schedule(int64_t K, int64_t P, int* unroll, int* cols, int* nontemporal, int* launches) {
   if (K <= 0 || P < 0) return set_error(FEDAVG_EINVAL, "fedavg_f32_schedule: bad sizes");
-  const Schedule sc = choose_schedule(K, P);
+  const Schedule sc = choose_f32_schedule(K, P);
   const int64_t nvec = (P + 3) / 4;
   const int64_t span = static_cast<int64_t>(kBlock) * sc.cols;
   const int64_t blocks = (nvec + span - 1) / span;

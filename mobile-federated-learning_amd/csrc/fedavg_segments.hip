@@ -63,20 +63,11 @@ __device__ __forceinline__ f32x4 ldu(const float* p) { return __builtin_nontempo
 // 64-bit VGPR address (with plain global pointers the compiler hoists the
 // loop-invariant part into one 64-bit VGPR pair per (client, slice) load,
 // which caps the loads it keeps in flight).  aux 2 = nt, as ldu().
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t unit_rsrc(const float* unit_base) {
-  const uint64_t a = reinterpret_cast<uint64_t>(unit_base);
-  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a));
-  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32));
-  void* p = reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo);
-  return __builtin_amdgcn_make_buffer_rsrc(p, 0, static_cast<int>(kSegSpanMaxBytes), 0x00020000);
+  return uniform_rsrc(unit_base, static_cast<int>(kSegSpanMaxBytes));
 }
 
-__device__ __forceinline__ f32x4 ldb(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
-  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(byte_off), 0, 2);
-  return __builtin_bit_cast(f32x4, v);
-}
+__device__ __forceinline__ f32x4 ldb(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) { return ld_rsrc_nt(r, byte_off); }
 
 // elements [col, col + 4) of a unit with n columns: a full 16-B vector, or
 // the valid head of one (the rest 0)

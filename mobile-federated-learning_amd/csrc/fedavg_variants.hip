@@ -563,4 +563,27 @@ int fedavg_reduce_f32_xcd(const float* clients, int64_t K, int64_t P, int64_t ld
   return launch_status(what);
 }
 
+int fedavg_reduce_f32_buf(const float* clients, int64_t K, int64_t P, int64_t ld, const float* weights, float* out,
+                          int unroll, int cols, int max_blocks, void* stream) {
+  const char* what = "fedavg_reduce_f32_buf";
+  if (K <= 0 || P <= 0 || ld < P || !clients || !weights || !out || K > INT32_MAX)
+    return set_error(FEDAVG_EINVAL, "%s: bad arguments", what);
+  if (!aligned16(clients) || !aligned16(out) || (ld % 4) != 0)
+    return set_error(FEDAVG_EALIGN, "%s: needs 16-B aligned clients/out and ld %% 4 == 0", what);
+  const int k = static_cast<int>(K);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  switch (unroll * 100 + cols) {
+    case 408: launch_split_buf<4, 8>(clients, k, ld, P, weights, out, max_blocks, s); break;
+    case 804: launch_split_buf<8, 4>(clients, k, ld, P, weights, out, max_blocks, s); break;
+    case 404: launch_split_buf<4, 4>(clients, k, ld, P, weights, out, max_blocks, s); break;
+    case 208: launch_split_buf<2, 8>(clients, k, ld, P, weights, out, max_blocks, s); break;
+    case 216: launch_split_buf<2, 16>(clients, k, ld, P, weights, out, max_blocks, s); break;
+    case 116: launch_split_buf<1, 16>(clients, k, ld, P, weights, out, max_blocks, s); break;
+    case 808: launch_split_buf<8, 8>(clients, k, ld, P, weights, out, max_blocks, s); break;
+    case 416: launch_split_buf<4, 16>(clients, k, ld, P, weights, out, max_blocks, s); break;
+    default: return set_error(FEDAVG_EMODE, "%s: unsupported unroll=%d cols=%d", what, unroll, cols);
+  }
+  return launch_status(what);
+}
+
 }  // extern "C"

@@ -1,0 +1,87 @@
+"""Row reduce through buffer descriptors vs the production row reduce.
+
+    python scripts/buf_probe.py [--K 100 --P 25000000] [--rounds 5] [--reps 6]
+
+fedavg_reduce_f32_buf (tuning hook: one descriptor per client row and column
+group, base in SGPRs, 32-bit lane offsets) against fedavg_reduce_f32 on the
+same [K, ld] rows, interleaved in one process, bit-identity checked.  One JSON
+line per variant: median ms per call (HIP events) and GB/s of algorithmic
+bytes (4K+4 B per element + weights).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+import numpy as np
+import torch
+
+import mfl_amd
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--K", type=int, default=100)
+    ap.add_argument("--P", type=int, default=25_000_000)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=6)
+    ap.add_argument("--buf", nargs="*", default=["4,8,0", "4,8,768", "8,4,0", "4,4,0", "2,8,0", "2,16,0", "1,16,0",
+                                                 "8,8,0"], help="U,C,max_blocks of fedavg_reduce_f32_buf")
+    ap.add_argument("--glob", nargs="*", default=[], help="U,C,max_blocks of the global-pointer variant kernel")
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    lib = mfl_amd._lib.load()
+    K, P = args.K, args.P
+    ld = (P + 63) // 64 * 64
+    g = torch.Generator(device=dev).manual_seed(5)
+    rows = torch.randn((K, ld), generator=g, device=dev) * 0.05
+    w = mfl_amd.weights_tensor(mfl_amd.sample_weights(list(range(1, K + 1))), torch.float32, dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    ap_sched = [tuple(int(t) for t in v.split(",")) for v in args.buf]
+    variants = {"production": None}
+    for u, c, b in ap_sched:
+        variants[f"buf-U{u}C{c}b{b}"] = (u, c, b)
+    for u, c, b in [tuple(int(t) for t in v.split(",")) for v in args.glob]:
+        variants[f"global-U{u}C{c}b{b}"] = ("var", u, c, b)
+    outs = {n: torch.empty(P, device=dev) for n in variants}
+
+    def run(n):
+        v = variants[n]
+        if v is None:
+            mfl_amd.reduce_packed(rows, w, P, outs[n])
+            return
+        if v[0] == "var":  # the global-pointer kernel, round-split (pipelined mode 4), nt loads
+            mfl_amd.reduce_packed(rows, w, P, outs[n], tuned=(v[1], 1, v[2], 4, v[3]))
+            return
+        mfl_amd._lib.check(lib.fedavg_reduce_f32_buf(rows.data_ptr(), K, P, ld, w.data_ptr(), outs[n].data_ptr(),
+                                                     v[0], v[1], v[2], stream), n)
+
+    for n in variants:
+        run(n)
+    torch.cuda.synchronize()
+    same = {n: bool(torch.equal(outs[n].view(torch.int32), outs["production"].view(torch.int32))) for n in outs}
+    times = {n: [] for n in variants}
+    for _ in range(args.rounds):
+        for n in variants:
+            for _ in range(args.reps):
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                run(n)
+                e.record()
+                times[n].append((s, e))
+        torch.cuda.synchronize()
+    alg = 4 * K * P + 4 * P + 4 * K
+    for n in variants:
+        ms = float(np.median([s.elapsed_time(e) for s, e in times[n]]))
+        print(json.dumps({"variant": n, "K": K, "P": P, "ms_median": round(ms, 4), "GBps": round(alg / ms / 1e6, 1),
+                          "bit_identical": same[n]}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -156,13 +156,16 @@ def test_reduce_f32_exact_large(K, P):
 def _schedule_boundary_cases():
     """(K, P) on both sides of every production-schedule switch: the slice
     count per thread steps at 2 x CUs x 256 threads x {2, 4, 8} float4
-    columns, the Infinity-Cache band spans 64-240 MiB of client rows, and
+    columns and at 3 x CUs x 256 x 16 (the buffer-descriptor U2 x C16
+    kernel), the Infinity-Cache band spans 64-240 MiB of client rows, and
     K <= 4 takes the single-launch path."""
     full = 2 * torch.cuda.get_device_properties(DEV).multi_processor_count
     cases = []
     for c in (2, 4, 8):
         t = full * 256 * c * 4  # elements at the switch
         cases += [(5, t - 4), (5, t - 1), (5, t), (5, t + 3)]
+    t = 3 * (full // 2) * 256 * 16 * 4  # fp32 only: U2 x C16 buffer-descriptor kernel from here
+    cases += [(5, t - 4), (5, t), (5, t + 3)]
     mib = 1 << 20
     cases += [(20, 64 * mib // 80 - 3), (20, 64 * mib // 80 + 5), (20, 240 * mib // 80 - 1), (20, 240 * mib // 80 + 7)]
     cases += [(4, 1_000_003), (5, 1_000_003), (1, 65), (2, 7)]
@@ -282,6 +285,24 @@ def test_schedule_variants_bit_identical():
         for v in _all_variants():
             got = mfl_amd.reduce_packed(x, w, P, tuned=v)
             assert torch.equal(got.view(torch.int32), base.view(torch.int32)), (K, P, v)
+
+
+@pytest.mark.parametrize("K,P", [(37, 123_457), (1, 4099), (9, 1_000_003), (3, 64 * 64 * 3 + 5), (5, 190),
+                                 (100, 600_372)])
+def test_buffer_descriptor_reduce_bit_identical(K, P):
+    """fedavg_reduce_f32_buf (per-row buffer descriptors, 32-bit lane offsets)
+    gives the production kernel's bits for every (U, C) and grid cap, with a
+    ragged last column group and a P % 4 tail."""
+    lib = mfl_amd._lib.load()
+    x = _clients(K, P, seed=K + 7 * P)
+    w = _w(_weights(K))
+    base = mfl_amd.reduce_packed(x, w, P)
+    for u, c, b in [(4, 8, 0), (4, 8, 3), (8, 4, 0), (4, 4, 5), (2, 8, 0), (2, 16, 0), (1, 16, 7), (8, 8, 0)]:
+        out = torch.full((P,), float("nan"), device=DEV)
+        mfl_amd._lib.check(lib.fedavg_reduce_f32_buf(x.data_ptr(), K, P, x.shape[1], w.data_ptr(), out.data_ptr(),
+                                                     u, c, b, None), f"U{u}C{c}b{b}")
+        torch.cuda.synchronize()
+        assert torch.equal(out.view(torch.int32), base.view(torch.int32)), (K, P, u, c, b)
 
 
 def test_misaligned_clients_take_scalar_path():
