@@ -145,6 +145,15 @@ int fedavg_reduce_segments_f32_variant(const int64_t* client_ptrs, const int64_t
 int fedavg_reduce_f32_buf(const float* clients, int64_t K, int64_t P, int64_t ld, const float* weights, float* out,
                           int unroll, int cols, int max_blocks, void* stream);
 
+/* The distance pass (fedavg_client_sqdist_f32) through buffer descriptors:
+ * per block, one descriptor per client row and one for glob whose record
+ * count ends at the last float4 (lanes past it read 0); (unroll, cols) in
+ * {(4,8), (8,4), (2,16), (2,8), (8,8)}; round-split launches of <= max_blocks
+ * blocks (0 = one launch).  Same workspace as fedavg_client_sqdist_f32. */
+int fedavg_client_sqdist_buf(const float* clients, int64_t K, int64_t P, int64_t ld, const float* glob,
+                             double* workspace, int64_t workspace_elems, double* sumsq, int unroll, int cols,
+                             int max_blocks, void* stream);
+
 int fedavg_probe_read_f32x4(const float* buf, int64_t nvec, int mode, int blocks, int launches, float* sink,
                             void* stream);
 

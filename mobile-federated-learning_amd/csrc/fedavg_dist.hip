@@ -82,6 +82,66 @@ __global__ __launch_bounds__(kBlock) void client_sqdist_f32x4_kernel(
   }
 }
 
+// The same pass through buffer descriptors: block b's slice of every client
+// row (and of the model) is one descriptor whose base sits in SGPRs and whose
+// record count ends at the window's last float4, so a lane past the end reads
+// 0 from the hardware range check (x = g = 0, d = 0) instead of a predicated
+// load; each lane's slices are 32-bit offsets shared by every row.  Same
+// per-wave partial layout and order as client_sqdist_f32x4_kernel<U, C>.
+template <int U, int C>
+__global__ __launch_bounds__(kBlock) void client_sqdist_buf_kernel(
+    const f32x4* __restrict__ X, int K, int64_t ld4, int64_t nvec, int tail, const f32x4* __restrict__ G,
+    double* __restrict__ partials, int64_t nwaves, int64_t wave_base) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave_id = wave_base + static_cast<int64_t>(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
+  const int64_t blk0 = static_cast<int64_t>(blockIdx.x) * kBlock * C;
+  const int64_t left = nvec - blk0;
+  const int bytes = static_cast<int>((left < kBlock * C ? left : kBlock * C) * 16);
+  uint32_t off[C];
+  int nv[C];  // valid elements of slice j (0..4): padding lanes never contribute
+  f32x4 g[C];
+  {
+    const __amdgpu_buffer_rsrc_t rg = uniform_rsrc(G + blk0, bytes);
+#pragma unroll
+    for (int j = 0; j < C; ++j) {
+      const int64_t v = blk0 + threadIdx.x + static_cast<int64_t>(j) * kBlock;
+      off[j] = 16u * (threadIdx.x + j * kBlock);
+      nv[j] = v >= nvec ? 0 : (tail != 0 && v == nvec - 1 ? tail : 4);
+      g[j] = ld_rsrc_nt(rg, off[j]);
+    }
+  }
+  for (int k = 0; k < K; k += U) {
+    const int rows = (K - k) < U ? (K - k) : U;
+    f32x4 xs[U][C];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (u < rows) {
+        const __amdgpu_buffer_rsrc_t r = uniform_rsrc(X + static_cast<int64_t>(k + u) * ld4 + blk0, bytes);
+#pragma unroll
+        for (int j = 0; j < C; ++j) xs[u][j] = ld_rsrc_nt(r, off[j]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (u >= rows) break;
+      double acc = 0.0;
+#pragma unroll
+      for (int j = 0; j < C; ++j) {
+        f32x4 d = xs[u][j] - g[j];  // fp32 difference, as the reference forms it
+        if (nv[j] < 4) {            // select (not multiply): padding may hold NaN/inf
+          d.x = nv[j] > 0 ? d.x : 0.f;
+          d.y = nv[j] > 1 ? d.y : 0.f;
+          d.z = nv[j] > 2 ? d.z : 0.f;
+          d.w = 0.f;
+        }
+        acc = sq4_add(acc, d);
+      }
+      acc = wave_sum(acc);
+      if (lane == 0) partials[static_cast<int64_t>(k + u) * nwaves + wave_id] = acc;
+    }
+  }
+}
+
 // sumsq[k] = sum over waves of partials[k][*], fixed order (block per client).
 __global__ __launch_bounds__(kBlock) void client_sqdist_finalize_kernel(const double* __restrict__ partials,
                                                                         int64_t nwaves, double* __restrict__ out) {
@@ -112,7 +172,7 @@ int64_t sqdist_waves_for(int64_t P, int cols) {
   return blocks * (kBlock / 64);
 }
 
-template <int U, int C>
+template <int U, int C, bool BUF = false>
 void launch_sqdist(const float* clients, int K, int64_t ld, int64_t P, const float* glob, double* partials,
                    int64_t nwaves, int max_blocks, hipStream_t s) {
   const int64_t nvec = (P + 3) / 4;
@@ -128,8 +188,12 @@ void launch_sqdist(const float* clients, int K, int64_t ld, int64_t P, const flo
     const int64_t v0 = b0 * span;
     const int64_t n = (nvec - v0) < nb * span ? (nvec - v0) : nb * span;
     const int tail = (v0 + n == nvec) ? static_cast<int>(P & 3) : 0;
-    hipLaunchKernelGGL((client_sqdist_f32x4_kernel<U, C>), dim3(static_cast<unsigned>(nb)), dim3(kBlock), 0, s,
-                       X + v0, K, ld / 4, n, tail, Gv + v0, partials, nwaves, b0 * (kBlock / 64));
+    if constexpr (BUF)
+      hipLaunchKernelGGL((client_sqdist_buf_kernel<U, C>), dim3(static_cast<unsigned>(nb)), dim3(kBlock), 0, s,
+                         X + v0, K, ld / 4, n, tail, Gv + v0, partials, nwaves, b0 * (kBlock / 64));
+    else
+      hipLaunchKernelGGL((client_sqdist_f32x4_kernel<U, C>), dim3(static_cast<unsigned>(nb)), dim3(kBlock), 0, s,
+                         X + v0, K, ld / 4, n, tail, Gv + v0, partials, nwaves, b0 * (kBlock / 64));
   }
 }
 
@@ -168,6 +232,36 @@ int fedavg_client_sqdist_variant(const float* clients, int64_t K, int64_t P, int
     case 804: launch_sqdist<8, 4>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
     case 408: launch_sqdist<4, 8>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
     case 208: launch_sqdist<2, 8>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    default: return set_error(FEDAVG_EMODE, "%s: unsupported unroll=%d cols=%d", what, unroll, cols);
+  }
+  rc = launch_status(what);
+  if (rc) return rc;
+  hipLaunchKernelGGL(client_sqdist_finalize_kernel, dim3(static_cast<unsigned>(K)), dim3(kBlock), 0, s, workspace,
+                     nwaves, sumsq);
+  return launch_status(what);
+}
+
+int fedavg_client_sqdist_buf(const float* clients, int64_t K, int64_t P, int64_t ld, const float* glob,
+                             double* workspace, int64_t workspace_elems, double* sumsq, int unroll, int cols,
+                             int max_blocks, void* stream) {
+  const char* what = "fedavg_client_sqdist_buf";
+  int rc = check_common(clients, K, P, ld, glob, sumsq, what);
+  if (rc) return rc;
+  if (P == 0) return set_error(FEDAVG_EINVAL, "%s: P must be >= 1", what);
+  if (!aligned16(clients) || !aligned16(glob) || (ld % 4) != 0)
+    return set_error(FEDAVG_EALIGN, "%s: needs 16-B aligned clients/glob and ld %% 4 == 0", what);
+  if (cols != 4 && cols != 8 && cols != 16) return set_error(FEDAVG_EMODE, "%s: cols must be 4, 8 or 16", what);
+  const int64_t nwaves = sqdist_waves_for(P, cols);
+  if (!workspace || workspace_elems < K * nwaves)
+    return set_error(FEDAVG_EINVAL, "%s: workspace needs %lld doubles", what, (long long)(K * nwaves));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int k = static_cast<int>(K);
+  switch (unroll * 100 + cols) {
+    case 408: launch_sqdist<4, 8, true>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    case 804: launch_sqdist<8, 4, true>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    case 216: launch_sqdist<2, 16, true>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    case 208: launch_sqdist<2, 8, true>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    case 808: launch_sqdist<8, 8, true>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
     default: return set_error(FEDAVG_EMODE, "%s: unsupported unroll=%d cols=%d", what, unroll, cols);
   }
   rc = launch_status(what);

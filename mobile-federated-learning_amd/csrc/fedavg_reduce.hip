@@ -541,16 +541,18 @@ Schedule choose_schedule(int64_t K, int64_t P) {
 }
 
 // The fp32 kernel's own refinement (the fp64/fp16/bf16 paths keep
-// choose_schedule): rows long enough to fill a whole round-split launch with
-// 16-slice groups take U2 x C16 through per-row buffer descriptors
+// choose_schedule): rows long enough for a full-chip launch (2 blocks per
+// CU) of 16-slice groups take U2 x C16 through per-row buffer descriptors
 // (reduce_f32x4_buf_kernel, 32-bit lane offsets shared by every row):
-// 7.09-7.13 vs 6.96-7.01 TB/s at K=100 x 25M, interleaved
-// (scripts/buf_probe.py, profiles/r01_buf_probe*.jsonl); below that width
-// the 16-slice groups leave the launch short of blocks (4.4 TB/s at K=500 x 5M).
+// 7.09-7.15 vs 6.96-7.05 TB/s at K=100 x 25M and 6.89 vs 6.49 at K=100 x 10M,
+// interleaved (scripts/buf_probe.py, profiles/r01_buf_probe*.jsonl); below
+// that width the 16-slice groups leave the launch short of blocks (4.4 TB/s
+// at K=100 x 5M).
 Schedule choose_f32_schedule(int64_t K, int64_t P) {
   Schedule sc = choose_schedule(K, P);
   const int64_t nvec = (P + 3) / 4;
-  if (sc.nt && sc.unroll == 4 && sc.cols == 8 && nvec >= static_cast<int64_t>(sc.blocks_per_launch) * kBlock * 16) {
+  const int64_t full = 2 * static_cast<int64_t>(cu_count());
+  if (sc.nt && sc.unroll == 4 && sc.cols == 8 && nvec >= full * kBlock * 16) {
     sc.unroll = 2;
     sc.cols = 16;
   }

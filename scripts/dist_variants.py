@@ -47,6 +47,9 @@ def main():
     variants = [("production", None)] + [(f"U{u} C{c} mb{mb}", (u, c, mb)) for u, c, mb in
                                          [(4, 4, 0), (4, 4, 768), (8, 4, 768), (4, 8, 768), (2, 8, 768), (4, 8, 0),
                                           (4, 8, 512), (4, 8, 1024)]]
+    # the buffer-descriptor form (fedavg_client_sqdist_buf)
+    variants += [(f"buf U{u} C{c} mb{mb}", ("buf", u, c, mb)) for u, c, mb in
+                 [(4, 8, 0), (4, 8, 768), (2, 16, 0), (2, 16, 768), (8, 4, 768), (2, 8, 768), (8, 8, 0)]]
     outs = {name: torch.empty(K, dtype=torch.float64, device=dev) for name, _ in variants}
 
     def run(name, v):
@@ -54,6 +57,9 @@ def main():
         if v is None:
             rc = lib.fedavg_client_sqdist_f32(x.data_ptr(), K, P, ld, glob.data_ptr(), work.data_ptr(), n_ws,
                                               o.data_ptr(), stream)
+        elif v[0] == "buf":
+            rc = lib.fedavg_client_sqdist_buf(x.data_ptr(), K, P, ld, glob.data_ptr(), work.data_ptr(), n_ws,
+                                              o.data_ptr(), v[1], v[2], v[3], stream)
         else:
             rc = lib.fedavg_client_sqdist_variant(x.data_ptr(), K, P, ld, glob.data_ptr(), work.data_ptr(), n_ws,
                                                   o.data_ptr(), v[0], v[1], v[2], stream)

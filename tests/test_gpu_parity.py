@@ -156,7 +156,7 @@ def test_reduce_f32_exact_large(K, P):
 def _schedule_boundary_cases():
     """(K, P) on both sides of every production-schedule switch: the slice
     count per thread steps at 2 x CUs x 256 threads x {2, 4, 8} float4
-    columns and at 3 x CUs x 256 x 16 (the buffer-descriptor U2 x C16
+    columns and at 2 x CUs x 256 x 16 (the buffer-descriptor U2 x C16
     kernel), the Infinity-Cache band spans 64-240 MiB of client rows, and
     K <= 4 takes the single-launch path."""
     full = 2 * torch.cuda.get_device_properties(DEV).multi_processor_count
@@ -164,7 +164,7 @@ def _schedule_boundary_cases():
     for c in (2, 4, 8):
         t = full * 256 * c * 4  # elements at the switch
         cases += [(5, t - 4), (5, t - 1), (5, t), (5, t + 3)]
-    t = 3 * (full // 2) * 256 * 16 * 4  # fp32 only: U2 x C16 buffer-descriptor kernel from here
+    t = full * 256 * 16 * 4  # fp32 only: U2 x C16 buffer-descriptor kernel from here
     cases += [(5, t - 4), (5, t), (5, t + 3)]
     mib = 1 << 20
     cases += [(20, 64 * mib // 80 - 3), (20, 64 * mib // 80 + 5), (20, 240 * mib // 80 - 1), (20, 240 * mib // 80 + 7)]
@@ -661,6 +661,34 @@ def test_client_sqdist_large_vs_fp64():
     again = mfl_amd.client_sqdist(x, glob, P)
     assert torch.equal(got, again)  # deterministic
     del x
+
+
+@pytest.mark.parametrize("K,P", [(7, 1001), (3, 4096 * 16 + 5), (13, 300_007), (100, 600_372), (2, 3)])
+def test_client_sqdist_buffer_descriptor_variants(K, P):
+    """fedavg_client_sqdist_buf (hardware range check instead of predicated
+    loads; NaN in the row padding past P) matches the fp64 reference for every
+    schedule, deterministically."""
+    lib = mfl_amd._lib.load()
+    ld = (P + 63) // 64 * 64
+    g = torch.Generator(device=DEV).manual_seed(K + P)
+    x = torch.full((K, ld), float("nan"), device=DEV)
+    x[:, :P] = torch.randn((K, P), generator=g, device=DEV) * 0.05
+    glob = torch.full((ld,), float("nan"), device=DEV)
+    glob[:P] = torch.randn(P, generator=g, device=DEV) * 0.05
+    ref = torch.stack([((x[k, :P] - glob[:P]).double() ** 2).sum() for k in range(K)])
+    n_ws = lib.fedavg_client_sqdist_workspace(K, P)
+    work = torch.empty(n_ws, dtype=torch.float64, device=DEV)
+    for u, c, mb in [(4, 8, 0), (2, 16, 0), (2, 16, 3), (8, 4, 5), (2, 8, 0), (8, 8, 1)]:
+        outs = []
+        for _ in range(2):
+            o = torch.empty(K, dtype=torch.float64, device=DEV)
+            mfl_amd._lib.check(lib.fedavg_client_sqdist_buf(x.data_ptr(), K, P, ld, glob.data_ptr(), work.data_ptr(),
+                                                            n_ws, o.data_ptr(), u, c, mb, None), f"U{u}C{c}mb{mb}")
+            outs.append(o)
+        torch.cuda.synchronize()
+        rel = ((outs[0] - ref).abs() / ref).max().item()
+        assert rel < 1e-12, (u, c, mb, rel)
+        assert torch.equal(outs[0], outs[1]), (u, c, mb)
 
 
 def test_client_sqdist_padding_nan_ignored():
