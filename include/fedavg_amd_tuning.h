@@ -154,6 +154,14 @@ int fedavg_client_sqdist_buf(const float* clients, int64_t K, int64_t P, int64_t
                              double* workspace, int64_t workspace_elems, double* sumsq, int unroll, int cols,
                              int max_blocks, void* stream);
 
+/* fp16 (dtype 0) / bf16 (1) / fp64 (2) exact reduce through per-row buffer
+ * descriptors (reduce_vec_buf_kernel; weights fp32 for fp16/bf16, fp64 for
+ * fp64), (unroll, cols) in {(8,4), (4,8), (2,16), (4,4), (2,8)}; round-split
+ * launches of <= max_blocks blocks (0 = one launch).  Same bits as
+ * fedavg_reduce_f16 / _bf16 / _f64. */
+int fedavg_reduce_vec_buf(int dtype, const void* clients, int64_t K, int64_t P, int64_t ld, const void* weights,
+                          void* out, int unroll, int cols, int max_blocks, void* stream);
+
 int fedavg_probe_read_f32x4(const float* buf, int64_t nvec, int mode, int blocks, int launches, float* sink,
                             void* stream);
 

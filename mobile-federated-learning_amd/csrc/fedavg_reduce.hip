@@ -627,6 +627,102 @@ void launch_vec_split(const void* clients, int K, int64_t ld, int64_t P, const v
   }
 }
 
+// fp64 / fp16 / bf16 through per-row buffer descriptors (the fp32
+// reduce_f32x4_buf_kernel's addressing: SGPR-held row bases, 32-bit lane
+// offsets shared by every row) -- same per-element rules and order as
+// reduce_vec_kernel, so the same bits; the ragged last group takes the
+// global-pointer path.
+template <class Op, int U, int C>
+__global__ __launch_bounds__(kBlock) void reduce_vec_buf_kernel(
+    const typename Op::vec* __restrict__ X, int K, int64_t ldv, int64_t nvec, int tail,
+    const typename Op::wt* __restrict__ W, typename Op::elem* __restrict__ out) {
+  using vec = typename Op::vec;
+  static_assert(sizeof(vec) == 16, "16-B vectors");
+  constexpr int64_t span = static_cast<int64_t>(kBlock) * C;
+  constexpr int bytes = static_cast<int>(span * 16);
+  uint32_t off[C];
+#pragma unroll
+  for (int j = 0; j < C; ++j) off[j] = 16u * (threadIdx.x + j * kBlock);
+  for (int64_t base = static_cast<int64_t>(blockIdx.x) * span; base < nvec;
+       base += static_cast<int64_t>(gridDim.x) * span) {
+    if (base + span <= nvec) {
+      vec acc[C];
+      {
+        const __amdgpu_buffer_rsrc_t r0 = uniform_rsrc(X + base, bytes);
+        const typename Op::wt w0 = W[0];
+#pragma unroll
+        for (int j = 0; j < C; ++j) acc[j] = Op::first(__builtin_bit_cast(vec, ld_rsrc_nt(r0, off[j])), w0);
+      }
+      int k = 1;
+      for (; k + U <= K; k += U) {
+        vec xs[U][C];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const __amdgpu_buffer_rsrc_t r = uniform_rsrc(X + static_cast<int64_t>(k + u) * ldv + base, bytes);
+#pragma unroll
+          for (int j = 0; j < C; ++j) xs[u][j] = __builtin_bit_cast(vec, ld_rsrc_nt(r, off[j]));
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const typename Op::wt w = W[k + u];
+#pragma unroll
+          for (int j = 0; j < C; ++j) acc[j] = Op::step(acc[j], xs[u][j], w);
+        }
+      }
+      for (; k < K; ++k) {
+        const __amdgpu_buffer_rsrc_t r = uniform_rsrc(X + static_cast<int64_t>(k) * ldv + base, bytes);
+        const typename Op::wt w = W[k];
+#pragma unroll
+        for (int j = 0; j < C; ++j) acc[j] = Op::step(acc[j], __builtin_bit_cast(vec, ld_rsrc_nt(r, off[j])), w);
+      }
+#pragma unroll
+      for (int j = 0; j < C; ++j) store_vec<Op>(out, base + threadIdx.x + j * kBlock, nvec, tail, acc[j]);
+    } else {
+      for (int j = 0; j < C; ++j) {
+        const int64_t v = base + threadIdx.x + j * kBlock;
+        if (v >= nvec) break;
+        vec acc1[1];
+        reduce_vec_group<Op, U, 1, true>(acc1, X + v, K, ldv, W);
+        store_vec<Op>(out, v, nvec, tail, acc1[0]);
+      }
+    }
+  }
+}
+
+template <class Op, int U, int C>
+void launch_vec_split_buf(const void* clients, int K, int64_t ld, int64_t P, const void* W, void* out, int bpl,
+                          hipStream_t s) {
+  using vec = typename Op::vec;
+  const int64_t lanes = Op::kLanes;
+  const int64_t nvec = (P + lanes - 1) / lanes;
+  const int64_t span = static_cast<int64_t>(kBlock) * C;
+  const int64_t blocks = (nvec + span - 1) / span;
+  const int64_t nl = (blocks + bpl - 1) / bpl;
+  const int64_t per = ((nvec + nl - 1) / nl + span - 1) / span * span;
+  const vec* X = reinterpret_cast<const vec*>(clients);
+  auto* O = reinterpret_cast<typename Op::elem*>(out);
+  for (int64_t v0 = 0; v0 < nvec; v0 += per) {
+    const int64_t n = (nvec - v0) < per ? (nvec - v0) : per;
+    const int tail = (v0 + n == nvec) ? static_cast<int>(P % lanes) : 0;
+    hipLaunchKernelGGL((reduce_vec_buf_kernel<Op, U, C>), dim3(static_cast<unsigned>((n + span - 1) / span)),
+                       dim3(kBlock), 0, s, X + v0, K, ld / lanes, n, tail,
+                       reinterpret_cast<const typename Op::wt*>(W), O + v0 * lanes);
+  }
+}
+
+template <class Op>
+bool launch_vec_buf(int U, int C, const void* clients, int K, int64_t ld, int64_t P, const void* W, void* out,
+                    int bpl, hipStream_t s) {
+  switch (U * 100 + C) {
+    case 804: launch_vec_split_buf<Op, 8, 4>(clients, K, ld, P, W, out, bpl, s); return true;
+    case 408: launch_vec_split_buf<Op, 4, 8>(clients, K, ld, P, W, out, bpl, s); return true;
+    case 216: launch_vec_split_buf<Op, 2, 16>(clients, K, ld, P, W, out, bpl, s); return true;
+    case 404: launch_vec_split_buf<Op, 4, 4>(clients, K, ld, P, W, out, bpl, s); return true;
+    case 208: launch_vec_split_buf<Op, 2, 8>(clients, K, ld, P, W, out, bpl, s); return true;
+    default: return false;
+  }
+}
+
 // fp16/bf16 schedule from the fp32 one for the same bytes per row.  Each 16-B
 // vector unpacks into 8 fp32 lanes of work, so the deep fp32 batches are cut
 // to stay spill-free -- except the large-P key: there the packed kernel wants
@@ -684,6 +780,16 @@ template <class Op>
 void launch_production_vec(const void* clients, int K, int64_t ld, int64_t P, const void* W, void* out,
                            hipStream_t s) {
   const int64_t f32_equiv = P * static_cast<int64_t>(16 / Op::kLanes) / 4;  // same bytes per row
+  if constexpr (Op::kLanes == 2) {
+    // fp64 follows the fp32 kernel onto per-row buffer descriptors for long
+    // rows: 7,113 vs 6,992 GB/s at K=100 x 12.5M fp64 (scripts/vec_buf_probe.py,
+    // profiles/r01_vec_buf_probe.jsonl).  fp16/bf16 measured no gain (+0-1 %).
+    const Schedule f = choose_f32_schedule(K, f32_equiv);
+    if (f.cols == 16) {
+      launch_vec_split_buf<Op, 2, 16>(clients, K, ld, P, W, out, f.blocks_per_launch, s);
+      return;
+    }
+  }
   const Schedule sc = choose_schedule(K, f32_equiv);
   if (sc.nt)
     launch_vec_nt<Op, true>(sc, clients, K, ld, P, W, out, s);
@@ -835,6 +941,30 @@ int fedavg_reduce_f16(const uint16_t* clients, int64_t K, int64_t P, int64_t ld,
 int fedavg_reduce_bf16(const uint16_t* clients, int64_t K, int64_t P, int64_t ld, const float* weights,
                        uint16_t* out, void* stream) {
   return reduce_half_entry(true, clients, K, P, ld, weights, out, stream, "fedavg_reduce_bf16");
+}
+
+int fedavg_reduce_vec_buf(int dtype, const void* clients, int64_t K, int64_t P, int64_t ld, const void* weights,
+                          void* out, int unroll, int cols, int max_blocks, void* stream) {
+  const char* what = "fedavg_reduce_vec_buf";
+  int rc = check_common(clients, K, P, ld, weights, out, what);
+  if (rc) return rc;
+  if (P == 0) return FEDAVG_OK;
+  const int lanes = dtype == 2 ? 2 : 8;
+  if (dtype < 0 || dtype > 2) return set_error(FEDAVG_EMODE, "%s: dtype must be 0 (f16), 1 (bf16) or 2 (f64)", what);
+  if (!aligned16(clients) || !aligned16(out) || (ld % lanes) != 0)
+    return set_error(FEDAVG_EALIGN, "%s: needs 16-B aligned clients/out and ld %% %d == 0", what, lanes);
+  const int bpl = max_blocks > 0 ? max_blocks : (1 << 30);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int k = static_cast<int>(K);
+  bool ok;
+  if (dtype == 2)
+    ok = launch_vec_buf<OpF64>(unroll, cols, clients, k, ld, P, weights, out, bpl, s);
+  else if (dtype == 1)
+    ok = launch_vec_buf<OpHalfPk<BF16Pk>>(unroll, cols, clients, k, ld, P, weights, out, bpl, s);
+  else
+    ok = launch_vec_buf<OpHalfPk<F16Pk>>(unroll, cols, clients, k, ld, P, weights, out, bpl, s);
+  if (!ok) return set_error(FEDAVG_EMODE, "%s: unsupported unroll=%d cols=%d", what, unroll, cols);
+  return launch_status(what);
 }
 
 int fedavg_reduce_half_variant(int bf16, const uint16_t* clients, int64_t K, int64_t P, int64_t ld,

@@ -786,6 +786,26 @@ def test_reduce_vec_dtypes_multilaunch(dtype, K, P):
     del x
 
 
+@pytest.mark.parametrize("dtype,K,P", [(torch.bfloat16, 7, 300_011), (torch.float16, 13, 4096 * 8 * 3 + 5),
+                                       (torch.float64, 5, 100_003), (torch.bfloat16, 1, 77)])
+def test_vec_buffer_descriptor_bit_identical(dtype, K, P):
+    """fedavg_reduce_vec_buf gives the production fp16/bf16/fp64 kernel's bits
+    for every schedule, ragged last group and P tail included."""
+    lib = mfl_amd._lib.load()
+    x = _clients(K, P, seed=K + P, dtype=dtype)
+    wdt = torch.float64 if dtype == torch.float64 else torch.float32
+    w = _w(_weights(K), wdt)
+    base = mfl_amd.reduce_packed(x, w, P)
+    iv = torch.int64 if dtype == torch.float64 else torch.int16
+    code = {torch.float16: 0, torch.bfloat16: 1, torch.float64: 2}[dtype]
+    for u, c, b in [(8, 4, 0), (4, 8, 3), (2, 16, 0), (4, 4, 1), (2, 8, 0)]:
+        out = torch.empty(P, dtype=dtype, device=DEV)
+        mfl_amd._lib.check(lib.fedavg_reduce_vec_buf(code, x.data_ptr(), K, P, x.shape[1], w.data_ptr(),
+                                                     out.data_ptr(), u, c, b, None), f"U{u}C{c}b{b}")
+        torch.cuda.synchronize()
+        assert torch.equal(out.view(iv), base.view(iv)), (dtype, K, P, u, c, b)
+
+
 def test_open_session_blocks_aggregate():
     _, w_locals, _ = load_case("mnist_lr_k10")
     agg = mfl_amd.DeviceAggregator(DEV)
