@@ -9,7 +9,7 @@
 // (numel, output offset, source kind) and a pointer table [n_keys][K] (client
 // k's address of key j).  Each key is cut into units of kSegSpan columns; a
 // workgroup reduces one unit over all K clients with the production schedule
-// (U4 client rows per batch, C8 16-B column slices per thread), reading each
+// (U4 client rows per batch, C4 16-B column slices per thread), reading each
 // client through its pointer with dword-aligned 16-B loads (client tensors
 // need only fp32 alignment; full units through a buffer descriptor per
 // client, tails through global pointers), in the reference's client order with
@@ -25,8 +25,13 @@ using namespace fedavg_impl;
 
 typedef f32x4 f32x4_a4 __attribute__((aligned(4)));  // dword-aligned 16-B vector (client tensors, outputs)
 
+// U4 x C4: units of 4,096 columns.  The multi-key sweep (scripts/
+// segments_probe.py --model, profiles/r01_segments_models.jsonl) measured
+// resnet56 x 100 at 113 us against 161 us for U4 x C8 (more units for the
+// mid-size keys, cheaper masked tails), FEMNIST 19.1 vs 20.2 us, and the flat
+// 25M-element key level (6,256 vs 6,226 GB/s); U2 x C16 loses 2.7x on resnet56.
 constexpr int kSegU = 4;
-constexpr int kSegC = 8;
+constexpr int kSegC = 4;
 constexpr int64_t kSegSpan = static_cast<int64_t>(kBlock) * kSegC * 4;  // columns per unit
 constexpr int kSegBlocksPerCU = 3;
 constexpr int64_t kSegSpanMaxBytes = static_cast<int64_t>(kBlock) * 16 * 16;  // widest unit (C = 16), bytes

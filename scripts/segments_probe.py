@@ -28,6 +28,70 @@ import torch
 import mfl_amd
 
 
+def model_mode(args, dev, lib):
+    """Multi-key models (scripts/bench_e2e.py shapes) as K separately allocated
+    device state_dicts: production zero-copy reduce vs (U, C, blocks/CU)
+    schedules of fedavg_reduce_segments_f32_variant, interleaved, bits checked."""
+    sys.path.insert(0, str(ROOT / "scripts"))
+    from bench_e2e import CONFIGS
+    K, shapes = CONFIGS[args.model]
+    g = torch.Generator(device=dev).manual_seed(4)
+    clients = []
+    for _ in range(K):
+        sd = []
+        for name, shp in shapes:
+            if name.endswith("num_batches_tracked"):
+                sd.append(torch.randint(0, 1000, shp, generator=g, device=dev))
+            else:
+                sd.append(torch.randn(shp, generator=g, device=dev) * 0.05)
+        clients.append(sd)
+    numel = np.array([t.numel() for t in clients[0]], dtype=np.int64)
+    offset = np.concatenate([[0], np.cumsum(numel)[:-1]]).astype(np.int64)
+    kind = np.array([1 if t.dtype == torch.int64 else 0 for t in clients[0]], dtype=np.int64)
+    ptrs = np.array([[t.data_ptr() for t in sd] for sd in clients], dtype=np.int64)
+    P = int(numel.sum())
+    w = mfl_amd.weights_tensor(mfl_amd.sample_weights(list(range(1, K + 1))), torch.float32, dev)
+    nk = len(numel)
+    need = lib.fedavg_segments_workspace(K, nk)
+    stream = torch.cuda.current_stream(dev)
+    sched = [None, (4, 8, 3), (2, 16, 3), (4, 4, 3), (1, 16, 3), (8, 4, 3), (2, 8, 3)]
+    names = ["production" if v is None else f"U{v[0]}C{v[1]}b{v[2]}" for v in sched]
+    ws = {n: (torch.empty(need, dtype=torch.uint8, pin_memory=True), torch.empty(need, dtype=torch.uint8, device=dev))
+          for n in names}
+    outs = {n: torch.empty(P, device=dev) for n in names}
+    a = (ptrs.ctypes.data, numel.ctypes.data, offset.ctypes.data, kind.ctypes.data, nk, K, w.data_ptr())
+
+    def run(n, v):
+        h, d = ws[n]
+        if v is None:
+            rc = lib.fedavg_reduce_segments_f32(*a, outs[n].data_ptr(), h.data_ptr(), d.data_ptr(), need,
+                                                stream.cuda_stream)
+        else:
+            rc = lib.fedavg_reduce_segments_f32_variant(*a, outs[n].data_ptr(), h.data_ptr(), d.data_ptr(), need,
+                                                        v[0], v[1], v[2], stream.cuda_stream)
+        mfl_amd._lib.check(rc, n)
+
+    for n, v in zip(names, sched):
+        run(n, v)
+    torch.cuda.synchronize()
+    same = {n: bool(torch.equal(outs[n].view(torch.int32), outs["production"].view(torch.int32))) for n in names}
+    times = {n: [] for n in names}
+    for _ in range(args.rounds):
+        for n, v in zip(names, sched):
+            for _ in range(args.reps):
+                s0, e0 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s0.record()
+                run(n, v)
+                e0.record()
+                times[n].append((s0, e0))
+            torch.cuda.synchronize()  # the pinned table of the next call
+    alg = 4 * K * P + 4 * P + 4 * K
+    for n in names:
+        ms = float(np.median([s0.elapsed_time(e0) for s0, e0 in times[n]]))
+        print(json.dumps({"model": args.model, "variant": n, "K": K, "P": P, "keys": nk, "ms_median": round(ms, 4),
+                          "GBps": round(alg / ms / 1e6, 1), "bit_identical": same[n]}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--K", type=int, default=100)
@@ -37,10 +101,14 @@ def main():
     ap.add_argument("--sweep", action="store_true",
                     help="also time fedavg_reduce_segments_f32_variant schedules (U, C, blocks per CU) on the "
                          "separate tensors and on the rows")
+    ap.add_argument("--model", default="", help="multi-key mode: a scripts/bench_e2e.py config name")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     lib = mfl_amd._lib.load()
+    if args.model:
+        model_mode(args, dev, lib)
+        return
     K, P = args.K, args.P
     ld = (P + 63) // 64 * 64
     rows = torch.empty((K, ld), device=dev)

@@ -282,6 +282,7 @@ def _segment_case(K, specs, seed, offset_base=3):
 
 
 _SEG_SPECS = [((8192,), torch.float32), ((8191,), torch.float32), ((8193,), torch.float32), ((0,), torch.float32),
+              ((4096,), torch.float32), ((4095,), torch.float32), ((4097,), torch.float32),
               ((3, 5), torch.float32), ((), torch.int64), ((7,), torch.int32), ((1,), torch.float32),
               ((40_001,), torch.float32), ((5, 2), torch.bool), ((16_384 * 3 + 2,), torch.float32)]
 
