@@ -760,7 +760,9 @@ def test_int64_indexing_beyond_2_31_elements():
 
 @pytest.mark.parametrize("dtype,K,P", [(torch.float64, 8, 10_000_003), (torch.float16, 6, 40_000_005),
                                        (torch.bfloat16, 5, 40_000_001), (torch.float64, 600, 200_001),
-                                       (torch.bfloat16, 3, 1_000_003)])
+                                       (torch.bfloat16, 3, 1_000_003),
+                                       # fp64 on both sides of its switch to the buffer-descriptor kernel
+                                       (torch.float64, 5, 4_194_301), (torch.float64, 5, 4_194_307)])
 def test_reduce_vec_dtypes_multilaunch(dtype, K, P):
     """fp64/fp16/bf16 production schedule (round-split, multi-slice, nt) is
     bit-exact on sampled windows incl. launch boundaries and the ragged tail."""
