@@ -507,6 +507,8 @@ struct Schedule {
 constexpr int kBlocksPerCU = 3;
 inline int blocks_per_launch() { return kBlocksPerCU * cu_count(); }
 
+constexpr int64_t kManyClients = 64;  // K from which the wider short-row schedules apply
+
 Schedule choose_schedule(int64_t K, int64_t P) {
   const int64_t nvec = (P + 3) / 4;
   Schedule sc{8, 1, 1, blocks_per_launch()};
@@ -555,6 +557,14 @@ Schedule choose_f32_schedule(int64_t K, int64_t P) {
   if (sc.nt && sc.unroll == 4 && sc.cols == 8 && nvec >= full * kBlock * 16) {
     sc.unroll = 2;
     sc.cols = 16;
+  }
+  // short rows with many clients (the N > 1 all-gather chunks): 4 slices per
+  // thread -- K=100 x 1.56M (N=2 chunk) 6,695 vs 6,178 GB/s at U8 x C2, and
+  // K=100 x 781K (N=4 chunk) 6,741 vs 5,668 at U16 x C1
+  // (profiles/r01_chunk_shapes.jsonl, interleaved)
+  if (sc.nt && K >= kManyClients) {
+    if (sc.unroll == 8 && sc.cols == 2) sc.cols = 4;
+    if (sc.unroll == 16 && sc.cols == 1 && nvec >= full / 4 * kBlock * 4) sc.cols = 4;
   }
   return sc;
 }

@@ -166,6 +166,9 @@ def _schedule_boundary_cases():
         cases += [(5, t - 4), (5, t - 1), (5, t), (5, t + 3)]
     t = full * 256 * 16 * 4  # fp32 only: U2 x C16 buffer-descriptor kernel from here
     cases += [(5, t - 4), (5, t), (5, t + 3)]
+    # K >= 64: 4 slices per thread in the short-row bands (from full/4 x 256 x 4 float4 columns)
+    for t in (full // 4 * 256 * 4 * 4, full * 256 * 2 * 4):
+        cases += [(64, t - 4), (64, t + 1), (63, t + 1), (100, t - 1)]
     mib = 1 << 20
     cases += [(20, 64 * mib // 80 - 3), (20, 64 * mib // 80 + 5), (20, 240 * mib // 80 - 1), (20, 240 * mib // 80 + 7)]
     cases += [(4, 1_000_003), (5, 1_000_003), (1, 65), (2, 7)]
