@@ -102,6 +102,7 @@ def main():
                     help="also time fedavg_reduce_segments_f32_variant schedules (U, C, blocks per CU) on the "
                          "separate tensors and on the rows")
     ap.add_argument("--model", default="", help="multi-key mode: a scripts/bench_e2e.py config name")
+    ap.add_argument("--only", default="", help="time only 'rows' and this variant (for per-kernel PMC passes)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -129,6 +130,8 @@ def main():
              (4, 4, 3), (4, 4, 6), (8, 2, 6), (16, 2, 3), (2, 16, 3), (1, 16, 3), (1, 16, 6)]
     if args.sweep:
         names += [f"var-{src}-U{u}C{c}b{b}" for src in ("tensors", "rows") for u, c, b in sched]
+    if args.only:
+        names = ["rows", args.only]
     outs = {n: torch.empty(P, device=dev) for n in names}
     meta = [np.array([v], dtype=np.int64) for v in (P, 0, 0)]
     ptr_rows = np.array([[rows[k].data_ptr()] for k in range(K)], dtype=np.int64)
