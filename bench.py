@@ -235,7 +235,7 @@ def main():
         tuned = (args.unroll or 8, max(args.nt, 0))
 
     S = red.plan.block
-    sched = mfl_amd._lib.f32_schedule(K, S) if tuned is None else None
+    sched = mfl_amd._lib.f32_schedule(K, S, red.plan.local_cols) if tuned is None else None
     launches_per_call = sched["launches"] if sched else 1
     ev_pairs = []
 

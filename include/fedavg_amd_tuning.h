@@ -23,6 +23,10 @@ extern "C" {
  * the number of round-split launches.  Host-only query.
  */
 int fedavg_f32_schedule(int64_t K, int64_t P, int* unroll, int* cols, int* nontemporal, int* launches);
+/* The same for P columns of a row buffer with row stride ld (a column chunk
+ * of a wider shard when ld > P: no Infinity-Cache-resident schedule). */
+int fedavg_f32_schedule_ld(int64_t K, int64_t P, int64_t ld, int* unroll, int* cols, int* nontemporal,
+                           int* launches);
 
 /*
  * fedavg_reduce_f32 with explicit variant knobs:

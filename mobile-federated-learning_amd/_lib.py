@@ -56,6 +56,7 @@ SIGNATURES = {
     "fedavg_copy_to_host": (_c_int, [_vp, _vp, _c_i64, _c_int, _vp]),
     "fedavg_upload_shard": (_c_int, [_vp, _c_i64, _vp, _c_i64, _c_i64, _c_i64, _vp]),
     "fedavg_f32_schedule": (_c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp]),
+    "fedavg_f32_schedule_ld": (_c_int, [_c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _vp]),
     "fedavg_reduce_f32_tuned": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_int, _c_int, _vp]),
     "fedavg_reduce_f32_variant": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_int, _c_int, _c_int, _c_int,
                                            _c_int, _vp]),
@@ -122,10 +123,14 @@ def load() -> ctypes.CDLL:
     return _lib
 
 
-def f32_schedule(K: int, P: int) -> dict:
-    """The schedule fedavg_reduce_f32 picks for an aligned [K, P] problem."""
+def f32_schedule(K: int, P: int, ld: int = 0) -> dict:
+    """The schedule fedavg_reduce_f32 picks for an aligned [K, P] problem
+    (P columns of rows with stride ld, when given)."""
     vals = [ctypes.c_int() for _ in range(4)]
-    check(load().fedavg_f32_schedule(K, P, *[ctypes.byref(v) for v in vals]), "fedavg_f32_schedule")
+    if ld:
+        check(load().fedavg_f32_schedule_ld(K, P, ld, *[ctypes.byref(v) for v in vals]), "fedavg_f32_schedule_ld")
+    else:
+        check(load().fedavg_f32_schedule(K, P, *[ctypes.byref(v) for v in vals]), "fedavg_f32_schedule")
     return dict(zip(("unroll", "cols", "nontemporal", "launches"), (v.value for v in vals)))
 
 

@@ -509,7 +509,10 @@ inline int blocks_per_launch() { return kBlocksPerCU * cu_count(); }
 
 constexpr int64_t kManyClients = 64;  // K from which the wider short-row schedules apply
 
-Schedule choose_schedule(int64_t K, int64_t P) {
+// `resident_rows`: bytes of the row buffer the caller streams (K x ld); the
+// Infinity-Cache band applies only when that whole buffer fits the band, so a
+// column chunk of a wider shard (N > 1 pipeline) streams from HBM instead.
+Schedule choose_schedule(int64_t K, int64_t P, double resident_rows = -1.0) {
   const int64_t nvec = (P + 3) / 4;
   Schedule sc{8, 1, 1, blocks_per_launch()};
   const int64_t full = 2 * static_cast<int64_t>(cu_count());  // blocks for a full-chip launch (512 on MI355X)
@@ -532,7 +535,8 @@ Schedule choose_schedule(int64_t K, int64_t P) {
     sc.cols = (K >= 500 && nvec >= full / 4 * kBlock * 4) ? 4 : 1;
   }
   const double bytes = 4.0 * static_cast<double>(K) * static_cast<double>(P);
-  if (K > 4 && bytes > 64.0 * (1 << 20) && bytes <= 240.0 * (1 << 20)) {
+  const double span_bytes = resident_rows > bytes ? resident_rows : bytes;
+  if (K > 4 && bytes > 64.0 * (1 << 20) && span_bytes <= 240.0 * (1 << 20)) {
     // Infinity-Cache-resident band: default-policy loads, and a deep, wide
     // per-thread batch (16 rows x 4 slices) measured fastest there
     sc.nt = 0;
@@ -550,8 +554,12 @@ Schedule choose_schedule(int64_t K, int64_t P) {
 // interleaved (scripts/buf_probe.py, profiles/r01_buf_probe*.jsonl); below
 // that width the 16-slice groups leave the launch short of blocks (4.4 TB/s
 // at K=100 x 5M).
-Schedule choose_f32_schedule(int64_t K, int64_t P) {
-  Schedule sc = choose_schedule(K, P);
+Schedule choose_f32_schedule(int64_t K, int64_t P, int64_t ld) {
+  // a chunk of a wider row buffer (ld > P) is not cache-resident between
+  // calls: K=100 x 390K chunks of a 3.125M-column shard (the N=8 pipeline)
+  // run 3,971 GB/s in the Infinity-Cache schedule and 5,065 streamed
+  // (U16 x C1 nt; profiles/r01_chunk_rotating.jsonl)
+  Schedule sc = choose_schedule(K, P, 4.0 * static_cast<double>(K) * static_cast<double>(ld > P ? ld : P));
   const int64_t nvec = (P + 3) / 4;
   const int64_t full = 2 * static_cast<int64_t>(cu_count());
   if (sc.nt && sc.unroll == 4 && sc.cols == 8 && nvec >= full * kBlock * 16) {
@@ -571,7 +579,7 @@ Schedule choose_f32_schedule(int64_t K, int64_t P) {
 
 void launch_production_f32(const float* clients, int K, int64_t ld, int64_t P, const float* W, float* out,
                            hipStream_t s) {
-  const Schedule sc = choose_f32_schedule(K, P);
+  const Schedule sc = choose_f32_schedule(K, P, ld);
   const int bpl = sc.blocks_per_launch;
   const int key = sc.unroll * 100 + sc.cols;
   if (sc.nt) {
@@ -794,7 +802,7 @@ void launch_production_vec(const void* clients, int K, int64_t ld, int64_t P, co
     // fp64 follows the fp32 kernel onto per-row buffer descriptors for long
     // rows: 7,113 vs 6,992 GB/s at K=100 x 12.5M fp64 (scripts/vec_buf_probe.py,
     // profiles/r01_vec_buf_probe.jsonl).  fp16/bf16 measured no gain (+0-1 %).
-    const Schedule f = choose_f32_schedule(K, f32_equiv);
+    const Schedule f = choose_f32_schedule(K, f32_equiv, f32_equiv);
     if (f.cols == 16) {
       launch_vec_split_buf<Op, 2, 16>(clients, K, ld, P, W, out, f.blocks_per_launch, s);
       return;
@@ -862,9 +870,23 @@ int fedavg_reduce_f32(const float* clients, int64_t K, int64_t P, int64_t ld, co
   return reduce_f32_unaligned(clients, K, P, ld, weights, out, static_cast<hipStream_t>(stream), what);
 }
 
+int fedavg_f32_schedule_ld(int64_t K, int64_t P, int64_t ld, int* unroll, int* cols, int* nontemporal,
+                           int* launches) {
+  if (K <= 0 || P < 0 || ld < P) return set_error(FEDAVG_EINVAL, "fedavg_f32_schedule_ld: bad sizes");
+  const Schedule sc = choose_f32_schedule(K, P, ld);
+  const int64_t nvec = (P + 3) / 4;
+  const int64_t span = static_cast<int64_t>(kBlock) * sc.cols;
+  const int64_t blocks = (nvec + span - 1) / span;
+  if (unroll) *unroll = sc.unroll;
+  if (cols) *cols = sc.cols;
+  if (nontemporal) *nontemporal = sc.nt;
+  if (launches) *launches = static_cast<int>((blocks + sc.blocks_per_launch - 1) / sc.blocks_per_launch);
+  return FEDAVG_OK;
+}
+
 int fedavg_f32_schedule(int64_t K, int64_t P, int* unroll, int* cols, int* nontemporal, int* launches) {
   if (K <= 0 || P < 0) return set_error(FEDAVG_EINVAL, "fedavg_f32_schedule: bad sizes");
-  const Schedule sc = choose_f32_schedule(K, P);
+  const Schedule sc = choose_f32_schedule(K, P, P);
   const int64_t nvec = (P + 3) / 4;
   const int64_t span = static_cast<int64_t>(kBlock) * sc.cols;
   const int64_t blocks = (nvec + span - 1) / span;

@@ -236,6 +236,21 @@ def test_random_shapes_strides_and_offsets_bit_exact():
         assert torch.isnan(big[:4]).all() and torch.isnan(big[4 + P:]).all(), f"case {case}: wrote outside out"
 
 
+def test_chunk_of_wider_shard_streams_and_is_bit_exact():
+    """A column chunk of a wider row buffer (ld > P, the N > 1 pipeline) does
+    not take the Infinity-Cache schedule; the result is bit-exact either way."""
+    from mfl_amd import _lib
+    K, S, C = 100, 390_656, 3
+    assert _lib.f32_schedule(K, S)["nontemporal"] == 0          # alone: cache-resident band
+    assert _lib.f32_schedule(K, S, S * C)["nontemporal"] == 1   # chunk of a 3x wider shard: streamed
+    x = _clients(K, S * C, seed=3)
+    w = _weights(K, seed=4)
+    for j in range(C):
+        out = mfl_amd.reduce_packed(x[:, j * S:(j + 1) * S], _w(w), S)
+        exp = O.reduce_f32(x[:, j * S:(j + 1) * S].cpu().numpy(), w)
+        assert_bits(out, torch.from_numpy(exp), f"chunk {j}")
+
+
 def test_schedule_switch_boundaries_bit_exact():
     for K, P in _schedule_boundary_cases():
         x = _clients(K, P, seed=K * 7 + P)
