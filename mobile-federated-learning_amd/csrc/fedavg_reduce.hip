@@ -802,13 +802,14 @@ void launch_production_vec(const void* clients, int K, int64_t ld, int64_t P, co
     // fp64 follows the fp32 kernel onto per-row buffer descriptors for long
     // rows: 7,113 vs 6,992 GB/s at K=100 x 12.5M fp64 (scripts/vec_buf_probe.py,
     // profiles/r01_vec_buf_probe.jsonl).  fp16/bf16 measured no gain (+0-1 %).
-    const Schedule f = choose_f32_schedule(K, f32_equiv, f32_equiv);
+    const Schedule f = choose_f32_schedule(K, f32_equiv, ld * static_cast<int64_t>(16 / Op::kLanes) / 4);
     if (f.cols == 16) {
       launch_vec_split_buf<Op, 2, 16>(clients, K, ld, P, W, out, f.blocks_per_launch, s);
       return;
     }
   }
-  const Schedule sc = choose_schedule(K, f32_equiv);
+  const int64_t ld_equiv = ld * static_cast<int64_t>(16 / Op::kLanes) / 4;
+  const Schedule sc = choose_schedule(K, f32_equiv, 4.0 * static_cast<double>(K) * static_cast<double>(ld_equiv));
   if (sc.nt)
     launch_vec_nt<Op, true>(sc, clients, K, ld, P, W, out, s);
   else

@@ -251,6 +251,21 @@ def test_chunk_of_wider_shard_streams_and_is_bit_exact():
         assert_bits(out, torch.from_numpy(exp), f"chunk {j}")
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float64])
+def test_chunk_of_wider_shard_other_dtypes(dtype):
+    """fp16/bf16/fp64 chunks of a wider row buffer (streamed schedule) give
+    the bits of the same columns reduced from a contiguous copy."""
+    K, S, C = 100, 390_656, 3
+    x = _clients(K, S * C, seed=5, dtype=dtype)
+    w = _w(_weights(K, seed=6), torch.float64 if dtype == torch.float64 else torch.float32)
+    iv = torch.int64 if dtype == torch.float64 else torch.int16
+    for j in (0, C - 1):
+        view = x[:, j * S:(j + 1) * S]
+        got = mfl_amd.reduce_packed(view, w, S)
+        ref = mfl_amd.reduce_packed(view.contiguous(), w, S)
+        assert torch.equal(got.view(iv), ref.view(iv)), (dtype, j)
+
+
 def test_schedule_switch_boundaries_bit_exact():
     for K, P in _schedule_boundary_cases():
         x = _clients(K, P, seed=K * 7 + P)
