@@ -1,6 +1,6 @@
 """Benchmark: device-resident FedAvg weighted reduction on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME] [--scaling strong|weak]
     python bench.py --e2e [...]   # host state_dicts in/out vs the CPU loop (scripts/bench_e2e.py)
     python bench.py --fpf [...]   # FPF2 bookkeeping per round (scripts/bench_fpf.py)
 
@@ -11,18 +11,34 @@ already resident in HBM: the exact sequential HIP kernel over this rank's
 P-shard and, for N > 1, the RCCL all-gather that reassembles the averaged
 model on every rank (overlapped chunk by chunk).
 
-Default workload = the north-star target, K = 100 clients x P = 25M fp32
-params per GPU (weak scaling: P grows with N; each rank owns a 25M-column
-shard).  Algorithmic bytes per step = 4*K*P + 4*P + 4*K (reads of every
-client row, the averaged-model write, the weights).
+Multi-GPU: one process per GPU.  Under torch.distributed.run the ranks come
+from the environment; ``python bench.py --gpus N`` without it starts
+``torch.distributed.run`` itself as a child process (this process never
+touches the GPU) and exits with its status.
+
+Scaling (``--scaling``):
+  strong (default): the workload's P is the GLOBAL model, split over the N
+          ranks -- the BASELINE configurations: the target is 100 clients x
+          25M params in total (3.125M columns per rank at N = 8),
+          cfg4 500 x 11.2M, cfg5 1000 x 100M (12.5M per rank at N = 8);
+  weak:   every rank owns P columns (the model has N x P params).
+Algorithmic bytes per step = 4*K*P + 4*P + 4*K for the global P (reads of
+every client row, the averaged-model write, the weights).
+
+Inputs: ``mfl_amd.synthetic`` -- every value a pure function of (client,
+global column), so the model does not depend on N and any window of the
+gathered model is re-derived on the host by numpy + the oracle.
 
 Rank 0 prints ONE JSON line.  Besides the contract keys it carries:
   roofline      : the reduce kernel's algorithmic HBM bytes / its average
                   launch time (HIP events on the launch stream), vs 8 TB/s;
   cpu_baseline  : the reference's torch CPU loop (oracle restatement, the
-                  same expression as fedavg_trainer.py:450-457) on a bounded
-                  sample, rank 0, N = 1 only;
-  parity        : sampled columns compared bit for bit with the oracle.
+                  same expression as fedavg_trainer.py:450-457) on bounded
+                  samples, rank 0, N = 1 only: one flat key and the
+                  model-shaped resnet56 state_dict (350 keys);
+  parity        : sampled windows bit for bit vs the oracle on host-derived
+                  inputs (at N > 1: windows of the gathered model owned by
+                  any rank, plus per-rank checksums of the reassembly).
 """
 from __future__ import annotations
 
@@ -30,31 +46,37 @@ import argparse
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent
-sys.path.insert(0, str(ROOT))
-
-import numpy as np
-import torch
-import torch.distributed as dist
-
-import mfl_amd
-from mfl_amd.distributed import ShardedReducer
 
 METRIC = "aggregated GB/s device-resident, K-client × P-param fp32 weighted reduce"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 WORKLOADS = {
-    # name: (K, P per GPU, description)
-    "target": (100, 25_000_000, "north-star target: 100 clients x 25M fp32 params per GPU"),
+    # name: (K, P, description); P is the global model under strong scaling
+    # and the per-rank shard under weak scaling
+    "target": (100, 25_000_000, "north-star target: 100 clients x 25M fp32 params"),
     "femnist_cnn": (10, 1_206_590, "cfg2 FEMNIST + CNN_DropOut, 10 clients (fits the 256 MiB MALL)"),
     "resnet56": (100, 600_372, "cfg3 CIFAR10 + resnet56, 100 clients (fits the 256 MiB MALL)"),
     "resnet18_gn": (500, 11_227_812, "cfg4 fed_cifar100 + resnet18_gn, 500 clients"),
-    "synthetic_1000x100m_slice": (1000, 12_500_000, "cfg5 1000 clients, 12.5M-param P-slice per GPU"),
+    "synthetic_1000x100m": (1000, 100_000_000, "cfg5 synthetic 1000 clients x 100M fp32 params"),
+    "synthetic_1000x100m_slice": (1000, 12_500_000, "cfg5's per-GPU slice at N = 8 (1000 x 12.5M)"),
 }
+
+# One rank's client rows may take this much HBM (MI355X: 288 GB); a larger
+# single-GPU workload (cfg5 at N = 1: 400 GB) runs as P-chunked passes over
+# one resident buffer ("each pass device-resident; time = sum").
+ROW_BUDGET_BYTES = int(float(os.environ.get("FEDAVG_BENCH_ROW_BUDGET_GB", "230")) * 1e9)
+
+# N > 1 pipeline: chunk count so that every chunk keeps enough columns for a
+# full-chip launch of the short-row schedule (see auto_chunks)
+MIN_CHUNK_COLS = 700_000
+MAX_CHUNKS = 8
 
 
 def env_int(name, default):
@@ -66,89 +88,240 @@ def algorithmic_bytes(K: int, P: int) -> int:
     return 4 * K * P + 4 * P + 4 * K
 
 
-def sample_counts(K: int):
-    return [int(v) for v in np.random.default_rng(1234).integers(1, 1001, size=K)]
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
 
-def fill_synthetic(clients: torch.Tensor, rank: int):
-    """client k = base + N(0, 1e-3^2), base ~ N(0, 0.05^2) (BASELINE.md inputs)."""
-    K, cols = clients.shape
-    g = torch.Generator(device=clients.device).manual_seed(rank * 7919)
-    base = torch.randn(cols, generator=g, device=clients.device) * 0.05
-    for k in range(K):
-        gk = torch.Generator(device=clients.device).manual_seed(1000 + k + rank * 100_003)
-        torch.randn(cols, generator=gk, device=clients.device, out=clients[k])
-        clients[k].mul_(1e-3).add_(base)
-    del base
+def self_launch(argv) -> "int | None":
+    """``--gpus N`` (N > 1) outside torch.distributed.run: start the N ranks
+    with torch.distributed.run as a CHILD process -- nothing here has touched
+    the GPU -- relay its output (rank 0 prints the JSON line) and return its
+    exit status (non-zero if any rank failed).  None: run in this process."""
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--gpus", type=int, default=1)
+    known, _ = ap.parse_known_args(argv)
+    if known.gpus <= 1 or os.environ.get("WORLD_SIZE") not in (None, ""):
+        return None
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # the box supports dmabuf IPC only
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={known.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(Path(__file__).resolve()), *argv]
+    return subprocess.call(cmd, env=env)
 
 
-def cpu_baseline(P: int, target_seconds: float = 12.0):
+def auto_chunks(K: int, shard_cols: int, world: int, host_out: bool) -> int:
+    """All-gather pipeline depth.  One chunk at N = 1 (no exchange; the
+    host-out consumer overlaps 4 D2H chunks).  At N > 1 the deepest of
+    8/4/2/1 whose chunks keep >= MIN_CHUNK_COLS columns: the gather of chunk
+    c overlaps the reduce of chunk c + 1, and each chunk launch still fills
+    the chip."""
+    if host_out:
+        return 4
+    if world == 1:
+        return 1
+    c = MAX_CHUNKS
+    while c > 1 and shard_cols // c < MIN_CHUNK_COLS:
+        c //= 2
+    return c
+
+
+def _thread_count():
+    """Host threads for the CPU baseline: the CPUs this process may run on
+    (sched_getaffinity), capped by OMP_NUM_THREADS when the box sets it (the
+    GPU box gives each 1-GPU job a 16-CPU share of a larger machine)."""
+    n_aff = len(os.sched_getaffinity(0))
+    omp = env_int("OMP_NUM_THREADS", 0)
+    return (min(n_aff, omp) if omp > 0 else n_aff), n_aff
+
+
+def cpu_baseline(P: int, flat_seconds: float = 10.0, model_seconds: float = 5.0):
     """The reference's torch CPU loop (fedavg_trainer.py:444-458, restated in
-    oracle/fedavg_oracle.py) on a bounded sample of the bench workload: a
-    K-slice -- 10 clients with the workload's full P-element key (1 GB at
-    P = 25M), so every tensor has the workload's size and the same cache
-    behaviour (a P-slice of 10 MB tensors can sit in a large host L3 and
-    overstate the CPU); repeated until ~target_seconds."""
-    sys.path.insert(0, str(ROOT / "oracle"))
-    import fedavg_oracle as O
+    oracle/fedavg_oracle.py) on bounded samples, with as many torch threads
+    as the host gives this process:
 
-    threads = torch.get_num_threads()
+    * flat: a K-slice -- 10 clients with the workload's full P-element key
+      (1 GB at P = 25M), so every tensor has the workload's size and cache
+      behaviour; repeated for ~flat_seconds.  This is ``value``.
+    * model-shaped: cfg3's resnet56 state_dict (350 keys, 58 int64
+      num_batches_tracked buffers), all 100 clients -- the per-key dispatch
+      cost the reference pays on real models (slowest layout)."""
+    import torch
+
+    sys.path.insert(0, str(ROOT / "oracle"))
+    sys.path.insert(0, str(ROOT / "scripts"))
+    import fedavg_oracle as O
+    from model_shapes import CONFIGS, numel
+
+    threads, n_aff = _thread_count()
+    torch.set_num_threads(threads)
+
+    def timed(w_locals_factory, seconds):
+        times = []
+        t_end = time.perf_counter() + seconds
+        while time.perf_counter() < t_end or len(times) < 3:
+            w_locals = w_locals_factory()  # fresh dicts: the loop mutates dict 0
+            t0 = time.perf_counter()
+            O.aggregate_torch(w_locals)
+            times.append(time.perf_counter() - t0)
+            if len(times) >= 50:
+                break
+        return min(times[1:]), len(times) - 1
+
+    from mfl_amd.synthetic import sample_counts
+
     K = 10
     g = torch.Generator().manual_seed(0)
     base = torch.randn(P, generator=g) * 0.05
     clients = [base + torch.randn(P, generator=g) * 1e-3 for _ in range(K)]
     counts = sample_counts(K)
-    times = []
-    t_end = time.perf_counter() + target_seconds
-    while time.perf_counter() < t_end or len(times) < 2:
-        w_locals = [(counts[i], {"w": clients[i]}) for i in range(K)]  # fresh dicts: the loop mutates dict 0
-        t0 = time.perf_counter()
-        O.aggregate_torch(w_locals)
-        times.append(time.perf_counter() - t0)
-        if len(times) >= 50:
-            break
-    best = min(times[1:]) if len(times) > 1 else times[0]
+    best, reps = timed(lambda: [(counts[i], {"w": clients[i]}) for i in range(K)], flat_seconds)
+    del clients, base
+    flat = {"layout": "flat", "value": round(algorithmic_bytes(K, P) / best / 1e9, 3), "unit": "GB/s",
+            "sample": f"K-slice: K={K} x P={P} fp32, one flat key; best of {reps} reps after 1 warm-up, "
+                      f"{best * 1e3:.1f} ms/reduce"}
+
+    Km, shapes = CONFIGS["resnet56"]
+    Pm = numel(shapes)
+    base = {k: torch.randn(s, generator=g) * 0.05 for k, s in shapes}
+    dicts = []
+    for i in range(Km):
+        sd = {}
+        for k, s in shapes:
+            sd[k] = (torch.tensor(1000 + i, dtype=torch.int64) if k.endswith("num_batches_tracked")
+                     else base[k] + torch.randn(s, generator=g) * 1e-3)
+        dicts.append(sd)
+    mcounts = sample_counts(Km)
+    best_m, reps_m = timed(lambda: [(mcounts[0], dict(dicts[0]))] + list(zip(mcounts[1:], dicts[1:])), model_seconds)
+    model = {"layout": "model-shaped (resnet56)", "value": round(algorithmic_bytes(Km, Pm) / best_m / 1e9, 3),
+             "unit": "GB/s",
+             "sample": f"cfg3 resnet56 state_dicts: K={Km} x P={Pm}, {len(shapes)} keys; best of {reps_m} reps "
+                       f"after 1 warm-up, {best_m * 1e3:.1f} ms/reduce"}
     return {
-        "value": round(algorithmic_bytes(K, P) / best / 1e9, 3),
+        "value": flat["value"],
         "unit": "GB/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"K-slice: K={K} x P={P} fp32 (the workload's key size), one flat key; reference torch CPU loop restated "
-                  f"(oracle/fedavg_oracle.py aggregate_torch); best of {len(times) - 1} reps "
-                  f"after 1 warm-up, {best * 1e3:.1f} ms/reduce, torch threads={threads}",
+        "sample": flat["sample"] + " (value); reference torch CPU loop restated (oracle/fedavg_oracle.py "
+                                   "aggregate_torch)",
+        "affinity_cpus": n_aff,
+        "layouts": [flat, model],
     }
 
 
-def sampled_parity(red: ShardedReducer, weights, n_windows=6, width=2048):
-    """Bit-compare sampled local columns of the device result with the oracle."""
+# ---------------------------------------------------------------------------
+# parity: device results vs the oracle on host-derived inputs
+# ---------------------------------------------------------------------------
+def _oracle_window(K, weights, g0, n):
     sys.path.insert(0, str(ROOT / "oracle"))
     import fedavg_oracle as O
+    from mfl_amd.synthetic import client_columns_numpy
 
-    segs = red.plan.local_segments()
-    rng = np.random.default_rng(7)
+    return O.reduce_f32(client_columns_numpy(K, g0, n), weights)
+
+
+def _bits_equal(a, b) -> bool:
+    return a.tobytes() == b.tobytes()
+
+
+def sampled_parity(red, weights, *, passes=1, pass_cols=0, n_windows=6, width=2048):
+    """Windows of this rank's result, bit for bit against the oracle applied to
+    the same (client, column) inputs regenerated on the host:
+
+    * local: windows of ``local_out`` (the rank's own columns), including the
+      first and last valid column; the host copy too when there is one;
+    * gathered (N > 1 or a forced gather): windows of ``full[:P]`` at random
+      GLOBAL positions (any rank's columns), and ``full`` == ``local_out`` on
+      every column this rank owns;
+    * passes > 1 (single-GPU P-chunked passes over one resident buffer):
+      windows of every pass's output slice against pass 0's columns."""
+    import numpy as np
+    import torch
+
+    K = red.K
+    plan = red.plan
+    segs = plan.local_segments()
+    rng = np.random.default_rng(7 + plan.rank)
     checked = 0
+    picks = [(segs[0][0], segs[0][1], min(width, segs[0][2])),  # first valid column
+             (segs[-1][0] + segs[-1][2] - min(width, segs[-1][2]), segs[-1][1] + segs[-1][2] - min(width, segs[-1][2]),
+              min(width, segs[-1][2]))]  # last valid column
     for _ in range(n_windows):
         lstart, gstart, n = segs[int(rng.integers(0, len(segs)))]
         w = min(width, n)
-        s = lstart + int(rng.integers(0, n - w + 1))
-        exp = O.reduce_f32(red.clients[:, s:s + w].cpu().numpy(), weights)
-        got = red.local_out[s:s + w].cpu().numpy()
-        if red.host_out is not None:  # the copy the host consumer reads
-            g = gstart + (s - lstart)
-            if red.host_out[g:g + w].numpy().tobytes() != got.tobytes():
-                return {"ok": False, "columns_checked": checked, "bar": "host_out == device shard"}
-        if got.tobytes() != exp.tobytes():
-            return {"ok": False, "columns_checked": checked, "bar": "bit-exact vs oracle"}
+        off = int(rng.integers(0, n - w + 1))
+        picks.append((lstart + off, gstart + off, w))
+    for l, g, w in picks:
+        exp = _oracle_window(K, weights, g, w)
+        got = red.local_out[l:l + w].cpu().numpy()
+        if not _bits_equal(got, exp):
+            return {"ok": False, "columns_checked": checked, "failed": f"local window at global column {g}"}
+        if red.host_out is not None and not _bits_equal(red.host_out[g:g + w].numpy(), exp):
+            return {"ok": False, "columns_checked": checked, "failed": f"host_out window at {g}"}
         checked += w
-    return {"ok": True, "columns_checked": checked, "bar": "bit-exact vs oracle (sampled windows)"}
+    if passes > 1:
+        for p in range(1, passes):
+            for l, g, w in picks[:3]:
+                got = red.pass_out[p * pass_cols + l:p * pass_cols + l + w].cpu().numpy()
+                if not _bits_equal(got, _oracle_window(K, weights, g, w)):
+                    return {"ok": False, "columns_checked": checked, "failed": f"pass {p} window at {g}"}
+                checked += w
+    out = {"ok": True, "columns_checked": checked}
+    if red.gather:
+        P = plan.P
+        for _ in range(n_windows):
+            w = min(width, P)
+            g = int(rng.integers(0, P - w + 1))
+            if not _bits_equal(red.full[g:g + w].cpu().numpy(), _oracle_window(K, weights, g, w)):
+                return {"ok": False, "columns_checked": checked, "failed": f"gathered window at {g}"}
+            checked += w
+        for l, g, n in segs:  # the reassembled model holds this rank's columns unchanged
+            if not torch.equal(red.full[g:g + n].view(torch.int32), red.local_out[l:l + n].view(torch.int32)):
+                return {"ok": False, "columns_checked": checked, "failed": f"full != local_out at {g}"}
+        out["gathered_checked"] = True
+    out["columns_checked"] = checked
+    out["bar"] = "bit-exact vs oracle on host-regenerated inputs (sampled windows, first and last column)"
+    return out
 
 
-def overlap_diagnostics(red: ShardedReducer, w_dev, steps: int, step_elapsed: float, reps: int = 5) -> dict:
+def reassembly_checksums(red, dist, dev):
+    """Checksum of checksums: every rank sums the int32 bit patterns of its own
+    valid columns (int64, exact); all ranks exchange them; each rank then
+    recomputes every rank's sum from ITS gathered model at that rank's global
+    positions.  A layout or stream-ordering error anywhere in the exchange
+    shows up on every rank."""
+    import torch
+
+    from mfl_amd.distributed import plan_shards
+
+    plan = red.plan
+    ws = plan.world_size
+
+    def csum(t):
+        return t.view(torch.int32).to(torch.int64).sum()
+
+    own = torch.zeros(1, dtype=torch.int64, device=dev)
+    for l, _, n in plan.local_segments():
+        own += csum(red.local_out[l:l + n])
+    allsums = torch.zeros(ws, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(allsums, own)
+    mine = torch.zeros(ws, dtype=torch.int64, device=dev)
+    for r in range(ws):
+        for _, g, n in plan_shards(plan.P, ws, r, plan.chunks).local_segments():
+            mine[r] += csum(red.full[g:g + n])
+    return bool(torch.equal(allsums, mine))
+
+
+def overlap_diagnostics(red, w_dev, steps: int, step_elapsed: float, reps: int = 5) -> dict:
     """N > 1, after the timed region (not part of `value`): the reduce alone
     and the all-gather alone, each timed like a step (barrier + sync on both
     sides, max over ranks), so the JSON line shows how much of the exchange
     the chunked pipeline hides.  overlap = (reduce + gather - step) /
     min(reduce, gather): 1 = fully hidden, 0 = serialised."""
+    import torch
+    import torch.distributed as dist
+
     def timed(fn):
         torch.cuda.synchronize()
         dist.barrier()
@@ -171,20 +344,51 @@ def overlap_diagnostics(red: ShardedReducer, w_dev, steps: int, step_elapsed: fl
         red.gather = gather
     gather_ms = timed(red.gather_only)
     step_ms = step_elapsed / steps * 1e3
+    recv = (red.plan.padded_P - red.plan.local_cols) * 4
     return {"reduce_only_ms": round(reduce_ms, 4), "gather_only_ms": round(gather_ms, 4), "step_ms": round(step_ms, 4),
             "overlap": round((reduce_ms + gather_ms - step_ms) / max(min(reduce_ms, gather_ms), 1e-9), 3),
-            "gather_bytes_in_per_rank": int(red.plan.padded_P - red.plan.local_cols) * 4,
+            "gather_bytes_in_per_rank": int(recv),
+            "gather_GBps_in_per_rank": round(recv / (gather_ms * 1e-3) / 1e9, 1),
             "note": "after the timed region; not part of value"}
 
 
-def main():
+def launch_check(args):
+    """``--launch-check``: the multi-rank launch path alone, on CPU (gloo) --
+    every rank joins the group and all-reduces its rank; rank 0 prints one
+    JSON line.  ``--fail-rank R`` makes rank R exit with status 3 (the parent
+    must relay a failing rank as a non-zero exit)."""
+    import torch
+    import torch.distributed as dist
+
+    world, rank = env_int("WORLD_SIZE", 1), env_int("RANK", 0)
+    if world > 1:
+        dist.init_process_group("gloo")
+    if rank == args.fail_rank:
+        raise SystemExit(3)
+    t = torch.tensor([rank + 1], dtype=torch.int64)
+    if world > 1:
+        dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "world": world, "rank_sum": int(t.item()),
+                          "expected": world * (world + 1) // 2}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="target", choices=sorted(WORKLOADS))
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                    help="strong: the workload's P is the global model split over the ranks (BASELINE configs); "
+                         "weak: every rank owns P columns")
     ap.add_argument("--chunks", type=int, default=0, help="all-gather pipeline chunks (0 = auto)")
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the all-gather (reduce only)")
+    ap.add_argument("--force-gather", action="store_true",
+                    help="run the RCCL all-gather even at N=1 (world-size-1 nccl group)")
     ap.add_argument("--unroll", type=int, default=0, help="kernel variant: loads in flight per thread")
     ap.add_argument("--nt", type=int, default=-1, help="kernel variant: 1 = nontemporal loads")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -192,14 +396,25 @@ def main():
     ap.add_argument("--traffic-json", default="", help="PMC traffic summary (profiles/*.json) to attach")
     ap.add_argument("--host-out", action="store_true",
                     help="host consumer (SURVEY 8e): D2H each rank's shard into pinned host memory, no collective")
-    args = ap.parse_args()
+    ap.add_argument("--launch-check", action="store_true", help="CPU-only: check the multi-rank launch path")
+    ap.add_argument("--fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
+    args = ap.parse_args(argv)
+    if args.launch_check:
+        return launch_check(args)
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    sys.path.insert(0, str(ROOT))
+    import mfl_amd
+    from mfl_amd import synthetic
+    from mfl_amd.distributed import ShardedReducer
 
     world = env_int("WORLD_SIZE", 1)
     rank = env_int("RANK", 0)
     local_rank = env_int("LOCAL_RANK", 0)
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus > 1 needs torch.distributed.run (one process per GPU)")
         raise SystemExit(f"--gpus {args.gpus} does not match WORLD_SIZE={world} (one process per GPU)")
     # Rehearsal knobs (a 1-GPU box): FEDAVG_DIST_BACKEND=gloo and
     # FEDAVG_SAME_DEVICE=1 run N ranks on cuda:0.  The driver's runs use the
@@ -208,25 +423,39 @@ def main():
     dev_index = 0 if os.environ.get("FEDAVG_SAME_DEVICE") == "1" else local_rank
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
-    if world > 1:
+    use_pg = world > 1 or args.force_gather
+    if use_pg:
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
     mfl_amd._lib.load()
 
-    K, P_local, desc = WORKLOADS[args.workload]
-    # N > 1: 8 chunks.  scripts/overlap_probe.py: with a
-    # stand-in for RCCL's kernel that stays resident like an xGMI-bound
-    # all-gather, 8 chunks hide 82-87 % of the shorter leg (4 chunks: 52-70 %)
-    # for gathers of 1.0-3.0 ms per step
-    chunks = args.chunks or (1 if world == 1 and not args.host_out else 4 if args.host_out else 8)
-    P_total = P_local * world
-    host_out = torch.empty(P_total, dtype=torch.float32, pin_memory=True) if args.host_out else None
-    # Each rank owns exactly P_local valid columns: plan over the global P.
-    red = ShardedReducer(K, P_total, chunks=chunks, device=dev, gather=not args.no_gather, host_out=host_out)
-    fill_synthetic(red.clients, rank)
-    counts = sample_counts(K)
+    K, P_w, desc = WORKLOADS[args.workload]
+    P_global = P_w if args.scaling == "strong" else P_w * world
+    shard_cols = -(-P_global // world)
+    chunks = args.chunks or auto_chunks(K, shard_cols, world, args.host_out)
+
+    # single-GPU workloads larger than the row budget: P-chunked passes
+    passes = 1
+    if 4 * K * shard_cols > ROW_BUDGET_BYTES:
+        if world > 1:
+            raise SystemExit(f"{args.workload} needs {4 * K * shard_cols / 1e9:.0f} GB of rows per rank; "
+                             f"use more GPUs")
+        passes = math.ceil(4 * K * shard_cols / ROW_BUDGET_BYTES)
+    P_pass = -(-P_global // passes) if passes > 1 else P_global
+    P_pass = (P_pass + 63) // 64 * 64 if passes > 1 else P_pass
+
+    host_out = torch.empty(P_pass, dtype=torch.float32, pin_memory=True) if args.host_out else None
+    gather = False if args.no_gather else (True if args.force_gather else None)
+    red = ShardedReducer(K, P_pass, chunks=chunks, device=dev, gather=gather, host_out=host_out)
+    synthetic.fill_rows(red.clients, red.plan.local_segments())
+    counts = synthetic.sample_counts(K)
     weights = mfl_amd.sample_weights(counts)
     w_dev = mfl_amd.weights_tensor(weights, torch.float32, dev)
 
@@ -235,7 +464,8 @@ def main():
         tuned = (args.unroll or 8, max(args.nt, 0))
 
     S = red.plan.block
-    sched = mfl_amd._lib.f32_schedule(K, S, red.plan.local_cols) if tuned is None else None
+    ld = red.clients.stride(0)
+    sched = mfl_amd._lib.f32_schedule(K, S, ld) if tuned is None else None
     launches_per_call = sched["launches"] if sched else 1
     ev_pairs = []
 
@@ -250,29 +480,44 @@ def main():
         e.record()
         ev_pairs.append((s, e))
 
+    if passes > 1:
+        # every pass reduces the resident [K, P_pass] rows into its own slice
+        # of the [passes * P_pass] model (the pass's columns; the data of
+        # pass p is pass 0's buffer -- 400 GB of distinct rows do not fit)
+        red.pass_out = torch.empty(passes * red.plan.local_cols, dtype=torch.float32, device=dev)
+        one_pass = red.step
+
+        def step_passes(w):
+            for p in range(passes):
+                red.local_out = red.pass_out[p * red.plan.local_cols:(p + 1) * red.plan.local_cols]
+                one_pass(w)
+        red_step = step_passes
+    else:
+        red_step = red.step
+
     red.local_reduce = local_reduce
     for _ in range(args.warmup):
-        red.step(w_dev)
+        red_step(w_dev)
     torch.cuda.synchronize()
-    if world > 1:
+    if use_pg:
         dist.barrier()
     torch.cuda.synchronize()
 
-    step = lambda: red.step(w_dev)  # noqa: E731
+    step = lambda: red_step(w_dev)  # noqa: E731
     if args.graph:
         # one step captured into a hipGraph and replayed: removes the per-step
         # host launch path (Python + ctypes + hipLaunchKernel) that dominates
         # small, cache-resident workloads
-        if world > 1:
+        if use_pg:
             raise SystemExit("--graph is single-GPU only (RCCL capture is not used)")
         graph = torch.cuda.CUDAGraph()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
-            red.step(w_dev)  # warm the capture stream
+            red_step(w_dev)  # warm the capture stream
             torch.cuda.synchronize()
             with torch.cuda.graph(graph, stream=s):
-                red.step(w_dev)
+                red_step(w_dev)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
 
@@ -288,20 +533,23 @@ def main():
             graph.replay()
         torch.cuda.synchronize()
         ev_pairs.clear()
+        calls_per_event = red.plan.chunks * passes
     else:
         red.local_reduce = timed_local_reduce
+        calls_per_event = 1
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if use_pg:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    red.local_reduce = local_reduce
 
-    kernel_ms = [s.elapsed_time(e) for s, e in ev_pairs]
+    kernel_ms = [s.elapsed_time(e) / calls_per_event for s, e in ev_pairs]
     t = torch.tensor([elapsed, float(np.mean(kernel_ms))], dtype=torch.float64, device=dev)
-    if world > 1:
+    if use_pg:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed_max, kernel_ms_max = float(t[0]), float(t[1])
 
@@ -309,24 +557,29 @@ def main():
     if world > 1 and red.gather:
         diagnostics = overlap_diagnostics(red, w_dev, args.steps, elapsed_max)
 
-    parity = sampled_parity(red, weights)
-    if world > 1:
+    parity = sampled_parity(red, weights, passes=passes, pass_cols=red.plan.local_cols if passes > 1 else 0)
+    if red.gather:
+        parity["reassembly_checksums_ok"] = reassembly_checksums(red, dist, dev)
+        parity["ok"] = parity["ok"] and parity["reassembly_checksums_ok"]
+    if use_pg:
         ok = torch.tensor([1.0 if parity["ok"] else 0.0], device=dev)
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         parity["ok"] = bool(ok.item() == 1.0)
         parity["ranks"] = world
 
     if rank == 0:
-        bytes_step = algorithmic_bytes(K, P_total)
+        P_done = P_pass * passes if passes > 1 else P_global
+        bytes_step = algorithmic_bytes(K, P_done)
         value = bytes_step * args.steps / elapsed_max / 1e9
         # one reduce call = one chunk of one rank's shard = `launches_per_call`
         # round-split kernel launches of equal size
         bytes_call = algorithmic_bytes(K, S)
         achieved = bytes_call / (kernel_ms_max * 1e-3) / 1e9
         if sched:
-            kern = "reduce_f32x4_buf_kernel" if sched["cols"] == 16 else "reduce_f32x4_var_kernel"
-            kname = (f"{kern}<U={sched['unroll']},C={sched['cols']},nt={sched['nontemporal']}> "
-                     f"(exact, sequential client order; round-split x{launches_per_call})")
+            kname = f"{sched['kernel']}<U={sched['unroll']},C={sched['cols']},nt={sched['nontemporal']}"
+            if sched.get("block", 256) != 256:
+                kname += f",B={sched['block']}"
+            kname += f"> (exact, sequential client order; round-split x{launches_per_call})"
         else:
             kname = f"tuned variant {tuned}"
         roofline = {
@@ -339,7 +592,7 @@ def main():
             "kernel": kname,
             "bytes_per_launch": bytes_call // launches_per_call,
             "avg_launch_ms": round(kernel_ms_max / launches_per_call, 4),
-            "launches": len(kernel_ms) * launches_per_call,
+            "launches": len(kernel_ms) * calls_per_event * launches_per_call,
         }
         tj = args.traffic_json or str(ROOT / "profiles" / f"traffic_{args.workload}.json")
         if Path(tj).exists():
@@ -350,13 +603,37 @@ def main():
                     roofline["traffic"] = tr.get("hbm_bytes_per_launch")
                     roofline["traffic_source"] = src
                 elif tr.get("traffic_over_algorithmic"):
-                    # other launch geometry (e.g. N > 1: 8 chunks per rank): the PMC
+                    # other launch geometry (e.g. N > 1: chunks per rank): the PMC
                     # traffic/algorithmic ratio of the same kernel, applied to this launch
                     ratio = float(tr["traffic_over_algorithmic"])
                     roofline["traffic"] = int(round(ratio * roofline["bytes_per_launch"]))
                     roofline["traffic_source"] = f"{src} (PMC ratio {ratio} x this launch's algorithmic bytes)"
             except (ValueError, OSError, KeyError):
                 pass
+        if red.gather:
+            exchange = "rccl all_gather_into_tensor, overlapped per chunk"
+        elif host_out is not None:
+            exchange = "none: each rank D2Hs its shard chunks into pinned host memory (host consumer)"
+        else:
+            exchange = "none (single GPU or --no-gather)"
+        config = {
+            "workload": desc,
+            "K": K,
+            "P_total": P_done,
+            "P_per_gpu": red.plan.valid_local_cols() * passes,
+            "scaling_mode": args.scaling,
+            "chunks": red.plan.chunks,
+            "chunk_cols": S,
+            "exchange": exchange,
+            "parallelism": f"p-shard{world}",
+            "kernel_variant": {"unroll": tuned[0], "nt": tuned[1]} if tuned else "default",
+            "launch": "hipGraph replay" if args.graph else "eager (stream-ordered)",
+        }
+        if passes > 1:
+            config["passes"] = passes
+            config["pass_note"] = (f"{K} x {P_done} fp32 = {4 * K * P_done / 1e9:.0f} GB of rows exceeds one GPU; "
+                                   f"{passes} P-chunked passes over one resident {K} x {P_pass} buffer "
+                                   f"(each pass streams it from HBM; time = sum of passes)")
         out = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -366,23 +643,12 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed_max / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (device-generated: base~N(0,0.05^2) + per-client N(0,1e-3^2); counts U{1..1000})",
-            "config": {
-                "workload": desc,
-                "K": K,
-                "P_per_gpu": P_local,
-                "P_total": P_total,
-                "chunks": chunks,
-                "exchange": ("rccl all_gather_into_tensor, overlapped per chunk" if red.gather else
-                             "none: each rank D2Hs its shard chunks into pinned host memory (host consumer)"
-                             if host_out is not None else "none (single GPU or --no-gather)"),
-                "parallelism": f"p-shard{world}",
-                "kernel_variant": {"unroll": tuned[0], "nt": tuned[1]} if tuned else "default",
-                "launch": "hipGraph replay" if args.graph else "eager (stream-ordered)",
-            },
+            "data": "synthetic (device-generated counter-hash uniform, base std 0.05 + per-client std 1e-3, "
+                    "reproducible on the host; counts U{1..1000})",
+            "config": config,
             "roofline": roofline,
             # the whole step against the node's HBM-read roofline (N x 8 TB/s):
             # north_star's "fraction of the HBM-read roofline" at N GPUs
@@ -392,9 +658,9 @@ def main():
         if diagnostics is not None:
             out["diagnostics"] = diagnostics
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(P_local)
+            out["cpu_baseline"] = cpu_baseline(min(P_global, 25_000_000))
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if use_pg:
         dist.barrier()
         dist.destroy_process_group()
 
@@ -406,6 +672,7 @@ def side_bench(argv) -> bool:
     reference's torch expressions (oracle/), handed in from here."""
     if not argv or argv[0] not in ("--e2e", "--fpf"):
         return False
+    sys.path.insert(0, str(ROOT))
     sys.path.insert(0, str(ROOT / "scripts"))
     sys.path.insert(0, str(ROOT / "oracle"))
     if argv[0] == "--e2e":
@@ -422,5 +689,9 @@ def side_bench(argv) -> bool:
 
 
 if __name__ == "__main__":
-    if not side_bench(sys.argv[1:]):
-        main()
+    _argv = sys.argv[1:]
+    _rc = self_launch(_argv)
+    if _rc is not None:
+        sys.exit(_rc)
+    if not side_bench(_argv):
+        main(_argv)

@@ -185,6 +185,18 @@ int fedavg_upload_shard(void* dst, int64_t dst_pitch_bytes, const void* host_src
 int fedavg_weights_f32(const int64_t* sample_nums, int64_t K, float* weights);
 
 /*
+ * The schedule fedavg_reduce_f32() uses for an aligned [K, P] problem:
+ * rows per load batch, 16-B column slices per thread, nontemporal loads, and
+ * the number of round-split launches.  Host-only query (bench.py names the kernel from it).
+ */
+int fedavg_f32_schedule(int64_t K, int64_t P, int* unroll, int* cols, int* nontemporal, int* launches);
+/* The same for P columns of a row buffer with row stride ld (a column chunk
+ * of a wider shard when ld > P: no Infinity-Cache-resident schedule). */
+int fedavg_f32_schedule_ld(int64_t K, int64_t P, int64_t ld, int* unroll, int* cols, int* nontemporal,
+                           int* launches);
+
+
+/*
  * Host runtime: pack client state_dicts into pinned client-major rows.
  *
  * One item per (client, key): copy `numel` elements from `src` (host, dense)

@@ -1,7 +1,11 @@
 /*
- * fedavg_amd_tuning.h -- benchmarking hooks of libfedavg_amd.so (not part of
- * the drop-in contract; bench.py uses them to A/B kernel variants in one
- * process, as the CDNA guide's rule 24 asks).
+ * fedavg_amd_tuning.h -- benchmarking hooks, exported ONLY by the probe
+ * library libfedavg_amd_probe.so (the product library libfedavg_amd.so is
+ * built without them).  Not part of the drop-in contract: scripts/ and the
+ * variant tests load the probe library to A/B kernel variants in one process,
+ * as the CDNA guide's rule 24 asks.  The probe library also exports every
+ * product entry point of fedavg_amd.h (same sources, built with
+ * -DFEDAVG_TUNING), so one handle serves a whole A/B run.
  */
 #ifndef FEDAVG_AMD_TUNING_H
 #define FEDAVG_AMD_TUNING_H
@@ -16,17 +20,6 @@ extern "C" {
  * path fedavg_reduce_f32 takes for buffers that are not 16-B aligned). */
 #define FEDAVG_DEFAULT_UNROLL 8
 #define FEDAVG_DEFAULT_NONTEMPORAL 0
-
-/*
- * The schedule fedavg_reduce_f32() uses for an aligned [K, P] problem:
- * rows per load batch, 16-B column slices per thread, nontemporal loads, and
- * the number of round-split launches.  Host-only query.
- */
-int fedavg_f32_schedule(int64_t K, int64_t P, int* unroll, int* cols, int* nontemporal, int* launches);
-/* The same for P columns of a row buffer with row stride ld (a column chunk
- * of a wider shard when ld > P: no Infinity-Cache-resident schedule). */
-int fedavg_f32_schedule_ld(int64_t K, int64_t P, int64_t ld, int* unroll, int* cols, int* nontemporal,
-                           int* launches);
 
 /*
  * fedavg_reduce_f32 with explicit variant knobs:
@@ -144,10 +137,13 @@ int fedavg_reduce_segments_f32_variant(const int64_t* client_ptrs, const int64_t
 
 /* The exact fp32 row reduce through buffer descriptors (one per client row
  * and column group, base in SGPRs, 32-bit lane offsets) in launch_split's
- * round-split schedule; (unroll, cols) in {(4,8), (8,4), (4,4), (2,8),
- * (2,16), (1,16), (8,8), (4,16)}; max_blocks 0 = resident blocks.  Same bits. */
+ * round-split schedule, workgroups of `block` threads (64, 128 or 256).
+ * (unroll, cols, block): 256-thread groups (4,8) (8,4) (4,4) (2,8) (2,16)
+ * (1,16) (8,8) (4,16) (16,1) (16,2) (16,4) (8,2) (8,1); 128 and 64 threads
+ * (8,1) (8,2) (8,4) (16,1) (16,2) (16,4) (4,4) (4,8), plus (32,1) (32,2) at
+ * 64.  max_blocks 0 = resident blocks.  Same bits. */
 int fedavg_reduce_f32_buf(const float* clients, int64_t K, int64_t P, int64_t ld, const float* weights, float* out,
-                          int unroll, int cols, int max_blocks, void* stream);
+                          int unroll, int cols, int block, int max_blocks, void* stream);
 
 /* The distance pass (fedavg_client_sqdist_f32) through buffer descriptors:
  * per block, one descriptor per client row and one for glob whose record

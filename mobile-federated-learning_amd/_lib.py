@@ -9,14 +9,14 @@ import ctypes
 import threading
 from pathlib import Path
 
-from .build import LIB_PATH
+from .build import LIB_PATH, PROBE_LIB_PATH
 
 _c_i64 = ctypes.c_int64
 _c_int = ctypes.c_int
 _vp = ctypes.c_void_p
 _c_float = ctypes.c_float
 
-# name -> (restype, argtypes); mirrors include/fedavg_amd.h + fedavg_amd_tuning.h
+# name -> (restype, argtypes); mirrors include/fedavg_amd.h
 SIGNATURES = {
     "fedavg_abi_version": (_c_int, []),
     "fedavg_last_error": (ctypes.c_char_p, []),
@@ -32,9 +32,6 @@ SIGNATURES = {
     "fedavg_segments_workspace": (_c_i64, [_c_i64, _c_i64]),
     "fedavg_segments_partials": (_c_i64, [_vp, _c_i64, _c_i64]),
     "fedavg_reduce_segments_f32": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _c_i64, _vp]),
-    "fedavg_reduce_f32_buf": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_int, _c_int, _c_int, _vp]),
-    "fedavg_reduce_segments_f32_variant": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _c_i64,
-                                                    _c_int, _c_int, _c_int, _vp]),
     "fedavg_client_sqdist_segments_f32": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_i64, _vp, _vp, _c_i64, _vp, _vp,
                                                    _vp, _c_i64, _vp]),
     "fedavg_pack_rows_device": (_c_int, [_vp, _c_i64, _vp, _c_i64, _vp, _vp, _c_i64, _vp]),
@@ -49,14 +46,21 @@ SIGNATURES = {
     "fedavg_fpf_update_g": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_float, _c_int, _c_float, _vp]),
     "fedavg_fpf_index_f32": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _vp]),
     "fedavg_fpf_index_lru": (_c_int, [_vp, _vp, _c_i64, _vp, _vp]),
-    "fedavg_fpf_index_workspace": (_c_i64, [_c_i64, _c_i64]),
-    "fedavg_fpf_index_variant": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _c_i64, _c_int, _c_int,
-                                          _c_int, _vp]),
-    "fedavg_probe_cvt16": (_c_int, [_vp, _c_i64, _c_int, _vp, _vp]),
     "fedavg_copy_to_host": (_c_int, [_vp, _vp, _c_i64, _c_int, _vp]),
     "fedavg_upload_shard": (_c_int, [_vp, _c_i64, _vp, _c_i64, _c_i64, _c_i64, _vp]),
     "fedavg_f32_schedule": (_c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp]),
     "fedavg_f32_schedule_ld": (_c_int, [_c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _vp]),
+}
+
+# exported only by libfedavg_amd_probe.so (include/fedavg_amd_tuning.h)
+TUNING_SIGNATURES = {
+    "fedavg_reduce_f32_buf": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _vp]),
+    "fedavg_reduce_segments_f32_variant": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _c_i64,
+                                                    _c_int, _c_int, _c_int, _vp]),
+    "fedavg_fpf_index_workspace": (_c_i64, [_c_i64, _c_i64]),
+    "fedavg_fpf_index_variant": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _c_i64, _c_int, _c_int,
+                                          _c_int, _vp]),
+    "fedavg_probe_cvt16": (_c_int, [_vp, _c_i64, _c_int, _vp, _vp]),
     "fedavg_reduce_f32_tuned": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_int, _c_int, _vp]),
     "fedavg_reduce_f32_variant": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_int, _c_int, _c_int, _c_int,
                                            _c_int, _vp]),
@@ -89,6 +93,7 @@ class FedAvgLibraryError(RuntimeError):
 
 _lock = threading.Lock()
 _lib = None
+_probe = None
 
 
 def library_path() -> Path:
@@ -123,6 +128,30 @@ def load() -> ctypes.CDLL:
     return _lib
 
 
+def load_probe() -> ctypes.CDLL:
+    """The probe library (product entry points + the tuning hooks of
+    include/fedavg_amd_tuning.h).  Scripts and variant tests only; the
+    product path never loads it."""
+    global _probe
+    if _probe is not None:
+        return _probe
+    with _lock:
+        if _probe is not None:
+            return _probe
+        if not PROBE_LIB_PATH.exists():
+            raise FedAvgLibraryError(f"{PROBE_LIB_PATH} not built: run __graft_entry__.build()")
+        lib = ctypes.CDLL(str(PROBE_LIB_PATH))
+        for name, (res, args) in {**SIGNATURES, **TUNING_SIGNATURES}.items():
+            try:
+                fn = getattr(lib, name)
+            except AttributeError as e:
+                raise FedAvgLibraryError(f"{PROBE_LIB_PATH} does not export {name}") from e
+            fn.restype = res
+            fn.argtypes = args
+        _probe = lib
+    return _probe
+
+
 def f32_schedule(K: int, P: int, ld: int = 0) -> dict:
     """The schedule fedavg_reduce_f32 picks for an aligned [K, P] problem
     (P columns of rows with stride ld, when given)."""
@@ -131,10 +160,22 @@ def f32_schedule(K: int, P: int, ld: int = 0) -> dict:
         check(load().fedavg_f32_schedule_ld(K, P, ld, *[ctypes.byref(v) for v in vals]), "fedavg_f32_schedule_ld")
     else:
         check(load().fedavg_f32_schedule(K, P, *[ctypes.byref(v) for v in vals]), "fedavg_f32_schedule")
-    return dict(zip(("unroll", "cols", "nontemporal", "launches"), (v.value for v in vals)))
+    sc = dict(zip(("unroll", "cols", "nontemporal", "launches"), (v.value for v in vals)))
+    # launch_production_f32 (csrc/fedavg_reduce.hip): 16-slice groups go
+    # through per-row buffer descriptors, every other schedule through the
+    # global-pointer variant kernel; 256-thread workgroups
+    sc["kernel"] = "reduce_f32x4_buf_kernel" if sc["cols"] == 16 else "reduce_f32x4_var_kernel"
+    sc["block"] = 256
+    return sc
 
 
-def check(rc: int, what: str) -> None:
+def check(rc: int, what: str, lib: ctypes.CDLL = None) -> None:
+    """Raise on a non-zero status; the message comes from the library that
+    made the call (``lib``; default: the product library, or the probe
+    library when only that one is loaded)."""
     if rc != 0:
-        msg = load().fedavg_last_error().decode(errors="replace")
+        src = lib if lib is not None else (_lib if _lib is not None or _probe is None else _probe)
+        if src is None:
+            src = load()
+        msg = src.fedavg_last_error().decode(errors="replace")
         raise FedAvgLibraryError(f"{what} failed (rc={rc}): {msg}")

@@ -43,6 +43,50 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef double f64x2 __attribute__((ext_vector_type(2)));
 typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
 
+// Packed 16-bit element rules (fp16 / bf16), shared by the reduce
+// (fedavg_reduce.hip) and the distance pass (fedavg_dist.hip): two elements
+// per 32-bit word, fp32 math on the pair, gfx950's two-at-a-time RNE
+// conversions (v_cvt_pk_f16_f32 / v_cvt_pk_bf16_f32).  opaque2 keeps the
+// compiler from fusing fpext -> op -> fptrunc into one mixed-precision op
+// (which would round once instead of fp32-then-16-bit, as ATen does).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x2 opaque2(f32x2 v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
+struct BF16Pk {
+  __device__ static f32x2 unpack(unsigned int u) {
+    return f32x2{__uint_as_float(u << 16), __uint_as_float(u & 0xFFFF0000u)};
+  }
+  __device__ static unsigned int pack(f32x2 f) {
+    const bf16x2 b = __builtin_convertvector(f, bf16x2);
+    unsigned int u;
+    __builtin_memcpy(&u, &b, 4);
+    return u;
+  }
+  __device__ static unsigned short canon(unsigned short h) { return (h & 0x7FFFu) > 0x7F80u ? 0x7FC0u : h; }
+};
+
+struct F16Pk {
+  __device__ static f32x2 unpack(unsigned int u) {
+    f16x2 h;
+    __builtin_memcpy(&h, &u, 4);
+    return __builtin_convertvector(h, f32x2);
+  }
+  __device__ static unsigned int pack(f32x2 f) {
+    const f16x2 h = __builtin_convertvector(f, f16x2);
+    unsigned int u;
+    __builtin_memcpy(&u, &h, 4);
+    return u;
+  }
+  __device__ static unsigned short canon(unsigned short h) { return h; }  // NaN payloads are not specified
+};
+
 // Error state (thread-local message), defined in fedavg_reduce.hip.
 int set_error(int code, const char* fmt, ...);
 int launch_status(const char* what);
@@ -275,7 +319,7 @@ void launch_f32x4(const float* clients, int K, int64_t ld, int64_t P, const floa
 // per (device, kernel) -- kernels of one signature share a template
 // instantiation of this function, so the cache must be keyed by the kernel.
 template <typename Kern>
-int64_t resident_blocks(Kern kernel) {
+int64_t resident_blocks(Kern kernel, int block = kBlock) {
   static std::mutex mu;
   static std::map<std::pair<int, const void*>, int64_t> cache;
   int dev = 0;
@@ -287,7 +331,7 @@ int64_t resident_blocks(Kern kernel) {
     if (it != cache.end()) return it->second;
   }
   int per_cu = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, 0) != hipSuccess || per_cu <= 0) per_cu = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, 0) != hipSuccess || per_cu <= 0) per_cu = 1;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
   const int64_t n = static_cast<int64_t>(per_cu) * cus;
   std::lock_guard<std::mutex> lk(mu);
@@ -353,15 +397,15 @@ __device__ __forceinline__ f32x4 ld_rsrc_nt(__amdgpu_buffer_rsrc_t r, uint32_t b
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(byte_off), 0, 2));
 }
 
-template <int U, int C>
-__global__ __launch_bounds__(kBlock) void reduce_f32x4_buf_kernel(const f32x4* __restrict__ X, int K, int64_t ld4,
-                                                                  int64_t nvec, int tail, const float* __restrict__ W,
-                                                                  float* __restrict__ out) {
-  constexpr int64_t span = static_cast<int64_t>(kBlock) * C;  // float4 columns per group
+template <int U, int C, int BS = kBlock>
+__global__ __launch_bounds__(BS) void reduce_f32x4_buf_kernel(const f32x4* __restrict__ X, int K, int64_t ld4,
+                                                              int64_t nvec, int tail, const float* __restrict__ W,
+                                                              float* __restrict__ out) {
+  constexpr int64_t span = static_cast<int64_t>(BS) * C;  // float4 columns per group
   constexpr int bytes = static_cast<int>(span * 16);
   uint32_t off[C];
 #pragma unroll
-  for (int j = 0; j < C; ++j) off[j] = 16u * (threadIdx.x + j * kBlock);
+  for (int j = 0; j < C; ++j) off[j] = 16u * (threadIdx.x + j * BS);
   for (int64_t base = static_cast<int64_t>(blockIdx.x) * span; base < nvec;
        base += static_cast<int64_t>(gridDim.x) * span) {
     if (base + span <= nvec) {
@@ -394,10 +438,10 @@ __global__ __launch_bounds__(kBlock) void reduce_f32x4_buf_kernel(const f32x4* _
         }
       }
 #pragma unroll
-      for (int j = 0; j < C; ++j) store_slice(out, base + threadIdx.x + j * kBlock, nvec, tail, acc[j]);
+      for (int j = 0; j < C; ++j) store_slice(out, base + threadIdx.x + j * BS, nvec, tail, acc[j]);
     } else {
       for (int j = 0; j < C; ++j) {
-        const int64_t v = base + threadIdx.x + j * kBlock;
+        const int64_t v = base + threadIdx.x + j * BS;
         if (v >= nvec) break;
         f32x4 acc[1];
         reduce_full_group<U, 1, true, false>(acc, X + v, K, ld4, W);
@@ -407,13 +451,16 @@ __global__ __launch_bounds__(kBlock) void reduce_f32x4_buf_kernel(const f32x4* _
   }
 }
 
-// launch_split's round-split schedule with the buffer-descriptor kernel
-template <int U, int C>
+// launch_split's round-split schedule with the buffer-descriptor kernel, in
+// blocks of BS threads (BS = 64: one wave per workgroup, for short rows whose
+// 256-thread groups would leave the CUs unevenly loaded)
+template <int U, int C, int BS = kBlock>
 void launch_split_buf(const float* clients, int K, int64_t ld, int64_t P, const float* W, float* out, int max_blocks,
                       hipStream_t s) {
   const int64_t nvec = (P + 3) / 4;
-  const int64_t span = static_cast<int64_t>(kBlock) * C;
-  const int64_t resident = max_blocks > 0 ? max_blocks : resident_blocks(reduce_f32x4_buf_kernel<U, C>);
+  const int64_t span = static_cast<int64_t>(BS) * C;
+  const int64_t resident =
+      max_blocks > 0 ? max_blocks : resident_blocks(reduce_f32x4_buf_kernel<U, C, BS>, BS);
   const int64_t blocks = (nvec + span - 1) / span;
   const int64_t nl = (blocks + resident - 1) / resident;
   const int64_t per = ((nvec + nl - 1) / nl + span - 1) / span * span;
@@ -421,8 +468,8 @@ void launch_split_buf(const float* clients, int K, int64_t ld, int64_t P, const 
   for (int64_t v0 = 0; v0 < nvec; v0 += per) {
     const int64_t n = (nvec - v0) < per ? (nvec - v0) : per;
     const int tail = (v0 + n == nvec) ? static_cast<int>(P & 3) : 0;
-    hipLaunchKernelGGL((reduce_f32x4_buf_kernel<U, C>), dim3(static_cast<unsigned>((n + span - 1) / span)),
-                       dim3(kBlock), 0, s, X + v0, K, ld / 4, n, tail, W, out + v0 * 4);
+    hipLaunchKernelGGL((reduce_f32x4_buf_kernel<U, C, BS>), dim3(static_cast<unsigned>((n + span - 1) / span)),
+                       dim3(BS), 0, s, X + v0, K, ld / 4, n, tail, W, out + v0 * 4);
   }
 }
 

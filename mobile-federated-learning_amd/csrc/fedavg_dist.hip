@@ -197,24 +197,8 @@ void launch_sqdist(const float* clients, int K, int64_t ld, int64_t P, const flo
   }
 }
 
-}  // namespace
-
-extern "C" {
-
-int64_t fedavg_client_sqdist_workspace(int64_t K, int64_t P) {
-  if (K <= 0 || P <= 0) return 0;
-  return K * sqdist_waves_for(P, 4);  // enough for every variant (cols = 4 has the most waves)
-}
-
-int fedavg_client_sqdist_f32(const float* clients, int64_t K, int64_t P, int64_t ld, const float* glob,
-                             double* workspace, int64_t workspace_elems, double* sumsq, void* stream) {
-  return fedavg_client_sqdist_variant(clients, K, P, ld, glob, workspace, workspace_elems, sumsq, kDistRows,
-                                      kDistCols, kDistBlocksPerLaunch, stream);
-}
-
-int fedavg_client_sqdist_variant(const float* clients, int64_t K, int64_t P, int64_t ld, const float* glob,
-                                 double* workspace, int64_t workspace_elems, double* sumsq, int unroll, int cols,
-                                 int max_blocks, void* stream) {
+int sqdist_impl(const float* clients, int64_t K, int64_t P, int64_t ld, const float* glob, double* workspace,
+                int64_t workspace_elems, double* sumsq, int unroll, int cols, int max_blocks, void* stream) {
   const char* what = "fedavg_client_sqdist_f32";
   int rc = check_common(clients, K, P, ld, glob, sumsq, what);
   if (rc) return rc;
@@ -241,6 +225,30 @@ int fedavg_client_sqdist_variant(const float* clients, int64_t K, int64_t P, int
   return launch_status(what);
 }
 
+}  // namespace
+
+extern "C" {
+
+int64_t fedavg_client_sqdist_workspace(int64_t K, int64_t P) {
+  if (K <= 0 || P <= 0) return 0;
+  return K * sqdist_waves_for(P, 4);  // enough for every variant (cols = 4 has the most waves)
+}
+
+int fedavg_client_sqdist_f32(const float* clients, int64_t K, int64_t P, int64_t ld, const float* glob,
+                             double* workspace, int64_t workspace_elems, double* sumsq, void* stream) {
+  return sqdist_impl(clients, K, P, ld, glob, workspace, workspace_elems, sumsq, kDistRows, kDistCols,
+                     kDistBlocksPerLaunch, stream);
+}
+
+#ifdef FEDAVG_TUNING  // probe library only (libfedavg_amd_probe.so)
+int fedavg_client_sqdist_variant(const float* clients, int64_t K, int64_t P, int64_t ld, const float* glob,
+                                 double* workspace, int64_t workspace_elems, double* sumsq, int unroll, int cols,
+                                 int max_blocks, void* stream) {
+  return sqdist_impl(clients, K, P, ld, glob, workspace, workspace_elems, sumsq, unroll, cols, max_blocks, stream);
+}
+#endif  // FEDAVG_TUNING
+
+#ifdef FEDAVG_TUNING  // probe library only (libfedavg_amd_probe.so)
 int fedavg_client_sqdist_buf(const float* clients, int64_t K, int64_t P, int64_t ld, const float* glob,
                              double* workspace, int64_t workspace_elems, double* sumsq, int unroll, int cols,
                              int max_blocks, void* stream) {
@@ -270,5 +278,6 @@ int fedavg_client_sqdist_buf(const float* clients, int64_t K, int64_t P, int64_t
                      nwaves, sumsq);
   return launch_status(what);
 }
+#endif  // FEDAVG_TUNING
 
 }  // extern "C"

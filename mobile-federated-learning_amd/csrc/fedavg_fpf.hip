@@ -184,6 +184,7 @@ __global__ __launch_bounds__(kBlock) void fpf_index_kernel(const f32x4* __restri
   }
 }
 
+#ifdef FEDAVG_TUNING  // the column-window index variant (measurement only)
 // :272 as a column-window pass (the reduce's access pattern).  Block
 // (bx, by) covers C*256 column slices of rows [by*R, (by+1)*R) and walks
 // those rows U at a time, so the blocks of a row group read one compact window
@@ -267,6 +268,8 @@ void launch_index_windows(const float* diffs, int64_t n_rows, int64_t ld, int64_
   hipLaunchKernelGGL(fpf_index_finalize_kernel, dim3(static_cast<unsigned>((n_rows + kBlock - 1) / kBlock)),
                      dim3(kBlock), 0, s, ws, nwc, n_rows, g_mat, fpf);
 }
+
+#endif  // FEDAVG_TUNING
 
 // :274, :276-278  fpf = LRU_itr_lst / G_mat, NaN/inf -> 0.
 __global__ __launch_bounds__(kBlock) void fpf_index_lru_kernel(const float* __restrict__ lru,
@@ -374,11 +377,14 @@ int fedavg_fpf_index_f32(const float* diffs, int64_t n_rows, int64_t ld, int64_t
   return launch_status(what);
 }
 
+#ifdef FEDAVG_TUNING  // probe library only (libfedavg_amd_probe.so)
 int64_t fedavg_fpf_index_workspace(int64_t n_rows, int64_t P) {
   if (n_rows <= 0 || P <= 0) return 0;
   return n_rows * index_col_blocks(P, 1) * (kBlock / 64);  // enough for every column width
 }
+#endif  // FEDAVG_TUNING
 
+#ifdef FEDAVG_TUNING  // probe library only (libfedavg_amd_probe.so)
 int fedavg_fpf_index_variant(const float* diffs, int64_t n_rows, int64_t ld, int64_t P, const float* a_mat,
                              const float* g_mat, float* fpf, double* workspace, int64_t workspace_elems, int unroll,
                              int cols, int row_groups, void* stream) {
@@ -405,6 +411,7 @@ int fedavg_fpf_index_variant(const float* diffs, int64_t n_rows, int64_t ld, int
   }
   return launch_status(what);
 }
+#endif  // FEDAVG_TUNING
 
 int fedavg_fpf_index_lru(const float* lru_itr, const float* g_mat, int64_t n_rows, float* fpf, void* stream) {
   const char* what = "fedavg_fpf_index_lru";

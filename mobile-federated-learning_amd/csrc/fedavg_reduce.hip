@@ -216,44 +216,6 @@ struct OpF64 {
 // via fedavg_probe_cvt16); NaN is absorbing through the remaining mul/add
 // steps, so canonicalising NaN to c10's 0x7FC0 once at the store (bf16) gives
 // c10's bits for the whole reduction.
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ f32x2 opaque2(f32x2 v) {
-  asm volatile("" : "+v"(v));
-  return v;
-}
-
-struct BF16Pk {
-  __device__ static f32x2 unpack(unsigned int u) {
-    return f32x2{__uint_as_float(u << 16), __uint_as_float(u & 0xFFFF0000u)};
-  }
-  __device__ static unsigned int pack(f32x2 f) {
-    const bf16x2 b = __builtin_convertvector(f, bf16x2);
-    unsigned int u;
-    __builtin_memcpy(&u, &b, 4);
-    return u;
-  }
-  __device__ static unsigned short canon(unsigned short h) { return (h & 0x7FFFu) > 0x7F80u ? 0x7FC0u : h; }
-};
-
-struct F16Pk {
-  __device__ static f32x2 unpack(unsigned int u) {
-    f16x2 h;
-    __builtin_memcpy(&h, &u, 4);
-    return __builtin_convertvector(h, f32x2);
-  }
-  __device__ static unsigned int pack(f32x2 f) {
-    const f16x2 h = __builtin_convertvector(f, f16x2);
-    unsigned int u;
-    __builtin_memcpy(&u, &h, 4);
-    return u;
-  }
-  __device__ static unsigned short canon(unsigned short h) { return h; }  // NaN payloads are not specified
-};
-
 template <typename R>
 struct OpHalfPk {
   using vec = u16x8;
@@ -773,6 +735,7 @@ void launch_vec_nt(const Schedule& sc, const void* clients, int K, int64_t ld, i
   }
 }
 
+#ifdef FEDAVG_TUNING
 // Conversion probe (tests only): out[i] = the 16-bit rounding of the fp32
 // bit pattern in[i] by mode 0 = BF16Pk (hardware), 1 = c10 integer RNE,
 // 2 = F16Pk (hardware, packed), 3 = F16Rule (scalar v_cvt_f16_f32).
@@ -791,6 +754,8 @@ __global__ __launch_bounds__(kBlock) void probe_cvt16_kernel(const unsigned int*
   }
   out[i] = h;
 }
+
+#endif  // FEDAVG_TUNING
 
 // elem_bytes: 8 (fp64) or 2 (fp16/bf16).  The fp32 schedule is chosen for the
 // problem with the same 16-B slice count and byte footprint.
@@ -847,6 +812,7 @@ extern "C" {
 
 int fedavg_abi_version(void) { return 1; }
 
+#ifdef FEDAVG_TUNING  // probe library only (libfedavg_amd_probe.so)
 int fedavg_probe_cvt16(const uint32_t* in, int64_t n, int mode, uint16_t* out, void* stream) {
   if (n < 0 || !in || !out || mode < 0 || mode > 3)
     return set_error(FEDAVG_EINVAL, "fedavg_probe_cvt16: bad arguments");
@@ -855,6 +821,7 @@ int fedavg_probe_cvt16(const uint32_t* in, int64_t n, int mode, uint16_t* out, v
                      static_cast<hipStream_t>(stream), in, n, mode, out);
   return launch_status("fedavg_probe_cvt16");
 }
+#endif  // FEDAVG_TUNING
 
 const char* fedavg_last_error(void) { return last_error_message(); }
 
@@ -976,6 +943,7 @@ int fedavg_reduce_bf16(const uint16_t* clients, int64_t K, int64_t P, int64_t ld
   return reduce_half_entry(true, clients, K, P, ld, weights, out, stream, "fedavg_reduce_bf16");
 }
 
+#ifdef FEDAVG_TUNING  // probe library only (libfedavg_amd_probe.so)
 int fedavg_reduce_vec_buf(int dtype, const void* clients, int64_t K, int64_t P, int64_t ld, const void* weights,
                           void* out, int unroll, int cols, int max_blocks, void* stream) {
   const char* what = "fedavg_reduce_vec_buf";
@@ -999,7 +967,9 @@ int fedavg_reduce_vec_buf(int dtype, const void* clients, int64_t K, int64_t P, 
   if (!ok) return set_error(FEDAVG_EMODE, "%s: unsupported unroll=%d cols=%d", what, unroll, cols);
   return launch_status(what);
 }
+#endif  // FEDAVG_TUNING
 
+#ifdef FEDAVG_TUNING  // probe library only (libfedavg_amd_probe.so)
 int fedavg_reduce_half_variant(int bf16, const uint16_t* clients, int64_t K, int64_t P, int64_t ld,
                                const float* weights, uint16_t* out, int unroll, int cols, int max_blocks,
                                void* stream) {
@@ -1018,7 +988,9 @@ int fedavg_reduce_half_variant(int bf16, const uint16_t* clients, int64_t K, int
   if (!ok) return set_error(FEDAVG_EMODE, "%s: unsupported unroll=%d cols=%d", what, unroll, cols);
   return launch_status(what);
 }
+#endif  // FEDAVG_TUNING
 
+#ifdef FEDAVG_TUNING  // probe library only (libfedavg_amd_probe.so)
 int fedavg_half_schedule(int64_t K, int64_t P, int* unroll, int* cols, int* nontemporal, int* launches) {
   if (K <= 0 || P < 0) return set_error(FEDAVG_EINVAL, "fedavg_half_schedule: bad sizes");
   const Schedule sc = choose_schedule(K, P * 2 / 4);  // the fp32 problem with the same bytes per row
@@ -1032,6 +1004,7 @@ int fedavg_half_schedule(int64_t K, int64_t P, int* unroll, int* cols, int* nont
   if (launches) *launches = static_cast<int>((blocks + sc.blocks_per_launch - 1) / sc.blocks_per_launch);
   return FEDAVG_OK;
 }
+#endif  // FEDAVG_TUNING
 
 int fedavg_reduce_splitk_f32(const float* clients, int64_t K, int64_t P, int64_t ld, const float* weights,
                              float* out, int splits, void* stream) {

@@ -447,6 +447,7 @@ int fedavg_client_sqdist_segments_f32(const int64_t* client_ptrs, const int64_t*
 
 // tuning hook (fedavg_amd_tuning.h): the zero-copy reduce with an explicit
 // (U, C) schedule -- units of 1,024 x C columns -- and launch size; same bits
+#ifdef FEDAVG_TUNING  // probe library only (libfedavg_amd_probe.so)
 int fedavg_reduce_segments_f32_variant(const int64_t* client_ptrs, const int64_t* key_numel, const int64_t* key_offset,
                                        const int64_t* key_kind, int64_t n_keys, int64_t K, const float* weights,
                                        float* out, void* host_ws, void* dev_ws, int64_t ws_bytes, int unroll, int cols,
@@ -479,5 +480,6 @@ int fedavg_reduce_segments_f32_variant(const int64_t* client_ptrs, const int64_t
   }
   return launch_status(what);
 }
+#endif  // FEDAVG_TUNING
 
 }  // extern "C"

@@ -564,7 +564,7 @@ int fedavg_reduce_f32_xcd(const float* clients, int64_t K, int64_t P, int64_t ld
 }
 
 int fedavg_reduce_f32_buf(const float* clients, int64_t K, int64_t P, int64_t ld, const float* weights, float* out,
-                          int unroll, int cols, int max_blocks, void* stream) {
+                          int unroll, int cols, int block, int max_blocks, void* stream) {
   const char* what = "fedavg_reduce_f32_buf";
   if (K <= 0 || P <= 0 || ld < P || !clients || !weights || !out || K > INT32_MAX)
     return set_error(FEDAVG_EINVAL, "%s: bad arguments", what);
@@ -572,17 +572,44 @@ int fedavg_reduce_f32_buf(const float* clients, int64_t K, int64_t P, int64_t ld
     return set_error(FEDAVG_EALIGN, "%s: needs 16-B aligned clients/out and ld %% 4 == 0", what);
   const int k = static_cast<int>(K);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  switch (unroll * 100 + cols) {
-    case 408: launch_split_buf<4, 8>(clients, k, ld, P, weights, out, max_blocks, s); break;
-    case 804: launch_split_buf<8, 4>(clients, k, ld, P, weights, out, max_blocks, s); break;
-    case 404: launch_split_buf<4, 4>(clients, k, ld, P, weights, out, max_blocks, s); break;
-    case 208: launch_split_buf<2, 8>(clients, k, ld, P, weights, out, max_blocks, s); break;
-    case 216: launch_split_buf<2, 16>(clients, k, ld, P, weights, out, max_blocks, s); break;
-    case 116: launch_split_buf<1, 16>(clients, k, ld, P, weights, out, max_blocks, s); break;
-    case 808: launch_split_buf<8, 8>(clients, k, ld, P, weights, out, max_blocks, s); break;
-    case 416: launch_split_buf<4, 16>(clients, k, ld, P, weights, out, max_blocks, s); break;
-    default: return set_error(FEDAVG_EMODE, "%s: unsupported unroll=%d cols=%d", what, unroll, cols);
+#define FEDAVG_BUF_CASE(U, C, B) \
+  case (B) * 10000 + (U) * 100 + (C): launch_split_buf<U, C, B>(clients, k, ld, P, weights, out, max_blocks, s); break;
+  switch (block * 10000 + unroll * 100 + cols) {
+    FEDAVG_BUF_CASE(4, 8, 256)
+    FEDAVG_BUF_CASE(8, 4, 256)
+    FEDAVG_BUF_CASE(4, 4, 256)
+    FEDAVG_BUF_CASE(2, 8, 256)
+    FEDAVG_BUF_CASE(2, 16, 256)
+    FEDAVG_BUF_CASE(1, 16, 256)
+    FEDAVG_BUF_CASE(8, 8, 256)
+    FEDAVG_BUF_CASE(4, 16, 256)
+    FEDAVG_BUF_CASE(16, 1, 256)
+    FEDAVG_BUF_CASE(16, 2, 256)
+    FEDAVG_BUF_CASE(16, 4, 256)
+    FEDAVG_BUF_CASE(8, 2, 256)
+    FEDAVG_BUF_CASE(8, 1, 256)
+    FEDAVG_BUF_CASE(8, 1, 128)
+    FEDAVG_BUF_CASE(8, 2, 128)
+    FEDAVG_BUF_CASE(8, 4, 128)
+    FEDAVG_BUF_CASE(16, 1, 128)
+    FEDAVG_BUF_CASE(16, 2, 128)
+    FEDAVG_BUF_CASE(16, 4, 128)
+    FEDAVG_BUF_CASE(4, 4, 128)
+    FEDAVG_BUF_CASE(4, 8, 128)
+    FEDAVG_BUF_CASE(8, 1, 64)
+    FEDAVG_BUF_CASE(8, 2, 64)
+    FEDAVG_BUF_CASE(8, 4, 64)
+    FEDAVG_BUF_CASE(16, 1, 64)
+    FEDAVG_BUF_CASE(16, 2, 64)
+    FEDAVG_BUF_CASE(16, 4, 64)
+    FEDAVG_BUF_CASE(4, 4, 64)
+    FEDAVG_BUF_CASE(4, 8, 64)
+    FEDAVG_BUF_CASE(32, 1, 64)
+    FEDAVG_BUF_CASE(32, 2, 64)
+    default:
+      return set_error(FEDAVG_EMODE, "%s: unsupported unroll=%d cols=%d block=%d", what, unroll, cols, block);
   }
+#undef FEDAVG_BUF_CASE
   return launch_status(what);
 }
 

@@ -137,6 +137,10 @@ class ShardedReducer:
     ``local_reduce`` is injectable so the sharding/gather logic can be tested
     with the ``gloo`` backend on CPU; the product default is the HIP kernel.
 
+    ``gather``: None (default) all-gathers when the group has more than one
+    rank; True forces the collective even at world size 1 (so the RCCL
+    exchange runs, and is tested, on a single GPU); False never gathers.
+
     ``host_out`` (SURVEY §8e's alternative for a host consumer): a pinned
     host tensor of >= P elements -- e.g. one mapping shared by all ranks of
     the node.  Each rank then copies its finished chunks straight to their
@@ -147,7 +151,7 @@ class ShardedReducer:
 
     def __init__(self, K: int, P: int, *, chunks: int = 1, group=None, device=None,
                  dtype: torch.dtype = torch.float32, local_reduce: Optional[LocalReduce] = None,
-                 gather: bool = True, host_out: Optional[torch.Tensor] = None):
+                 gather: Optional[bool] = None, host_out: Optional[torch.Tensor] = None):
         self.group = group
         ws = dist.get_world_size(group) if dist.is_initialized() else 1
         rank = dist.get_rank(group) if dist.is_initialized() else 0
@@ -163,7 +167,11 @@ class ShardedReducer:
             if self.device.type == "cuda" and not host_out.is_pinned():
                 raise ValueError("host_out must be pinned (async D2H)")
             gather = False
-        self.gather = gather and ws > 1
+        if gather and not dist.is_initialized():
+            raise ValueError("gather=True needs an initialised process group")
+        # None: gather whenever there is more than one rank.  True forces the
+        # collective at world size 1 too (the RCCL path under test on one GPU).
+        self.gather = (ws > 1) if gather is None else bool(gather)
         self._copy_stream = (torch.cuda.Stream(self.device)
                              if host_out is not None and self.device.type == "cuda" else None)
         # per chunk: (local start, global start, n) of its valid columns

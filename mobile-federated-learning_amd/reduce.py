@@ -71,7 +71,8 @@ def reduce_packed(
               (tolerance-gated, not bit-exact).
     tuned   : benchmarking hook for the fp32 kernel: (unroll, nontemporal) or
               (unroll, nontemporal, cols, pipelined, max_blocks), see
-              include/fedavg_amd_tuning.h.  Every variant gives the same bits.
+              include/fedavg_amd_tuning.h (probe library).  Every variant gives
+              the same bits.
     """
     _check_device_tensor(clients, "clients")
     _check_device_tensor(weights, "weights")
@@ -107,16 +108,17 @@ def reduce_packed(
     elif tuned is not None:
         if dtype != torch.float32:
             raise TypeError("tuned variants are fp32 only")
+        lib = _lib.load_probe()  # tuning hooks live in the probe library only
         if len(tuned) == 2:
             unroll, nt = tuned
             rc = lib.fedavg_reduce_f32_tuned(clients.data_ptr(), K, P, ld, weights.data_ptr(), out.data_ptr(),
                                              int(unroll), int(nt), s)
-            _lib.check(rc, "fedavg_reduce_f32_tuned")
+            _lib.check(rc, "fedavg_reduce_f32_tuned", lib)
         else:
             unroll, nt, cols, pipe, max_blocks = tuned
             rc = lib.fedavg_reduce_f32_variant(clients.data_ptr(), K, P, ld, weights.data_ptr(), out.data_ptr(),
                                                int(unroll), int(nt), int(cols), int(pipe), int(max_blocks), s)
-            _lib.check(rc, "fedavg_reduce_f32_variant")
+            _lib.check(rc, "fedavg_reduce_f32_variant", lib)
     else:
         fn = getattr(lib, _ENTRY[dtype])
         rc = fn(clients.data_ptr(), K, P, ld, weights.data_ptr(), out.data_ptr(), s)

@@ -33,46 +33,7 @@ import numpy as np
 import torch
 
 import mfl_amd
-
-
-def resnet56_shapes(num_classes=10):
-    """FedML resnet56 (Bottleneck, [6, 6, 6]) state_dict: 350 keys, 600,372 elements."""
-    shapes = []
-
-    def bn(prefix, c):
-        shapes.extend([(f"{prefix}.weight", (c,)), (f"{prefix}.bias", (c,)), (f"{prefix}.running_mean", (c,)),
-                       (f"{prefix}.running_var", (c,)), (f"{prefix}.num_batches_tracked", ())])
-
-    shapes.append(("conv1.weight", (16, 3, 3, 3)))
-    bn("bn1", 16)
-    inplanes = 16
-    for li, (planes, stride) in enumerate([(16, 1), (32, 2), (64, 2)], 1):
-        for b in range(6):
-            p = f"layer{li}.{b}"
-            shapes.append((f"{p}.conv1.weight", (planes, inplanes, 1, 1)))
-            bn(f"{p}.bn1", planes)
-            shapes.append((f"{p}.conv2.weight", (planes, planes, 3, 3)))
-            bn(f"{p}.bn2", planes)
-            shapes.append((f"{p}.conv3.weight", (planes * 4, planes, 1, 1)))
-            bn(f"{p}.bn3", planes * 4)
-            if b == 0 and (stride != 1 or inplanes != planes * 4):
-                shapes.append((f"{p}.downsample.0.weight", (planes * 4, inplanes, 1, 1)))
-                bn(f"{p}.downsample.1", planes * 4)
-            inplanes = planes * 4
-    shapes.append(("fc.weight", (num_classes, 256)))
-    shapes.append(("fc.bias", (num_classes,)))
-    return shapes
-
-
-CONFIGS = {
-    "mnist_lr": (10, [("linear.weight", (10, 784)), ("linear.bias", (10,))]),
-    "femnist_cnn": (10, [("conv2d_1.weight", (32, 1, 3, 3)), ("conv2d_1.bias", (32,)),
-                         ("conv2d_2.weight", (64, 32, 3, 3)), ("conv2d_2.bias", (64,)),
-                         ("linear_1.weight", (128, 9216)), ("linear_1.bias", (128,)),
-                         ("linear_2.weight", (62, 128)), ("linear_2.bias", (62,))]),
-    "resnet56": (100, resnet56_shapes()),
-    "target_flat": (100, [("w", (25_000_000,))]),
-}
+from model_shapes import CONFIGS, resnet56_shapes  # noqa: F401
 
 
 def make_clients(K, shapes, seed=0):

@@ -31,7 +31,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=6)
     ap.add_argument("--buf", nargs="*", default=["4,8,0", "4,8,768", "8,4,0", "4,4,0", "2,8,0", "2,16,0", "1,16,0",
-                                                 "8,8,0"], help="U,C,max_blocks of fedavg_reduce_f32_buf")
+                                                 "8,8,0"], help="U,C,max_blocks[,block] of fedavg_reduce_f32_buf (block: 256 default, 128, 64)")
     ap.add_argument("--glob", nargs="*", default=[], help="U,C,max_blocks of the global-pointer variant kernel")
     ap.add_argument("--nt", nargs="*", default=[], help="U,C,max_blocks,nt of the global-pointer variant kernel")
     ap.add_argument("--chunks", type=int, default=1,
@@ -40,7 +40,7 @@ def main():
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    lib = mfl_amd._lib.load()
+    lib = mfl_amd._lib.load_probe()
     K, P = args.K, args.P
     C = max(1, args.chunks)
     if C > 1:
@@ -53,8 +53,10 @@ def main():
     stream = torch.cuda.current_stream(dev).cuda_stream
     ap_sched = [tuple(int(t) for t in v.split(",")) for v in args.buf]
     variants = {"production": None}
-    for u, c, b in ap_sched:
-        variants[f"buf-U{u}C{c}b{b}"] = (u, c, b)
+    for sch in ap_sched:
+        u, c, b = sch[:3]
+        bs = sch[3] if len(sch) > 3 else 256
+        variants[f"buf-U{u}C{c}b{b}" + (f"B{bs}" if bs != 256 else "")] = (u, c, b, bs)
     for u, c, b in [tuple(int(t) for t in v.split(",")) for v in args.glob]:
         variants[f"global-U{u}C{c}b{b}"] = ("var", u, c, b)
     for u, c, b, nt in [tuple(int(t) for t in v.split(",")) for v in args.nt]:
@@ -73,7 +75,7 @@ def main():
             mfl_amd.reduce_packed(x, w, P, outs[n], tuned=(v[1], v[4] if len(v) > 4 else 1, v[2], 4, v[3]))
             return
         mfl_amd._lib.check(lib.fedavg_reduce_f32_buf(x.data_ptr(), K, P, ld, w.data_ptr(), outs[n].data_ptr(),
-                                                     v[0], v[1], v[2], stream), n)
+                                                     v[0], v[1], v[3], v[2], stream), n, lib)
 
     for n in variants:
         run(n, check=True)

@@ -32,7 +32,7 @@ def main():
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    lib = mfl_amd._lib.load()
+    lib = mfl_amd._lib.load_probe()
     n, P = args.n, args.P
     ld = (P + 63) // 64 * 64
     g = torch.Generator(device=dev).manual_seed(0)

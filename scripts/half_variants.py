@@ -34,7 +34,7 @@ def main():
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    lib = mfl_amd._lib.load()
+    lib = mfl_amd._lib.load_probe()
     K, P = args.K, args.P
     dt = torch.bfloat16 if args.dtype == "bf16" else torch.float16
     ld = (P + 63) // 64 * 64

@@ -37,7 +37,7 @@ def main():
     K, P = args.K, args.P
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    lib = _lib.load()
+    lib = _lib.load_probe()
     ld = (P + 63) // 64 * 64
     g = torch.Generator(device=dev).manual_seed(0)
     x = torch.randn((K, ld), generator=g, device=dev) * 0.05

@@ -49,7 +49,7 @@ def main():
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    lib = mfl_amd._lib.load()
+    lib = mfl_amd._lib.load_probe()
     K = args.K
     cols = (args.cols + 511) // 512 * 512
     x = torch.empty((K, cols), device=dev)

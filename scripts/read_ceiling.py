@@ -34,7 +34,7 @@ def main():
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    lib = mfl_amd._lib.load()
+    lib = mfl_amd._lib.load_probe()
     K, P = args.K, args.P
     ld = (P + 63) // 64 * 64
     x = torch.empty((K, ld), device=dev)

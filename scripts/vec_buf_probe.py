@@ -35,7 +35,7 @@ def main():
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    lib = mfl_amd._lib.load()
+    lib = mfl_amd._lib.load_probe()
     stream = torch.cuda.current_stream(dev).cuda_stream
     K, P = args.K, args.P
     for name in args.dtypes:

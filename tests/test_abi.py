@@ -16,9 +16,9 @@ from mfl_amd import _lib, build
 INCLUDE = Path(__file__).resolve().parents[1] / "include"
 
 
-def declared_functions():
+def declared_functions(headers=("fedavg_amd.h", "fedavg_amd_tuning.h")):
     names = []
-    for h in sorted(INCLUDE.glob("*.h")):
+    for h in [INCLUDE / n for n in headers]:
         text = re.sub(r"/\*.*?\*/", "", h.read_text(), flags=re.S)
         names += re.findall(r"^\s*(?:const\s+)?\w+\**\s+\**(fedavg_\w+)\s*\(", text, flags=re.M)
     return sorted(set(names))
@@ -34,26 +34,40 @@ def test_header_parse_finds_entry_points():
     names = declared_functions()
     for required in ("fedavg_reduce_f32", "fedavg_reduce_ptrs_f32", "fedavg_reduce_f64", "fedavg_reduce_f16",
                      "fedavg_reduce_bf16", "fedavg_reduce_splitk_f32", "fedavg_last_error", "fedavg_weights_f32",
-                     "fedavg_abi_version", "fedavg_reduce_f32_tuned"):
+                     "fedavg_abi_version", "fedavg_reduce_f32_tuned", "fedavg_f32_schedule_ld"):
         assert required in names
+
+
+def _exported(path):
+    import subprocess
+    nm = subprocess.run(["nm", "-D", "--defined-only", str(path)], capture_output=True, text=True, check=True).stdout
+    return sorted({ln.split()[-1] for ln in nm.splitlines() if ln.split() and ln.split()[-1].startswith("fedavg_")})
 
 
 def test_library_exports_every_declared_symbol(lib):
     raw = ctypes.CDLL(str(_lib.library_path()))
-    for name in declared_functions():
+    for name in declared_functions(("fedavg_amd.h",)):
         assert hasattr(raw, name), name
         assert name in _lib.SIGNATURES, f"{name} declared but not typed in _lib.SIGNATURES"
 
 
 def test_every_exported_entry_point_is_declared(lib):
-    """The reverse direction: no fedavg_* symbol of the .so is missing from
-    include/*.h (the C ABI is exactly what the headers declare)."""
-    import subprocess
-    nm = subprocess.run(["nm", "-D", "--defined-only", str(_lib.library_path())], capture_output=True, text=True,
-                        check=True).stdout
-    exported = sorted({ln.split()[-1] for ln in nm.splitlines() if ln.split() and ln.split()[-1].startswith("fedavg_")})
-    declared = set(declared_functions())
-    assert exported and [n for n in exported if n not in declared] == []
+    """The reverse direction: the product .so exports exactly what
+    include/fedavg_amd.h declares -- no tuning hook leaks into it."""
+    exported = _exported(_lib.library_path())
+    assert exported == declared_functions(("fedavg_amd.h",))
+
+
+def test_probe_library_exports_product_and_tuning_hooks(lib):
+    """libfedavg_amd_probe.so = the product entry points + every hook of
+    include/fedavg_amd_tuning.h, each typed in _lib.TUNING_SIGNATURES."""
+    probe = _lib.load_probe()
+    assert probe is not lib
+    exported = _exported(_lib.PROBE_LIB_PATH)
+    assert exported == declared_functions()
+    for name in declared_functions(("fedavg_amd_tuning.h",)):
+        assert name in _lib.TUNING_SIGNATURES, name
+        assert name not in _lib.SIGNATURES, name
 
 
 def test_library_is_gfx950_code_object():

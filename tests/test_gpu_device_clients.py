@@ -381,7 +381,7 @@ def test_segments_variants_bit_identical(K):
     kind = np.array([kinds[wl[0][1][k].dtype] for k in keys], dtype=np.int64)
     ptrs = np.array([[sd[k].data_ptr() for k in keys] for _, sd in wl], dtype=np.int64)
     w = mfl_amd.weights_tensor(mfl_amd.sample_weights([n for n, _ in wl]), torch.float32, DEV)
-    lib = mfl_amd._lib.load()
+    lib = mfl_amd._lib.load_probe()
     need = lib.fedavg_segments_workspace(K, len(keys))
     P = int(numel.sum())
     args = (ptrs.ctypes.data, numel.ctypes.data, offset.ctypes.data, kind.ctypes.data, len(keys), K, w.data_ptr())

@@ -326,16 +326,19 @@ def test_buffer_descriptor_reduce_bit_identical(K, P):
     """fedavg_reduce_f32_buf (per-row buffer descriptors, 32-bit lane offsets)
     gives the production kernel's bits for every (U, C) and grid cap, with a
     ragged last column group and a P % 4 tail."""
-    lib = mfl_amd._lib.load()
+    lib = mfl_amd._lib.load_probe()
     x = _clients(K, P, seed=K + 7 * P)
     w = _w(_weights(K))
     base = mfl_amd.reduce_packed(x, w, P)
-    for u, c, b in [(4, 8, 0), (4, 8, 3), (8, 4, 0), (4, 4, 5), (2, 8, 0), (2, 16, 0), (1, 16, 7), (8, 8, 0)]:
+    for u, c, bs, b in [(4, 8, 256, 0), (4, 8, 256, 3), (8, 4, 256, 0), (4, 4, 256, 5), (2, 8, 256, 0),
+                        (2, 16, 256, 0), (1, 16, 256, 7), (8, 8, 256, 0), (16, 1, 256, 0), (16, 4, 256, 0),
+                        (16, 1, 64, 0), (16, 2, 64, 11), (8, 4, 64, 0), (32, 1, 64, 0), (16, 1, 128, 0),
+                        (8, 2, 128, 3), (4, 8, 128, 0)]:
         out = torch.full((P,), float("nan"), device=DEV)
         mfl_amd._lib.check(lib.fedavg_reduce_f32_buf(x.data_ptr(), K, P, x.shape[1], w.data_ptr(), out.data_ptr(),
-                                                     u, c, b, None), f"U{u}C{c}b{b}")
+                                                     u, c, bs, b, None), f"U{u}C{c}B{bs}b{b}", lib)
         torch.cuda.synchronize()
-        assert torch.equal(out.view(torch.int32), base.view(torch.int32)), (K, P, u, c, b)
+        assert torch.equal(out.view(torch.int32), base.view(torch.int32)), (K, P, u, c, bs, b)
 
 
 def test_misaligned_clients_take_scalar_path():
@@ -428,7 +431,7 @@ def test_cvt16_hardware_rounding_equals_c10_all_fp32_inputs():
     Over all 2^32 fp32 bit patterns: bf16 equals c10's integer
     round_to_nearest_even and fp16 the scalar v_cvt_f16_f32, for every
     non-NaN input (subnormals and overflow included); NaN stays NaN."""
-    lib = mfl_amd._lib.load()
+    lib = mfl_amd._lib.load_probe()
     n = 1 << 28
     a = torch.empty(n, dtype=torch.int16, device=DEV)
     b = torch.empty(n, dtype=torch.int16, device=DEV)
@@ -701,7 +704,7 @@ def test_client_sqdist_buffer_descriptor_variants(K, P):
     """fedavg_client_sqdist_buf (hardware range check instead of predicated
     loads; NaN in the row padding past P) matches the fp64 reference for every
     schedule, deterministically."""
-    lib = mfl_amd._lib.load()
+    lib = mfl_amd._lib.load_probe()
     ld = (P + 63) // 64 * 64
     g = torch.Generator(device=DEV).manual_seed(K + P)
     x = torch.full((K, ld), float("nan"), device=DEV)
@@ -826,7 +829,7 @@ def test_reduce_vec_dtypes_multilaunch(dtype, K, P):
 def test_vec_buffer_descriptor_bit_identical(dtype, K, P):
     """fedavg_reduce_vec_buf gives the production fp16/bf16/fp64 kernel's bits
     for every schedule, ragged last group and P tail included."""
-    lib = mfl_amd._lib.load()
+    lib = mfl_amd._lib.load_probe()
     x = _clients(K, P, seed=K + P, dtype=dtype)
     wdt = torch.float64 if dtype == torch.float64 else torch.float32
     w = _w(_weights(K), wdt)

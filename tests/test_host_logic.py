@@ -306,3 +306,23 @@ def test_client_device_and_mixed_device_rejection():
         KeyTable(meta0[0]).client_device(meta0)
     # a retained table never accepts clients on another device than it was asked for
     assert table.try_collect(mixed) is None
+
+
+def test_synthetic_inputs_torch_and_numpy_bit_identical():
+    """bench.py's device-generated clients (mfl_amd.synthetic) are reproduced
+    bit for bit by the numpy form the parity checks regenerate them with."""
+    from mfl_amd import synthetic
+
+    for g0, n, K in [(0, 1000, 3), (123_456_789, 4_099, 5), (2**40 + 7, 65, 2)]:
+        g = torch.arange(g0, g0 + n, dtype=torch.int64)
+        dev = torch.stack([synthetic.client_columns_torch(k, g) for k in range(K)]).numpy()
+        host = synthetic.client_columns_numpy(K, g0, n)
+        assert dev.tobytes() == host.tobytes()
+    x = synthetic.client_columns_numpy(2, 0, 200_000)
+    assert abs(float(x[0].std()) - 0.05) < 1e-3 and abs(float(x[0].mean())) < 1e-3
+    assert abs(float((x[1] - x[0]).std()) - 1e-3 * 2 ** 0.5) < 1e-4
+    rows = torch.empty(3, 300)
+    synthetic.fill_rows(rows, [(0, 7, 100), (128, 1000, 150)])
+    assert rows[:, 0:100].numpy().tobytes() == synthetic.client_columns_numpy(3, 7, 100).tobytes()
+    assert rows[:, 128:278].numpy().tobytes() == synthetic.client_columns_numpy(3, 1000, 150).tobytes()
+    assert float(rows[:, 100:128].abs().sum()) == 0.0 and float(rows[:, 278:].abs().sum()) == 0.0
