@@ -396,6 +396,9 @@ def main(argv=None):
     ap.add_argument("--traffic-json", default="", help="PMC traffic summary (profiles/*.json) to attach")
     ap.add_argument("--host-out", action="store_true",
                     help="host consumer (SURVEY 8e): D2H each rank's shard into pinned host memory, no collective")
+    ap.add_argument("--shard-of", type=int, default=0,
+                    help="N=1 only: reduce rank 0's shard of an N-GPU strong-scaled plan (its chunks, no exchange) "
+                         "-- the per-rank kernel at the N-GPU geometry, measured on one GPU")
     ap.add_argument("--launch-check", action="store_true", help="CPU-only: check the multi-rank launch path")
     ap.add_argument("--fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
     args = ap.parse_args(argv)
@@ -438,8 +441,13 @@ def main(argv=None):
 
     K, P_w, desc = WORKLOADS[args.workload]
     P_global = P_w if args.scaling == "strong" else P_w * world
-    shard_cols = -(-P_global // world)
-    chunks = args.chunks or auto_chunks(K, shard_cols, world, args.host_out)
+    plan_world = world
+    if args.shard_of > 1:
+        if world != 1 or args.host_out or args.force_gather:
+            raise SystemExit("--shard-of is a single-GPU rehearsal without exchange")
+        plan_world = args.shard_of
+    shard_cols = -(-P_global // plan_world)
+    chunks = args.chunks or auto_chunks(K, shard_cols, plan_world, args.host_out)
 
     # single-GPU workloads larger than the row budget: P-chunked passes
     passes = 1
@@ -453,7 +461,8 @@ def main(argv=None):
 
     host_out = torch.empty(P_pass, dtype=torch.float32, pin_memory=True) if args.host_out else None
     gather = False if args.no_gather else (True if args.force_gather else None)
-    red = ShardedReducer(K, P_pass, chunks=chunks, device=dev, gather=gather, host_out=host_out)
+    red = ShardedReducer(K, P_pass, chunks=chunks, device=dev, gather=gather, host_out=host_out,
+                         as_rank=(plan_world, 0) if plan_world != world else None)
     synthetic.fill_rows(red.clients, red.plan.local_segments())
     counts = synthetic.sample_counts(K)
     weights = mfl_amd.sample_weights(counts)
@@ -569,6 +578,8 @@ def main(argv=None):
 
     if rank == 0:
         P_done = P_pass * passes if passes > 1 else P_global
+        if plan_world != world:
+            P_done = red.plan.valid_local_cols()  # the one shard this GPU reduced
         bytes_step = algorithmic_bytes(K, P_done)
         value = bytes_step * args.steps / elapsed_max / 1e9
         # one reduce call = one chunk of one rank's shard = `launches_per_call`
@@ -629,6 +640,10 @@ def main(argv=None):
             "kernel_variant": {"unroll": tuned[0], "nt": tuned[1]} if tuned else "default",
             "launch": "hipGraph replay" if args.graph else "eager (stream-ordered)",
         }
+        if plan_world != world:
+            config["rehearsal"] = (f"rank 0's shard of the {plan_world}-GPU strong-scaled plan of {K} x {P_global}, "
+                                   f"reduced on one GPU in its {red.plan.chunks} chunks, no exchange; value counts "
+                                   f"this shard only")
         if passes > 1:
             config["passes"] = passes
             config["pass_note"] = (f"{K} x {P_done} fp32 = {4 * K * P_done / 1e9:.0f} GB of rows exceeds one GPU; "

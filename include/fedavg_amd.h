@@ -113,6 +113,27 @@ int fedavg_client_sqdist_f32(const float* clients, int64_t K, int64_t P, int64_t
                              double* sumsq, void* stream);
 
 /*
+ * The same pass for fp64 / fp16 / bf16 keys (a state_dict group of that
+ * dtype).  `w[para] - w_glob[para]` at :291 forms the difference in the
+ * key's dtype -- fp64, or fp32 math rounded to fp16/bf16 (ATen opmath) --
+ * and torch.cat widens it exactly, so sumsq[i] = sum_p d_i[p]^2 with d the
+ * reference's rounded difference, squares and sum in fp64.  The caller adds
+ * the groups' sums and rounds sqrt() to torch.cat's promoted dtype.
+ * workspace : fedavg_client_sqdist_workspace_elems(K, P, elem_size) doubles
+ * (elem_size 2, 4 or 8); rows 16-B aligned with ld a multiple of 16 B.
+ */
+int64_t fedavg_client_sqdist_workspace_elems(int64_t K, int64_t P, int64_t elem_size);
+int fedavg_client_sqdist_f64(const double* clients, int64_t K, int64_t P, int64_t ld,
+                             const double* glob, double* workspace, int64_t workspace_elems,
+                             double* sumsq, void* stream);
+int fedavg_client_sqdist_f16(const uint16_t* clients, int64_t K, int64_t P, int64_t ld,
+                             const uint16_t* glob, double* workspace, int64_t workspace_elems,
+                             double* sumsq, void* stream);
+int fedavg_client_sqdist_bf16(const uint16_t* clients, int64_t K, int64_t P, int64_t ld,
+                              const uint16_t* glob, double* workspace, int64_t workspace_elems,
+                              double* sumsq, void* stream);
+
+/*
  * FPF2 bookkeeping (fedavg_trainer.py:108-119 state, :209-210, :271-278,
  * :314-327), on device-resident state owned by the caller:
  *   diffs   : local_w_diffs, [n_rows, ld] fp32 (n_rows = client_num_in_total),

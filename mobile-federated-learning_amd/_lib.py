@@ -39,6 +39,10 @@ SIGNATURES = {
                                   _vp]),
     "fedavg_client_sqdist_workspace": (_c_i64, [_c_i64, _c_i64]),
     "fedavg_client_sqdist_f32": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_i64, _vp, _vp]),
+    "fedavg_client_sqdist_workspace_elems": (_c_i64, [_c_i64, _c_i64, _c_i64]),
+    "fedavg_client_sqdist_f64": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_i64, _vp, _vp]),
+    "fedavg_client_sqdist_f16": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_i64, _vp, _vp]),
+    "fedavg_client_sqdist_bf16": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_i64, _vp, _vp]),
     "fedavg_fpf_set_rows_f32": (_c_int, [_vp, _c_i64, _c_i64, _vp, _c_i64, _vp, _c_i64, _vp, _c_i64, _vp]),
     "fedavg_fpf_workspace": (_c_i64, [_c_i64]),
     "fedavg_fpf_end_round_f32": (_c_int, [_vp, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _c_i64, _c_float, _vp, _c_i64,

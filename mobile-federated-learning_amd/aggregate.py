@@ -567,9 +567,15 @@ class DeviceAggregator:
         (the reference's order: :217 then :291); otherwise uploads them.
         A client whose dict IS ``w_glob`` (client 0 after aggregate, :449)
         gets ``w_glob - w_glob``: 0.0, or NaN where ``w_glob`` holds inf/NaN.
-        Norms are accumulated in fp64 and rounded to fp32 like torch.norm's
-        fp32 result (the reference's fp32 SIMD accumulation is
-        within its own rounding error of this value).
+
+        Every dtype group of the state_dict (fp32 with the integer keys,
+        fp64, fp16, bf16) is one pass: the difference rounded in the group's
+        dtype as ``w[para] - w_glob[para]`` rounds it, squares summed in fp64;
+        the groups' sums are added and the root is rounded to torch.cat's
+        promoted dtype (fp64 if any fp64 key; fp32 for fp32 or mixed 16-bit
+        kinds; fp16/bf16 when every key is that type).  The reference's norm
+        accumulates in its own dtype's SIMD lanes; this is the accurate value
+        it approximates.
         """
         import numpy as np
 
@@ -577,9 +583,11 @@ class DeviceAggregator:
             return np.zeros(0)
         last = self._last
         refs = last.get("refs")
+        devs = last.get("dev", {})
         cached = (refs is not None and last["acc"]() is w_glob and len(refs) == len(w_locals)
                   and all(r() is sd for r, (_, sd) in zip(refs, w_locals))
-                  and set(last.get("dev", {})) == {torch.float32})
+                  and bool(devs) and set(devs) == set(last["table"].groups)
+                  and all(rows is not None or dt == torch.float32 for dt, (rows, _) in devs.items()))
         # the reference's `w[para] - w_glob[para]` raises on bool buffers; the
         # round's key table already holds every client's (validated) dtypes
         if cached:
@@ -590,61 +598,89 @@ class DeviceAggregator:
             raise RuntimeError("Subtraction, the `-` operator, with a bool tensor is not supported "
                                "(fedavg_trainer.py:291 on a state_dict with bool buffers)")
         with torch.cuda.device(self.device):
+            parts = []  # (group dtype, [K] fp64 sums on the device, the group's averaged model)
             if cached:
-                devbuf, out_dev = last["dev"][torch.float32]
-                P = last["table"].groups[torch.float32].P
-                if devbuf is None:  # zero-copy round: read the clients' tensors where they lie
-                    # the dict aliased to w_glob (client 0, :449) holds the average
-                    # now; its own tensors stand in (its norm is overridden below)
-                    dicts = [last["seg_keep0"] if sd is w_glob else sd for _, sd in w_locals]
-                    sumsq_dev = self._sqdist_segments(last["table"], dicts, out_dev)
-                else:
-                    sumsq_dev = client_sqdist(devbuf, out_dev, P)
+                table = last["table"]
+                for dt, (devbuf, out_dev) in devs.items():
+                    P = table.groups[dt].P
+                    if devbuf is None:  # zero-copy round: read the clients' tensors where they lie
+                        # the dict aliased to w_glob (client 0, :449) holds the average
+                        # now; its own tensors stand in (its norm is overridden below)
+                        dicts = [last["seg_keep0"] if sd is w_glob else sd for _, sd in w_locals]
+                        parts.append((dt, self._sqdist_segments(table, dicts, out_dev), out_dev[:P]))
+                    else:
+                        parts.append((dt, client_sqdist(devbuf, out_dev, P), out_dev[:P]))
             else:
-                devbuf, out_dev, P = self._upload_for_distances(w_locals, w_glob)
-                sumsq_dev = client_sqdist(devbuf, out_dev, P)
+                for dt, devbuf, glob, P in self._upload_for_distances(w_locals, w_glob):
+                    parts.append((dt, client_sqdist(devbuf, glob, P), glob[:P]))
+            sumsq_dev = parts[0][1]
+            for _, s, _ in parts[1:]:
+                sumsq_dev = sumsq_dev + s
             sumsq = sumsq_dev.cpu().numpy()
-            glob_finite = bool(torch.isfinite(out_dev[:P]).all())
-        norms = np.sqrt(sumsq).astype(np.float32).astype(np.float64)
+            glob_finite = all(bool(torch.isfinite(g).all()) for _, _, g in parts)
+        cat_dtype = parts[0][0]
+        for dt, _, _ in parts[1:]:
+            cat_dtype = torch.promote_types(cat_dtype, dt)
+        norms = _round_to_dtype(np.sqrt(sumsq), cat_dtype)
         for i, (_, sd) in enumerate(w_locals):
             if sd is w_glob:
                 norms[i] = 0.0 if glob_finite else float("nan")
         return norms
 
     def _upload_for_distances(self, w_locals, w_glob):
+        """[(dtype, rows [K, ld], glob [ld], P)] per dtype group: the clients'
+        rows and the model, packed in HBM (on the device from device-resident
+        tensors, else through pinned host staging)."""
         others = [sd for _, sd in w_locals if sd is not w_glob]
         template = others[0] if others else w_glob
         table = KeyTable(template)
-        if set(table.groups) != {torch.float32}:
-            raise NotImplementedError("client_distances supports fp32/integer state_dicts (fp64/fp16/bf16 keys "
-                                      "change torch.cat's result dtype at fedavg_trainer.py:291)")
-        g = table.groups[torch.float32]
+        gtable = KeyTable(w_glob)
+        if set(table.groups) != set(gtable.groups) or any(
+                table.groups[dt].P != gtable.groups[dt].P for dt in table.groups):
+            raise ValueError("w_glob's keys/dtypes do not match the clients' (fedavg_trainer.py:291 subtracts "
+                             "w_glob[para] key by key; pass the aggregate's result)")
         K = len(w_locals)
         rows = [sd if sd is not w_glob else template for _, sd in w_locals]  # aliased rows are overridden
         cdev = self._client_device(table, rows)
         ptrs, keep = table.collect(rows, cdev)
-        gtable = KeyTable(w_glob)
         gptrs, gkeep = gtable.collect([w_glob], cdev)  # w - w_glob needs one device (TypeError otherwise)
-        gg = gtable.groups[torch.float32]
+        out = []
         if cdev.type == "cuda":
-            dev = torch.empty((K + 1, g.ld), dtype=torch.float32, device=self.device)
             stream = torch.cuda.current_stream(self.device)
-            self._pack_on_device(table, g, ptrs, 0, dev, stream)
-            self._pack_on_device(gtable, gg, gptrs, K, dev, stream)
+            for dt, g in table.groups.items():
+                gg = gtable.groups[dt]
+                dev = torch.empty((K + 1, g.ld), dtype=dt, device=self.device)
+                self._pack_on_device(table, g, ptrs, 0, dev, stream)
+                self._pack_on_device(gtable, gg, gptrs, K, dev, stream)
+                out.append((dt, dev[:K], dev[K], g.P))
             del keep, gkeep
-            return dev[:K], dev[K], g.P
+            return out
         lib = _lib.load()
-        host = torch.empty((K + 1, g.ld), dtype=torch.float32, pin_memory=True)
-        items = table.pack_items(g, ptrs, 0, g.ld)
-        _lib.check(lib.fedavg_pack_rows(items.ctypes.data, items.shape[0], host.data_ptr(), 4,
-                                        max(1, torch.get_num_threads())), "fedavg_pack_rows")
-        gitems = gtable.pack_items(gg, gptrs, K, g.ld)
-        _lib.check(lib.fedavg_pack_rows(gitems.ctypes.data, gitems.shape[0], host.data_ptr(), 4, 1),
-                   "fedavg_pack_rows")
-        dev = host.to(self.device, non_blocking=True)
+        for dt, g in table.groups.items():
+            gg = gtable.groups[dt]
+            host = torch.empty((K + 1, g.ld), dtype=dt, pin_memory=True)
+            es = host.element_size()
+            items = table.pack_items(g, ptrs, 0, g.ld)
+            _lib.check(lib.fedavg_pack_rows(items.ctypes.data, items.shape[0], host.data_ptr(), es,
+                                            max(1, torch.get_num_threads())), "fedavg_pack_rows")
+            gitems = gtable.pack_items(gg, gptrs, K, g.ld)
+            _lib.check(lib.fedavg_pack_rows(gitems.ctypes.data, gitems.shape[0], host.data_ptr(), es, 1),
+                       "fedavg_pack_rows")
+            dev = host.to(self.device, non_blocking=True)
+            out.append((dt, dev[:K], dev[K], g.P))
         torch.cuda.current_stream(self.device).synchronize()
         del keep, gkeep
-        return dev[:K], dev[K], g.P
+        return out
+
+
+def _round_to_dtype(x, dtype: torch.dtype):
+    """float64 array -> the values rounded to ``dtype`` (what ``.item()`` of
+    a norm of that dtype returns), as float64."""
+    import numpy as np
+
+    if dtype == torch.float64:
+        return np.asarray(x, dtype=np.float64).copy()
+    return torch.from_numpy(np.asarray(x, dtype=np.float64)).to(dtype).to(torch.float64).numpy()
 
 
 _default: Dict[int, DeviceAggregator] = {}

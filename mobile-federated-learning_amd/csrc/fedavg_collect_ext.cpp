@@ -18,6 +18,8 @@
 
 #include <vector>
 
+#include <pybind11/stl.h>
+
 namespace py = pybind11;
 
 static py::tuple collect(py::list dicts, py::list names, py::list templ, int64_t device_index) {
@@ -86,9 +88,139 @@ static py::list unpack(const at::Tensor& flat, py::list offsets, py::list shapes
   return out;
 }
 
+// small_round(w_locals, names, templ, numel, offset, kind, shapes, P, ld, rows_host, rows_dev, w_host, w_dev,
+//             round_fn, n_threads, stream, device_index) -> (status, out_dev, out_host)
+//
+// The whole host side of a small fp32 round in one call -- what aggregate()
+// does in Python for a round whose key table is already known: the
+// reference's weights n_i / N (fedavg_trainer.py:444-447, :453) from Python
+// ints, the walk over every client's tensors (checked against the table like
+// collect()), the pack-item list, ONE call of fedavg_round_f32 (pack + one
+// kernel + wait; its address comes from the loaded libfedavg_amd.so) with
+// the GIL released, and the averaged model's views written into
+// w_locals[0][1] in key order (fedavg_trainer.py:449-457: the result IS
+// client 0's dict).  status 0: done.  status 1: something the general path
+// must see (a non-int or negative count, a zero total, a missing key or
+// another shape/dtype/device, client 0 without exactly the table's keys in
+// order, a repeated dict) -- nothing was written and the caller runs the
+// general path, which raises the reference's exception or handles the case.
+// A failing native call returns its negative code as status.
+using round_fn_t = int (*)(const int64_t*, int64_t, float*, float*, int64_t, int64_t, int64_t, const double*, float*,
+                           float*, float*, float*, int, void*);
+
+static py::tuple small_round(py::list w_locals, py::list names, py::list templ, const std::vector<int64_t>& numel,
+                             const std::vector<int64_t>& offset, const std::vector<int64_t>& kind, py::list shapes,
+                             int64_t P, int64_t ld, int64_t rows_host, int64_t rows_dev, int64_t w_host,
+                             int64_t w_dev, int64_t round_fn, int n_threads, int64_t stream, int64_t device_index) {
+  const Py_ssize_t K = PyList_GET_SIZE(w_locals.ptr());
+  const Py_ssize_t N = PyList_GET_SIZE(names.ptr());
+  auto fallback = [] { return py::make_tuple(1, py::none(), py::none()); };
+  if (K <= 0 || N <= 0 || static_cast<Py_ssize_t>(numel.size()) != N) return fallback();
+  thread_local std::vector<double> weights;
+  thread_local std::vector<PyObject*> dicts;
+  thread_local std::vector<int64_t> items;
+  weights.resize(K);
+  dicts.resize(K);
+  // counts and dicts (:444-447): exact ints only, summed in order
+  int64_t total = 0;
+  for (Py_ssize_t i = 0; i < K; ++i) {
+    PyObject* pair = PyList_GET_ITEM(w_locals.ptr(), i);
+    if (!PyTuple_Check(pair) || PyTuple_GET_SIZE(pair) != 2) return fallback();
+    PyObject* n = PyTuple_GET_ITEM(pair, 0);
+    if (!PyLong_CheckExact(n)) return fallback();
+    int overflow = 0;
+    const long long v = PyLong_AsLongLongAndOverflow(n, &overflow);
+    if (overflow || v < 0 || v > (1LL << 53)) return fallback();
+    total += v;
+    if (total > (1LL << 53)) return fallback();
+    weights[i] = static_cast<double>(v);
+    dicts[i] = PyTuple_GET_ITEM(pair, 1);
+    for (Py_ssize_t j = 0; j < i; ++j)
+      if (dicts[j] == dicts[i]) return fallback();  // the general path raises (aliased rows)
+  }
+  if (total == 0) return fallback();  // ZeroDivisionError, raised by the general path
+  for (Py_ssize_t i = 0; i < K; ++i) weights[i] = weights[i] / static_cast<double>(total);  // == Python n / N
+  // client 0 must hold exactly the table's keys in order (the result replaces them in place)
+  PyObject* d0 = dicts[0];
+  if (!PyDict_Check(d0) || PyDict_Size(d0) != N) return fallback();
+  {
+    Py_ssize_t pos = 0, j = 0;
+    PyObject *key, *val;
+    while (PyDict_Next(d0, &pos, &key, &val)) {
+      if (j >= N) return fallback();
+      const int eq = PyObject_RichCompareBool(key, PyList_GET_ITEM(names.ptr(), j), Py_EQ);
+      if (eq != 1) {
+        if (eq < 0) PyErr_Clear();
+        return fallback();
+      }
+      ++j;
+    }
+  }
+  // the walk: every client's tensor for every key, checked against the table
+  items.resize(static_cast<size_t>(K) * N * 4);
+  for (Py_ssize_t i = 0; i < K; ++i) {
+    PyObject* d = dicts[i];
+    for (Py_ssize_t j = 0; j < N; ++j) {
+      PyObject* t = PyObject_GetItem(d, PyList_GET_ITEM(names.ptr(), j));
+      if (!t) {
+        PyErr_Clear();
+        return fallback();
+      }
+      bool ok = THPVariable_Check(t);
+      if (ok) {
+        const at::Tensor& ten = THPVariable_Unpack(t);
+        const at::Tensor& tp = THPVariable_Unpack(PyList_GET_ITEM(templ.ptr(), j));
+        ok = ten.scalar_type() == tp.scalar_type() && ten.sizes() == tp.sizes() && ten.is_contiguous() &&
+             (device_index < 0 ? ten.is_cpu() : (ten.is_cuda() && ten.get_device() == device_index));
+        if (ok) {
+          int64_t* it = &items[(static_cast<size_t>(i) * N + j) * 4];
+          it[0] = reinterpret_cast<int64_t>(ten.data_ptr());
+          it[1] = numel[j];
+          it[2] = static_cast<int64_t>(i) * ld + offset[j];
+          it[3] = kind[j];
+        }
+      }
+      Py_DECREF(t);  // the dict keeps the tensor alive
+      if (!ok) return fallback();
+    }
+  }
+  auto opts = at::TensorOptions().dtype(at::kFloat);
+  at::Tensor out_host = at::empty({P}, opts.pinned_memory(true));
+  at::Tensor out_dev = at::empty({P}, opts.device(at::Device(at::kCUDA, static_cast<c10::DeviceIndex>(
+                                                      device_index < 0 ? 0 : device_index))));
+  int rc;
+  {
+    py::gil_scoped_release nogil;
+    rc = reinterpret_cast<round_fn_t>(round_fn)(items.data(), static_cast<int64_t>(K) * N,
+                                                reinterpret_cast<float*>(rows_host), reinterpret_cast<float*>(rows_dev),
+                                                K, P, ld, weights.data(), reinterpret_cast<float*>(w_host),
+                                                reinterpret_cast<float*>(w_dev), out_dev.data_ptr<float>(),
+                                                out_host.data_ptr<float>(), n_threads, reinterpret_cast<void*>(stream));
+  }
+  if (rc != 0) return py::make_tuple(rc, py::none(), py::none());
+  // the averaged model's keys as views of out_host, written into client 0's dict
+  std::vector<int64_t> size, stride;
+  for (Py_ssize_t j = 0; j < N; ++j) {
+    PyObject* shp = PyList_GET_ITEM(shapes.ptr(), j);
+    const Py_ssize_t nd = PyTuple_GET_SIZE(shp);
+    size.resize(nd);
+    stride.resize(nd);
+    int64_t n = 1;
+    for (Py_ssize_t dd = nd - 1; dd >= 0; --dd) {
+      size[dd] = PyLong_AsLongLong(PyTuple_GET_ITEM(shp, dd));
+      stride[dd] = n;
+      n *= size[dd];
+    }
+    py::object view = py::reinterpret_steal<py::object>(THPVariable_Wrap(out_host.as_strided(size, stride, offset[j])));
+    if (PyObject_SetItem(d0, PyList_GET_ITEM(names.ptr(), j), view.ptr()) != 0) throw py::error_already_set();
+  }
+  return py::make_tuple(0, out_dev, out_host);
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "native state_dict walk for mfl_amd (host metadata only)";
   m.def("collect", &collect, "validate clients against client 0 and gather data pointers", py::arg("dicts"),
         py::arg("names"), py::arg("templ"), py::arg("device_index") = -1);
   m.def("unpack", &unpack, "views of a flat buffer shaped like the key table's keys");
+  m.def("small_round", &small_round, "the host side of a small fp32 round in one call");
 }

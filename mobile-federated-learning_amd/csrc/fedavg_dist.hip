@@ -142,6 +142,84 @@ __global__ __launch_bounds__(kBlock) void client_sqdist_buf_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// :291 for fp64 / fp16 / bf16 keys.  `w[para] - w_glob[para]` forms the
+// difference in the key's own dtype (ATen: fp64 math for fp64; fp32 opmath
+// rounded to fp16/bf16 for the 16-bit types), torch.cat then widens it
+// exactly to the promoted dtype, and the norm squares and sums.  Here: the
+// difference with the reference's rounding, then exact-ish fp64 squares and
+// sum (fused square-adds), same per-wave partial layout and fixed-order
+// finalize as the fp32 pass.  16-B slices: 2 fp64 or 8 fp16/bf16 elements.
+// ---------------------------------------------------------------------------
+struct DistF64 {
+  using vec = f64x2;
+  static constexpr int kLanes = 2;
+  __device__ static double sq_add(double acc, vec x, vec g, int nv) {
+    const vec d = x - g;  // fp64 difference, as the reference forms it
+    if (nv > 0) acc = __builtin_fma(d.x, d.x, acc);
+    if (nv > 1) acc = __builtin_fma(d.y, d.y, acc);
+    return acc;
+  }
+};
+
+template <typename R>
+struct DistHalf {
+  using vec = u16x8;
+  static constexpr int kLanes = 8;
+  __device__ static double sq_add(double acc, vec x, vec g, int nv) {
+    u32x4 xu, gu;
+    __builtin_memcpy(&xu, &x, 16);
+    __builtin_memcpy(&gu, &g, 16);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      // fl16(fl32(x) - fl32(g)): ATen's opmath subtraction rounded to the
+      // key's 16-bit type, then widened exactly
+      const f32x2 d = R::unpack(R::pack(opaque2(R::unpack(xu[j]) - R::unpack(gu[j]))));
+      const double a = d.x, b = d.y;
+      if (2 * j < nv) acc = __builtin_fma(a, a, acc);
+      if (2 * j + 1 < nv) acc = __builtin_fma(b, b, acc);
+    }
+    return acc;
+  }
+};
+
+template <class D, int U, int C>
+__global__ __launch_bounds__(kBlock) void client_sqdist_vec_kernel(
+    const typename D::vec* __restrict__ X, int K, int64_t ldv, int64_t nvec, int tail,
+    const typename D::vec* __restrict__ G, double* __restrict__ partials, int64_t nwaves) {
+  using vec = typename D::vec;
+  const int lane = threadIdx.x & 63;
+  const int64_t wave_id = static_cast<int64_t>(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * kBlock * C + threadIdx.x;
+  vec g[C];
+  int nv[C];  // valid elements of slice j: padding lanes never contribute
+#pragma unroll
+  for (int j = 0; j < C; ++j) {
+    const int64_t v = base + static_cast<int64_t>(j) * kBlock;
+    nv[j] = v >= nvec ? 0 : (tail != 0 && v == nvec - 1 ? tail : D::kLanes);
+    g[j] = nv[j] > 0 ? G[v] : vec{};
+  }
+  const vec* col = X + base;
+  for (int k = 0; k < K; k += U) {
+    const int rows = (K - k) < U ? (K - k) : U;
+    vec xs[U][C];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < C; ++j)
+        xs[u][j] = (u < rows && nv[j] > 0) ? ld<true>(col + static_cast<int64_t>(k + u) * ldv + j * kBlock) : g[j];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (u >= rows) break;
+      double acc = 0.0;
+#pragma unroll
+      for (int j = 0; j < C; ++j) acc = D::sq_add(acc, xs[u][j], g[j], nv[j]);
+      acc = wave_sum(acc);
+      if (lane == 0) partials[static_cast<int64_t>(k + u) * nwaves + wave_id] = acc;
+    }
+  }
+}
+
 // sumsq[k] = sum over waves of partials[k][*], fixed order (block per client).
 __global__ __launch_bounds__(kBlock) void client_sqdist_finalize_kernel(const double* __restrict__ partials,
                                                                         int64_t nwaves, double* __restrict__ out) {
@@ -225,6 +303,39 @@ int sqdist_impl(const float* clients, int64_t K, int64_t P, int64_t ld, const fl
   return launch_status(what);
 }
 
+int64_t sqdist_vec_waves(int64_t nvec, int cols) {
+  const int64_t blocks = (nvec + kBlock * cols - 1) / (kBlock * cols);
+  return blocks * (kBlock / 64);
+}
+
+// One launch of client_sqdist_vec_kernel<D, 4, kDistCols> + the finalize.
+// Rows: [K, ld] with 16-B aligned rows (ld a multiple of the 16-B lane count).
+template <class D>
+int sqdist_vec_impl(const void* clients, int64_t K, int64_t P, int64_t ld, const void* glob, double* workspace,
+                    int64_t workspace_elems, double* sumsq, void* stream, const char* what) {
+  int rc = check_common(clients, K, P, ld, glob, sumsq, what);
+  if (rc) return rc;
+  if (P == 0) return set_error(FEDAVG_EINVAL, "%s: P must be >= 1", what);
+  constexpr int64_t lanes = D::kLanes;
+  if (!aligned16(clients) || !aligned16(glob) || (ld % lanes) != 0)
+    return set_error(FEDAVG_EALIGN, "%s: needs 16-B aligned clients/glob and ld %% %d == 0", what, (int)lanes);
+  const int64_t nvec = (P + lanes - 1) / lanes;
+  const int64_t nwaves = sqdist_vec_waves(nvec, kDistCols);
+  if (!workspace || workspace_elems < K * nwaves)
+    return set_error(FEDAVG_EINVAL, "%s: workspace needs %lld doubles", what, (long long)(K * nwaves));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  using vec = typename D::vec;
+  const int64_t blocks = (nvec + kBlock * kDistCols - 1) / (kBlock * kDistCols);
+  hipLaunchKernelGGL((client_sqdist_vec_kernel<D, kDistRows, kDistCols>), dim3(static_cast<unsigned>(blocks)),
+                     dim3(kBlock), 0, s, reinterpret_cast<const vec*>(clients), static_cast<int>(K), ld / lanes, nvec,
+                     static_cast<int>(P % lanes), reinterpret_cast<const vec*>(glob), workspace, nwaves);
+  rc = launch_status(what);
+  if (rc) return rc;
+  hipLaunchKernelGGL(client_sqdist_finalize_kernel, dim3(static_cast<unsigned>(K)), dim3(kBlock), 0, s, workspace,
+                     nwaves, sumsq);
+  return launch_status(what);
+}
+
 }  // namespace
 
 extern "C" {
@@ -238,6 +349,30 @@ int fedavg_client_sqdist_f32(const float* clients, int64_t K, int64_t P, int64_t
                              double* workspace, int64_t workspace_elems, double* sumsq, void* stream) {
   return sqdist_impl(clients, K, P, ld, glob, workspace, workspace_elems, sumsq, kDistRows, kDistCols,
                      kDistBlocksPerLaunch, stream);
+}
+
+int64_t fedavg_client_sqdist_workspace_elems(int64_t K, int64_t P, int64_t elem_size) {
+  if (K <= 0 || P <= 0 || (elem_size != 2 && elem_size != 4 && elem_size != 8)) return 0;
+  const int64_t lanes = 16 / elem_size;
+  return K * sqdist_vec_waves((P + lanes - 1) / lanes, kDistCols);
+}
+
+int fedavg_client_sqdist_f64(const double* clients, int64_t K, int64_t P, int64_t ld, const double* glob,
+                             double* workspace, int64_t workspace_elems, double* sumsq, void* stream) {
+  return sqdist_vec_impl<DistF64>(clients, K, P, ld, glob, workspace, workspace_elems, sumsq, stream,
+                                  "fedavg_client_sqdist_f64");
+}
+
+int fedavg_client_sqdist_f16(const uint16_t* clients, int64_t K, int64_t P, int64_t ld, const uint16_t* glob,
+                             double* workspace, int64_t workspace_elems, double* sumsq, void* stream) {
+  return sqdist_vec_impl<DistHalf<F16Pk>>(clients, K, P, ld, glob, workspace, workspace_elems, sumsq, stream,
+                                          "fedavg_client_sqdist_f16");
+}
+
+int fedavg_client_sqdist_bf16(const uint16_t* clients, int64_t K, int64_t P, int64_t ld, const uint16_t* glob,
+                              double* workspace, int64_t workspace_elems, double* sumsq, void* stream) {
+  return sqdist_vec_impl<DistHalf<BF16Pk>>(clients, K, P, ld, glob, workspace, workspace_elems, sumsq, stream,
+                                           "fedavg_client_sqdist_bf16");
 }
 
 #ifdef FEDAVG_TUNING  // probe library only (libfedavg_amd_probe.so)

@@ -141,6 +141,10 @@ class ShardedReducer:
     rank; True forces the collective even at world size 1 (so the RCCL
     exchange runs, and is tested, on a single GPU); False never gathers.
 
+    ``as_rank=(G, r)``: plan rank r's shard of a G-rank run in this process
+    (no exchange) -- bench.py's single-GPU rehearsal of the per-rank kernel
+    at the 8-GPU geometry.
+
     ``host_out`` (SURVEY §8e's alternative for a host consumer): a pinned
     host tensor of >= P elements -- e.g. one mapping shared by all ranks of
     the node.  Each rank then copies its finished chunks straight to their
@@ -151,10 +155,16 @@ class ShardedReducer:
 
     def __init__(self, K: int, P: int, *, chunks: int = 1, group=None, device=None,
                  dtype: torch.dtype = torch.float32, local_reduce: Optional[LocalReduce] = None,
-                 gather: Optional[bool] = None, host_out: Optional[torch.Tensor] = None):
+                 gather: Optional[bool] = None, host_out: Optional[torch.Tensor] = None,
+                 as_rank: Optional[tuple] = None):
         self.group = group
         ws = dist.get_world_size(group) if dist.is_initialized() else 1
         rank = dist.get_rank(group) if dist.is_initialized() else 0
+        if as_rank is not None:  # (world_size, rank): one rank's shard of a larger plan, no exchange
+            if gather:
+                raise ValueError("as_rank plans a shard of another world size; it cannot gather")
+            ws, rank = int(as_rank[0]), int(as_rank[1])
+            gather = False
         self.plan = plan_shards(P, ws, rank, chunks)
         self.K = K
         self.dtype = dtype

@@ -157,18 +157,30 @@ def reduce_tensors(
     return out
 
 
+_SQDIST_ENTRY = {
+    torch.float32: "fedavg_client_sqdist_f32",
+    torch.float64: "fedavg_client_sqdist_f64",
+    torch.float16: "fedavg_client_sqdist_f16",
+    torch.bfloat16: "fedavg_client_sqdist_bf16",
+}
+
+
 def client_sqdist(clients: torch.Tensor, glob: torch.Tensor, P: Optional[int] = None, *,
                   stream: Optional[torch.cuda.Stream] = None) -> torch.Tensor:
-    """sumsq[i] = sum_p fl32(clients[i, p] - glob[p])^2 in fp64 (device [K] float64).
+    """sumsq[i] = sum_p d_i[p]^2 in fp64 (device [K] float64), with
+    d_i = clients[i, p] - glob[p] rounded as the reference's
+    ``w[para] - w_glob[para]`` rounds it in the rows' dtype (fp32; fp64;
+    fp16/bf16 via fp32 opmath).
 
     The squared distance behind fedavg_trainer.py:291; the norm is
-    ``fl32(sqrt(sumsq))``.  ``clients`` [K, ld] fp32 (16-B aligned rows),
-    ``glob`` [>= P] fp32 on the same device.
+    ``sqrt(sumsq)`` rounded to torch.cat's dtype.  ``clients`` [K, ld]
+    (16-B aligned rows), ``glob`` [>= P] of the same dtype and device.
     """
     _check_device_tensor(clients, "clients")
     _check_device_tensor(glob, "glob")
-    if clients.dtype != torch.float32 or glob.dtype != torch.float32:
-        raise TypeError("client_sqdist is fp32 only")
+    dtype = clients.dtype
+    if dtype not in _SQDIST_ENTRY or glob.dtype != dtype:
+        raise TypeError(f"client_sqdist: unsupported dtypes {dtype} / {glob.dtype}")
     if clients.dim() != 2 or clients.stride(1) != 1:
         raise ValueError("clients must be 2-D [K, ld] with unit column stride")
     K = clients.shape[0]
@@ -177,10 +189,14 @@ def client_sqdist(clients: torch.Tensor, glob: torch.Tensor, P: Optional[int] = 
     if glob.numel() < P or not glob.is_contiguous():
         raise ValueError("glob must be a contiguous tensor of >= P elements")
     lib = _lib.load()
-    n_ws = lib.fedavg_client_sqdist_workspace(K, P)
+    if dtype == torch.float32:
+        n_ws = lib.fedavg_client_sqdist_workspace(K, P)
+    else:
+        n_ws = lib.fedavg_client_sqdist_workspace_elems(K, P, clients.element_size())
     work = torch.empty(max(n_ws, 1), dtype=torch.float64, device=clients.device)
     out = torch.empty(K, dtype=torch.float64, device=clients.device)
-    rc = lib.fedavg_client_sqdist_f32(clients.data_ptr(), K, P, ld, glob.data_ptr(), work.data_ptr(), n_ws,
-                                      out.data_ptr(), _stream_handle(stream, clients.device))
-    _lib.check(rc, "fedavg_client_sqdist_f32")
+    entry = _SQDIST_ENTRY[dtype]
+    rc = getattr(lib, entry)(clients.data_ptr(), K, P, ld, glob.data_ptr(), work.data_ptr(), n_ws, out.data_ptr(),
+                             _stream_handle(stream, clients.device))
+    _lib.check(rc, entry)
     return out

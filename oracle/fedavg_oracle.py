@@ -206,15 +206,19 @@ def client_distances_torch(w_locals, w_glob, keys=None):
 
 
 def client_distances_exact(w_locals, w_glob, keys=None):
-    """Accurate form of :291: fp32 differences (as the reference forms them),
-    exact fp64 squares and sum, fp32-rounded sqrt."""
+    """Accurate form of :291: the differences rounded exactly as the
+    reference forms them (``w[k] - w_glob[k]`` in each key's promoted dtype:
+    fp32, fp64, or fp32 opmath rounded to fp16/bf16), widened exactly by
+    torch.cat, squares and sum in fp64, the root rounded to torch.cat's dtype
+    (what ``torch.norm(...).item()`` returns, without its accumulation error)."""
     import torch
 
     keys = list(w_glob.keys()) if keys is None else list(keys)
     out = []
     for _, w in w_locals:
         d = torch.cat([w[k].reshape((-1,)) - w_glob[k].reshape((-1,)) for k in keys])
-        out.append(float(np.float32(np.sqrt(np.sum(np.square(d.numpy().astype(np.float64)))))))
+        s = np.sqrt(np.sum(np.square(d.double().numpy())))
+        out.append(float(torch.tensor(s, dtype=torch.float64).to(d.dtype).double()))
     return np.array(out)
 
 

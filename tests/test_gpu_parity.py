@@ -684,6 +684,53 @@ def test_client_distances_after_aggregate(name):
     assert abs(d - d_ref) <= 1e-5 * abs(d_ref) + 1e-30
 
 
+@pytest.mark.parametrize("name", ["float64_key_k3", "float16_key_k3", "bfloat16_key_k3", "resnet_like_bn_k5"])
+def test_client_distances_other_dtypes(name):
+    """:291 with fp64 / fp16 / bf16 keys (the reference's torch.cat dtype
+    promotion): every group's pass, summed, rooted and rounded to the cat
+    dtype, against the oracle's accurate restatement (within one unit of
+    that dtype; fp64 within 1e-12) and ATen's own norm (two units)."""
+    import copy
+    _, w_locals, _ = load_case(name)
+    orig = copy.deepcopy(w_locals)  # the aggregates below alias and overwrite client 0's dict (:449)
+    ref_locals = copy.deepcopy(w_locals)
+    ref_glob = O.aggregate_torch(ref_locals)
+    cat = torch.cat([ref_locals[-1][1][k].reshape(-1) - ref_glob[k].reshape(-1) for k in ref_glob]).dtype
+    eps = 1e-12 if cat == torch.float64 else torch.finfo(cat).eps
+    exact = O.client_distances_exact(ref_locals, ref_glob)
+    torch_ref = O.client_distances_torch(ref_locals, ref_glob)
+    agg = mfl_amd.DeviceAggregator(DEV)
+    w_glob = agg.aggregate(w_locals)
+    for norms in (agg.client_distances(w_locals, w_glob),  # cached rows
+                  mfl_amd.DeviceAggregator(DEV).client_distances(w_locals, w_glob)):  # fresh upload
+        assert norms[0] == 0.0
+        assert np.allclose(norms, exact, rtol=eps, atol=0), (name, norms, exact)
+        assert np.allclose(norms, torch_ref, rtol=2 * max(eps, 1e-6), atol=0), (name, norms, torch_ref)
+    # device-resident clients: the same groups packed in HBM
+    dl = [(n, {k: v.to(DEV) for k, v in sd.items()}) for n, sd in orig]
+    dev_agg = mfl_amd.DeviceAggregator(DEV)
+    dglob = dev_agg.aggregate(dl)
+    norms = dev_agg.client_distances(dl, dglob)
+    assert np.allclose(norms, exact, rtol=eps, atol=0), (name, norms, exact)
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("K,P", [(3, 1), (5, 7), (7, 4099), (100, 1_000_003)])
+def test_client_sqdist_other_dtypes_vs_torch(dtype, K, P):
+    """The fp64 / fp16 / bf16 pass against torch on the device: differences in
+    the rows' dtype (torch's own rounding), squares summed in fp64."""
+    ld = (P + 63) // 64 * 64
+    g = torch.Generator(device=DEV).manual_seed(P + K)
+    x = (torch.randn((K, ld), generator=g, device=DEV) * 0.05).to(dtype)
+    glob = (torch.randn(ld, generator=g, device=DEV) * 0.05).to(dtype)
+    x[:, P:] = float("nan")  # padding never contributes
+    got = mfl_amd.client_sqdist(x, glob, P)
+    ref = torch.stack([((x[k, :P] - glob[:P]).double() ** 2).sum() for k in range(K)])
+    rel = ((got - ref).abs() / ref.clamp_min(1e-300)).max().item()
+    assert rel < 1e-12, rel
+    assert torch.equal(got, mfl_amd.client_sqdist(x, glob, P))  # deterministic
+
+
 def test_client_sqdist_large_vs_fp64():
     K, P = 100, 25_000_000 + 3
     ld = (P + 63) // 64 * 64

@@ -157,3 +157,23 @@ def test_fpf_oracle_matches_reference_loop(name):
     if case.meta["full"]:
         # empty round 6 -> A_mat NaN (0/0 at :319) -> every later index scrubbed to 0
         assert np.count_nonzero(case.fpf[6]) > 0 and not np.any(case.fpf[7])
+
+
+@pytest.mark.parametrize("name", ["float64_key_k3", "float16_key_k3", "bfloat16_key_k3"])
+def test_distance_oracles_agree_other_dtypes(name):
+    """:291 on fp64 / fp16 / bf16 keys: torch.cat promotes the per-key
+    differences (fp64 + fp32 -> fp64; fp16 alone -> fp16; bf16 alone -> bf16)
+    and the norm is of that dtype.  The accurate restatement rounds to the same
+    dtype and agrees with ATen's norm to within one unit of that dtype."""
+    import torch
+
+    _, w_locals, _ = load_case(name)
+    w_glob = O.aggregate_torch(w_locals)
+    t = O.client_distances_torch(w_locals, w_glob)
+    e = O.client_distances_exact(w_locals, w_glob)
+    d = torch.cat([w_locals[1][1][k].reshape(-1) - w_glob[k].reshape(-1) for k in w_glob]).dtype
+    assert d == {"float64_key_k3": torch.float64, "float16_key_k3": torch.float16,
+                 "bfloat16_key_k3": torch.bfloat16}[name]
+    eps = torch.finfo(d).eps
+    assert t[0] == 0.0 and e[0] == 0.0
+    assert np.allclose(t, e, rtol=2 * eps, atol=0), (t, e)
