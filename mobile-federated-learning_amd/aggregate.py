@@ -52,6 +52,7 @@ import torch
 
 from . import _lib
 from .layout import KeyTable
+from .layout import _collect_ext as layout_collect_ext
 from .reduce import client_sqdist, reduce_packed
 
 __all__ = [
@@ -264,6 +265,11 @@ class DeviceAggregator:
         self._seg_weights = None  # weights of the zero-copy (segments) reduce
         # one round at a time per aggregator: the staging buffers are shared
         self._lock = threading.Lock()
+        # after a small fp32 round (fedavg_round_f32), the next round with the
+        # same key table runs its whole host side in one native call
+        # (fedavg_collect_ext.small_round); any other path clears this
+        self._fast_small = None
+        self.fast_rounds = 0  # rounds finished by the one-call native path
 
     # ------------------------------------------------------------------
     def begin_round(self, template, max_clients: int):
@@ -275,6 +281,7 @@ class DeviceAggregator:
         from .session import RoundSession
 
         self._check_no_open_session("begin_round")
+        self._fast_small = None
         sess = RoundSession(self, template, max_clients)
         self._session = weakref.ref(sess)
         return sess
@@ -304,6 +311,12 @@ class DeviceAggregator:
 
     def aggregate(self, w_locals, model_global=None):
         """``FedAvgTrainer.aggregate`` semantics; see the module docstring."""
+        fast = self._fast_small
+        if fast is not None and type(w_locals) is list and w_locals:
+            done = self._small_round_native(w_locals, fast)
+            if done is not None:
+                return done
+        self._fast_small = None
         prep = prepare(w_locals, model_global, self._table_hint)
         if not isinstance(prep, _Prepared):
             return prep  # empty list / no keys: answered on the host like the reference
@@ -507,7 +520,54 @@ class DeviceAggregator:
         self._last = {"table": table, "K": K, "dev": {torch.float32: (st.dev[:K], out_dev)}}
         results = table.unpack(g, out_host)
         self.last_profile = {"pack_issue_ms": 0.0, "h2d_kernel_d2h_ms": (time.perf_counter() - t0) * 1e3}
+        ext = layout_collect_ext()
+        if ext is not None and hasattr(ext, "small_round"):
+            import ctypes
+
+            es = g.keys
+            self._fast_small = {
+                "ext": ext, "table": table, "st": st, "names": [e.name for e in es],
+                "numel": [int(e.numel) for e in es], "offset": [int(e.offset) for e in es],
+                "kind": [int(k) for k in g.kind], "shapes": [tuple(int(d) for d in e.shape) for e in es],
+                "fn": ctypes.cast(lib.fedavg_round_f32, ctypes.c_void_p).value,
+                "threads": max(1, torch.get_num_threads()),
+            }
         return results
+
+    def _small_round_native(self, w_locals, fast):
+        """The next small round with the same key table, host side in ONE
+        native call (fedavg_collect_ext.small_round): weights, the walk over
+        every client's tensors, packing, fedavg_round_f32 and the result views
+        written into ``w_locals[0][1]``.  Returns that dict, or None when the
+        round needs the general path (it then raises or handles whatever the
+        native walk refused -- nothing has been written)."""
+        table, st = fast["table"], fast["st"]
+        K = len(w_locals)
+        g = table.groups[torch.float32]
+        if K > st.K or K * g.ld * 4 > self.SMALL_ROUND_BYTES or self._session_open():
+            return None
+        with self._lock:
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+            status, out_dev, out_host = fast["ext"].small_round(
+                w_locals, fast["names"], table._template, fast["numel"], fast["offset"], fast["kind"],
+                fast["shapes"], g.P, g.ld, st.host.data_ptr(), st.dev.data_ptr(), st.w_host.data_ptr(),
+                st.w_dev.data_ptr(), fast["fn"], fast["threads"], stream, self.device.index)
+        if status == 1:
+            return None
+        _lib.check(status, "fedavg_round_f32")
+        acc = w_locals[0][1]
+        self.fast_rounds += 1
+        self._last = {"table": table, "K": K, "dev": {torch.float32: (st.dev[:K], out_dev)}}
+        try:
+            self._last["refs"] = [weakref.ref(sd) for _, sd in w_locals]
+            self._last["acc"] = weakref.ref(acc)
+        except TypeError:  # plain dicts cannot be weakly referenced: no reuse
+            self._last.pop("dev", None)
+        return acc
+
+    def _session_open(self) -> bool:
+        sess = self._session() if self._session is not None else None
+        return sess is not None and not sess._finished
 
     def _reduce_groups(self, table: KeyTable, ptrs, weights) -> "OrderedDict[str, torch.Tensor]":
         K = ptrs.shape[0]

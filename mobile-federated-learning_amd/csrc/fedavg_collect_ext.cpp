@@ -89,7 +89,7 @@ static py::list unpack(const at::Tensor& flat, py::list offsets, py::list shapes
 }
 
 // small_round(w_locals, names, templ, numel, offset, kind, shapes, P, ld, rows_host, rows_dev, w_host, w_dev,
-//             round_fn, n_threads, stream, device_index) -> (status, out_dev, out_host)
+//             round_fn, n_threads, stream, out_device) -> (status, out_dev, out_host)
 //
 // The whole host side of a small fp32 round in one call -- what aggregate()
 // does in Python for a round whose key table is already known: the
@@ -111,7 +111,7 @@ using round_fn_t = int (*)(const int64_t*, int64_t, float*, float*, int64_t, int
 static py::tuple small_round(py::list w_locals, py::list names, py::list templ, const std::vector<int64_t>& numel,
                              const std::vector<int64_t>& offset, const std::vector<int64_t>& kind, py::list shapes,
                              int64_t P, int64_t ld, int64_t rows_host, int64_t rows_dev, int64_t w_host,
-                             int64_t w_dev, int64_t round_fn, int n_threads, int64_t stream, int64_t device_index) {
+                             int64_t w_dev, int64_t round_fn, int n_threads, int64_t stream, int64_t out_device) {
   const Py_ssize_t K = PyList_GET_SIZE(w_locals.ptr());
   const Py_ssize_t N = PyList_GET_SIZE(names.ptr());
   auto fallback = [] { return py::make_tuple(1, py::none(), py::none()); };
@@ -170,8 +170,10 @@ static py::tuple small_round(py::list w_locals, py::list names, py::list templ, 
       if (ok) {
         const at::Tensor& ten = THPVariable_Unpack(t);
         const at::Tensor& tp = THPVariable_Unpack(PyList_GET_ITEM(templ.ptr(), j));
+        // host clients only (client.py:96 returns net.cpu().state_dict()): the
+        // packer reads them with the CPU
         ok = ten.scalar_type() == tp.scalar_type() && ten.sizes() == tp.sizes() && ten.is_contiguous() &&
-             (device_index < 0 ? ten.is_cpu() : (ten.is_cuda() && ten.get_device() == device_index));
+             ten.is_cpu();
         if (ok) {
           int64_t* it = &items[(static_cast<size_t>(i) * N + j) * 4];
           it[0] = reinterpret_cast<int64_t>(ten.data_ptr());
@@ -186,8 +188,7 @@ static py::tuple small_round(py::list w_locals, py::list names, py::list templ, 
   }
   auto opts = at::TensorOptions().dtype(at::kFloat);
   at::Tensor out_host = at::empty({P}, opts.pinned_memory(true));
-  at::Tensor out_dev = at::empty({P}, opts.device(at::Device(at::kCUDA, static_cast<c10::DeviceIndex>(
-                                                      device_index < 0 ? 0 : device_index))));
+  at::Tensor out_dev = at::empty({P}, opts.device(at::Device(at::kCUDA, static_cast<c10::DeviceIndex>(out_device))));
   int rc;
   {
     py::gil_scoped_release nogil;

@@ -60,17 +60,31 @@ def main():
     A.prepare = t_prepare
     A.DeviceAggregator._reduce_groups = t_reduce
     prof = []
+    phases.update({"native_one_call": [], "dropin_functional": []})
+    fresh = lambda: [(counts[0], OrderedDict(dicts[0]))] + list(zip(counts[1:], dicts[1:]))  # noqa: E731
     for r in range(args.reps):
-        wl = [(counts[0], OrderedDict(dicts[0]))] + list(zip(counts[1:], dicts[1:]))
+        wl = fresh()
+        agg._fast_small = None  # the general path (prepare + _reduce_groups)
         t0 = time.perf_counter()
         agg.aggregate(wl)
         phases["total"].append(time.perf_counter() - t0)
         prof.append(dict(agg.last_profile))
-        wl2 = [(counts[0], OrderedDict(dicts[0]))] + list(zip(counts[1:], dicts[1:]))
+        wl = fresh()  # the next round: the native one-call path (fedavg_collect_ext.small_round)
+        t0 = time.perf_counter()
+        out = agg.aggregate(wl)
+        phases["native_one_call"].append(time.perf_counter() - t0)
+        assert out is wl[0][1]
+        wl = fresh()  # what install()'d FedAvgTrainer.aggregate runs: the functional form
+        t0 = time.perf_counter()
+        mfl_amd.aggregate(wl, device=dev)
+        phases["dropin_functional"].append(time.perf_counter() - t0)
+        wl2 = fresh()
         t0 = time.perf_counter()
         O.aggregate_torch(wl2)
         phases["cpu_ref"].append(time.perf_counter() - t0)
     out = {k: round(float(np.median(v[10:])) * 1e6, 1) for k, v in phases.items()}
+    out["native_fast_rounds"] = agg.fast_rounds
+    out["dropin_vs_cpu"] = round(out["cpu_ref"] / out["dropin_functional"], 3)
     for k in prof[0]:
         out[k + "_us"] = round(float(np.median([p[k] for p in prof[10:]])) * 1e3, 1)
     out["K"] = args.K

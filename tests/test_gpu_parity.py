@@ -904,3 +904,53 @@ def test_open_session_blocks_aggregate():
         sess.add(n, sd)
     sess.finish(w_locals)
     agg.begin_round(w_locals[0][1], 10)  # allowed again
+
+
+# ---------------------------------------------------------------------------
+# small rounds: the one-call native host side (fedavg_collect_ext.small_round)
+# ---------------------------------------------------------------------------
+def test_small_round_native_path_rounds_bit_exact_and_fall_back():
+    """After one small fp32 round, the next rounds with the same key table run
+    their whole host side in one native call.  Every round is bit-exact vs the
+    reference's loop and returns w_locals[0][1]; the :291 cache stays valid;
+    and every input the native walk refuses falls back to the general path,
+    which raises the reference's exception (nothing written before)."""
+    import copy
+    for name in ["mnist_lr_k10", "mnist_lr_k100", "resnet_like_bn_k5", "flat_k10_p65"]:
+        meta, w_locals, expected = load_case(name)
+        agg = mfl_amd.DeviceAggregator(DEV)
+        for r in range(4):
+            wl = copy.deepcopy(w_locals)
+            out = agg.aggregate(wl)
+            assert out is wl[0][1]
+            for k, exp in expected.items():
+                assert_bits(out[k], exp, f"{name}/{k} round {r}")
+            assert list(out.keys()) == list(expected.keys())
+            if not any(t.dtype == torch.bool for _, sd in wl for t in sd.values()):
+                norms = agg.client_distances(wl, out)  # rows the native round left in HBM
+                assert norms[0] == 0.0 and np.all(np.isfinite(norms))
+        assert agg.fast_rounds == 3, name
+    # fallbacks: the general path sees (and raises for) what the walk refused
+    meta, w_locals, expected = load_case("mnist_lr_k10")
+    agg = mfl_amd.DeviceAggregator(DEV)
+    agg.aggregate(copy.deepcopy(w_locals))
+    wl = copy.deepcopy(w_locals)
+    wl = [(0, sd) for _, sd in wl]
+    with pytest.raises(ZeroDivisionError):
+        agg.aggregate(wl)
+    wl = copy.deepcopy(w_locals)
+    del wl[3][1][next(iter(wl[3][1]))]
+    with pytest.raises(KeyError):
+        agg.aggregate(wl)
+    wl = copy.deepcopy(w_locals)
+    wl = [(float(n), sd) for n, sd in wl]  # float counts: the general path (Python true division)
+    ref = O.aggregate_torch(copy.deepcopy(wl))
+    out = agg.aggregate(wl)
+    for k in ref:
+        assert_bits(out[k], ref[k], f"float counts {k}")
+    before = agg.fast_rounds
+    wl = copy.deepcopy(w_locals)
+    out = agg.aggregate(wl)  # back on the native path after the general one
+    for k, exp in expected.items():
+        assert_bits(out[k], exp, f"after fallback {k}")
+    assert agg.fast_rounds == before + 1
