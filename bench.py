@@ -478,33 +478,67 @@ def main(argv=None):
     launches_per_call = sched["launches"] if sched else 1
     ev_pairs = []
 
-    def local_reduce(clients, w, P, out):
-        mfl_amd.reduce_packed(clients, w, P, out, tuned=tuned)
+    # Kernel timing: event pairs attached to the reduce's own launches
+    # (fedavg_reduce_f32_timed / hipExtLaunchKernel: the first launch's start,
+    # the last one's end), handed to ShardedReducer.step per chunk.  A
+    # separate hipEventRecord pair around each call serialises back-to-back
+    # launches (~8 us per call on MI355X), and even launch-attached events
+    # cost ~5 us of wall time per call (profiled dispatch), so calls shorter
+    # than ~1 GB of traffic are timed on a sample: every `sample_every`-th
+    # reduce call of the timed region.  The pool is created and recorded once
+    # before the timed region (torch creates HIP events lazily).
+    bytes_call_est = algorithmic_bytes(K, red.plan.block)
+    sample_every = 1 if bytes_call_est >= 1e9 else (4 if bytes_call_est >= 2.5e8 else 8)
+    n_calls = args.steps * red.plan.chunks * passes
+    pool = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            for _ in range(-(-n_calls // sample_every))]
+    for a, b in pool:
+        a.record()
+        b.record()
+    torch.cuda.synchronize()
+    call_no = [0]
+    timing_on = [False]
 
-    def timed_local_reduce(clients, w, P, out):
-        s = torch.cuda.Event(enable_timing=True)
-        e = torch.cuda.Event(enable_timing=True)
-        s.record()
-        mfl_amd.reduce_packed(clients, w, P, out, tuned=tuned)
-        e.record()
-        ev_pairs.append((s, e))
+    def timing(c):
+        if not timing_on[0]:
+            return None
+        i = call_no[0]
+        call_no[0] += 1
+        if i % sample_every:
+            return None
+        pair = pool[len(ev_pairs)]
+        ev_pairs.append(pair)
+        return pair
+
+    if tuned is not None:
+        # tuning variants (probe library): record pairs around sampled calls
+        def local_reduce(clients, w, P, out):
+            if timing_on[0] and call_no[0] % sample_every == 0:
+                st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                st.record()
+                mfl_amd.reduce_packed(clients, w, P, out, tuned=tuned)
+                en.record()
+                ev_pairs.append((st, en))
+            else:
+                mfl_amd.reduce_packed(clients, w, P, out, tuned=tuned)
+            if timing_on[0]:
+                call_no[0] += 1
+        red.local_reduce = local_reduce
 
     if passes > 1:
         # every pass reduces the resident [K, P_pass] rows into its own slice
         # of the [passes * P_pass] model (the pass's columns; the data of
         # pass p is pass 0's buffer -- 400 GB of distinct rows do not fit)
         red.pass_out = torch.empty(passes * red.plan.local_cols, dtype=torch.float32, device=dev)
-        one_pass = red.step
 
-        def step_passes(w):
+        def red_step(w):
             for p in range(passes):
                 red.local_out = red.pass_out[p * red.plan.local_cols:(p + 1) * red.plan.local_cols]
-                one_pass(w)
-        red_step = step_passes
+                red.step(w, timing=timing)
     else:
-        red_step = red.step
+        def red_step(w):
+            red.step(w, timing=timing)
 
-    red.local_reduce = local_reduce
     for _ in range(args.warmup):
         red_step(w_dev)
     torch.cuda.synchronize()
@@ -544,7 +578,7 @@ def main(argv=None):
         ev_pairs.clear()
         calls_per_event = red.plan.chunks * passes
     else:
-        red.local_reduce = timed_local_reduce
+        timing_on[0] = True
         calls_per_event = 1
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -554,7 +588,7 @@ def main(argv=None):
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    red.local_reduce = local_reduce
+    timing_on[0] = False
 
     kernel_ms = [s.elapsed_time(e) / calls_per_event for s, e in ev_pairs]
     t = torch.tensor([elapsed, float(np.mean(kernel_ms))], dtype=torch.float64, device=dev)
@@ -604,6 +638,10 @@ def main(argv=None):
             "bytes_per_launch": bytes_call // launches_per_call,
             "avg_launch_ms": round(kernel_ms_max / launches_per_call, 4),
             "launches": len(kernel_ms) * calls_per_event * launches_per_call,
+            "timing": ("hipGraph replay bracketed by events" if args.graph else
+                       "launch-attached HIP events (hipExtLaunchKernel) on the launch stream, "
+                       + ("every reduce call" if sample_every == 1 else f"every {sample_every}th reduce call")
+                       + " of the timed region"),
         }
         tj = args.traffic_json or str(ROOT / "profiles" / f"traffic_{args.workload}.json")
         if Path(tj).exists():

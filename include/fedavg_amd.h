@@ -206,6 +206,19 @@ int fedavg_upload_shard(void* dst, int64_t dst_pitch_bytes, const void* host_src
 int fedavg_weights_f32(const int64_t* sample_nums, int64_t K, float* weights);
 
 /*
+ * fedavg_reduce_f32 (aligned production path) with its kernel launches
+ * bracketed by two caller-created hipEvent_t's attached to the launches
+ * themselves (hipExtLaunchKernel): start_event fires when the first launch
+ * starts, stop_event when the last one ends.  hipEventElapsedTime of the pair
+ * is the reduce's kernel time with no extra barrier packets in the stream
+ * (a separate hipEventRecord pair serialises back-to-back launches and cost
+ * ~8 us per call on MI355X).  Same bits as fedavg_reduce_f32; the
+ * measurement hook bench.py uses.  FEDAVG_EALIGN for the unaligned paths.
+ */
+int fedavg_reduce_f32_timed(const float* clients, int64_t K, int64_t P, int64_t ld, const float* weights,
+                            float* out, void* stream, void* start_event, void* stop_event);
+
+/*
  * The schedule fedavg_reduce_f32() uses for an aligned [K, P] problem:
  * rows per load batch, 16-B column slices per thread, nontemporal loads, and
  * the number of round-split launches.  Host-only query (bench.py names the kernel from it).

@@ -21,6 +21,7 @@ SIGNATURES = {
     "fedavg_abi_version": (_c_int, []),
     "fedavg_last_error": (ctypes.c_char_p, []),
     "fedavg_reduce_f32": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp]),
+    "fedavg_reduce_f32_timed": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp]),
     "fedavg_reduce_ptrs_f32": (_c_int, [_vp, _c_i64, _c_i64, _vp, _vp, _vp]),
     "fedavg_reduce_f64": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp]),
     "fedavg_reduce_f16": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp]),

@@ -19,6 +19,7 @@
 // distance pass).  Templates and inline helpers live here.
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -134,6 +135,36 @@ __device__ __forceinline__ int64_t wave_search_last_le(Start start, int64_t n, i
     hi = hi < lo + step ? hi : lo + step;
   }
   return lo;
+}
+
+// Wave-wide fp64 sum through DPP lane moves (VALU, no LDS round trips):
+// quad_perm [1,0,3,2] and [2,3,0,1] make quad sums, row_half_mirror and
+// row_mirror make 16-lane row sums, row_bcast:15 (rows 1, 3) and row_bcast:31
+// (rows 2, 3) carry them up to row 3; lane 63 then holds the total, read
+// back as a wave-uniform value.  A __shfl_xor tree (ds_bpermute, an LDS
+// round trip per step, 12 per fp64 sum) serialises ~6 LDS latencies per sum;
+// the per-client sums of the :291 pass do one per client row.  Same addends,
+// fixed order: deterministic, but not the shfl tree's bits.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ double dpp_move_f64(double v) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, static_cast<int>(static_cast<uint32_t>(u)), CTRL, ROW_MASK, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, static_cast<int>(static_cast<uint32_t>(u >> 32)), CTRL, ROW_MASK, 0xF,
+                                             false);
+  return __builtin_bit_cast(double, (static_cast<uint64_t>(static_cast<uint32_t>(hi)) << 32) | static_cast<uint32_t>(lo));
+}
+
+__device__ __forceinline__ double wave_sum_dpp(double v) {
+  v += dpp_move_f64<0xB1, 0xF>(v);   // quad_perm [1,0,3,2]
+  v += dpp_move_f64<0x4E, 0xF>(v);   // quad_perm [2,3,0,1]
+  v += dpp_move_f64<0x141, 0xF>(v);  // row_half_mirror
+  v += dpp_move_f64<0x140, 0xF>(v);  // row_mirror
+  v += dpp_move_f64<0x142, 0xA>(v);  // row_bcast:15 into rows 1 and 3
+  v += dpp_move_f64<0x143, 0xC>(v);  // row_bcast:31 into rows 2 and 3
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(u), 63);
+  const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(u >> 32), 63);
+  return __builtin_bit_cast(double, (static_cast<uint64_t>(hi) << 32) | lo);
 }
 
 inline unsigned grid_for(int64_t items, int per_block) {
@@ -360,8 +391,8 @@ inline int cu_count() {
 // launches re-aligns them (a multi-round launch lets blocks drift apart and
 // leaves a half-empty last round).
 template <int U, int C, bool NT>
-void launch_split(const float* clients, int K, int64_t ld, int64_t P, const float* W, float* out, int max_blocks,
-                  hipStream_t s) {
+void launch_split_ev(const float* clients, int K, int64_t ld, int64_t P, const float* W, float* out, int max_blocks,
+                     hipStream_t s, hipEvent_t ev_start, hipEvent_t ev_stop) {
   const int64_t nvec = (P + 3) / 4;
   const int64_t span = static_cast<int64_t>(kBlock) * C;
   const int64_t resident = max_blocks > 0 ? max_blocks : resident_blocks(reduce_f32x4_var_kernel<U, C, NT, false>);
@@ -372,9 +403,17 @@ void launch_split(const float* clients, int K, int64_t ld, int64_t P, const floa
   for (int64_t v0 = 0; v0 < nvec; v0 += per) {
     const int64_t n = (nvec - v0) < per ? (nvec - v0) : per;
     const int tail = (v0 + n == nvec) ? static_cast<int>(P & 3) : 0;
-    hipLaunchKernelGGL((reduce_f32x4_var_kernel<U, C, NT, false>), dim3(static_cast<unsigned>((n + span - 1) / span)),
-                       dim3(kBlock), 0, s, X + v0, K, ld / 4, n, tail, W, out + v0 * 4);
+    // launch-attached timing events: the first launch's start, the last one's end
+    hipExtLaunchKernelGGL((reduce_f32x4_var_kernel<U, C, NT, false>), dim3(static_cast<unsigned>((n + span - 1) / span)),
+                          dim3(kBlock), 0, s, v0 == 0 ? ev_start : nullptr, v0 + n >= nvec ? ev_stop : nullptr, 0,
+                          X + v0, K, ld / 4, n, tail, W, out + v0 * 4);
   }
+}
+
+template <int U, int C, bool NT>
+void launch_split(const float* clients, int K, int64_t ld, int64_t P, const float* W, float* out, int max_blocks,
+                  hipStream_t s) {
+  launch_split_ev<U, C, NT>(clients, K, ld, P, W, out, max_blocks, s, nullptr, nullptr);
 }
 
 // Row reduce through buffer descriptors: a full column group reads client
@@ -456,7 +495,7 @@ __global__ __launch_bounds__(BS) void reduce_f32x4_buf_kernel(const f32x4* __res
 // 256-thread groups would leave the CUs unevenly loaded)
 template <int U, int C, int BS = kBlock>
 void launch_split_buf(const float* clients, int K, int64_t ld, int64_t P, const float* W, float* out, int max_blocks,
-                      hipStream_t s) {
+                      hipStream_t s, hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr) {
   const int64_t nvec = (P + 3) / 4;
   const int64_t span = static_cast<int64_t>(BS) * C;
   const int64_t resident =
@@ -468,8 +507,9 @@ void launch_split_buf(const float* clients, int K, int64_t ld, int64_t P, const 
   for (int64_t v0 = 0; v0 < nvec; v0 += per) {
     const int64_t n = (nvec - v0) < per ? (nvec - v0) : per;
     const int tail = (v0 + n == nvec) ? static_cast<int>(P & 3) : 0;
-    hipLaunchKernelGGL((reduce_f32x4_buf_kernel<U, C, BS>), dim3(static_cast<unsigned>((n + span - 1) / span)),
-                       dim3(BS), 0, s, X + v0, K, ld / 4, n, tail, W, out + v0 * 4);
+    hipExtLaunchKernelGGL((reduce_f32x4_buf_kernel<U, C, BS>), dim3(static_cast<unsigned>((n + span - 1) / span)),
+                          dim3(BS), 0, s, v0 == 0 ? ev_start : nullptr, v0 + n >= nvec ? ev_stop : nullptr, 0,
+                          X + v0, K, ld / 4, n, tail, W, out + v0 * 4);
   }
 }
 

@@ -26,11 +26,7 @@ __device__ __forceinline__ double sq4_add(double acc, f32x4 d) {
   return __builtin_fma(w, w, acc);
 }
 
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
+__device__ __forceinline__ double wave_sum(double v) { return wave_sum_dpp(v); }
 
 // Block b of a launch covers C*256 column slices starting at slice
 // b*C*256 of that launch's window; its waves write partials at global wave
@@ -82,22 +78,68 @@ __global__ __launch_bounds__(kBlock) void client_sqdist_f32x4_kernel(
   }
 }
 
-// The same pass through buffer descriptors: block b's slice of every client
-// row (and of the model) is one descriptor whose base sits in SGPRs and whose
-// record count ends at the window's last float4, so a lane past the end reads
-// 0 from the hardware range check (x = g = 0, d = 0) instead of a predicated
-// load; each lane's slices are 32-bit offsets shared by every row.  Same
-// per-wave partial layout and order as client_sqdist_f32x4_kernel<U, C>.
+// The same pass through buffer descriptors, split by column group.  A FULL
+// group (every slice valid, no P % 4 tail) reads client row k through one
+// descriptor whose base sits in SGPRs, with each lane's slice as a 32-bit
+// offset shared by every row, and forms d = x - g with no masking at all --
+// the reduce's register budget (reduce_f32x4_buf_kernel) plus the group's
+// model slice g.  The ragged last group keeps per-slice masks and a record
+// count that ends at the window's last float4 (lanes past it read 0).  Same
+// per-wave partial layout as client_sqdist_f32x4_kernel<U, C>.
+template <int U, int C>
+__device__ __forceinline__ void sqdist_rows_store(double acc, double* partials, int64_t row, int64_t nwaves,
+                                                  int64_t wave_id) {
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) partials[row * nwaves + wave_id] = acc;
+}
+
 template <int U, int C>
 __global__ __launch_bounds__(kBlock) void client_sqdist_buf_kernel(
     const f32x4* __restrict__ X, int K, int64_t ld4, int64_t nvec, int tail, const f32x4* __restrict__ G,
     double* __restrict__ partials, int64_t nwaves, int64_t wave_base) {
-  const int lane = threadIdx.x & 63;
   const int64_t wave_id = wave_base + static_cast<int64_t>(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
-  const int64_t blk0 = static_cast<int64_t>(blockIdx.x) * kBlock * C;
-  const int64_t left = nvec - blk0;
-  const int bytes = static_cast<int>((left < kBlock * C ? left : kBlock * C) * 16);
+  constexpr int64_t span = static_cast<int64_t>(kBlock) * C;
+  const int64_t blk0 = static_cast<int64_t>(blockIdx.x) * span;
   uint32_t off[C];
+#pragma unroll
+  for (int j = 0; j < C; ++j) off[j] = 16u * (threadIdx.x + j * kBlock);
+  if (blk0 + span < nvec || (blk0 + span == nvec && tail == 0)) {
+    constexpr int bytes = static_cast<int>(span * 16);
+    f32x4 g[C];
+    {
+      const __amdgpu_buffer_rsrc_t rg = uniform_rsrc(G + blk0, bytes);
+#pragma unroll
+      for (int j = 0; j < C; ++j) g[j] = ld_rsrc_nt(rg, off[j]);
+    }
+    int k = 0;
+    for (; k + U <= K; k += U) {
+      f32x4 xs[U][C];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const __amdgpu_buffer_rsrc_t r = uniform_rsrc(X + static_cast<int64_t>(k + u) * ld4 + blk0, bytes);
+#pragma unroll
+        for (int j = 0; j < C; ++j) xs[u][j] = ld_rsrc_nt(r, off[j]);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        double acc = 0.0;
+#pragma unroll
+        for (int j = 0; j < C; ++j) acc = sq4_add(acc, xs[u][j] - g[j]);  // fp32 difference, as the reference
+        sqdist_rows_store<U, C>(acc, partials, k + u, nwaves, wave_id);
+      }
+    }
+    for (; k < K; ++k) {
+      const __amdgpu_buffer_rsrc_t r = uniform_rsrc(X + static_cast<int64_t>(k) * ld4 + blk0, bytes);
+      double acc = 0.0;
+#pragma unroll
+      for (int j = 0; j < C; ++j) acc = sq4_add(acc, ld_rsrc_nt(r, off[j]) - g[j]);
+      sqdist_rows_store<U, C>(acc, partials, k, nwaves, wave_id);
+    }
+    return;
+  }
+  // ragged last group: masked slices, record count ends at the last float4
+  const int64_t left = nvec - blk0;
+  const int bytes = static_cast<int>((left < span ? left : span) * 16);
   int nv[C];  // valid elements of slice j (0..4): padding lanes never contribute
   f32x4 g[C];
   {
@@ -105,40 +147,25 @@ __global__ __launch_bounds__(kBlock) void client_sqdist_buf_kernel(
 #pragma unroll
     for (int j = 0; j < C; ++j) {
       const int64_t v = blk0 + threadIdx.x + static_cast<int64_t>(j) * kBlock;
-      off[j] = 16u * (threadIdx.x + j * kBlock);
       nv[j] = v >= nvec ? 0 : (tail != 0 && v == nvec - 1 ? tail : 4);
       g[j] = ld_rsrc_nt(rg, off[j]);
     }
   }
-  for (int k = 0; k < K; k += U) {
-    const int rows = (K - k) < U ? (K - k) : U;
-    f32x4 xs[U][C];
+  for (int k = 0; k < K; ++k) {
+    const __amdgpu_buffer_rsrc_t r = uniform_rsrc(X + static_cast<int64_t>(k) * ld4 + blk0, bytes);
+    double acc = 0.0;
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (u < rows) {
-        const __amdgpu_buffer_rsrc_t r = uniform_rsrc(X + static_cast<int64_t>(k + u) * ld4 + blk0, bytes);
-#pragma unroll
-        for (int j = 0; j < C; ++j) xs[u][j] = ld_rsrc_nt(r, off[j]);
+    for (int j = 0; j < C; ++j) {
+      f32x4 d = ld_rsrc_nt(r, off[j]) - g[j];
+      if (nv[j] < 4) {  // select (not multiply): padding may hold NaN/inf
+        d.x = nv[j] > 0 ? d.x : 0.f;
+        d.y = nv[j] > 1 ? d.y : 0.f;
+        d.z = nv[j] > 2 ? d.z : 0.f;
+        d.w = 0.f;
       }
+      acc = sq4_add(acc, d);
     }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (u >= rows) break;
-      double acc = 0.0;
-#pragma unroll
-      for (int j = 0; j < C; ++j) {
-        f32x4 d = xs[u][j] - g[j];  // fp32 difference, as the reference forms it
-        if (nv[j] < 4) {            // select (not multiply): padding may hold NaN/inf
-          d.x = nv[j] > 0 ? d.x : 0.f;
-          d.y = nv[j] > 1 ? d.y : 0.f;
-          d.z = nv[j] > 2 ? d.z : 0.f;
-          d.w = 0.f;
-        }
-        acc = sq4_add(acc, d);
-      }
-      acc = wave_sum(acc);
-      if (lane == 0) partials[static_cast<int64_t>(k + u) * nwaves + wave_id] = acc;
-    }
+    sqdist_rows_store<U, C>(acc, partials, k, nwaves, wave_id);
   }
 }
 
@@ -236,13 +263,20 @@ __global__ __launch_bounds__(kBlock) void client_sqdist_finalize_kernel(const do
   if (threadIdx.x == 0) out[k] = red[0];
 }
 
-// Production schedule of the distance pass: 32 x 16-B loads in flight per
-// thread (U4 x C8, as the reduce) in one launch; scripts/dist_variants.py
-// (profiles/sweeps/r01_dist_*.jsonl) measured round-split launches within 1 %
-// of it and the first version (U4 x C4) 6 % behind.
+// Global-pointer schedule (the fp64/fp16/bf16 passes and the probe
+// variants): 32 x 16-B loads in flight per thread (U4 x C8) in one launch;
+// scripts/dist_variants.py (profiles/sweeps/r01_dist_*.jsonl) measured
+// round-split launches within 1 % of it and U4 x C4 6 % behind.
 constexpr int kDistCols = 8;
 constexpr int kDistRows = 4;
-constexpr int kDistBlocksPerLaunch = 0;  // one launch: measured 1 % ahead of round-split here
+// fp32 production (fedavg_client_sqdist_f32): the buffer-descriptor kernel at
+// U2 x C16 in one launch -- full column groups read each row through one
+// SGPR descriptor with no masking, 64 KiB contiguous per row per block, the
+// reduce's winning shape: 6,818-6,840 GB/s vs 6,520-6,531 for the
+// global-pointer U4 x C8 (scripts/dist_variants.py, profiles/r02/dist_variants.jsonl).
+// U4 x C8 remains the fp64/fp16/bf16 passes' schedule.
+constexpr int kDistBufRows = 2;
+constexpr int kDistBufCols = 16;
 
 int64_t sqdist_waves_for(int64_t P, int cols) {
   const int64_t nvec = (P + 3) / 4;
@@ -275,6 +309,7 @@ void launch_sqdist(const float* clients, int K, int64_t ld, int64_t P, const flo
   }
 }
 
+#ifdef FEDAVG_TUNING  // the global-pointer variants (probe library)
 int sqdist_impl(const float* clients, int64_t K, int64_t P, int64_t ld, const float* glob, double* workspace,
                 int64_t workspace_elems, double* sumsq, int unroll, int cols, int max_blocks, void* stream) {
   const char* what = "fedavg_client_sqdist_f32";
@@ -302,6 +337,7 @@ int sqdist_impl(const float* clients, int64_t K, int64_t P, int64_t ld, const fl
                      nwaves, sumsq);
   return launch_status(what);
 }
+#endif  // FEDAVG_TUNING
 
 int64_t sqdist_vec_waves(int64_t nvec, int cols) {
   const int64_t blocks = (nvec + kBlock * cols - 1) / (kBlock * cols);
@@ -336,6 +372,39 @@ int sqdist_vec_impl(const void* clients, int64_t K, int64_t P, int64_t ld, const
   return launch_status(what);
 }
 
+int sqdist_buf_impl(const float* clients, int64_t K, int64_t P, int64_t ld, const float* glob, double* workspace,
+                    int64_t workspace_elems, double* sumsq, int unroll, int cols, int max_blocks, void* stream,
+                    const char* what) {
+  int rc = check_common(clients, K, P, ld, glob, sumsq, what);
+  if (rc) return rc;
+  if (P == 0) return set_error(FEDAVG_EINVAL, "%s: P must be >= 1", what);
+  if (!aligned16(clients) || !aligned16(glob) || (ld % 4) != 0)
+    return set_error(FEDAVG_EALIGN, "%s: needs 16-B aligned clients/glob and ld %% 4 == 0", what);
+  if (cols != 4 && cols != 8 && cols != 12 && cols != 16)
+    return set_error(FEDAVG_EMODE, "%s: cols must be 4, 8, 12 or 16", what);
+  const int64_t nwaves = sqdist_waves_for(P, cols);
+  if (!workspace || workspace_elems < K * nwaves)
+    return set_error(FEDAVG_EINVAL, "%s: workspace needs %lld doubles", what, (long long)(K * nwaves));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int k = static_cast<int>(K);
+  switch (unroll * 100 + cols) {
+    case 408: launch_sqdist<4, 8, true>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    case 804: launch_sqdist<8, 4, true>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    case 216: launch_sqdist<2, 16, true>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    case 116: launch_sqdist<1, 16, true>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    case 112: launch_sqdist<1, 12, true>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    case 212: launch_sqdist<2, 12, true>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    case 208: launch_sqdist<2, 8, true>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    case 808: launch_sqdist<8, 8, true>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    default: return set_error(FEDAVG_EMODE, "%s: unsupported unroll=%d cols=%d", what, unroll, cols);
+  }
+  rc = launch_status(what);
+  if (rc) return rc;
+  hipLaunchKernelGGL(client_sqdist_finalize_kernel, dim3(static_cast<unsigned>(K)), dim3(kBlock), 0, s, workspace,
+                     nwaves, sumsq);
+  return launch_status(what);
+}
+
 }  // namespace
 
 extern "C" {
@@ -347,8 +416,8 @@ int64_t fedavg_client_sqdist_workspace(int64_t K, int64_t P) {
 
 int fedavg_client_sqdist_f32(const float* clients, int64_t K, int64_t P, int64_t ld, const float* glob,
                              double* workspace, int64_t workspace_elems, double* sumsq, void* stream) {
-  return sqdist_impl(clients, K, P, ld, glob, workspace, workspace_elems, sumsq, kDistRows, kDistCols,
-                     kDistBlocksPerLaunch, stream);
+  return sqdist_buf_impl(clients, K, P, ld, glob, workspace, workspace_elems, sumsq, kDistBufRows, kDistBufCols,
+                         0, stream, "fedavg_client_sqdist_f32");
 }
 
 int64_t fedavg_client_sqdist_workspace_elems(int64_t K, int64_t P, int64_t elem_size) {
@@ -387,31 +456,8 @@ int fedavg_client_sqdist_variant(const float* clients, int64_t K, int64_t P, int
 int fedavg_client_sqdist_buf(const float* clients, int64_t K, int64_t P, int64_t ld, const float* glob,
                              double* workspace, int64_t workspace_elems, double* sumsq, int unroll, int cols,
                              int max_blocks, void* stream) {
-  const char* what = "fedavg_client_sqdist_buf";
-  int rc = check_common(clients, K, P, ld, glob, sumsq, what);
-  if (rc) return rc;
-  if (P == 0) return set_error(FEDAVG_EINVAL, "%s: P must be >= 1", what);
-  if (!aligned16(clients) || !aligned16(glob) || (ld % 4) != 0)
-    return set_error(FEDAVG_EALIGN, "%s: needs 16-B aligned clients/glob and ld %% 4 == 0", what);
-  if (cols != 4 && cols != 8 && cols != 16) return set_error(FEDAVG_EMODE, "%s: cols must be 4, 8 or 16", what);
-  const int64_t nwaves = sqdist_waves_for(P, cols);
-  if (!workspace || workspace_elems < K * nwaves)
-    return set_error(FEDAVG_EINVAL, "%s: workspace needs %lld doubles", what, (long long)(K * nwaves));
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  const int k = static_cast<int>(K);
-  switch (unroll * 100 + cols) {
-    case 408: launch_sqdist<4, 8, true>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
-    case 804: launch_sqdist<8, 4, true>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
-    case 216: launch_sqdist<2, 16, true>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
-    case 208: launch_sqdist<2, 8, true>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
-    case 808: launch_sqdist<8, 8, true>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
-    default: return set_error(FEDAVG_EMODE, "%s: unsupported unroll=%d cols=%d", what, unroll, cols);
-  }
-  rc = launch_status(what);
-  if (rc) return rc;
-  hipLaunchKernelGGL(client_sqdist_finalize_kernel, dim3(static_cast<unsigned>(K)), dim3(kBlock), 0, s, workspace,
-                     nwaves, sumsq);
-  return launch_status(what);
+  return sqdist_buf_impl(clients, K, P, ld, glob, workspace, workspace_elems, sumsq, unroll, cols, max_blocks, stream,
+                         "fedavg_client_sqdist_buf");
 }
 #endif  // FEDAVG_TUNING
 

@@ -540,28 +540,28 @@ Schedule choose_f32_schedule(int64_t K, int64_t P, int64_t ld) {
 }
 
 void launch_production_f32(const float* clients, int K, int64_t ld, int64_t P, const float* W, float* out,
-                           hipStream_t s) {
+                           hipStream_t s, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
   const Schedule sc = choose_f32_schedule(K, P, ld);
   const int bpl = sc.blocks_per_launch;
   const int key = sc.unroll * 100 + sc.cols;
   if (sc.nt) {
     switch (key) {
-      case 216: launch_split_buf<2, 16>(clients, K, ld, P, W, out, bpl, s); return;
-      case 408: launch_split<4, 8, true>(clients, K, ld, P, W, out, bpl, s); return;
-      case 804: launch_split<8, 4, true>(clients, K, ld, P, W, out, bpl, s); return;
-      case 802: launch_split<8, 2, true>(clients, K, ld, P, W, out, bpl, s); return;
-      case 1604: launch_split<16, 4, true>(clients, K, ld, P, W, out, bpl, s); return;
-      case 1601: launch_split<16, 1, true>(clients, K, ld, P, W, out, bpl, s); return;
-      default: launch_split<8, 1, true>(clients, K, ld, P, W, out, bpl, s); return;
+      case 216: launch_split_buf<2, 16>(clients, K, ld, P, W, out, bpl, s, e0, e1); return;
+      case 408: launch_split_ev<4, 8, true>(clients, K, ld, P, W, out, bpl, s, e0, e1); return;
+      case 804: launch_split_ev<8, 4, true>(clients, K, ld, P, W, out, bpl, s, e0, e1); return;
+      case 802: launch_split_ev<8, 2, true>(clients, K, ld, P, W, out, bpl, s, e0, e1); return;
+      case 1604: launch_split_ev<16, 4, true>(clients, K, ld, P, W, out, bpl, s, e0, e1); return;
+      case 1601: launch_split_ev<16, 1, true>(clients, K, ld, P, W, out, bpl, s, e0, e1); return;
+      default: launch_split_ev<8, 1, true>(clients, K, ld, P, W, out, bpl, s, e0, e1); return;
     }
   }
   switch (key) {
-    case 408: launch_split<4, 8, false>(clients, K, ld, P, W, out, bpl, s); return;
-    case 804: launch_split<8, 4, false>(clients, K, ld, P, W, out, bpl, s); return;
-    case 802: launch_split<8, 2, false>(clients, K, ld, P, W, out, bpl, s); return;
-    case 1604: launch_split<16, 4, false>(clients, K, ld, P, W, out, bpl, s); return;
-    case 1601: launch_split<16, 1, false>(clients, K, ld, P, W, out, bpl, s); return;
-    default: launch_split<8, 1, false>(clients, K, ld, P, W, out, bpl, s); return;
+    case 408: launch_split_ev<4, 8, false>(clients, K, ld, P, W, out, bpl, s, e0, e1); return;
+    case 804: launch_split_ev<8, 4, false>(clients, K, ld, P, W, out, bpl, s, e0, e1); return;
+    case 802: launch_split_ev<8, 2, false>(clients, K, ld, P, W, out, bpl, s, e0, e1); return;
+    case 1604: launch_split_ev<16, 4, false>(clients, K, ld, P, W, out, bpl, s, e0, e1); return;
+    case 1601: launch_split_ev<16, 1, false>(clients, K, ld, P, W, out, bpl, s, e0, e1); return;
+    default: launch_split_ev<8, 1, false>(clients, K, ld, P, W, out, bpl, s, e0, e1); return;
   }
 }
 
@@ -836,6 +836,20 @@ int fedavg_reduce_f32(const float* clients, int64_t K, int64_t P, int64_t ld, co
     return launch_status(what);
   }
   return reduce_f32_unaligned(clients, K, P, ld, weights, out, static_cast<hipStream_t>(stream), what);
+}
+
+int fedavg_reduce_f32_timed(const float* clients, int64_t K, int64_t P, int64_t ld, const float* weights,
+                            float* out, void* stream, void* start_event, void* stop_event) {
+  const char* what = "fedavg_reduce_f32_timed";
+  if (!start_event || !stop_event) return set_error(FEDAVG_EINVAL, "%s: both events are required", what);
+  if (!(aligned16(clients) && aligned16(out) && (ld % 4) == 0 && P > 0 && K > 0))
+    return set_error(FEDAVG_EALIGN, "%s: the production (16-B aligned, P > 0) path only", what);
+  int rc = check_common(clients, K, P, ld, weights, out, what);
+  if (rc) return rc;
+  if (!aligned4(weights)) return set_error(FEDAVG_EALIGN, "%s: weights must be 4-byte aligned", what);
+  launch_production_f32(clients, static_cast<int>(K), ld, P, weights, out, static_cast<hipStream_t>(stream),
+                        static_cast<hipEvent_t>(start_event), static_cast<hipEvent_t>(stop_event));
+  return launch_status(what);
 }
 
 int fedavg_f32_schedule_ld(int64_t K, int64_t P, int64_t ld, int* unroll, int* cols, int* nontemporal,

@@ -33,7 +33,7 @@ from typing import Callable, List, Optional, Sequence
 import torch
 import torch.distributed as dist
 
-from .reduce import ALIGN_ELEMS, reduce_packed
+from .reduce import ALIGN_ELEMS, PreparedReduce, reduce_packed
 
 __all__ = ["ShardPlan", "plan_shards", "ShardedReducer", "upload_segments"]
 
@@ -220,16 +220,42 @@ class ShardedReducer:
                 self.clients[:, pos:a].zero_()
             pos = max(pos, b)
 
-    def step(self, weights: torch.Tensor) -> Optional[torch.Tensor]:
-        """Reduce every local chunk; all-gather each as soon as it is ready."""
+    def _prepared_calls(self, weights: torch.Tensor):
+        """Per-chunk PreparedReduce calls of the HIP kernel for these weights
+        and the current ``local_out`` (rebuilt when either changes)."""
+        key = (weights.data_ptr(), weights.numel(), self.local_out.data_ptr())
+        cache = self.__dict__.setdefault("_calls", {})
+        calls = cache.get(key)
+        if calls is None:
+            S = self.plan.block
+            # each PreparedReduce keeps its tensors (and so these weights) alive
+            calls = [PreparedReduce(self.clients[:, c * S:(c + 1) * S], weights, S, self.local_out[c * S:(c + 1) * S])
+                     for c in range(self.plan.chunks)]
+            if len(cache) >= 8:
+                cache.clear()
+            cache[key] = calls
+        return calls
+
+    def step(self, weights: torch.Tensor, timing: Optional[Callable[[int], Optional[tuple]]] = None
+             ) -> Optional[torch.Tensor]:
+        """Reduce every local chunk; all-gather each as soon as it is ready.
+
+        ``timing(c)`` (optional): a recorded (start, stop) event pair for
+        chunk c's reduce, or None -- launch-attached kernel timing for the
+        HIP kernel (bench.py); ignored by an injected ``local_reduce``."""
         plan = self.plan
         S = plan.block
         works: List = []
+        fast = (self.local_reduce is _hip_local_reduce and self.device.type == "cuda"
+                and weights.dtype == torch.float32 and self.dtype == torch.float32)
+        calls = self._prepared_calls(weights) if fast else None
         for c in range(plan.chunks):
-            cols = slice(c * S, (c + 1) * S)
-            out_c = self.local_out[cols]
-            self.local_reduce(self.clients[:, cols], weights, S, out_c)
+            if calls is not None:
+                calls[c](events=timing(c) if timing is not None else None)
+            else:
+                self.local_reduce(self.clients[:, c * S:(c + 1) * S], weights, S, self.local_out[c * S:(c + 1) * S])
             if self.gather:
+                out_c = self.local_out[c * S:(c + 1) * S]
                 dst = self.full[c * plan.world_size * S:(c + 1) * plan.world_size * S]
                 works.append(dist.all_gather_into_tensor(dst, out_c, group=self.group, async_op=True))
             elif self.host_out is not None:

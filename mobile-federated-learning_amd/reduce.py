@@ -52,28 +52,8 @@ def _check_device_tensor(t: torch.Tensor, name: str):
         raise ValueError(f"{name} must be a CUDA (HIP) device tensor")
 
 
-def reduce_packed(
-    clients: torch.Tensor,
-    weights: torch.Tensor,
-    P: Optional[int] = None,
-    out: Optional[torch.Tensor] = None,
-    *,
-    splits: int = 1,
-    stream: Optional[torch.cuda.Stream] = None,
-    tuned: Optional[tuple] = None,
-) -> torch.Tensor:
-    """out[p] = sum_i clients[i, p] * weights[i], client 0 first (bit-exact).
-
-    clients : [K, ld] device tensor, row stride ld >= P, unit column stride.
-    weights : [K] device tensor (fp32; fp64 for fp64 clients).
-    P       : number of valid columns (default ``clients.shape[1]``).
-    splits  : 1 = exact sequential kernel; 2/4/8 = split-client fp32 variant
-              (tolerance-gated, not bit-exact).
-    tuned   : benchmarking hook for the fp32 kernel: (unroll, nontemporal) or
-              (unroll, nontemporal, cols, pipelined, max_blocks), see
-              include/fedavg_amd_tuning.h (probe library).  Every variant gives
-              the same bits.
-    """
+def _check_packed(clients: torch.Tensor, weights: torch.Tensor, P: Optional[int], out: Optional[torch.Tensor]):
+    """reduce_packed's argument checks; returns (K, ld, P, dtype, out), allocating ``out`` if None."""
     _check_device_tensor(clients, "clients")
     _check_device_tensor(weights, "weights")
     if clients.dim() != 2 or clients.stride(1) != 1:
@@ -98,6 +78,38 @@ def reduce_packed(
         _check_device_tensor(out, "out")
         if out.dtype != dtype or out.numel() < P or not out.is_contiguous() or out.device != clients.device:
             raise ValueError(f"out must be a contiguous device tensor of >= {P} {dtype}")
+    return K, ld, P, dtype, out
+
+
+def reduce_packed(
+    clients: torch.Tensor,
+    weights: torch.Tensor,
+    P: Optional[int] = None,
+    out: Optional[torch.Tensor] = None,
+    *,
+    splits: int = 1,
+    stream: Optional[torch.cuda.Stream] = None,
+    tuned: Optional[tuple] = None,
+    events: Optional[tuple] = None,
+) -> torch.Tensor:
+    """out[p] = sum_i clients[i, p] * weights[i], client 0 first (bit-exact).
+
+    clients : [K, ld] device tensor, row stride ld >= P, unit column stride.
+    weights : [K] device tensor (fp32; fp64 for fp64 clients).
+    P       : number of valid columns (default ``clients.shape[1]``).
+    splits  : 1 = exact sequential kernel; 2/4/8 = split-client fp32 variant
+              (tolerance-gated, not bit-exact).
+    events  : (start, stop) torch.cuda.Event pair, each recorded once before
+              (so the HIP event exists): the fp32 production launches are
+              bracketed by them at the launches themselves
+              (fedavg_reduce_f32_timed, hipExtLaunchKernel) -- kernel time
+              without the stream serialisation of a separate record pair.
+    tuned   : benchmarking hook for the fp32 kernel: (unroll, nontemporal) or
+              (unroll, nontemporal, cols, pipelined, max_blocks), see
+              include/fedavg_amd_tuning.h (probe library).  Every variant gives
+              the same bits.
+    """
+    K, ld, P, dtype, out = _check_packed(clients, weights, P, out)
     lib = _lib.load()
     s = _stream_handle(stream, clients.device)
     if splits != 1:
@@ -119,11 +131,60 @@ def reduce_packed(
             rc = lib.fedavg_reduce_f32_variant(clients.data_ptr(), K, P, ld, weights.data_ptr(), out.data_ptr(),
                                                int(unroll), int(nt), int(cols), int(pipe), int(max_blocks), s)
             _lib.check(rc, "fedavg_reduce_f32_variant", lib)
+    elif events is not None:
+        if dtype != torch.float32:
+            raise TypeError("launch-attached timing events are fp32 only")
+        e0, e1 = events
+        if not e0.cuda_event or not e1.cuda_event:
+            raise ValueError("record each timing event once before use (torch creates the HIP event lazily)")
+        rc = lib.fedavg_reduce_f32_timed(clients.data_ptr(), K, P, ld, weights.data_ptr(), out.data_ptr(), s,
+                                         e0.cuda_event, e1.cuda_event)
+        _lib.check(rc, "fedavg_reduce_f32_timed")
     else:
         fn = getattr(lib, _ENTRY[dtype])
         rc = fn(clients.data_ptr(), K, P, ld, weights.data_ptr(), out.data_ptr(), s)
         _lib.check(rc, _ENTRY[dtype])
     return out
+
+
+def _raw_stream(device: torch.device) -> int:
+    """The current stream's hipStream_t for ``device`` (torch's raw getter
+    when present: ~0.3 us instead of ~1.5 us for the Stream object)."""
+    get = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+    if get is not None:
+        return int(get(device.index if device.index is not None else torch.cuda.current_device()))
+    return int(torch.cuda.current_stream(device).cuda_stream)
+
+
+class PreparedReduce:
+    """One fp32 ``reduce_packed`` call on fixed tensors, validated once and
+    re-issued with a single ctypes call -- the per-step host path of the
+    sharded reducer (small, cache-resident workloads are launch-bound: the
+    Python checks of ``reduce_packed`` cost about as much as the kernel).
+    ``__call__(stream=None, events=None)``: on ``stream`` (default: the
+    device's current stream); ``events`` = a recorded (start, stop)
+    torch.cuda.Event pair attached to the launches (fedavg_reduce_f32_timed)."""
+
+    def __init__(self, clients: torch.Tensor, weights: torch.Tensor, P: int, out: torch.Tensor):
+        K, ld, P, dtype, out = _check_packed(clients, weights, P, out)
+        if dtype != torch.float32:
+            raise TypeError("PreparedReduce is the fp32 path")
+        self._args = (clients.data_ptr(), K, P, ld, weights.data_ptr(), out.data_ptr())
+        self._keep = (clients, weights, out)
+        self._device = clients.device
+        self._lib = _lib.load()
+        self._aligned = (clients.data_ptr() % 16 == 0 and out.data_ptr() % 16 == 0 and ld % 4 == 0 and P > 0)
+
+    def __call__(self, stream: Optional[torch.cuda.Stream] = None, events: Optional[tuple] = None) -> None:
+        s = int(stream.cuda_stream) if stream is not None else _raw_stream(self._device)
+        if events is not None and self._aligned:
+            rc = self._lib.fedavg_reduce_f32_timed(*self._args, s, events[0].cuda_event, events[1].cuda_event)
+            if rc:
+                _lib.check(rc, "fedavg_reduce_f32_timed")
+            return
+        rc = self._lib.fedavg_reduce_f32(*self._args, s)
+        if rc:
+            _lib.check(rc, "fedavg_reduce_f32")
 
 
 def reduce_tensors(

@@ -31,6 +31,10 @@ def main():
     ap.add_argument("--P", type=int, default=25_000_000)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--glob", nargs="*", default=["4,8,0", "4,8,768"], help="U,C,max_blocks of the global form")
+    ap.add_argument("--buf", nargs="*", default=["2,16,0", "2,16,512", "1,16,0", "1,16,768", "1,12,0", "2,12,0",
+                                                 "2,12,512", "4,8,0", "2,8,0"],
+                    help="U,C,max_blocks of the buffer-descriptor form")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -44,12 +48,11 @@ def main():
     n_ws = lib.fedavg_client_sqdist_workspace(K, P)
     work = torch.empty(n_ws, dtype=torch.float64, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
-    variants = [("production", None)] + [(f"U{u} C{c} mb{mb}", (u, c, mb)) for u, c, mb in
-                                         [(4, 4, 0), (4, 4, 768), (8, 4, 768), (4, 8, 768), (2, 8, 768), (4, 8, 0),
-                                          (4, 8, 512), (4, 8, 1024)]]
+    ap_glob = [tuple(int(t) for t in v.split(",")) for v in args.glob]
+    ap_buf = [tuple(int(t) for t in v.split(",")) for v in args.buf]
+    variants = [("production", None)] + [(f"U{u} C{c} mb{mb}", (u, c, mb)) for u, c, mb in ap_glob]
     # the buffer-descriptor form (fedavg_client_sqdist_buf)
-    variants += [(f"buf U{u} C{c} mb{mb}", ("buf", u, c, mb)) for u, c, mb in
-                 [(4, 8, 0), (4, 8, 768), (2, 16, 0), (2, 16, 768), (8, 4, 768), (2, 8, 768), (8, 8, 0)]]
+    variants += [(f"buf U{u} C{c} mb{mb}", ("buf", u, c, mb)) for u, c, mb in ap_buf]
     outs = {name: torch.empty(K, dtype=torch.float64, device=dev) for name, _ in variants}
 
     def run(name, v):

@@ -954,3 +954,29 @@ def test_small_round_native_path_rounds_bit_exact_and_fall_back():
     for k, exp in expected.items():
         assert_bits(out[k], exp, f"after fallback {k}")
     assert agg.fast_rounds == before + 1
+
+
+@pytest.mark.parametrize("K,P", [(10, 1_206_590), (100, 781_312), (3, 4099), (100, 25_000_000)])
+def test_timed_reduce_same_bits_and_kernel_time(K, P):
+    """fedavg_reduce_f32_timed (launch-attached events, bench.py's timing
+    hook) gives fedavg_reduce_f32's bits, and its event pair brackets the
+    reduce's launches (a positive time, below the host-side wall time)."""
+    import time
+    x = _clients(K, P, seed=P + 1)
+    w = _w(_weights(K))
+    base = mfl_amd.reduce_packed(x, w, P)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    e1.record()
+    torch.cuda.synchronize()
+    out = torch.full((P,), float("nan"), device=DEV)
+    t0 = time.perf_counter()
+    mfl_amd.reduce_packed(x, w, P, out, events=(e0, e1))
+    torch.cuda.synchronize()
+    wall_ms = (time.perf_counter() - t0) * 1e3
+    assert torch.equal(out.view(torch.int32), base.view(torch.int32))
+    ms = e0.elapsed_time(e1)
+    assert 0.0 < ms <= wall_ms
+    fresh = torch.cuda.Event(enable_timing=True)
+    with pytest.raises(ValueError):  # never recorded: no HIP event behind it yet
+        mfl_amd.reduce_packed(x, w, P, out, events=(fresh, e1))
