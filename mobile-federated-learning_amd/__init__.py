@@ -19,6 +19,7 @@ from .aggregate import (
     DeviceAggregator,
     FedAvgAggregateMixin,
     aggregate,
+    client_arena,
     client_distances,
     estimate_delta,
     default_aggregator,
@@ -36,6 +37,7 @@ __all__ = [
     "DeviceAggregator",
     "FedAvgAggregateMixin",
     "aggregate",
+    "client_arena",
     "client_distances",
     "estimate_delta",
     "client_sqdist",

@@ -65,6 +65,7 @@ __all__ = [
     "FedAvgAggregateMixin",
     "install",
     "default_aggregator",
+    "client_arena",
 ]
 
 
@@ -270,6 +271,7 @@ class DeviceAggregator:
         # (fedavg_collect_ext.small_round); any other path clears this
         self._fast_small = None
         self.fast_rounds = 0  # rounds finished by the one-call native path
+        self.arena_rounds = 0  # device rounds whose fp32 rows were the clients' own (client_arena layout)
 
     # ------------------------------------------------------------------
     def begin_round(self, template, max_clients: int):
@@ -326,7 +328,7 @@ class DeviceAggregator:
         on_device = self._client_device(table, dicts).type == "cuda"
         with self._lock:
             if on_device:
-                results = self._reduce_groups_device(table, ptrs, weights)
+                results = self._reduce_groups_device(table, ptrs, weights, dicts)
             else:
                 results = self._reduce_groups(table, ptrs, weights)
         del keepalive
@@ -384,6 +386,8 @@ class DeviceAggregator:
     # tensors (fedavg_reduce_segments_f32: 4 B per element instead of the
     # rows' 12); FEDAVG_DEVICE_ROWS=1 packs rows first as the streaming path does
     DEVICE_SEGMENTS = os.environ.get("FEDAVG_DEVICE_ROWS", "0") != "1"
+    # device rounds from this many fp32 row bytes check for the client_arena layout
+    ARENA_MIN_BYTES = int(os.environ.get("FEDAVG_ARENA_MIN_BYTES", str(64 << 20)))
 
     @staticmethod
     def _segment_tables(g, ptrs):
@@ -455,12 +459,51 @@ class DeviceAggregator:
         del last["seg_keep0"]
         return st.dev[:K]
 
-    def _reduce_groups_device(self, table: KeyTable, ptrs, weights) -> "OrderedDict[str, torch.Tensor]":
+    @staticmethod
+    def _arena_rows(g, ptrs, dicts) -> Optional[torch.Tensor]:
+        """The clients' fp32 group as a ``[K, P]`` view with row stride ``ld``
+        when their tensors already ARE the packed layout: every client's keys
+        back to back at the group's offsets, clients one pitch apart, in one
+        allocation (``client_arena`` makes such dicts; so does any simulator
+        that keeps its client models in one buffer).  Then the row reduce runs
+        on the clients' memory directly -- no packing, and one allocation's
+        address translation instead of K.  None when
+        the pointers do not form that layout."""
+        import numpy as np
+
+        meta = g.__dict__.get("_arena_meta")
+        if meta is None:  # per table: the group's byte offsets, and whether it is every key in order
+            whole = bool(np.array_equal(g.key_index, np.arange(len(g.key_index))))
+            meta = g._arena_meta = (bool((g.kind == 0).all()) and len(g.key_index) > 0, whole, g.offset * 4)
+        ok, whole, off4 = meta
+        if dicts is None or not ok:
+            return None
+        cols = ptrs if whole and ptrs.shape[1] == len(off4) else ptrs[:, g.key_index]
+        base = int(cols[0, 0]) - int(off4[0])
+        K = cols.shape[0]
+        pitch = int(cols[1, 0] - cols[0, 0]) if K > 1 else (g.P + 3) // 4 * 16
+        if base % 16 or pitch % 16 or pitch < g.P * 4:
+            return None
+        expect = off4 + base if K == 1 else (np.arange(base, base + K * pitch, pitch)[:, None] + off4)
+        if not np.array_equal(cols, expect.reshape(cols.shape)):
+            return None
+        first = dicts[0][g.keys[0].name]
+        last = dicts[-1][g.keys[-1].name]
+        st = first.untyped_storage()
+        if last.untyped_storage().data_ptr() != st.data_ptr() or (base - st.data_ptr()) % 4:
+            return None
+        try:
+            return first.as_strided((K, g.P), (pitch // 4, 1), (base - st.data_ptr()) // 4)
+        except RuntimeError:  # outside the storage
+            return None
+
+    def _reduce_groups_device(self, table: KeyTable, ptrs, weights, dicts=None) -> "OrderedDict[str, torch.Tensor]":
         """Device-resident clients: the fp32 group reduced straight from the
-        clients' tensors (zero-copy), other groups packed in HBM and reduced;
-        the averaged model returned as device tensors on the current stream
-        (no host round trip, no synchronization: like the reference's torch
-        ops on device tensors)."""
+        clients' tensors (zero-copy: the row reduce on them when they already
+        form the packed layout, else the segments kernel), other groups packed
+        in HBM and reduced; the averaged model returned as device tensors on
+        the current stream (no host round trip, no synchronization: like the
+        reference's torch ops on device tensors)."""
         K, dev = ptrs.shape[0], self.device
         t0 = time.perf_counter()
         results: "OrderedDict[str, torch.Tensor]" = OrderedDict()
@@ -470,7 +513,19 @@ class DeviceAggregator:
                 compute.wait_stream(self._copy_stream)  # earlier users of the staging are done
             self._last = {"table": table, "K": K, "dev": {}}
             for g in table.groups.values():
-                if g.dtype == torch.float32 and self.DEVICE_SEGMENTS:
+                # the layout check costs tens of us of host time: worth it where the
+                # row kernel's advantage is (large rounds)
+                rows = (self._arena_rows(g, ptrs, dicts)
+                        if g.dtype == torch.float32 and K * g.P * 4 >= self.ARENA_MIN_BYTES else None)
+                if rows is not None:
+                    w = self._seg_weights
+                    if w is None or w.K < K:
+                        w = self._seg_weights = _Weights(K, torch.float32, self.device)
+                    out_dev = torch.empty(g.P, dtype=torch.float32, device=dev)
+                    reduce_packed(rows, w.upload(weights, compute), g.P, out_dev)
+                    self._last["dev"][g.dtype] = (rows, out_dev)  # the clients' own rows: :291 / FPF read them
+                    self.arena_rounds += 1
+                elif g.dtype == torch.float32 and self.DEVICE_SEGMENTS:
                     out_dev = self._reduce_segments(g, ptrs, weights, compute)
                     self._last["dev"][g.dtype] = (None, out_dev)  # no rows: see materialize_rows
                     self._last["segments"] = True
@@ -741,6 +796,35 @@ def _round_to_dtype(x, dtype: torch.dtype):
     if dtype == torch.float64:
         return np.asarray(x, dtype=np.float64).copy()
     return torch.from_numpy(np.asarray(x, dtype=np.float64)).to(dtype).to(torch.float64).numpy()
+
+
+def client_arena(template, K: int, device=None):
+    """K device state_dicts shaped like ``template`` whose tensors are views
+    into ONE ``[K, ld]`` fp32 buffer in the aggregate's packed layout (row i
+    = client i, keys back to back in ``template``'s order, ``ld`` = the
+    row length rounded to 64 elements).  Returns ``(rows, dicts)``.
+
+    A device-resident round whose clients write their results into these
+    dicts (``copy_`` into the views, or models whose parameters are these
+    views) is reduced by the row kernel straight from ``rows`` -- the
+    zero-copy path without per-client allocations (DESIGN.md section 6:
+    7.1 TB/s on one buffer against 6.3-6.5 on separately allocated tensors,
+    whose address translation costs the difference).  fp32 state_dicts
+    only (every key of one dtype group, as the reference's models)."""
+    table = KeyTable(template)
+    if set(table.groups) != {torch.float32} or any(e.src_dtype != torch.float32 for e in table.entries):
+        raise TypeError("client_arena holds fp32 state_dicts (every key fp32)")
+    g = table.groups[torch.float32]
+    if device is None:
+        device = torch.device("cuda", torch.cuda.current_device())
+    rows = torch.zeros((K, g.ld), dtype=torch.float32, device=device)
+    dicts = []
+    for i in range(K):
+        sd = OrderedDict()
+        for e in table.entries:
+            sd[e.name] = rows[i, e.offset:e.offset + e.numel].view(e.shape)
+        dicts.append(sd)
+    return rows, dicts
 
 
 _default: Dict[int, DeviceAggregator] = {}

@@ -158,6 +158,32 @@ def run(name, reps, cpu_aggregate, cpu_distances, train_ms=0.0):
     same_dev = same_dev and all(torch.equal(dsout[k].cpu().reshape(-1).view(torch.int32),
                                             out[k].reshape(-1).view(torch.int32)) for k in out)
     del ddicts, wl, dout, dsout
+    # the same clients written into ONE buffer in the packed layout
+    # (mfl_amd.client_arena): the aggregate runs the row kernel on them
+    arena_t, arena_dist_t, arena_same = [], [], None
+    if all(t.dtype == torch.float32 for t in dicts[0].values()):
+        rows, adicts = mfl_amd.client_arena(dicts[0], K, dev)
+        for a, sd in zip(adicts, dicts):
+            for k, v in sd.items():
+                a[k].copy_(v)
+        before = agg.arena_rounds
+        for r in range(reps + 1):
+            wl = [(counts[0], OrderedDict(adicts[0]))] + list(zip(counts[1:], adicts[1:]))
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            aout = agg.aggregate(wl)
+            torch.cuda.synchronize()
+            t = time.perf_counter() - t0
+            if r:
+                arena_t.append(t)
+            t0 = time.perf_counter()
+            agg.client_distances(wl, aout)
+            t = time.perf_counter() - t0
+            if r:
+                arena_dist_t.append(t)
+        arena_same = (agg.arena_rounds - before == reps + 1) and all(
+            torch.equal(aout[k].cpu().reshape(-1).view(torch.int32), out[k].reshape(-1).view(torch.int32)) for k in out)
+        del rows, adicts, wl, aout
     gd = float(np.median(dev_t))
     same = all(torch.equal(out[k].reshape(-1).view(torch.int32), ref[k].reshape(-1).view(torch.int32)) for k in ref)
     g, c = float(np.median(gpu_t)), float(np.median(cpu_t))
@@ -177,6 +203,10 @@ def run(name, reps, cpu_aggregate, cpu_distances, train_ms=0.0):
         "device_clients_ms_median": round(gd * 1e3, 3), "device_clients_GBps": round(alg / gd / 1e9, 2),
         "device_clients_stream_finish_ms_median": round(float(np.median(dcrit)) * 1e3, 3),
         "device_clients_bit_exact": bool(same_dev),
+        "arena_clients_ms_median": round(float(np.median(arena_t)) * 1e3, 3) if arena_t else None,
+        "arena_clients_GBps": round(alg / float(np.median(arena_t)) / 1e9, 2) if arena_t else None,
+        "arena_clients_dist_ms_median": round(float(np.median(arena_dist_t)) * 1e3, 3) if arena_dist_t else None,
+        "arena_clients_bit_exact_and_row_path": arena_same,
         "device_clients_dist_ms_median": round(float(np.median(ddist_t)) * 1e3, 3) if ddist_t else None,
         "device_clients_dist_max_rel_vs_host": (float(np.max(np.abs(dnorms - norms) / np.maximum(np.abs(norms), 1e-30)))
                                                 if ddist_t and dist_t else None),

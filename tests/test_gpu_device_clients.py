@@ -405,3 +405,47 @@ def test_segments_variants_bit_identical(K):
     bad = lib.fedavg_reduce_segments_f32_variant(*args, ref.data_ptr(), ws[0][0].data_ptr(), ws[0][1].data_ptr(),
                                                  need, 3, 8, 3, None)
     assert bad == -10003
+
+
+def test_client_arena_rounds_use_the_row_kernel_bit_exact():
+    """client_arena dicts (views into one [K, ld] buffer in the packed layout)
+    are reduced by the row kernel straight from that buffer: bit-exact vs the
+    reference's loop, :291 from the same rows, and a layout that is NOT the
+    packed one (keys in another order) takes the segments path, same bits."""
+    import copy
+    from collections import OrderedDict
+    for name in ["mnist_lr_k10", "mnist_lr_k100", "flat_k10_p65", "thirds_k3"]:
+        meta, w_locals, expected = load_case(name)
+        if not all(t.dtype == torch.float32 for t in w_locals[0][1].values()):
+            continue
+        ref_locals = copy.deepcopy(w_locals)
+        ref_glob = O.aggregate_torch(ref_locals)
+        rows, adicts = mfl_amd.client_arena(w_locals[0][1], len(w_locals), DEV)
+        for a, (_, sd) in zip(adicts, w_locals):
+            for k, v in sd.items():
+                a[k].copy_(v)
+        agg = mfl_amd.DeviceAggregator(DEV)
+        agg.ARENA_MIN_BYTES = 0  # golden cases are small
+        wl = [(n, OrderedDict(a)) for (n, _), a in zip(w_locals, adicts)]
+        out = agg.aggregate(wl)
+        assert agg.arena_rounds == 1, name
+        assert out is wl[0][1]
+        for k, exp in expected.items():
+            assert out[k].is_cuda
+            assert torch.equal(out[k].cpu().reshape(-1).view(torch.int32), exp.reshape(-1).view(torch.int32)), (name, k)
+        # the arena itself is untouched (client 0's row still holds its update)
+        first = next(iter(w_locals[0][1]))
+        assert torch.equal(adicts[0][first].cpu(), w_locals[0][1][first])
+        norms = agg.client_distances(wl, out)
+        exact = O.client_distances_exact(ref_locals, ref_glob)
+        assert norms[0] == 0.0
+        assert np.allclose(norms, exact, rtol=1.2e-7, atol=0), (name, norms, exact)
+        # keys in another order than the buffer's: not the packed layout -> segments path
+        if len(adicts[0]) > 1:
+            agg2 = mfl_amd.DeviceAggregator(DEV)
+            agg2.ARENA_MIN_BYTES = 0
+            wl2 = [(n, OrderedDict(reversed(list(a.items())))) for (n, _), a in zip(w_locals, adicts)]
+            out2 = agg2.aggregate(wl2)
+            assert agg2.arena_rounds == 0
+            for k, exp in expected.items():
+                assert torch.equal(out2[k].cpu().reshape(-1).view(torch.int32), exp.reshape(-1).view(torch.int32))

@@ -254,16 +254,27 @@ def test_chunk_of_wider_shard_streams_and_is_bit_exact():
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float64])
 def test_chunk_of_wider_shard_other_dtypes(dtype):
     """fp16/bf16/fp64 chunks of a wider row buffer (streamed schedule) give
-    the bits of the same columns reduced from a contiguous copy."""
+    the oracle's bits (O.reduce_f64 / O.reduce_half on the same columns) and
+    those of the same columns reduced from a contiguous copy."""
     K, S, C = 100, 390_656, 3
     x = _clients(K, S * C, seed=5, dtype=dtype)
-    w = _w(_weights(K, seed=6), torch.float64 if dtype == torch.float64 else torch.float32)
+    wl = _weights(K, seed=6)
+    w = _w(wl, torch.float64 if dtype == torch.float64 else torch.float32)
     iv = torch.int64 if dtype == torch.float64 else torch.int16
     for j in (0, C - 1):
         view = x[:, j * S:(j + 1) * S]
         got = mfl_amd.reduce_packed(view, w, S)
         ref = mfl_amd.reduce_packed(view.contiguous(), w, S)
         assert torch.equal(got.view(iv), ref.view(iv)), (dtype, j)
+        host = view.cpu()
+        if dtype == torch.float64:
+            exp = torch.from_numpy(O.reduce_f64(host.numpy(), wl))
+        elif dtype == torch.float16:
+            exp = torch.from_numpy(O.reduce_half(host.numpy(), wl, "float16"))
+        else:
+            bits = O.reduce_half(host.view(torch.int16).numpy(), wl, "bfloat16")
+            exp = torch.from_numpy(bits.view(np.int16).copy()).view(torch.bfloat16)
+        assert_bits(got, exp, f"{dtype} chunk {j} vs oracle")
 
 
 def test_schedule_switch_boundaries_bit_exact():

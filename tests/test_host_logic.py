@@ -326,3 +326,31 @@ def test_synthetic_inputs_torch_and_numpy_bit_identical():
     assert rows[:, 0:100].numpy().tobytes() == synthetic.client_columns_numpy(3, 7, 100).tobytes()
     assert rows[:, 128:278].numpy().tobytes() == synthetic.client_columns_numpy(3, 1000, 150).tobytes()
     assert float(rows[:, 100:128].abs().sum()) == 0.0 and float(rows[:, 278:].abs().sum()) == 0.0
+
+
+def test_client_arena_layout_is_detected_on_host_pointers():
+    """DeviceAggregator._arena_rows (host-side pointer arithmetic, no GPU):
+    client_arena dicts are recognised as the packed [K, ld] layout and viewed
+    as [K, P] with stride ld; reordered keys or a gap between clients are not."""
+    from collections import OrderedDict
+
+    from mfl_amd.aggregate import DeviceAggregator
+
+    for name in ["mnist_lr_k10", "flat_k10_p65", "flat_k1_p1"]:
+        _, wl, _ = load_case(name)
+        rows, adicts = mfl_amd.client_arena(wl[0][1], len(wl), "cpu")
+        t = KeyTable(adicts[0])
+        ptrs, _ = t.collect(adicts)
+        g = t.groups[torch.float32]
+        v = DeviceAggregator._arena_rows(g, ptrs, adicts)
+        assert v is not None and v.shape == (len(wl), g.P) and (len(wl) == 1 or v.stride(0) == g.ld)
+        assert v.data_ptr() == rows.data_ptr()
+        if len(adicts[0]) > 1:
+            rev = [OrderedDict(reversed(list(a.items()))) for a in adicts]
+            t2 = KeyTable(rev[0])
+            p2, _ = t2.collect(rev)
+            assert DeviceAggregator._arena_rows(t2.groups[torch.float32], p2, rev) is None
+        if len(adicts) > 2:  # every other client: a non-uniform pitch
+            sub = adicts[:1] + adicts[2:]
+            p3, _ = t.collect(sub)
+            assert DeviceAggregator._arena_rows(g, p3, sub) is None
