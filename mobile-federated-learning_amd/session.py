@@ -27,6 +27,7 @@ Results are bit-identical to ``aggregate`` (and to the reference).
 """
 from __future__ import annotations
 
+import os
 import time
 import weakref
 from collections import OrderedDict
@@ -36,7 +37,6 @@ import torch
 
 from . import _lib
 from .layout import KeyTable
-from .reduce import weights_tensor
 
 __all__ = ["RoundSession"]
 
@@ -98,6 +98,7 @@ class RoundSession:
                 # allocation costs 5.6-8.6 ms
                 self._out_host = {g.dtype: torch.empty(g.P, dtype=g.dtype, pin_memory=True)
                                   for g in self.table.groups.values()}
+                self._warm_finish_path()
         ptrs, keep = self.table.collect([state_dict], self._client_dev)
         if self._client_dev.type == "cuda":
             # device-resident client: one packing kernel on the copy stream,
@@ -112,6 +113,41 @@ class RoundSession:
         if keep:
             self._keepalive.append(keep)
         self.add_ms += (time.perf_counter() - t0) * 1e3
+
+    # The first finish() of a process paid ~10 ms of one-time runtime work on
+    # its critical path: creating the D2H stream (6.4 ms in
+    # hipStreamCreateWithPriority) and the first launch of the reduce kernel
+    # (3.8 ms in hipExtLaunchKernel: code-object load), per the HIP API trace
+    # of scripts/stream_probe.py.  The first session of
+    # an aggregator does both at its first add(), while clients still train:
+    # it creates the stream, reduces column chunk 0 of the staging rows into a
+    # scratch output with the finish() schedule (same K, chunk width and row
+    # stride, so the same kernel) and copies that chunk to the result buffer
+    # on the D2H stream.  Scratch bytes only; finish() overwrites them in
+    # stream order.  FEDAVG_FINISH_WARMUP=0 turns it off.
+    FINISH_WARMUP = os.environ.get("FEDAVG_FINISH_WARMUP", "1") != "0"
+
+    def _warm_finish_path(self):
+        agg = self.agg
+        if getattr(agg, "_finish_warm", False) or not self.FINISH_WARMUP:
+            return
+        agg._finish_warm = True
+        from .aggregate import _fetch
+        from .reduce import reduce_packed
+
+        with torch.cuda.device(self.dev):
+            d2h = agg._d2h_stream_for()
+            for g in self.table.groups.values():
+                st = self._staging[g.dtype]
+                c0, c1 = self._chunks[g.dtype][0]
+                K = self.max_clients
+                # all on the D2H stream: the caller's (training) stream is not touched
+                w = st.upload_weights([1.0 / K] * K, d2h)
+                scratch = torch.empty(c1 - c0, dtype=g.dtype, device=self.dev)
+                with torch.cuda.stream(d2h):
+                    reduce_packed(st.dev[:K, c0:c1], w, c1 - c0, scratch)
+                _fetch(scratch, self._out_host[g.dtype][c0:c1], d2h)
+                scratch.record_stream(d2h)
 
     def _add_host(self, i, ptrs):
         """Pack host client ``i`` into its pinned row and start its H2D (unless the round is small)."""
@@ -160,7 +196,10 @@ class RoundSession:
             d2h = self.agg._d2h_stream_for()
             for g in self.table.groups.values():
                 st = self._staging[g.dtype]
-                out_dev, out_host = reduce_and_fetch(st.dev[:K], weights_tensor(weights, g.dtype, self.dev), g.P,
+                # the staging's own pinned weight buffer: no pinned allocation
+                # inside finish (a fresh one costs milliseconds to issue)
+                w_dev = st.upload_weights(weights, self._compute)
+                out_dev, out_host = reduce_and_fetch(st.dev[:K], w_dev, g.P,
                                                      d2h, ready=self._ready[g.dtype],
                                                      out_host=self._out_host.get(g.dtype))
                 outs.append((g, out_host))
