@@ -436,7 +436,18 @@ __device__ __forceinline__ f32x4 ld_rsrc_nt(__amdgpu_buffer_rsrc_t r, uint32_t b
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(byte_off), 0, 2));
 }
 
-template <int U, int C, int BS = kBlock>
+// Column group of workgroup `b` in a one-round launch of `g` workgroups when
+// the co-resident groups of a CU should take ADJACENT column groups: the
+// dispatcher hands workgroup w to XCD w % 8 and, within it, fills the CUs in
+// order, so w, w + S, w + 2S (S = slots per round, the CU count) share a CU.
+// Slot r = b % S gets columns start_r + b / S with start_r = r*m + min(r, e)
+// (g = S*m + e): a bijection that gives each CU one contiguous run.
+__device__ __forceinline__ int64_t cu_contiguous_group(int64_t b, int64_t g, int64_t slots) {
+  const int64_t m = g / slots, e = g % slots, r = b % slots, q = b / slots;
+  return r * m + (r < e ? r : e) + q;
+}
+
+template <int U, int C, int BS = kBlock, int REMAP = 0>
 __global__ __launch_bounds__(BS) void reduce_f32x4_buf_kernel(const f32x4* __restrict__ X, int K, int64_t ld4,
                                                               int64_t nvec, int tail, const float* __restrict__ W,
                                                               float* __restrict__ out) {
@@ -445,7 +456,8 @@ __global__ __launch_bounds__(BS) void reduce_f32x4_buf_kernel(const f32x4* __res
   uint32_t off[C];
 #pragma unroll
   for (int j = 0; j < C; ++j) off[j] = 16u * (threadIdx.x + j * BS);
-  for (int64_t base = static_cast<int64_t>(blockIdx.x) * span; base < nvec;
+  const int64_t b0 = REMAP > 0 ? cu_contiguous_group(blockIdx.x, gridDim.x, REMAP) : blockIdx.x;
+  for (int64_t base = b0 * span; base < nvec;
        base += static_cast<int64_t>(gridDim.x) * span) {
     if (base + span <= nvec) {
       f32x4 acc[C];
@@ -493,13 +505,13 @@ __global__ __launch_bounds__(BS) void reduce_f32x4_buf_kernel(const f32x4* __res
 // launch_split's round-split schedule with the buffer-descriptor kernel, in
 // blocks of BS threads (BS = 64: one wave per workgroup, for short rows whose
 // 256-thread groups would leave the CUs unevenly loaded)
-template <int U, int C, int BS = kBlock>
+template <int U, int C, int BS = kBlock, int REMAP = 0>
 void launch_split_buf(const float* clients, int K, int64_t ld, int64_t P, const float* W, float* out, int max_blocks,
                       hipStream_t s, hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr) {
   const int64_t nvec = (P + 3) / 4;
   const int64_t span = static_cast<int64_t>(BS) * C;
   const int64_t resident =
-      max_blocks > 0 ? max_blocks : resident_blocks(reduce_f32x4_buf_kernel<U, C, BS>, BS);
+      max_blocks > 0 ? max_blocks : resident_blocks(reduce_f32x4_buf_kernel<U, C, BS, REMAP>, BS);
   const int64_t blocks = (nvec + span - 1) / span;
   const int64_t nl = (blocks + resident - 1) / resident;
   const int64_t per = ((nvec + nl - 1) / nl + span - 1) / span * span;
@@ -507,7 +519,7 @@ void launch_split_buf(const float* clients, int K, int64_t ld, int64_t P, const 
   for (int64_t v0 = 0; v0 < nvec; v0 += per) {
     const int64_t n = (nvec - v0) < per ? (nvec - v0) : per;
     const int tail = (v0 + n == nvec) ? static_cast<int>(P & 3) : 0;
-    hipExtLaunchKernelGGL((reduce_f32x4_buf_kernel<U, C, BS>), dim3(static_cast<unsigned>((n + span - 1) / span)),
+    hipExtLaunchKernelGGL((reduce_f32x4_buf_kernel<U, C, BS, REMAP>), dim3(static_cast<unsigned>((n + span - 1) / span)),
                           dim3(BS), 0, s, v0 == 0 ? ev_start : nullptr, v0 + n >= nvec ? ev_stop : nullptr, 0,
                           X + v0, K, ld / 4, n, tail, W, out + v0 * 4);
   }

@@ -606,6 +606,11 @@ int fedavg_reduce_f32_buf(const float* clients, int64_t K, int64_t P, int64_t ld
     FEDAVG_BUF_CASE(4, 8, 64)
     FEDAVG_BUF_CASE(32, 1, 64)
     FEDAVG_BUF_CASE(32, 2, 64)
+    // block 1256 / 1512: the 256-thread U2 x C16 kernel with co-resident
+    // workgroups remapped to adjacent column groups (cu_contiguous_group,
+    // 256 / 512 slots per round)
+    case 1256 * 10000 + 216: launch_split_buf<2, 16, 256, 256>(clients, k, ld, P, weights, out, max_blocks, s); break;
+    case 1512 * 10000 + 216: launch_split_buf<2, 16, 256, 512>(clients, k, ld, P, weights, out, max_blocks, s); break;
     default:
       return set_error(FEDAVG_EMODE, "%s: unsupported unroll=%d cols=%d block=%d", what, unroll, cols, block);
   }
