@@ -93,8 +93,8 @@ __device__ __forceinline__ void sqdist_rows_store(double acc, double* partials, 
   if ((threadIdx.x & 63) == 0) partials[row * nwaves + wave_id] = acc;
 }
 
-template <int U, int C>
-__global__ __launch_bounds__(kBlock) void client_sqdist_buf_kernel(
+template <int U, int C, int MINW = 1>
+__global__ __launch_bounds__(kBlock, MINW) void client_sqdist_buf_kernel(
     const f32x4* __restrict__ X, int K, int64_t ld4, int64_t nvec, int tail, const f32x4* __restrict__ G,
     double* __restrict__ partials, int64_t nwaves, int64_t wave_base) {
   const int64_t wave_id = wave_base + static_cast<int64_t>(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
@@ -284,7 +284,7 @@ int64_t sqdist_waves_for(int64_t P, int cols) {
   return blocks * (kBlock / 64);
 }
 
-template <int U, int C, bool BUF = false>
+template <int U, int C, bool BUF = false, int MINW = 1>
 void launch_sqdist(const float* clients, int K, int64_t ld, int64_t P, const float* glob, double* partials,
                    int64_t nwaves, int max_blocks, hipStream_t s) {
   const int64_t nvec = (P + 3) / 4;
@@ -301,7 +301,7 @@ void launch_sqdist(const float* clients, int K, int64_t ld, int64_t P, const flo
     const int64_t n = (nvec - v0) < nb * span ? (nvec - v0) : nb * span;
     const int tail = (v0 + n == nvec) ? static_cast<int>(P & 3) : 0;
     if constexpr (BUF)
-      hipLaunchKernelGGL((client_sqdist_buf_kernel<U, C>), dim3(static_cast<unsigned>(nb)), dim3(kBlock), 0, s,
+      hipLaunchKernelGGL((client_sqdist_buf_kernel<U, C, MINW>), dim3(static_cast<unsigned>(nb)), dim3(kBlock), 0, s,
                          X + v0, K, ld / 4, n, tail, Gv + v0, partials, nwaves, b0 * (kBlock / 64));
     else
       hipLaunchKernelGGL((client_sqdist_f32x4_kernel<U, C>), dim3(static_cast<unsigned>(nb)), dim3(kBlock), 0, s,
@@ -391,6 +391,11 @@ int sqdist_buf_impl(const float* clients, int64_t K, int64_t P, int64_t ld, cons
     case 408: launch_sqdist<4, 8, true>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
     case 804: launch_sqdist<8, 4, true>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
     case 216: launch_sqdist<2, 16, true>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    // register-capped forms (launch_bounds min waves per SIMD 3 / 4): more
+    // waves resident, fewer loads in flight per wave
+    case 30216: launch_sqdist<2, 16, true, 3>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    case 40216: launch_sqdist<2, 16, true, 4>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    case 30408: launch_sqdist<4, 8, true, 3>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
     case 116: launch_sqdist<1, 16, true>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
     case 112: launch_sqdist<1, 12, true>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
     case 212: launch_sqdist<2, 12, true>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;

@@ -31,7 +31,7 @@ import os
 import time
 import weakref
 from collections import OrderedDict
-from typing import Mapping, Optional
+from typing import Mapping
 
 import torch
 

@@ -55,7 +55,7 @@ def test_single_gpu_does_not_self_launch():
     assert bench.self_launch(["--gpus", "1"]) is None
 
 
-def test_gpus_mismatch_is_refused_under_torchrun(monkeypatch):
+def test_no_self_launch_under_torchrun(monkeypatch):
     monkeypatch.setenv("WORLD_SIZE", "2")
     assert bench.self_launch(["--gpus", "2"]) is None  # already launched: run in-process
 
