@@ -160,3 +160,16 @@ def test_sampled_parity_single_rank_and_passes():
     red.pass_out[red.plan.local_cols + 5] += 1.0  # pass 1, inside the first-column window
     par = bench.sampled_parity(red, w, passes=3, pass_cols=red.plan.local_cols, n_windows=2, width=100)
     assert not par["ok"]
+
+
+def test_as_rank_plans_one_shard_of_a_larger_world():
+    """bench.py --shard-of N: ShardedReducer(as_rank=(N, r)) owns exactly rank
+    r's block-cyclic segments of the N-rank plan and never gathers."""
+    from mfl_amd.distributed import plan_shards
+    for P, N, chunks in [(25_000_000, 8, 4), (11_227_812, 8, 2), (7_001, 3, 2)]:
+        for r in (0, N - 1):
+            red = ShardedReducer(4, P, chunks=chunks, device="cpu", local_reduce=_torch_loop_reduce, as_rank=(N, r))
+            assert not red.gather and red.full is None
+            assert red.plan.local_segments() == plan_shards(P, N, r, chunks).local_segments()
+    with pytest.raises(ValueError):
+        ShardedReducer(4, 100, device="cpu", local_reduce=_torch_loop_reduce, as_rank=(2, 0), gather=True)
