@@ -639,8 +639,9 @@ def main(argv=None):
             "avg_launch_ms": round(kernel_ms_max / launches_per_call, 4),
             "launches": len(kernel_ms) * calls_per_event * launches_per_call,
             "timing": ("hipGraph replay bracketed by events" if args.graph else
-                       "launch-attached HIP events (hipExtLaunchKernel) on the launch stream, "
-                       + ("every reduce call" if sample_every == 1 else f"every {sample_every}th reduce call")
+                       ("hipEventRecord pairs around" if tuned is not None else
+                        "launch-attached HIP events (hipExtLaunchKernel) on the launch stream of")
+                       + (" every reduce call" if sample_every == 1 else f" every {sample_every}th reduce call")
                        + " of the timed region"),
         }
         tj = args.traffic_json or str(ROOT / "profiles" / f"traffic_{args.workload}.json")
