@@ -535,6 +535,21 @@ Schedule choose_f32_schedule(int64_t K, int64_t P, int64_t ld) {
   if (sc.nt && K >= kManyClients) {
     if (sc.unroll == 8 && sc.cols == 2) sc.cols = 4;
     if (sc.unroll == 16 && sc.cols == 1 && nvec >= full / 4 * kBlock * 4) sc.cols = 4;
+    // Rows that give 3/4 to 1 block per CU at 6 (K >= 64) or 3 (K >= 256)
+    // slices per thread: one resident block on (nearly) every CU beats
+    // 1.5 blocks per CU at 4 slices.  Rotating-chunk sweep, interleaved,
+    // bit-identical (profiles/r02/sweeps/short_row_c3_c6.jsonl): K=100 x 1.56M
+    // (the N=2 chunk) 6,822 vs 6,585 GB/s at U8 x C4; K=500 x 702K (cfg4's
+    // N=8 chunk) 6,856 vs 6,627 at U16 x C4.  (K=100 x 781K keeps U16 x C4:
+    // 6,527 vs 6,200 at C3.)
+    const int64_t cus = cu_count();
+    if (nvec >= cus * 3 / 4 * kBlock * 6 && nvec <= cus * kBlock * 6) {
+      sc.unroll = 4;
+      sc.cols = 6;
+    } else if (K >= 256 && nvec >= cus * 3 / 4 * kBlock * 3 && nvec <= cus * kBlock * 3) {
+      sc.unroll = 8;
+      sc.cols = 3;
+    }
   }
   return sc;
 }
@@ -552,6 +567,8 @@ void launch_production_f32(const float* clients, int K, int64_t ld, int64_t P, c
       case 802: launch_split_ev<8, 2, true>(clients, K, ld, P, W, out, bpl, s, e0, e1); return;
       case 1604: launch_split_ev<16, 4, true>(clients, K, ld, P, W, out, bpl, s, e0, e1); return;
       case 1601: launch_split_ev<16, 1, true>(clients, K, ld, P, W, out, bpl, s, e0, e1); return;
+      case 406: launch_split_ev<4, 6, true>(clients, K, ld, P, W, out, bpl, s, e0, e1); return;
+      case 803: launch_split_ev<8, 3, true>(clients, K, ld, P, W, out, bpl, s, e0, e1); return;
       default: launch_split_ev<8, 1, true>(clients, K, ld, P, W, out, bpl, s, e0, e1); return;
     }
   }

@@ -285,6 +285,12 @@ var_launcher pick_var1(int cols, int nt, int pipe) {
     case 1: return pick_var2<U, 1>(nt, pipe);
     case 2: return pick_var2<U, 2>(nt, pipe);
     case 4: return pick_var2<U, 4>(nt, pipe);
+    case 3:  // 768-float4 groups: a 781K-column chunk (N = 8) fills 255 CUs instead of 191 at C4
+      if constexpr (U == 8 || U == 16) return pick_var2<U, 3>(nt, pipe);
+      return nullptr;
+    case 6:
+      if constexpr (U == 4 || U == 8) return pick_var2<U, 6>(nt, pipe);
+      return nullptr;
     case 8:
       if constexpr (U <= 8) return pick_var2<U, 8>(nt, pipe);
       return nullptr;

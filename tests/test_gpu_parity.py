@@ -169,6 +169,11 @@ def _schedule_boundary_cases():
     # K >= 64: 4 slices per thread in the short-row bands (from full/4 x 256 x 4 float4 columns)
     for t in (full // 4 * 256 * 4 * 4, full * 256 * 2 * 4):
         cases += [(64, t - 4), (64, t + 1), (63, t + 1), (100, t - 1)]
+    # one block per CU at 6 slices (K >= 64) or 3 slices (K >= 256) per thread
+    cus = full // 2
+    for c, K in ((6, 100), (3, 256)):
+        lo, hi = cus * 3 // 4 * 256 * c * 4, cus * 256 * c * 4
+        cases += [(K, lo - 4), (K, lo + 1), (K, hi - 1), (K, hi + 4), (K - 1, lo + 1)]
     mib = 1 << 20
     cases += [(20, 64 * mib // 80 - 3), (20, 64 * mib // 80 + 5), (20, 240 * mib // 80 - 1), (20, 240 * mib // 80 + 7)]
     cases += [(4, 1_000_003), (5, 1_000_003), (1, 65), (2, 7)]
