@@ -64,7 +64,9 @@ int fedavg_reduce_f32(const float* clients, int64_t K, int64_t P, int64_t ld,
 /*
  * Same reduction over K separate device buffers (no packing):
  *   client_ptrs : DEVICE array [K] of device pointers, each to >= P floats.
- * Each pointer may have any 4-byte alignment (checked per client on device).
+ * Each pointer needs only fp32 (4-byte) alignment.  Runs the zero-copy
+ * segments kernel (fedavg_segments.hip) on one key of P columns: units of
+ * 4,096 columns, U4 client rows per batch, dword-aligned 16-B loads.
  */
 int fedavg_reduce_ptrs_f32(const float* const* client_ptrs, int64_t K, int64_t P,
                            const float* weights, float* out, void* stream);

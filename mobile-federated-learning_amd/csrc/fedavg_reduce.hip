@@ -57,45 +57,6 @@ __global__ __launch_bounds__(kBlock) void reduce_f32_scalar_kernel(
   out[p] = acc;
 }
 
-// fp32, bit-exact, pointer-array path: client k lives at ptrs[k] (device).
-// Alignment is a per-client property, so the branch is wave-uniform.
-template <bool OUT_VEC>
-__global__ __launch_bounds__(kBlock) void reduce_ptrs_f32_kernel(
-    const float* const* __restrict__ ptrs, int K, int64_t P,
-    const float* __restrict__ W, float* __restrict__ out) {
-  const int64_t v = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
-  const int64_t p0 = v * 4;
-  if (p0 >= P) return;
-  const int n = (P - p0) >= 4 ? 4 : static_cast<int>(P - p0);
-  f32x4 acc;
-  for (int k = 0; k < K; ++k) {
-    const float* base = ptrs[k];
-    f32x4 x;
-    if (n == 4 && aligned16(base)) {
-      x = *reinterpret_cast<const f32x4*>(base + p0);
-    } else {
-      x.x = base[p0];
-      x.y = n > 1 ? base[p0 + 1] : 0.f;
-      x.z = n > 2 ? base[p0 + 2] : 0.f;
-      x.w = n > 3 ? base[p0 + 3] : 0.f;
-    }
-    const f32x4 term = x * W[k];
-    acc = (k == 0) ? term : acc + term;
-  }
-  float* o = out + p0;
-  if (n == 4) {
-    if constexpr (OUT_VEC) {
-      *reinterpret_cast<f32x4*>(o) = acc;
-    } else {
-      o[0] = acc.x; o[1] = acc.y; o[2] = acc.z; o[3] = acc.w;
-    }
-  } else {
-    o[0] = acc.x;
-    if (n > 1) o[1] = acc.y;
-    if (n > 2) o[2] = acc.z;
-  }
-}
-
 // ---------------------------------------------------------------------------
 // fp64: the weight stays a double (ATen opmath for double).  Scalar path for
 // unaligned buffers; the production path is reduce_vec_kernel<OpF64> below.
@@ -894,25 +855,6 @@ int fedavg_f32_schedule(int64_t K, int64_t P, int* unroll, int* cols, int* nonte
   if (nontemporal) *nontemporal = sc.nt;
   if (launches) *launches = static_cast<int>((blocks + sc.blocks_per_launch - 1) / sc.blocks_per_launch);
   return FEDAVG_OK;
-}
-
-int fedavg_reduce_ptrs_f32(const float* const* client_ptrs, int64_t K, int64_t P, const float* weights,
-                           float* out, void* stream) {
-  const char* what = "fedavg_reduce_ptrs_f32";
-  int rc = check_common(client_ptrs, K, P, P, weights, out, what);
-  if (rc) return rc;
-  if (P == 0) return FEDAVG_OK;
-  if (!aligned4(out) || !aligned4(weights)) return set_error(FEDAVG_EALIGN, "%s: out/weights misaligned", what);
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  const int64_t nvec = (P + 3) / 4;
-  if (aligned16(out)) {
-    hipLaunchKernelGGL(reduce_ptrs_f32_kernel<true>, dim3(grid_for(nvec, kBlock)), dim3(kBlock), 0, s,
-                       client_ptrs, static_cast<int>(K), P, weights, out);
-  } else {
-    hipLaunchKernelGGL(reduce_ptrs_f32_kernel<false>, dim3(grid_for(nvec, kBlock)), dim3(kBlock), 0, s,
-                       client_ptrs, static_cast<int>(K), P, weights, out);
-  }
-  return launch_status(what);
 }
 
 int fedavg_reduce_f64(const double* clients, int64_t K, int64_t P, int64_t ld, const double* weights,

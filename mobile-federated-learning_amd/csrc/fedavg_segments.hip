@@ -232,6 +232,21 @@ __global__ __launch_bounds__(kBlock) void reduce_segments_f32_kernel(const SegKe
   }
 }
 
+// fedavg_reduce_ptrs_f32: one key of P columns whose client addresses are
+// already a device array [K] -- the same units, no table staging
+template <int U, int C>
+__global__ __launch_bounds__(kBlock) void reduce_ptrs_f32_kernel(const int64_t* __restrict__ ptrs, int64_t P,
+                                                                 int64_t unit0, int K, const float* __restrict__ W,
+                                                                 float* __restrict__ out) {
+  constexpr int64_t span = static_cast<int64_t>(kBlock) * C * 4;
+  const int64_t c0 = (unit0 + blockIdx.x) * span;
+  const int64_t n = P - c0 < span ? P - c0 : span;
+  if (n == span)
+    reduce_raw_unit<U, C, true>(ptrs, K, c0, n, W, out + c0);
+  else
+    reduce_raw_unit<1, C, false>(ptrs, K, c0, n, W, out + c0);
+}
+
 __device__ __forceinline__ double sq4_add(double acc, f32x4 d) {
   const double x = d.x, y = d.y, z = d.z, w = d.w;
   acc = __builtin_fma(x, x, acc);
@@ -394,6 +409,27 @@ int64_t fedavg_segments_workspace(int64_t K, int64_t n_keys) {
 int64_t fedavg_segments_partials(const int64_t* key_numel, int64_t n_keys, int64_t K) {
   if (!key_numel || n_keys <= 0 || K <= 0) return 0;
   return K * units_of(key_numel, n_keys) * (kBlock / 64);
+}
+
+int fedavg_reduce_ptrs_f32(const float* const* client_ptrs, int64_t K, int64_t P, const float* weights,
+                           float* out, void* stream) {
+  const char* what = "fedavg_reduce_ptrs_f32";
+  int rc = check_common(client_ptrs, K, P, P, weights, out, what);
+  if (rc) return rc;
+  if (P == 0) return FEDAVG_OK;
+  if (!aligned4(out) || !aligned4(weights)) return set_error(FEDAVG_EALIGN, "%s: out/weights misaligned", what);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t units = (P + kSegSpan - 1) / kSegSpan;
+  const int64_t cap = static_cast<int64_t>(kSegBlocksPerCU) * cu_count();
+  const int64_t nl = (units + cap - 1) / cap;
+  const int64_t per = (units + nl - 1) / nl;
+  const auto* ptrs = reinterpret_cast<const int64_t*>(client_ptrs);
+  for (int64_t u0 = 0; u0 < units; u0 += per) {
+    const int64_t nb = units - u0 < per ? units - u0 : per;
+    hipLaunchKernelGGL((reduce_ptrs_f32_kernel<kSegU, kSegC>), dim3(static_cast<unsigned>(nb)), dim3(kBlock), 0, s,
+                       ptrs, P, u0, static_cast<int>(K), weights, out);
+  }
+  return launch_status(what);
 }
 
 int fedavg_reduce_segments_f32(const int64_t* client_ptrs, const int64_t* key_numel, const int64_t* key_offset,

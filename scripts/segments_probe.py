@@ -8,7 +8,9 @@ Three variants, interleaved in one process, all bit-identical:
                that same buffer (one key of P elements per client),
   seg-tensors  fedavg_reduce_segments_f32 on K separately allocated client
                tensors (the device-resident drop-in's case),
-  *-pow2-pitch the first two on rows at a power-of-two pitch (128 MiB).
+  *-pow2-pitch the first two on rows at a power-of-two pitch (128 MiB),
+  ptrs-*       fedavg_reduce_ptrs_f32 (device pointer array) on the rows and
+               on the separate tensors.
 Separates the kernel's own cost from where the clients' memory lies.  One
 JSON line per variant: median ms per call (HIP events) and GB/s.
 """
@@ -125,7 +127,7 @@ def main():
     ld2 = 1 << max(0, (P - 1).bit_length())
     rows2 = torch.empty((K, ld2), device=dev)
     rows2[:, :P].copy_(rows[:, :P])
-    names = ["rows", "rows-pow2-pitch", "seg-rows", "seg-pow2-pitch", "seg-tensors"]
+    names = ["rows", "rows-pow2-pitch", "seg-rows", "seg-pow2-pitch", "seg-tensors", "ptrs-rows", "ptrs-tensors"]
     sched = [(4, 8, 3), (4, 8, 0), (4, 8, 2), (4, 8, 4), (4, 8, 6), (8, 4, 3), (8, 4, 6), (2, 8, 3), (2, 8, 6),
              (4, 4, 3), (4, 4, 6), (8, 2, 6), (16, 2, 3), (2, 16, 3), (1, 16, 3), (1, 16, 6)]
     if args.sweep:
@@ -140,6 +142,8 @@ def main():
     starts = [int(t.data_ptr()) for t in tensors]
     print(json.dumps({"tensor_start_alignment_log2": [min(31, (a & -a).bit_length() - 1) for a in starts[:8]],
                       "pitch_bytes_rows": ld * 4, "pitch_bytes_pow2": ld2 * 4}), flush=True)
+    dptrs = {"ptrs-rows": torch.from_numpy(ptr_rows[:, 0].copy()).to(dev),
+             "ptrs-tensors": torch.from_numpy(ptr_tens[:, 0].copy()).to(dev)}
     need = lib.fedavg_segments_workspace(K, 1)
     ws = {n: (torch.empty(need, dtype=torch.uint8, pin_memory=True), torch.empty(need, dtype=torch.uint8, device=dev))
           for n in names if n.startswith(("seg-", "var-"))}
@@ -151,6 +155,10 @@ def main():
             return
         if n == "rows-pow2-pitch":
             mfl_amd.reduce_packed(rows2, w, P, outs[n])
+            return
+        if n in dptrs:  # fedavg_reduce_ptrs_f32: device pointer array, no table staging
+            mfl_amd._lib.check(lib.fedavg_reduce_ptrs_f32(dptrs[n].data_ptr(), K, P, w.data_ptr(), outs[n].data_ptr(),
+                                                          stream.cuda_stream), n)
             return
         h, d = ws[n]
         if n.startswith("var-"):

@@ -387,6 +387,19 @@ def test_ptrs_variant_mixed_alignment():
     assert_bits(out, torch.from_numpy(exp))
 
 
+# units of 4,096 columns: below one unit, exact units, one past, the U4 batch
+# remainder (K - 1) % 4 in 0..3, and more units than one launch (3 x CUs)
+@pytest.mark.parametrize("K,P", [(1, 3), (2, 4096), (4, 4097), (5, 8192 + 5), (8, 12_288), (13, 777),
+                                 (100, 3_200_003)])
+def test_ptrs_variant_units(K, P):
+    clients = [_clients(1, P, seed=500 + i)[0, :P].clone() for i in range(K)]
+    w = _weights(K)
+    out_big = torch.empty(P + 1, device=DEV)
+    out = mfl_amd.reduce_tensors(clients, _w(w), out=out_big[1:])  # dword-aligned output
+    exp = O.reduce_f32(torch.stack(clients).cpu().numpy(), w)
+    assert_bits(out, torch.from_numpy(exp))
+
+
 @pytest.mark.parametrize("K,P", [(3, 33), (10, 4099), (64, 100_000)])
 def test_reduce_f64_exact(K, P):
     x = _clients(K, P, seed=P, dtype=torch.float64)
