@@ -93,7 +93,25 @@ __device__ __forceinline__ void sqdist_rows_store(double acc, double* partials, 
   if ((threadIdx.x & 63) == 0) partials[row * nwaves + wave_id] = acc;
 }
 
-template <int U, int C, int MINW = 1>
+// sum over a row's C slices of fl32(x - g)^2 in fp64, in ACC interleaved
+// chains (slice j feeds chain j % ACC, the chains add pairwise at the end):
+// ACC = 1 is one dependent chain of 4C fused square-adds per row
+template <int C, int ACC>
+__device__ __forceinline__ double sq_row(const f32x4 (&x)[C], const f32x4 (&g)[C]) {
+  double a[ACC];
+#pragma unroll
+  for (int i = 0; i < ACC; ++i) a[i] = 0.0;
+#pragma unroll
+  for (int j = 0; j < C; ++j) a[j % ACC] = sq4_add(a[j % ACC], x[j] - g[j]);  // fp32 difference, as the reference
+#pragma unroll
+  for (int w = 1; w < ACC; w *= 2) {
+#pragma unroll
+    for (int i = 0; i + w < ACC; i += 2 * w) a[i] += a[i + w];
+  }
+  return a[0];
+}
+
+template <int U, int C, int MINW = 1, int ACC = 1>
 __global__ __launch_bounds__(kBlock, MINW) void client_sqdist_buf_kernel(
     const f32x4* __restrict__ X, int K, int64_t ld4, int64_t nvec, int tail, const f32x4* __restrict__ G,
     double* __restrict__ partials, int64_t nwaves, int64_t wave_base) {
@@ -111,29 +129,43 @@ __global__ __launch_bounds__(kBlock, MINW) void client_sqdist_buf_kernel(
 #pragma unroll
       for (int j = 0; j < C; ++j) g[j] = ld_rsrc_nt(rg, off[j]);
     }
-    int k = 0;
-    for (; k + U <= K; k += U) {
-      f32x4 xs[U][C];
+    if constexpr (U == 0) {  // one row in flight while the previous one is summed
+      const auto load_row = [&](f32x4 (&x)[C], int row) {
+        const __amdgpu_buffer_rsrc_t r = uniform_rsrc(X + static_cast<int64_t>(row) * ld4 + blk0, bytes);
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
+        for (int j = 0; j < C; ++j) x[j] = ld_rsrc_nt(r, off[j]);
+      };
+      f32x4 a[C], b[C];
+      load_row(a, 0);
+      int k = 0;
+      for (; k + 2 <= K; k += 2) {
+        load_row(b, k + 1);
+        sqdist_rows_store<1, C>(sq_row<C, ACC>(a, g), partials, k, nwaves, wave_id);
+        if (k + 2 < K) load_row(a, k + 2);
+        sqdist_rows_store<1, C>(sq_row<C, ACC>(b, g), partials, k + 1, nwaves, wave_id);
+      }
+      if (k < K) sqdist_rows_store<1, C>(sq_row<C, ACC>(a, g), partials, k, nwaves, wave_id);
+      return;
+    }
+    constexpr int UU = U > 0 ? U : 1;
+    int k = 0;
+    for (; k + UU <= K; k += UU) {
+      f32x4 xs[UU][C];
+#pragma unroll
+      for (int u = 0; u < UU; ++u) {
         const __amdgpu_buffer_rsrc_t r = uniform_rsrc(X + static_cast<int64_t>(k + u) * ld4 + blk0, bytes);
 #pragma unroll
         for (int j = 0; j < C; ++j) xs[u][j] = ld_rsrc_nt(r, off[j]);
       }
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        double acc = 0.0;
-#pragma unroll
-        for (int j = 0; j < C; ++j) acc = sq4_add(acc, xs[u][j] - g[j]);  // fp32 difference, as the reference
-        sqdist_rows_store<U, C>(acc, partials, k + u, nwaves, wave_id);
-      }
+      for (int u = 0; u < UU; ++u) sqdist_rows_store<U, C>(sq_row<C, ACC>(xs[u], g), partials, k + u, nwaves, wave_id);
     }
     for (; k < K; ++k) {
       const __amdgpu_buffer_rsrc_t r = uniform_rsrc(X + static_cast<int64_t>(k) * ld4 + blk0, bytes);
-      double acc = 0.0;
+      f32x4 x[C];
 #pragma unroll
-      for (int j = 0; j < C; ++j) acc = sq4_add(acc, ld_rsrc_nt(r, off[j]) - g[j]);
-      sqdist_rows_store<U, C>(acc, partials, k, nwaves, wave_id);
+      for (int j = 0; j < C; ++j) x[j] = ld_rsrc_nt(r, off[j]);
+      sqdist_rows_store<U, C>(sq_row<C, ACC>(x, g), partials, k, nwaves, wave_id);
     }
     return;
   }
@@ -274,9 +306,15 @@ constexpr int kDistRows = 4;
 // SGPR descriptor with no masking, 64 KiB contiguous per row per block, the
 // reduce's winning shape: 6,818-6,840 GB/s vs 6,520-6,531 for the
 // global-pointer U4 x C8 (scripts/dist_variants.py, profiles/r02/dist_variants.jsonl).
-// U4 x C8 remains the fp64/fp16/bf16 passes' schedule.
+// U4 x C8 remains the fp64/fp16/bf16 passes' schedule.  Each row's fp64 sum
+// runs as 4 interleaved chains (slice j into chain j % 4, added pairwise):
+// 0.9-1.5 % faster than one chain of 64 dependent square-adds in three
+// interleaved runs, 8 chains no better, 16 slower; a one-row-ahead pipeline
+// (U = 0) loses 5 % -- two rows in flight per wave beat compute overlap
+// (profiles/r02/sweeps/dist_chains.jsonl).
 constexpr int kDistBufRows = 2;
 constexpr int kDistBufCols = 16;
+constexpr int kDistBufChains = 4;
 
 int64_t sqdist_waves_for(int64_t P, int cols) {
   const int64_t nvec = (P + 3) / 4;
@@ -284,7 +322,7 @@ int64_t sqdist_waves_for(int64_t P, int cols) {
   return blocks * (kBlock / 64);
 }
 
-template <int U, int C, bool BUF = false, int MINW = 1>
+template <int U, int C, bool BUF = false, int MINW = 1, int ACC = 1>
 void launch_sqdist(const float* clients, int K, int64_t ld, int64_t P, const float* glob, double* partials,
                    int64_t nwaves, int max_blocks, hipStream_t s) {
   const int64_t nvec = (P + 3) / 4;
@@ -301,7 +339,7 @@ void launch_sqdist(const float* clients, int K, int64_t ld, int64_t P, const flo
     const int64_t n = (nvec - v0) < nb * span ? (nvec - v0) : nb * span;
     const int tail = (v0 + n == nvec) ? static_cast<int>(P & 3) : 0;
     if constexpr (BUF)
-      hipLaunchKernelGGL((client_sqdist_buf_kernel<U, C, MINW>), dim3(static_cast<unsigned>(nb)), dim3(kBlock), 0, s,
+      hipLaunchKernelGGL((client_sqdist_buf_kernel<U, C, MINW, ACC>), dim3(static_cast<unsigned>(nb)), dim3(kBlock), 0, s,
                          X + v0, K, ld / 4, n, tail, Gv + v0, partials, nwaves, b0 * (kBlock / 64));
     else
       hipLaunchKernelGGL((client_sqdist_f32x4_kernel<U, C>), dim3(static_cast<unsigned>(nb)), dim3(kBlock), 0, s,
@@ -401,6 +439,19 @@ int sqdist_buf_impl(const float* clients, int64_t K, int64_t P, int64_t ld, cons
     case 212: launch_sqdist<2, 12, true>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
     case 208: launch_sqdist<2, 8, true>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
     case 808: launch_sqdist<8, 8, true>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    // 2 / 4 interleaved fp64 chains per row (codes + 1,000,000 x ACC)
+    case 2000216: launch_sqdist<2, 16, true, 1, 2>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    case 4000216: launch_sqdist<2, 16, true, 1, 4>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    case 2000408: launch_sqdist<4, 8, true, 1, 2>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    case 4000408: launch_sqdist<4, 8, true, 1, 4>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    case 8000216: launch_sqdist<2, 16, true, 1, 8>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    case 16000216: launch_sqdist<2, 16, true, 1, 16>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    // U = 0: row k + 1 loads while row k is summed (one row of registers each)
+    case 16: launch_sqdist<0, 16, true>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    case 4000016: launch_sqdist<0, 16, true, 1, 4>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    case 4000012: launch_sqdist<0, 12, true, 1, 4>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    case 4000008: launch_sqdist<0, 8, true, 1, 4>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    case 4000116: launch_sqdist<1, 16, true, 1, 4>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
     default: return set_error(FEDAVG_EMODE, "%s: unsupported unroll=%d cols=%d", what, unroll, cols);
   }
   rc = launch_status(what);
@@ -421,7 +472,8 @@ int64_t fedavg_client_sqdist_workspace(int64_t K, int64_t P) {
 
 int fedavg_client_sqdist_f32(const float* clients, int64_t K, int64_t P, int64_t ld, const float* glob,
                              double* workspace, int64_t workspace_elems, double* sumsq, void* stream) {
-  return sqdist_buf_impl(clients, K, P, ld, glob, workspace, workspace_elems, sumsq, kDistBufRows, kDistBufCols,
+  return sqdist_buf_impl(clients, K, P, ld, glob, workspace, workspace_elems, sumsq,
+                         kDistBufChains * 10000 + kDistBufRows, kDistBufCols,
                          0, stream, "fedavg_client_sqdist_f32");
 }
 
