@@ -451,6 +451,11 @@ int sqdist_buf_impl(const float* clients, int64_t K, int64_t P, int64_t ld, cons
     case 4000016: launch_sqdist<0, 16, true, 1, 4>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
     case 4000012: launch_sqdist<0, 12, true, 1, 4>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
     case 4000008: launch_sqdist<0, 8, true, 1, 4>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    // 4 chains under a register cap (min waves per SIMD 3 / 4)
+    case 4030212: launch_sqdist<2, 12, true, 3, 4>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    case 4030216: launch_sqdist<2, 16, true, 3, 4>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    case 4040208: launch_sqdist<2, 8, true, 4, 4>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    case 4030308: launch_sqdist<3, 8, true, 3, 4>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
     case 4000116: launch_sqdist<1, 16, true, 1, 4>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
     default: return set_error(FEDAVG_EMODE, "%s: unsupported unroll=%d cols=%d", what, unroll, cols);
   }
