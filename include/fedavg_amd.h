@@ -175,6 +175,42 @@ int fedavg_fpf_index_lru(const float* lru_itr, const float* g_mat, int64_t n_row
                          void* stream);
 
 /*
+ * FPF2 for models with fp64 / fp16 / bf16 keys (fedavg_trainer.py:210, :316-319,
+ * :272 under torch.cat's promotion).  T = the promoted dtype of all keys.
+ * The model is a DEVICE key table keys[n_keys][5] in state_dict order:
+ *   numel, cat offset, dtype group (0..3), element offset in the group row,
+ *   rounding of an fp32-stored integer key's difference (0 none, 2 fp16, 3 bf16:
+ *   the integer difference cast to a 16-bit T)
+ * and per-group row bases (fedavg_fpf_groups: row 0 of each group, row stride
+ * in elements, kind 0 fp32 / 1 fp64 / 2 fp16 / 3 bf16; unused groups any kind
+ * equal in cur and last).
+ *
+ * cat_diff (:210 / :316): out[r][c] = cat(cur_k - last)[c] for k < K, with
+ *   r = row_idx[k] (DEVICE int64, out-of-range skipped) or k when row_idx is
+ *   NULL; each key's difference is formed in the key's dtype; out is fp32
+ *   (out_f64 = 0: fl32 of it, local_w_diffs) or fp64 (the T value itself).
+ * end_round_promoted (:316-319): rows with keep_rows[r] == 0 get
+ *   fl32(row - gdiff) computed in promote(fp32, T); A_mat EMA in T's arithmetic
+ *   (t_kind 0 fp32 / 1 fp64 / 2 fp16 / 3 bf16; a_mat is fp64 [P] when t_kind
+ *   is 1, else fp32) with the mean of gdiff (fp64 [P], T values) rounded to T.
+ * index_f64 (:272 once A_mat is fp64): fpf[r] = norm(diffs[r] * a_mat) /
+ *   g_mat[r] in fp64, NaN/inf replaced by 0.  fpf is DEVICE fp64.
+ */
+typedef struct fedavg_fpf_groups {
+  const void* base[4];
+  int64_t ld[4];
+  int32_t kind[4];
+} fedavg_fpf_groups;
+int fedavg_fpf_cat_diff(const int64_t* keys, int64_t n_keys, int64_t P, const fedavg_fpf_groups* cur,
+                        int64_t K, const fedavg_fpf_groups* last, const int64_t* row_idx,
+                        int64_t n_rows, void* out, int64_t ld_out, int out_f64, void* stream);
+int fedavg_fpf_end_round_promoted(float* diffs, int64_t n_rows, int64_t ld, const uint8_t* keep_rows,
+                                  void* a_mat, const double* gdiff, int64_t P, int t_kind, float g2,
+                                  double* workspace, int64_t workspace_elems, void* stream);
+int fedavg_fpf_index_f64(const float* diffs, int64_t n_rows, int64_t ld, int64_t P,
+                         const double* a_mat, const float* g_mat, double* fpf, void* stream);
+
+/*
  * Device -> pinned-host transfer of `bytes` bytes (the averaged model's D2H
  * feeding fedavg_trainer.py:219).  blocks == 0: the runtime's DMA copy
  * (hipMemcpyAsync; the production choice, fastest end to end).  blocks > 0:

@@ -51,6 +51,10 @@ SIGNATURES = {
     "fedavg_fpf_update_g": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_float, _c_int, _c_float, _vp]),
     "fedavg_fpf_index_f32": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _vp]),
     "fedavg_fpf_index_lru": (_c_int, [_vp, _vp, _c_i64, _vp, _vp]),
+    "fedavg_fpf_cat_diff": (_c_int, [_vp, _c_i64, _c_i64, _vp, _c_i64, _vp, _vp, _c_i64, _vp, _c_i64, _c_int, _vp]),
+    "fedavg_fpf_end_round_promoted": (_c_int, [_vp, _c_i64, _c_i64, _vp, _vp, _vp, _c_i64, _c_int, _c_float, _vp,
+                                               _c_i64, _vp]),
+    "fedavg_fpf_index_f64": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _vp]),
     "fedavg_copy_to_host": (_c_int, [_vp, _vp, _c_i64, _c_int, _vp]),
     "fedavg_upload_shard": (_c_int, [_vp, _c_i64, _vp, _c_i64, _c_i64, _c_i64, _vp]),
     "fedavg_f32_schedule": (_c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp]),
@@ -90,6 +94,13 @@ ABI_VERSION = 1
 FEDAVG_EINVAL = -10001
 FEDAVG_EALIGN = -10002
 FEDAVG_EMODE = -10003
+
+
+class FpfGroups(ctypes.Structure):
+    """fedavg_fpf_groups (include/fedavg_amd.h): row 0 of each dtype group,
+    its row stride in elements, its kind (0 fp32, 1 fp64, 2 fp16, 3 bf16)."""
+
+    _fields_ = [("base", ctypes.c_void_p * 4), ("ld", ctypes.c_int64 * 4), ("kind", ctypes.c_int32 * 4)]
 
 
 class FedAvgLibraryError(RuntimeError):

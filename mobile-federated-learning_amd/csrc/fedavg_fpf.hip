@@ -281,6 +281,169 @@ __global__ __launch_bounds__(kBlock) void fpf_index_lru_kernel(const float* __re
   out[r] = isfinite(f) ? f : 0.f;
 }
 
+// ---------------------------------------------------------------------------
+// Models with fp64 / fp16 / bf16 keys.  torch.cat at :210 and :316 promotes the
+// per-key differences (each computed in its key's dtype) to T, the promoted
+// dtype of all keys: local_w_diffs (fp32) receives fl32 of that, :317 runs in
+// promote(fp32, T), and :319 runs in T -- so A_mat becomes fp64 after the first
+// round of a model with an fp64 key, and a pure fp16/bf16 model forms the
+// A_mat term in 16-bit arithmetic.  The model is described key by key in
+// state_dict order (numel, cat offset, dtype group, offset in the group row,
+// rounding of an fp32-stored integer key's difference to T); the clients'
+// rows are the aggregate's per-dtype group rows.
+// ---------------------------------------------------------------------------
+struct FpfGroups {  // = fedavg_fpf_groups (include/fedavg_amd.h)
+  const void* base[4];
+  int64_t ld[4];
+  int32_t kind[4];
+};
+enum : int { kF32 = 0, kF64 = 1, kF16 = 2, kBF16 = 3 };
+constexpr int kFpfKeyFields = 5;  // numel, cat_off, grp, grp_off, rnd
+
+__device__ __forceinline__ float opaque1(float v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
+// fp32 -> fp16 / bf16 (RNE) -> fp32
+__device__ __forceinline__ float rnd16(float x, int kind) {
+  x = opaque1(x);
+  return kind == kF16 ? static_cast<float>(static_cast<_Float16>(x)) : static_cast<float>(static_cast<__bf16>(x));
+}
+
+// element i of group grp: row `row` of cur minus row 0 of last, in the key's
+// arithmetic (ATen computes a 16-bit difference in fp32 and rounds it)
+__device__ __forceinline__ double cat_diff(const FpfGroups& cur, int64_t row, const FpfGroups& last, int grp,
+                                           int64_t i, int rnd) {
+  const int64_t o = row * cur.ld[grp] + i;
+  switch (cur.kind[grp]) {
+    case kF64:
+      return static_cast<const double*>(cur.base[grp])[o] - static_cast<const double*>(last.base[grp])[i];
+    case kF16:
+      return rnd16(static_cast<float>(static_cast<const _Float16*>(cur.base[grp])[o]) -
+                       static_cast<float>(static_cast<const _Float16*>(last.base[grp])[i]),
+                   kF16);
+    case kBF16:
+      return rnd16(static_cast<float>(static_cast<const __bf16*>(cur.base[grp])[o]) -
+                       static_cast<float>(static_cast<const __bf16*>(last.base[grp])[i]),
+                   kBF16);
+    default: {
+      const float d = static_cast<const float*>(cur.base[grp])[o] - static_cast<const float*>(last.base[grp])[i];
+      return rnd ? rnd16(d, rnd) : d;
+    }
+  }
+}
+
+// :210 / :316  out[row_idx[k]][c] = cat(w_k - last_w)[c] (fl32 of it into fp32
+// rows, or the T value itself into an fp64 vector).  Column c belongs to the
+// last key whose cat offset is <= c (empty keys lose the tie).
+__global__ __launch_bounds__(kBlock) void fpf_cat_diff_kernel(const int64_t* __restrict__ keys, int64_t n_keys,
+                                                              int64_t P, FpfGroups cur, FpfGroups last,
+                                                              const int64_t* __restrict__ row_idx, int64_t n_rows,
+                                                              void* __restrict__ out, int64_t ld_out, int out_f64) {
+  const int64_t c = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (c >= P) return;
+  const int64_t k = blockIdx.y;
+  const int64_t r = row_idx ? row_idx[k] : k;
+  if (r < 0 || r >= n_rows) return;  // the host layer raises IndexError before launching
+  int64_t lo = 0, hi = n_keys - 1;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi + 1) >> 1;
+    if (keys[mid * kFpfKeyFields + 1] <= c)
+      lo = mid;
+    else
+      hi = mid - 1;
+  }
+  const int64_t* kj = keys + lo * kFpfKeyFields;
+  const double v = cat_diff(cur, k, last, static_cast<int>(kj[2]), kj[3] + (c - kj[1]), static_cast<int>(kj[4]));
+  if (out_f64)
+    static_cast<double*>(out)[r * ld_out + c] = v;
+  else
+    static_cast<float*>(out)[r * ld_out + c] = static_cast<float>(v);
+}
+
+// :319 (first half) on the T-valued global_w_diff
+__global__ __launch_bounds__(kBlock) void fpf_sum_f64_kernel(const double* __restrict__ x, int64_t P,
+                                                             double* __restrict__ partials) {
+  __shared__ double red[kBlock / 64];
+  double s = 0.0;
+  for (int64_t c = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; c < P;
+       c += static_cast<int64_t>(gridDim.x) * kBlock)
+    s += x[c];
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) partials[blockIdx.x] = s;
+}
+
+// :316-319 with global_w_diff of dtype T (values in gd):
+//   rows not in client_indexes: fl32(row - g) computed in promote(fp32, T);
+//   A_mat = A_mat * (1 - 1/G2) + g / G2 / mean(g): fp64 for T = fp64 (A in
+//   fp64), fp32 for T = fp32, and for T = fp16/bf16 the term g / G2 / mean is
+//   16-bit (each op in fp32, rounded) and added to the fp32 A_mat.
+template <int T>
+__global__ __launch_bounds__(kBlock) void fpf_end_round_promoted_kernel(
+    float* __restrict__ D, int64_t ld, int64_t n_rows, const uint8_t* __restrict__ keep_rows, void* __restrict__ A,
+    const double* __restrict__ gd, int64_t P, const double* __restrict__ partials, int nparts, double g2, double c2) {
+  __shared__ double red[kBlock / 64];
+  __shared__ double mean_s;
+  double s = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += kBlock) s += partials[i];
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) {
+    const double m = s / static_cast<double>(P);
+    mean_s = T == kF64 ? m : (T == kF32 ? static_cast<double>(static_cast<float>(m)) : rnd16(static_cast<float>(m), T));
+  }
+  __syncthreads();
+  const double mean = mean_s;
+  const float meanf = static_cast<float>(mean);
+  const float g2f = static_cast<float>(g2), c2f = static_cast<float>(c2);
+  const int64_t r0 = static_cast<int64_t>(blockIdx.y) * kFpfRowsPerBlock;
+  const int64_t r1 = r0 + kFpfRowsPerBlock < n_rows ? r0 + kFpfRowsPerBlock : n_rows;
+  for (int64_t c = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; c < P;
+       c += static_cast<int64_t>(gridDim.x) * kBlock) {
+    const double g = gd[c];
+    if (blockIdx.y == 0) {
+      if constexpr (T == kF64) {
+        double* a = static_cast<double*>(A);
+        a[c] = a[c] * c2 + (g / g2) / mean;
+      } else if constexpr (T == kF32) {
+        float* a = static_cast<float*>(A);
+        a[c] = a[c] * c2f + (static_cast<float>(g) / g2f) / meanf;
+      } else {
+        float* a = static_cast<float*>(A);
+        const float t = rnd16(rnd16(static_cast<float>(g) / g2f, T) / meanf, T);
+        a[c] = a[c] * c2f + t;
+      }
+    }
+    for (int64_t r = r0; r < r1; ++r) {
+      if (keep_rows[r]) continue;
+      float* p = D + r * ld + c;
+      if constexpr (T == kF64)
+        *p = static_cast<float>(static_cast<double>(*p) - g);
+      else
+        *p = *p - static_cast<float>(g);
+    }
+  }
+}
+
+// :272, :276-278 once A_mat is fp64: norm(fl64(diff * A)) / G_mat in fp64
+__global__ __launch_bounds__(kBlock) void fpf_index_f64a_kernel(const float* __restrict__ D, int64_t ld, int64_t P,
+                                                                const double* __restrict__ A,
+                                                                const float* __restrict__ G, double* __restrict__ out) {
+  __shared__ double red[kBlock / 64];
+  const int64_t r = blockIdx.x;
+  const float* row = D + r * ld;
+  double s = 0.0;
+  for (int64_t c = threadIdx.x; c < P; c += kBlock) {
+    const double q = static_cast<double>(row[c]) * A[c];
+    s = __builtin_fma(q, q, s);
+  }
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) {
+    const double f = sqrt(s) / static_cast<double>(G[r]);
+    out[r] = isfinite(f) ? f : 0.0;
+  }
+}
+
 unsigned col_blocks(int64_t P, int64_t cap) {
   const int64_t nvec = (P + 3) / 4;
   int64_t b = (nvec + kBlock - 1) / kBlock;
@@ -412,6 +575,82 @@ int fedavg_fpf_index_variant(const float* diffs, int64_t n_rows, int64_t ld, int
   return launch_status(what);
 }
 #endif  // FEDAVG_TUNING
+
+int fedavg_fpf_cat_diff(const int64_t* keys, int64_t n_keys, int64_t P, const fedavg_fpf_groups* cur, int64_t K,
+                        const fedavg_fpf_groups* last, const int64_t* row_idx, int64_t n_rows, void* out,
+                        int64_t ld_out, int out_f64, void* stream) {
+  const char* what = "fedavg_fpf_cat_diff";
+  if (!keys || n_keys <= 0 || !cur || !last || !out) return set_error(FEDAVG_EINVAL, "%s: bad arguments", what);
+  if (P <= 0 || ld_out < P) return set_error(FEDAVG_EINVAL, "%s: need 1 <= P <= ld_out", what);
+  if (K <= 0 || K > 65535) return set_error(FEDAVG_EINVAL, "%s: K must be in [1, 65535] (got %lld)", what, (long long)K);
+  if (n_rows <= 0 || (!row_idx && n_rows < K)) return set_error(FEDAVG_EINVAL, "%s: bad n_rows", what);
+  FpfGroups c{}, l{};
+  for (int g = 0; g < 4; ++g) {
+    if (cur->kind[g] < kF32 || cur->kind[g] > kBF16 || cur->kind[g] != last->kind[g])
+      return set_error(FEDAVG_EINVAL, "%s: group %d: bad or mismatched kind", what, g);
+    c.base[g] = cur->base[g];
+    c.ld[g] = cur->ld[g];
+    c.kind[g] = cur->kind[g];
+    l.base[g] = last->base[g];
+    l.ld[g] = last->ld[g];
+    l.kind[g] = last->kind[g];
+  }
+  hipLaunchKernelGGL(fpf_cat_diff_kernel, dim3(static_cast<unsigned>((P + kBlock - 1) / kBlock), static_cast<unsigned>(K)),
+                     dim3(kBlock), 0, static_cast<hipStream_t>(stream), keys, n_keys, P, c, l, row_idx, n_rows, out,
+                     ld_out, out_f64 ? 1 : 0);
+  return launch_status(what);
+}
+
+int fedavg_fpf_end_round_promoted(float* diffs, int64_t n_rows, int64_t ld, const uint8_t* keep_rows, void* a_mat,
+                                  const double* gdiff, int64_t P, int t_kind, float g2, double* workspace,
+                                  int64_t workspace_elems, void* stream) {
+  const char* what = "fedavg_fpf_end_round_promoted";
+  int rc = check_state(diffs, n_rows, ld, P, what);
+  if (rc) return rc;
+  if (!keep_rows || !a_mat || !gdiff || !workspace) return set_error(FEDAVG_EINVAL, "%s: null buffer", what);
+  const unsigned nparts = col_blocks(P, kFpfMaxPartials);
+  if (workspace_elems < nparts) return set_error(FEDAVG_EINVAL, "%s: workspace needs %u doubles", what, nparts);
+  if (!(g2 != 0.f)) return set_error(FEDAVG_EINVAL, "%s: G2 must be nonzero", what);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(fpf_sum_f64_kernel, dim3(nparts), dim3(kBlock), 0, s, gdiff, P, workspace);
+  rc = launch_status(what);
+  if (rc) return rc;
+  const double c2 = 1.0 - 1.0 / static_cast<double>(g2);  // (1 - 1/G2) as a Python float
+  const dim3 grid(static_cast<unsigned>((P + kBlock - 1) / kBlock < 512 ? (P + kBlock - 1) / kBlock : 512),
+                  static_cast<unsigned>((n_rows + kFpfRowsPerBlock - 1) / kFpfRowsPerBlock));
+  const int np = static_cast<int>(nparts);
+  switch (t_kind) {
+    case kF32:
+      hipLaunchKernelGGL(fpf_end_round_promoted_kernel<kF32>, grid, dim3(kBlock), 0, s, diffs, ld, n_rows, keep_rows,
+                         a_mat, gdiff, P, workspace, np, static_cast<double>(g2), c2);
+      break;
+    case kF64:
+      hipLaunchKernelGGL(fpf_end_round_promoted_kernel<kF64>, grid, dim3(kBlock), 0, s, diffs, ld, n_rows, keep_rows,
+                         a_mat, gdiff, P, workspace, np, static_cast<double>(g2), c2);
+      break;
+    case kF16:
+      hipLaunchKernelGGL(fpf_end_round_promoted_kernel<kF16>, grid, dim3(kBlock), 0, s, diffs, ld, n_rows, keep_rows,
+                         a_mat, gdiff, P, workspace, np, static_cast<double>(g2), c2);
+      break;
+    case kBF16:
+      hipLaunchKernelGGL(fpf_end_round_promoted_kernel<kBF16>, grid, dim3(kBlock), 0, s, diffs, ld, n_rows, keep_rows,
+                         a_mat, gdiff, P, workspace, np, static_cast<double>(g2), c2);
+      break;
+    default: return set_error(FEDAVG_EINVAL, "%s: t_kind must be 0..3 (got %d)", what, t_kind);
+  }
+  return launch_status(what);
+}
+
+int fedavg_fpf_index_f64(const float* diffs, int64_t n_rows, int64_t ld, int64_t P, const double* a_mat,
+                         const float* g_mat, double* fpf, void* stream) {
+  const char* what = "fedavg_fpf_index_f64";
+  int rc = check_state(diffs, n_rows, ld, P, what);
+  if (rc) return rc;
+  if (!a_mat || !g_mat || !fpf) return set_error(FEDAVG_EINVAL, "%s: null buffer", what);
+  hipLaunchKernelGGL(fpf_index_f64a_kernel, dim3(static_cast<unsigned>(n_rows)), dim3(kBlock), 0,
+                     static_cast<hipStream_t>(stream), diffs, ld, P, a_mat, g_mat, fpf);
+  return launch_status(what);
+}
 
 int fedavg_fpf_index_lru(const float* lru_itr, const float* g_mat, int64_t n_rows, float* fpf, void* stream) {
   const char* what = "fedavg_fpf_index_lru";

@@ -33,16 +33,26 @@ fp64-accumulated reduction each (``mean`` at :319, ``norm`` at :272) and agree
 with the reference to its own fp32 rounding error (tests/test_gpu_parity.py,
 pinned by the reference's own round loop: tests/golden/fpf).
 
+Models with fp64 / fp16 / bf16 keys follow ``torch.cat``'s promotion at
+:210/:316: each key's difference is formed in its own dtype and the
+concatenation has the promoted dtype T of all keys.  ``local_w_diffs`` stays
+fp32 (it receives fl32 of the T values), :317 runs in promote(fp32, T), and
+:319 in T: ``A_mat`` becomes fp64 after the first ``end_round`` of a model
+with an fp64 key (and the FPF2 index fp64 with it), while a pure fp16/bf16
+model forms ``g / G2 / g.mean()`` in 16-bit arithmetic before adding it to
+the fp32 ``A_mat``.  These run the per-key kernels of the promoted path
+(``fedavg_fpf_cat_diff`` / ``fedavg_fpf_end_round_promoted`` /
+``fedavg_fpf_index_f64``) over the aggregate's per-dtype group rows.
+
 Error behaviour kept: a client index outside ``[-N, N)`` raises
 ``IndexError`` where the reference's tensor indexing does (:210 in full mode,
 :322 when iterations are recorded); ``round_idx`` outside
 ``[-comm_round, comm_round)`` raises ``IndexError`` (:322/:327); a bool key
-raises ``RuntimeError`` at :210 (torch refuses ``bool - bool``).  fp64 and
-fp16/bf16 keys are refused at construction (they change ``torch.cat``'s
-result dtype at :210/:316).
+raises ``RuntimeError`` at :210 (torch refuses ``bool - bool``).
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Mapping, Optional, Sequence
 
 import numpy as np
@@ -50,12 +60,15 @@ import torch
 
 from . import _lib
 from .layout import KeyTable
+from .reduce import ALIGN_ELEMS
 
 __all__ = ["FPFTracker", "G1", "G2", "THRESHOLD_WEIGHT_SIZE"]
 
 G1 = 2  # config.py:74
 G2 = 2  # config.py:75
 THRESHOLD_WEIGHT_SIZE = 100000  # config.py:83
+
+_KIND = {torch.float32: 0, torch.float64: 1, torch.float16: 2, torch.bfloat16: 3}  # fedavg_fpf_groups.kind
 
 
 class FPFTracker:
@@ -85,11 +98,14 @@ class FPFTracker:
         self._g = torch.zeros(self.n, dtype=torch.float32, device=dev)  # :110
         self._out = torch.empty(self.n, dtype=torch.float32, device=dev)
         self._out_host = torch.empty(self.n, dtype=torch.float32, pin_memory=True)
+        self._mixed = False
+        self._a_is64 = False
         if self.full:
             self.table = KeyTable(model_state)
+            self._has_bool = any(e.src_dtype == torch.bool for e in self.table.entries)
             if set(self.table.groups) != {torch.float32}:
-                raise NotImplementedError("FPF2 diffs support fp32/integer state_dicts (fp64/fp16/bf16 keys change "
-                                          "torch.cat's result dtype at fedavg_trainer.py:210/:316)")
+                self._init_promoted(dev)
+        if self.full and not self._mixed:
             self.P = self.table.groups[torch.float32].P
             self.ld = self.table.groups[torch.float32].ld
             self._has_bool = any(e.src_dtype == torch.bool for e in self.table.entries)
@@ -101,10 +117,43 @@ class FPFTracker:
             self._host = torch.zeros((1, self.ld), dtype=torch.float32, pin_memory=True)
             self._ws = torch.empty(max(1, self._lib.fedavg_fpf_workspace(self.P)), dtype=torch.float64, device=dev)
             self._lru = None
-        else:
+        elif not self.full:
             self.P = self.weight_size
             self._lru = torch.zeros(self.n, dtype=torch.float32, device=dev)  # :118
         self._have_last_w = False
+
+    def _init_promoted(self, dev) -> None:
+        """State for a model with fp64/fp16/bf16 keys: local_w_diffs / A_mat in
+        torch.cat's column order over every key, per-dtype group rows for
+        last_w, one client and w_glob, and the device key table."""
+        self._mixed = True
+        T = None
+        for e in self.table.entries:
+            T = e.src_dtype if T is None else torch.promote_types(T, e.src_dtype)
+        self.T = T  # torch.cat's result dtype at :210/:316
+        self.P = self.weight_size
+        self.ld = max((self.P + ALIGN_ELEMS - 1) // ALIGN_ELEMS * ALIGN_ELEMS, ALIGN_ELEMS)
+        gidx = {dt: i for i, dt in enumerate(self.table.groups)}
+        # an integer key's difference (held as fp32 in the fp32 group) is cast to a 16-bit T by the cat
+        rnd = _KIND[T] if T in (torch.float16, torch.bfloat16) else 0
+        keys, cat = [], 0
+        for e in self.table.entries:
+            keys.append([e.numel, cat, gidx[e.dtype], e.offset, 0 if e.src_dtype.is_floating_point else rnd])
+            cat += e.numel
+        self._keys = torch.tensor(keys, dtype=torch.int64).to(dev)
+        groups = self.table.groups
+        self._gl = {dt: torch.zeros(g.ld, dtype=dt, device=dev) for dt, g in groups.items()}  # last_w (:165)
+        self._gr = {dt: torch.zeros((1, g.ld), dtype=dt, device=dev) for dt, g in groups.items()}  # one client
+        self._gg = {dt: torch.zeros(g.ld, dtype=dt, device=dev) for dt, g in groups.items()}  # w_glob
+        self._gh = {dt: torch.zeros((1, g.ld), dtype=dt, pin_memory=True) for dt, g in groups.items()}
+        self._diffs = torch.zeros((self.n, self.ld), dtype=torch.float32, device=dev)  # :115
+        self._a = torch.ones(self.ld, dtype=torch.float32, device=dev)  # :114
+        self._a64 = torch.ones(self.ld, dtype=torch.float64, device=dev) if T == torch.float64 else None
+        self._gd = torch.zeros(self.ld, dtype=torch.float64, device=dev)  # global_w_diff (:316), T values
+        self._ws = torch.empty(max(1, self._lib.fedavg_fpf_workspace(self.P)), dtype=torch.float64, device=dev)
+        self._out64 = torch.empty(self.n, dtype=torch.float64, device=dev)
+        self._out64_host = torch.empty(self.n, dtype=torch.float64, pin_memory=True)
+        self._lru = None
 
     # -- state views (the reference's tensors) ---------------------------
     @property
@@ -113,7 +162,7 @@ class FPFTracker:
 
     @property
     def A_mat(self) -> torch.Tensor:
-        return self._a[:self.P]
+        return (self._a64 if self._a_is64 else self._a)[:self.P]
 
     @property
     def G_mat(self) -> torch.Tensor:
@@ -166,10 +215,93 @@ class FPFTracker:
 
     def _check_glob_table(self, w_glob) -> KeyTable:
         gt = KeyTable(w_glob)
-        if (set(gt.groups) != {torch.float32}
-                or [(e.name, e.numel) for e in gt.entries] != [(e.name, e.numel) for e in self.table.entries]):
-            raise ValueError("w_glob does not hold the tracked model's keys/shapes as fp32")
+        if (set(gt.groups) != set(self.table.groups)
+                or [(e.name, e.numel, e.dtype) for e in gt.entries]
+                != [(e.name, e.numel, e.dtype) for e in self.table.entries]):
+            raise ValueError("w_glob does not hold the tracked model's keys/shapes/dtypes")
         return gt
+
+    def _same_round_table(self, table: KeyTable) -> bool:
+        return ([(e.name, e.numel, e.dtype) for e in table.entries]
+                == [(e.name, e.numel, e.dtype) for e in self.table.entries])
+
+    # -- promoted (fp64 / fp16 / bf16 keys) path ---------------------------
+    def _upload_groups(self, table: KeyTable, sd: Mapping[str, torch.Tensor], dsts) -> None:
+        """Pack one state_dict's dtype groups into ``dsts[dtype]`` (device,
+        row 0): on the device from device tensors, else through the pinned rows."""
+        agg = self._aggregator()
+        where = agg._client_device(table, [sd])  # ValueError for another GPU
+        ptrs, keep = table.collect([sd], where)
+        with torch.cuda.device(self.device):
+            stream = torch.cuda.current_stream(self.device)
+            if where.type == "cuda":
+                for dt, g in table.groups.items():
+                    agg._pack_on_device(table, g, ptrs, 0, dsts[dt], stream)
+            else:
+                stream.synchronize()  # the pinned rows are free again
+                for dt, g in table.groups.items():
+                    host = self._gh[dt]
+                    items = table.pack_items(g, ptrs, 0, g.ld)
+                    _lib.check(self._lib.fedavg_pack_rows(items.ctypes.data, items.shape[0], host.data_ptr(),
+                                                          host.element_size(), max(1, torch.get_num_threads())),
+                               "fedavg_pack_rows")
+                    dsts[dt].reshape(-1)[:g.ld].copy_(host[0], non_blocking=True)
+        del keep
+
+    def _groups(self, rows) -> "_lib.FpfGroups":
+        """fedavg_fpf_groups from {dtype: (device tensor whose first element is
+        row 0, row stride in elements)}; unused groups stay kind 0."""
+        s = _lib.FpfGroups()
+        for i, dt in enumerate(self.table.groups):
+            t, ld = rows[dt]
+            s.base[i] = t.data_ptr()
+            s.ld[i] = int(ld)
+            s.kind[i] = _KIND[dt]
+        return s
+
+    def _cat_rows(self, rows, idx: Sequence[int]) -> None:
+        """:210 for client rows ``rows[dtype]`` [K, ld_g] -> local_w_diffs[idx]
+        (duplicates: the reference's sequential writes leave the last one)."""
+        last = {}
+        for k, r in enumerate(idx):
+            last[r] = k
+        ks = sorted(last.values())
+        groups = [(0, list(idx))] if len(ks) == len(idx) else [(k, [idx[k]]) for k in ks]
+        lastg = self._groups({dt: (self._gl[dt], self.table.groups[dt].ld) for dt in self.table.groups})
+        with torch.cuda.device(self.device):
+            for k0, rs in groups:
+                cur = self._groups({dt: (t[k0], t.stride(0)) for dt, t in rows.items()})
+                ridx = torch.tensor(rs, dtype=torch.int64).to(self.device, non_blocking=True)
+                _lib.check(self._lib.fedavg_fpf_cat_diff(
+                    self._keys.data_ptr(), self._keys.shape[0], self.P, ctypes.addressof(cur), len(rs),
+                    ctypes.addressof(lastg), ridx.data_ptr(), self.n, self._diffs.data_ptr(), self.ld, 0,
+                    self._stream()), "fedavg_fpf_cat_diff")
+
+    def _glob_groups(self, w_glob):
+        """w_glob's dtype groups on the device: the averaged groups the
+        aggregate left in HBM, else uploaded."""
+        last = self._aggregator()._last
+        acc = last.get("acc")
+        if (acc is not None and acc() is w_glob and set(last.get("dev", {})) == set(self.table.groups)
+                and self._same_round_table(last["table"])):
+            return {dt: (last["dev"][dt][1], self.table.groups[dt].ld) for dt in self.table.groups}
+        gt = self._check_glob_table(w_glob)
+        self._upload_groups(gt, w_glob, self._gg)
+        return {dt: (self._gg[dt], self.table.groups[dt].ld) for dt in self.table.groups}
+
+    def _end_round_promoted(self, w_glob, keep_dev, s) -> None:
+        """:316-319 under torch.cat's promotion."""
+        cur = self._groups(self._glob_groups(w_glob))
+        lastg = self._groups({dt: (self._gl[dt], self.table.groups[dt].ld) for dt in self.table.groups})
+        _lib.check(self._lib.fedavg_fpf_cat_diff(
+            self._keys.data_ptr(), self._keys.shape[0], self.P, ctypes.addressof(cur), 1, ctypes.addressof(lastg),
+            None, 1, self._gd.data_ptr(), self.ld, 1, s), "fedavg_fpf_cat_diff")
+        a = self._a64 if self.T == torch.float64 else self._a
+        _lib.check(self._lib.fedavg_fpf_end_round_promoted(
+            self._diffs.data_ptr(), self.n, self.ld, keep_dev.data_ptr(), a.data_ptr(), self._gd.data_ptr(), self.P,
+            _KIND[self.T], self.g2, self._ws.data_ptr(), self._ws.numel(), s), "fedavg_fpf_end_round_promoted")
+        if self.T == torch.float64:
+            self._a_is64 = True  # A_mat * 0.5 (fp32) + fp64 term -> fp64 from now on
 
     def _check_bool(self):
         if self._has_bool:
@@ -200,7 +332,9 @@ class FPFTracker:
     # -- the reference's steps -------------------------------------------
     def begin_round(self, last_w: Mapping[str, torch.Tensor]) -> None:
         """:165 -- the global model the round's clients start from."""
-        if self.full:
+        if self.full and self._mixed:
+            self._upload_groups(self.table, last_w, self._gl)
+        elif self.full:
             self._upload(self.table, last_w, self._last_w)
         self._have_last_w = True
 
@@ -211,6 +345,10 @@ class FPFTracker:
         self._need_last_w()
         r = self._row_index(client_idx)
         self._check_bool()
+        if self._mixed:
+            self._upload_groups(self.table, w, {dt: t[0] for dt, t in self._gr.items()})
+            self._cat_rows(self._gr, [r])
+            return
         self._upload(self.table, w, self._row[0])
         self._set_rows(self._row, self.ld, [r])
 
@@ -234,21 +372,35 @@ class FPFTracker:
         refs = last.get("refs")
         ok = (refs is not None and last["acc"]() is w_glob and len(refs) == len(w_locals)
               and all(r() is sd for r, (_, sd) in zip(refs, w_locals))
-              and set(last.get("dev", {})) == {torch.float32}
-              and [(e.name, e.numel) for e in last["table"].entries]
-              == [(e.name, e.numel) for e in self.table.entries])
+              and set(last.get("dev", {})) == set(self.table.groups)
+              and self._same_round_table(last["table"]))
         if not ok:
             raise ValueError("record_round needs the device rows of the aggregate that produced w_glob; "
                              "call record_client(client_idx, w) before aggregate instead")
-        devbuf = self._aggregator().materialize_rows()  # packed on demand after a zero-copy round
-        if devbuf is None:
+        has_f32 = torch.float32 in self.table.groups
+        devbuf = self._aggregator().materialize_rows() if has_f32 else None  # packed on demand after zero-copy
+        if devbuf is None and has_f32:
             raise ValueError("record_round: the round's client dicts are gone; call record_client before aggregate")
+        if self._mixed:
+            rows = {dt: (devbuf if dt == torch.float32 else last["dev"][dt][0]) for dt in self.table.groups}
+            if any(v is None for v in rows.values()):
+                raise ValueError("record_round: the round left no device rows for every dtype group; "
+                                 "call record_client before aggregate")
+            self._cat_rows(rows, idx)
+            return
         self._set_rows(devbuf, devbuf.stride(0), idx)
 
     def fpf_index(self) -> np.ndarray:
         """:271-278 -- the FPF2 index per vehicle, NaN/inf replaced by 0 (float32)."""
         with torch.cuda.device(self.device):
             s = self._stream()
+            if self._a_is64:  # A_mat is fp64 (a model with an fp64 key, after its first end_round)
+                _lib.check(self._lib.fedavg_fpf_index_f64(self._diffs.data_ptr(), self.n, self.ld, self.P,
+                                                          self._a64.data_ptr(), self._g.data_ptr(),
+                                                          self._out64.data_ptr(), s), "fedavg_fpf_index_f64")
+                self._out64_host.copy_(self._out64, non_blocking=True)
+                torch.cuda.current_stream(self.device).synchronize()
+                return self._out64_host.numpy().copy()
             if self.full:
                 _lib.check(self._lib.fedavg_fpf_index_f32(self._diffs.data_ptr(), self.n, self.ld, self.P,
                                                           self._a.data_ptr(), self._g.data_ptr(),
@@ -274,10 +426,13 @@ class FPFTracker:
                 self._need_last_w()
                 if w_glob is None:
                     raise ValueError("full FPF2 mode needs w_glob (fedavg_trainer.py:316)")
-                glob_dev = self._glob_on_device(w_glob)
+                glob_dev = None if self._mixed else self._glob_on_device(w_glob)
                 keep = np.ones(self.n, dtype=np.uint8)  # rows NOT in set(range(N)) - set(client_indexes)
                 keep[list(set(range(self.n)) - set(client_indexes))] = 0
                 keep_dev = torch.from_numpy(keep).to(self.device, non_blocking=True)
+            if self.full and self._mixed:
+                self._end_round_promoted(w_glob, keep_dev, s)
+            elif self.full:
                 _lib.check(self._lib.fedavg_fpf_end_round_f32(
                     self._diffs.data_ptr(), self.n, self.ld, keep_dev.data_ptr(), self._a.data_ptr(),
                     glob_dev.data_ptr(), self._last_w.data_ptr(), self.P, self.g2, self._ws.data_ptr(),

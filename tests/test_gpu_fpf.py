@@ -231,9 +231,115 @@ def test_fpf_errors_like_reference():
         t.end_round(0, [9], 1, init)
     with pytest.raises(ValueError):
         t.record_round([0], [(1, copy.deepcopy(init))], init)  # no device rows of this round
-    with pytest.raises(NotImplementedError):
-        mfl_amd.FPFTracker(8, OrderedDict(w=torch.zeros(3, dtype=torch.float64)), 3, device=DEV)
     tb = mfl_amd.FPFTracker(8, OrderedDict(w=torch.zeros(3), m=torch.zeros(2, dtype=torch.bool)), 3, device=DEV)
     tb.begin_round(OrderedDict(w=torch.zeros(3), m=torch.zeros(2, dtype=torch.bool)))
     with pytest.raises(RuntimeError):
         tb.record_client(0, OrderedDict(w=torch.ones(3), m=torch.ones(2, dtype=torch.bool)))
+
+
+# ---------------------------------------------------------------------------
+# models with fp64 / fp16 / bf16 keys: torch.cat's promotion at :210 / :316
+# ---------------------------------------------------------------------------
+F16, BF16, F32, F64 = torch.float16, torch.bfloat16, torch.float32, torch.float64
+
+# (weight dtype, bias dtype, integer buffer?) -> torch.cat's dtype T
+MIXED = {
+    "f32w_f64b": ((F32, F64, False), F64),
+    "f64_only": ((F64, F64, False), F64),
+    "f64w_int": ((F64, F32, True), F64),
+    "f32w_f16b": ((F32, F16, False), F32),
+    "bf16w_f32b_int": ((BF16, F32, True), F32),
+    "f16w_bf16b": ((F16, BF16, False), F32),
+    "f16_only_int": ((F16, F16, True), F16),
+    "bf16_only": ((BF16, BF16, False), BF16),
+}
+# A_mat / index tolerance by T: one fp64 / fp32 mean each (ours summed in fp64
+# in a fixed order); a 16-bit T rounds the mean and the :319 term to 16 bits,
+# where a different mean rounding moves the term by one 16-bit ulp
+MIXED_RTOL = {F64: 1e-12, F32: RTOL, F16: 2e-3, BF16: 1.6e-2}
+
+
+def _mixed_case(n_total, P, rounds, seed, wdt, bdt, int_key):
+    rng = np.random.default_rng(seed)
+    g = torch.Generator().manual_seed(seed)
+    nb = 10
+    init = OrderedDict(weight=torch.randn(P - nb - int(int_key), generator=g).to(wdt),
+                       bias=torch.randn(nb, generator=g).to(bdt))
+    if int_key:
+        init["num_batches_tracked"] = torch.tensor(5, dtype=torch.int64)
+    meta = {"client_num_in_total": n_total, "comm_round": len(rounds), "threshold": FO.THRESHOLD_WEIGHT_SIZE,
+            "rounds": []}
+    states = []
+    for t, (K, itr) in enumerate(rounds):
+        K = min(K, n_total)
+        idx = sorted(rng.choice(n_total, size=K, replace=False).tolist())
+        if t == 2 and K >= 3:
+            idx[-1] = idx[0]
+        rng.shuffle(idx)
+        meta["rounds"].append({"client_indexes": idx, "local_itr": itr,
+                               "sample_nums": rng.integers(1, 500, size=K).tolist()})
+        round_states = []
+        for _ in range(K):
+            sd = OrderedDict()
+            for k, v in init.items():
+                sd[k] = (v + 1 if v.dtype == torch.int64
+                         else (v.float() + 0.05 * torch.randn(v.shape, generator=g) * (1 + t)).to(v.dtype))
+            round_states.append(sd)
+        states.append(round_states)
+    return fpf_replay.FPFCase(meta, init, states, None)
+
+
+@pytest.mark.parametrize("after", [False, True], ids=["record_client", "record_round"])
+@pytest.mark.parametrize("name", list(MIXED))
+def test_fpf_promoted_dtypes_vs_oracle(name, after):
+    """fedavg_trainer.py:210/:316-319/:272 on models whose keys promote torch.cat
+    to fp64 / fp32 / fp16 / bf16: local_w_diffs, G_mat and local_itr_lst
+    bit-identical to the oracle (the reference's own torch expressions), A_mat
+    of the reference's dtype (fp64 once an fp64 key is in the model) and the
+    FPF2 index of its dtype, within MIXED_RTOL."""
+    (wdt, bdt, int_key), T = MIXED[name]
+    case = _mixed_case(60, 1500, ROUNDS, seed=17, wdt=wdt, bdt=bdt, int_key=int_key)
+    t, o, rows_t, rows_o = _replay_both(case, after)
+    assert t._mixed and t.T == T
+    assert torch.equal(t.local_w_diffs.cpu(), o.local_w_diffs)  # bit-identical
+    assert torch.equal(t.G_mat.cpu(), o.G_mat)
+    assert torch.equal(t.local_itr_lst.cpu(), o.local_itr_lst)
+    assert t.A_mat.dtype == o.A_mat.dtype  # fp64 after the first round when T is fp64
+    rtol = MIXED_RTOL[T]
+    a_t, a_o = t.A_mat.cpu().double().numpy(), o.A_mat.double().numpy()
+    np.testing.assert_allclose(a_t, a_o, rtol=rtol, atol=rtol * np.abs(a_o).max())
+    got, exp = t.fpf_index(), o.fpf_index()
+    assert got.dtype == exp.dtype  # fp64 index once A_mat is fp64
+    assert np.array_equal(got == 0, exp == 0)
+    np.testing.assert_allclose(got, exp, rtol=rtol, atol=0)
+    for r in range(len(ROUNDS)):
+        assert np.array_equal(rows_t[r] == 0, rows_o[r] == 0)
+        np.testing.assert_allclose(rows_t[r], rows_o[r], rtol=max(rtol, RTOL), atol=0)
+
+
+@pytest.mark.parametrize("name", ["f32w_f64b", "f16_only_int"])
+def test_fpf_promoted_device_clients(name):
+    """The promoted path with every state_dict on the GPU: same bits as the
+    host-client loop."""
+    (wdt, bdt, int_key), T = MIXED[name]
+    case = _mixed_case(40, 900, ROUNDS[:4], seed=23, wdt=wdt, bdt=bdt, int_key=int_key)
+    for after in (False, True):
+        got = fpf_replay.replay(case, _DeviceTrackerImpl(case.meta, case.init), record_after_aggregate=after)
+        host = fpf_replay.replay(case, _TrackerImpl(case.meta, case.init), record_after_aggregate=after)
+        assert np.array_equal(got.view(np.uint32), host.view(np.uint32))
+
+
+def test_fpf_promoted_first_round_index_is_fp32():
+    """Before the first end_round A_mat is the fp32 ones of :114, so the
+    index of a model with an fp64 key is still fp32 (norm of fp32 * fp32)."""
+    init = OrderedDict(w=torch.randn(50), b=torch.randn(5, dtype=torch.float64))
+    t = mfl_amd.FPFTracker(8, init, 3, device=DEV)
+    o = FO.FPFOracle(8, 55, 3)
+    t.begin_round(init)
+    w = OrderedDict(w=init["w"] + 0.5, b=init["b"] - 0.25)
+    t.record_client(3, w)
+    o.record_client(3, w, init)
+    got, exp = t.fpf_index(), o.fpf_index()
+    assert got.dtype == exp.dtype == np.float32
+    assert torch.equal(t.local_w_diffs.cpu(), o.local_w_diffs)
+    np.testing.assert_array_equal(got, exp)  # G_mat = 0: inf/NaN scrubbed to 0 on both sides
