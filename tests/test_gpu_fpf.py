@@ -343,3 +343,32 @@ def test_fpf_promoted_first_round_index_is_fp32():
     assert got.dtype == exp.dtype == np.float32
     assert torch.equal(t.local_w_diffs.cpu(), o.local_w_diffs)
     np.testing.assert_array_equal(got, exp)  # G_mat = 0: inf/NaN scrubbed to 0 on both sides
+
+
+@pytest.mark.parametrize("name", ["float64_key_k3", "float16_key_k3", "bfloat16_key_k3"])
+def test_fpf_promoted_on_reference_dtype_goldens(name):
+    """One FPF2 round over the reference-captured dtype goldens: last_w is the
+    first client's model, the K clients are the round's, w_glob is the
+    reference's own aggregate output (tests/golden)."""
+    from golden_io import load_case
+
+    meta, w_locals, expected = load_case(name)
+    last_w = copy.deepcopy(w_locals[0][1])
+    P = sum(v.numel() for v in last_w.values())
+    n = len(w_locals) + 2
+    t = mfl_amd.FPFTracker(n, last_w, 2, device=DEV)
+    o = FO.FPFOracle(n, P, 2)
+    t.begin_round(last_w)
+    idx = list(range(1, len(w_locals) + 1))
+    for c, (_, w) in zip(idx, w_locals):
+        t.record_client(c, w)
+        o.record_client(c, w, last_w)
+    t.end_round(0, idx, 2, expected)
+    o.end_round(0, idx, 2, expected, last_w)
+    assert torch.equal(t.local_w_diffs.cpu(), o.local_w_diffs)
+    assert t.A_mat.dtype == o.A_mat.dtype
+    rtol = MIXED_RTOL[t.T]
+    np.testing.assert_allclose(t.A_mat.cpu().double().numpy(), o.A_mat.double().numpy(), rtol=rtol)
+    got, exp = t.fpf_index(), o.fpf_index()
+    assert got.dtype == exp.dtype
+    np.testing.assert_allclose(got, exp, rtol=rtol, atol=0)
