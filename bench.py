@@ -621,7 +621,7 @@ def main(argv=None):
         bytes_call = algorithmic_bytes(K, S)
         achieved = bytes_call / (kernel_ms_max * 1e-3) / 1e9
         if sched:
-            kname = f"{sched['kernel']}<U={sched['unroll']},C={sched['cols']},nt={sched['nontemporal']}"
+            kname = f"{sched['kernel']}<U={sched['unroll']},C={sched['cols']},nt={min(1, sched['nontemporal'])}"
             if sched.get("block", 256) != 256:
                 kname += f",B={sched['block']}"
             kname += f"> (exact, sequential client order; round-split x{launches_per_call})"

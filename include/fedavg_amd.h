@@ -258,8 +258,10 @@ int fedavg_reduce_f32_timed(const float* clients, int64_t K, int64_t P, int64_t 
 
 /*
  * The schedule fedavg_reduce_f32() uses for an aligned [K, P] problem:
- * rows per load batch, 16-B column slices per thread, nontemporal loads, and
- * the number of round-split launches.  Host-only query (bench.py names the kernel from it).
+ * rows per load batch, 16-B column slices per thread, the kernel and load
+ * policy (nontemporal: 0 default-policy loads, 1 nontemporal loads through
+ * global pointers, 2 nontemporal loads through per-row buffer descriptors),
+ * and the number of round-split launches.  Host-only query (bench.py names the kernel from it).
  */
 int fedavg_f32_schedule(int64_t K, int64_t P, int* unroll, int* cols, int* nontemporal, int* launches);
 /* The same for P columns of a row buffer with row stride ld (a column chunk

@@ -177,10 +177,10 @@ def f32_schedule(K: int, P: int, ld: int = 0) -> dict:
     else:
         check(load().fedavg_f32_schedule(K, P, *[ctypes.byref(v) for v in vals]), "fedavg_f32_schedule")
     sc = dict(zip(("unroll", "cols", "nontemporal", "launches"), (v.value for v in vals)))
-    # launch_production_f32 (csrc/fedavg_reduce.hip): 16-slice groups go
-    # through per-row buffer descriptors, every other schedule through the
-    # global-pointer variant kernel; 256-thread workgroups
-    sc["kernel"] = "reduce_f32x4_buf_kernel" if sc["cols"] == 16 else "reduce_f32x4_var_kernel"
+    # launch_production_f32 (csrc/fedavg_reduce.hip): nontemporal == 2 marks
+    # the per-row buffer-descriptor kernel (nontemporal loads), 1 / 0 the
+    # global-pointer variant kernel with / without them; 256-thread workgroups
+    sc["kernel"] = "reduce_f32x4_buf_kernel" if sc["nontemporal"] == 2 else "reduce_f32x4_var_kernel"
     sc["block"] = 256
     return sc
 

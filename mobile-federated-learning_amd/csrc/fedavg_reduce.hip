@@ -422,6 +422,7 @@ __global__ __launch_bounds__(kBlock) void round_small_f32x4_kernel(
 
 struct Schedule {
   int unroll, cols, nt, blocks_per_launch;
+  int buf = 0;  // 1: reduce_f32x4_buf_kernel (per-row buffer descriptors); blocks_per_launch 0 = resident blocks
 };
 
 // Round-split launches hold 3 blocks per CU (768 on the 256-CU MI355X); the
@@ -488,6 +489,25 @@ Schedule choose_f32_schedule(int64_t K, int64_t P, int64_t ld) {
   if (sc.nt && sc.unroll == 4 && sc.cols == 8 && nvec >= full * kBlock * 16) {
     sc.unroll = 2;
     sc.cols = 16;
+    sc.buf = 1;
+  }
+  // Few clients (5 <= K < 64) on rows below the 8-slice band: per-row buffer
+  // descriptors with 1-2 slices per thread and a launch of every resident
+  // block.  rocprofv3 kernel time, variants interleaved in one process, two
+  // sweeps (scripts/buf_probe.py; profiles/r02/sweeps/small_k_*.json):
+  //   4-slice band (2.1M <= P < 4.2M): U8 x C2 -- K=5 x 2.4M 0.68-0.73 x the
+  //     time of U8 x C4 (nt), K=10 x 2.4M 0.72-0.73 x U16 x C4 (Infinity-Cache
+  //     band), K=32 / 50 x 2.4M 0.89 / 0.94 x;
+  //   shorter rows, 8 <= K <= 32, P >= 262K: U8 x C1 -- K=10 x 1.2M (FEMNIST)
+  //     0.88 x, K=10 x 300K 0.69-0.73 x, K=20 / 32 x 1.2M 0.81-0.85 / 0.73 x,
+  //     K=32 x 300K 0.80 x; K=5 and K=50 gain nothing there.
+  // (K >= 64 keeps the rules above, tuned on the all-gather chunk shapes.)
+  if (K >= 5 && K < kManyClients && nvec < full * kBlock * 8) {
+    if (nvec >= full * kBlock * 4) {
+      sc = Schedule{8, 2, 1, 0, 1};
+    } else if (K >= 8 && K <= 32 && nvec >= full * kBlock / 2) {
+      sc = Schedule{8, 1, 1, 0, 1};
+    }
   }
   // short rows with many clients (the N > 1 all-gather chunks): 4 slices per
   // thread -- K=100 x 1.56M (N=2 chunk) 6,695 vs 6,178 GB/s at U8 x C2, and
@@ -520,9 +540,15 @@ void launch_production_f32(const float* clients, int K, int64_t ld, int64_t P, c
   const Schedule sc = choose_f32_schedule(K, P, ld);
   const int bpl = sc.blocks_per_launch;
   const int key = sc.unroll * 100 + sc.cols;
+  if (sc.buf) {
+    switch (key) {
+      case 801: launch_split_buf<8, 1>(clients, K, ld, P, W, out, bpl, s, e0, e1); return;
+      case 802: launch_split_buf<8, 2>(clients, K, ld, P, W, out, bpl, s, e0, e1); return;
+      default: launch_split_buf<2, 16>(clients, K, ld, P, W, out, bpl, s, e0, e1); return;
+    }
+  }
   if (sc.nt) {
     switch (key) {
-      case 216: launch_split_buf<2, 16>(clients, K, ld, P, W, out, bpl, s, e0, e1); return;
       case 408: launch_split_ev<4, 8, true>(clients, K, ld, P, W, out, bpl, s, e0, e1); return;
       case 804: launch_split_ev<8, 4, true>(clients, K, ld, P, W, out, bpl, s, e0, e1); return;
       case 802: launch_split_ev<8, 2, true>(clients, K, ld, P, W, out, bpl, s, e0, e1); return;
@@ -830,30 +856,42 @@ int fedavg_reduce_f32_timed(const float* clients, int64_t K, int64_t P, int64_t 
   return launch_status(what);
 }
 
-int fedavg_f32_schedule_ld(int64_t K, int64_t P, int64_t ld, int* unroll, int* cols, int* nontemporal,
-                           int* launches) {
-  if (K <= 0 || P < 0 || ld < P) return set_error(FEDAVG_EINVAL, "fedavg_f32_schedule_ld: bad sizes");
-  const Schedule sc = choose_f32_schedule(K, P, ld);
+namespace {
+// launches of launch_production_f32 for this schedule (buffer-descriptor
+// schedules without a cap launch every resident block at once)
+int production_launches(const Schedule& sc, int64_t P) {
   const int64_t nvec = (P + 3) / 4;
   const int64_t span = static_cast<int64_t>(kBlock) * sc.cols;
   const int64_t blocks = (nvec + span - 1) / span;
+  int64_t per = sc.blocks_per_launch;
+  if (per <= 0) {
+    switch (sc.unroll * 100 + sc.cols) {
+      case 801: per = resident_blocks(reduce_f32x4_buf_kernel<8, 1, kBlock, 0>, kBlock); break;
+      case 802: per = resident_blocks(reduce_f32x4_buf_kernel<8, 2, kBlock, 0>, kBlock); break;
+      default: per = resident_blocks(reduce_f32x4_buf_kernel<2, 16, kBlock, 0>, kBlock); break;
+    }
+  }
+  return static_cast<int>((blocks + per - 1) / per);
+}
+
+void report_schedule(const Schedule& sc, int64_t P, int* unroll, int* cols, int* nontemporal, int* launches) {
   if (unroll) *unroll = sc.unroll;
   if (cols) *cols = sc.cols;
-  if (nontemporal) *nontemporal = sc.nt;
-  if (launches) *launches = static_cast<int>((blocks + sc.blocks_per_launch - 1) / sc.blocks_per_launch);
+  if (nontemporal) *nontemporal = sc.buf ? 2 : sc.nt;
+  if (launches) *launches = production_launches(sc, P);
+}
+}  // namespace
+
+int fedavg_f32_schedule_ld(int64_t K, int64_t P, int64_t ld, int* unroll, int* cols, int* nontemporal,
+                           int* launches) {
+  if (K <= 0 || P < 0 || ld < P) return set_error(FEDAVG_EINVAL, "fedavg_f32_schedule_ld: bad sizes");
+  report_schedule(choose_f32_schedule(K, P, ld), P, unroll, cols, nontemporal, launches);
   return FEDAVG_OK;
 }
 
 int fedavg_f32_schedule(int64_t K, int64_t P, int* unroll, int* cols, int* nontemporal, int* launches) {
   if (K <= 0 || P < 0) return set_error(FEDAVG_EINVAL, "fedavg_f32_schedule: bad sizes");
-  const Schedule sc = choose_f32_schedule(K, P, P);
-  const int64_t nvec = (P + 3) / 4;
-  const int64_t span = static_cast<int64_t>(kBlock) * sc.cols;
-  const int64_t blocks = (nvec + span - 1) / span;
-  if (unroll) *unroll = sc.unroll;
-  if (cols) *cols = sc.cols;
-  if (nontemporal) *nontemporal = sc.nt;
-  if (launches) *launches = static_cast<int>((blocks + sc.blocks_per_launch - 1) / sc.blocks_per_launch);
+  report_schedule(choose_f32_schedule(K, P, P), P, unroll, cols, nontemporal, launches);
   return FEDAVG_OK;
 }
 

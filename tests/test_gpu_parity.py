@@ -174,6 +174,12 @@ def _schedule_boundary_cases():
     for c, K in ((6, 100), (3, 256)):
         lo, hi = cus * 3 // 4 * 256 * c * 4, cus * 256 * c * 4
         cases += [(K, lo - 4), (K, lo + 1), (K, hi - 1), (K, hi + 4), (K - 1, lo + 1)]
+    # 5 <= K < 64: buffer-descriptor U8 x C2 in the 4-slice band, U8 x C1 for
+    # 8 <= K <= 32 from full/2 x 256 float4 columns
+    for t in (full * 256 * 4 * 4, full * 256 * 8 * 4):
+        cases += [(5, t - 1), (5, t + 1), (63, t - 4), (63, t + 3), (64, t + 3)]
+    t = full * 256 // 2 * 4
+    cases += [(8, t - 4), (8, t + 1), (32, t + 3), (33, t + 3), (7, t + 5), (10, 1_206_590)]
     mib = 1 << 20
     cases += [(20, 64 * mib // 80 - 3), (20, 64 * mib // 80 + 5), (20, 240 * mib // 80 - 1), (20, 240 * mib // 80 + 7)]
     cases += [(4, 1_000_003), (5, 1_000_003), (1, 65), (2, 7)]
