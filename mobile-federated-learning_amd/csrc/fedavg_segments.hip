@@ -34,6 +34,15 @@ constexpr int kSegU = 4;
 constexpr int kSegC = 4;
 constexpr int64_t kSegSpan = static_cast<int64_t>(kBlock) * kSegC * 4;  // columns per unit
 constexpr int kSegBlocksPerCU = 3;
+// Small models (fewer than 4 units of 4,096 columns per CU): units of 1,024
+// columns (U4 x C1), up to 8 blocks per CU per launch -- 4x the workgroups.
+// rocprofv3 kernel time per call (scripts/segments_probe.py --model,
+// profiles/r02/sweeps/segments_small_models.json): resnet56 x 100 (350 keys)
+// 90.0 -> 77.1 us, FEMNIST x 10 12.1 -> 10.9 us, MNIST-LR x 10 6.3 -> 4.3 us;
+// the flat 25M key stays on C4 (1,577 vs 1,717 us at C1).
+constexpr int kSegSmallC = 1;
+constexpr int kSegSmallBlocksPerCU = 8;
+constexpr int64_t kSegSmallUnitsPerCU = 4;
 constexpr int64_t kSegSpanMaxBytes = static_cast<int64_t>(kBlock) * 16 * 16;  // widest unit (C = 16), bytes
 
 enum : int64_t { kRaw = 0, kI64 = 1, kI32 = 2, kI16 = 3, kI8 = 4, kU8 = 5, kBool = 6 };
@@ -419,15 +428,21 @@ int fedavg_reduce_ptrs_f32(const float* const* client_ptrs, int64_t K, int64_t P
   if (P == 0) return FEDAVG_OK;
   if (!aligned4(out) || !aligned4(weights)) return set_error(FEDAVG_EALIGN, "%s: out/weights misaligned", what);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const int64_t units = (P + kSegSpan - 1) / kSegSpan;
-  const int64_t cap = static_cast<int64_t>(kSegBlocksPerCU) * cu_count();
+  const bool small = (P + kSegSpan - 1) / kSegSpan < kSegSmallUnitsPerCU * static_cast<int64_t>(cu_count());
+  const int64_t span = small ? static_cast<int64_t>(kBlock) * kSegSmallC * 4 : kSegSpan;
+  const int64_t units = (P + span - 1) / span;
+  const int64_t cap = static_cast<int64_t>(small ? kSegSmallBlocksPerCU : kSegBlocksPerCU) * cu_count();
   const int64_t nl = (units + cap - 1) / cap;
   const int64_t per = (units + nl - 1) / nl;
   const auto* ptrs = reinterpret_cast<const int64_t*>(client_ptrs);
   for (int64_t u0 = 0; u0 < units; u0 += per) {
     const int64_t nb = units - u0 < per ? units - u0 : per;
-    hipLaunchKernelGGL((reduce_ptrs_f32_kernel<kSegU, kSegC>), dim3(static_cast<unsigned>(nb)), dim3(kBlock), 0, s,
-                       ptrs, P, u0, static_cast<int>(K), weights, out);
+    if (small)
+      hipLaunchKernelGGL((reduce_ptrs_f32_kernel<kSegU, kSegSmallC>), dim3(static_cast<unsigned>(nb)), dim3(kBlock), 0,
+                         s, ptrs, P, u0, static_cast<int>(K), weights, out);
+    else
+      hipLaunchKernelGGL((reduce_ptrs_f32_kernel<kSegU, kSegC>), dim3(static_cast<unsigned>(nb)), dim3(kBlock), 0, s,
+                         ptrs, P, u0, static_cast<int>(K), weights, out);
   }
   return launch_status(what);
 }
@@ -439,14 +454,21 @@ int fedavg_reduce_segments_f32(const int64_t* client_ptrs, const int64_t* key_nu
   if (!weights || !out) return set_error(FEDAVG_EINVAL, "%s: null weights/out", what);
   if (!is_device_memory(out)) return set_error(FEDAVG_EINVAL, "%s: out must be device memory", what);
   hipStream_t s = static_cast<hipStream_t>(stream);
+  const bool small = key_numel && n_keys > 0 &&
+                     units_of(key_numel, n_keys) < kSegSmallUnitsPerCU * static_cast<int64_t>(cu_count());
+  const int64_t span = small ? static_cast<int64_t>(kBlock) * kSegSmallC * 4 : kSegSpan;
   const int64_t units = stage_tables(what, client_ptrs, key_numel, key_offset, key_kind, n_keys, K, host_ws, dev_ws,
-                                     ws_bytes, s);
+                                     ws_bytes, s, span);
   if (units <= 0) return static_cast<int>(units);
   const auto* keys = static_cast<const SegKey*>(dev_ws);
   const auto* ptrs = reinterpret_cast<const int64_t*>(static_cast<const char*>(dev_ws) +
                                                       n_keys * static_cast<int64_t>(sizeof(SegKey)));
-  launch_reduce_segments<kSegU, kSegC>(keys, ptrs, n_keys, units, K, weights, out,
-                                       static_cast<int64_t>(kSegBlocksPerCU) * cu_count(), s);
+  if (small)
+    launch_reduce_segments<kSegU, kSegSmallC>(keys, ptrs, n_keys, units, K, weights, out,
+                                              static_cast<int64_t>(kSegSmallBlocksPerCU) * cu_count(), s);
+  else
+    launch_reduce_segments<kSegU, kSegC>(keys, ptrs, n_keys, units, K, weights, out,
+                                         static_cast<int64_t>(kSegBlocksPerCU) * cu_count(), s);
   return launch_status(what);
 }
 
@@ -492,7 +514,8 @@ int fedavg_reduce_segments_f32_variant(const int64_t* client_ptrs, const int64_t
   if (!weights || !out) return set_error(FEDAVG_EINVAL, "%s: null weights/out", what);
   if (!is_device_memory(out)) return set_error(FEDAVG_EINVAL, "%s: out must be device memory", what);
   const int uc = unroll * 100 + cols;
-  if (uc != 408 && uc != 804 && uc != 208 && uc != 404 && uc != 802 && uc != 1602 && uc != 216 && uc != 116)
+  if (uc != 408 && uc != 804 && uc != 208 && uc != 404 && uc != 802 && uc != 1602 && uc != 216 && uc != 116 &&
+      uc != 801 && uc != 401 && uc != 1601 && uc != 402)
     return set_error(FEDAVG_EMODE, "%s: unsupported (unroll, cols) = (%d, %d)", what, unroll, cols);
   if (blocks_per_cu < 0) return set_error(FEDAVG_EINVAL, "%s: blocks_per_cu < 0", what);
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -512,6 +535,10 @@ int fedavg_reduce_segments_f32_variant(const int64_t* client_ptrs, const int64_t
     case 802: launch_reduce_segments<8, 2>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;
     case 1602: launch_reduce_segments<16, 2>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;
     case 216: launch_reduce_segments<2, 16>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;
+    case 801: launch_reduce_segments<8, 1>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;
+    case 401: launch_reduce_segments<4, 1>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;
+    case 1601: launch_reduce_segments<16, 1>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;
+    case 402: launch_reduce_segments<4, 2>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;
     default: launch_reduce_segments<1, 16>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;
   }
   return launch_status(what);

@@ -56,7 +56,8 @@ def model_mode(args, dev, lib):
     nk = len(numel)
     need = lib.fedavg_segments_workspace(K, nk)
     stream = torch.cuda.current_stream(dev)
-    sched = [None, (4, 8, 3), (2, 16, 3), (4, 4, 3), (1, 16, 3), (8, 4, 3), (2, 8, 3)]
+    sched = [None] + ([tuple(int(t) for t in v.split(",")) for v in args.sched] if args.sched else
+                      [(4, 8, 3), (2, 16, 3), (4, 4, 3), (1, 16, 3), (8, 4, 3), (2, 8, 3)])
     names = ["production" if v is None else f"U{v[0]}C{v[1]}b{v[2]}" for v in sched]
     ws = {n: (torch.empty(need, dtype=torch.uint8, pin_memory=True), torch.empty(need, dtype=torch.uint8, device=dev))
           for n in names}
@@ -104,6 +105,7 @@ def main():
                     help="also time fedavg_reduce_segments_f32_variant schedules (U, C, blocks per CU) on the "
                          "separate tensors and on the rows")
     ap.add_argument("--model", default="", help="multi-key mode: a scripts/bench_e2e.py config name")
+    ap.add_argument("--sched", nargs="*", default=[], help="multi-key mode: U,C,blocks_per_cu variants to time")
     ap.add_argument("--only", default="", help="time only 'rows' and this variant (for per-kernel PMC passes)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
