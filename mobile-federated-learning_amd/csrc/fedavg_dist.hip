@@ -316,6 +316,21 @@ constexpr int kDistBufRows = 2;
 constexpr int kDistBufCols = 16;
 constexpr int kDistBufChains = 4;
 
+// fp32 production column groups per thread: 16 while that still gives two
+// workgroups per CU (the 25M-column target: 1,526), else 4 while it gives
+// ~one per CU, else 2.  A small model's rows are short, and at 16 slices the
+// launch had 37 workgroups for resnet56 (100 x 600K) and 74 for FEMNIST
+// (10 x 1.2M).  rocprofv3 kernel time (profiles/r02/sweeps/dist_small_models.json):
+// resnet56 275 -> 72 us (U8 x C2), FEMNIST 30.8 -> 12.7 us (U4 x C4),
+// cfg4 500 x 1M 1,383 -> 391 us (U4 x C4), 100 x 3.125M 309 -> 197 us (U4 x C4).
+int dist_cols(int64_t P) {
+  const int64_t nvec = (P + 3) / 4;
+  const int64_t cus = cu_count();
+  if ((nvec + kBlock * 16 - 1) / (kBlock * 16) >= 2 * cus) return 16;
+  if ((nvec + kBlock * 4 - 1) / (kBlock * 4) >= cus * 9 / 10) return 4;
+  return 2;
+}
+
 int64_t sqdist_waves_for(int64_t P, int cols) {
   const int64_t nvec = (P + 3) / 4;
   const int64_t blocks = (nvec + kBlock * cols - 1) / (kBlock * cols);
@@ -418,8 +433,8 @@ int sqdist_buf_impl(const float* clients, int64_t K, int64_t P, int64_t ld, cons
   if (P == 0) return set_error(FEDAVG_EINVAL, "%s: P must be >= 1", what);
   if (!aligned16(clients) || !aligned16(glob) || (ld % 4) != 0)
     return set_error(FEDAVG_EALIGN, "%s: needs 16-B aligned clients/glob and ld %% 4 == 0", what);
-  if (cols != 4 && cols != 8 && cols != 12 && cols != 16)
-    return set_error(FEDAVG_EMODE, "%s: cols must be 4, 8, 12 or 16", what);
+  if (cols != 1 && cols != 2 && cols != 4 && cols != 8 && cols != 12 && cols != 16)
+    return set_error(FEDAVG_EMODE, "%s: cols must be 1, 2, 4, 8, 12 or 16", what);
   const int64_t nwaves = sqdist_waves_for(P, cols);
   if (!workspace || workspace_elems < K * nwaves)
     return set_error(FEDAVG_EINVAL, "%s: workspace needs %lld doubles", what, (long long)(K * nwaves));
@@ -456,6 +471,13 @@ int sqdist_buf_impl(const float* clients, int64_t K, int64_t P, int64_t ld, cons
     case 4030216: launch_sqdist<2, 16, true, 3, 4>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
     case 4040208: launch_sqdist<2, 8, true, 4, 4>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
     case 4030308: launch_sqdist<3, 8, true, 3, 4>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    // narrow column groups for small models (more workgroups per launch)
+    case 4000404: launch_sqdist<4, 4, true, 1, 4>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    case 4000804: launch_sqdist<8, 4, true, 1, 4>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    case 4000402: launch_sqdist<4, 2, true, 1, 2>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    case 4000802: launch_sqdist<8, 2, true, 1, 2>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    case 4000801: launch_sqdist<8, 1, true, 1, 1>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    case 4001601: launch_sqdist<16, 1, true, 1, 1>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
     case 4000116: launch_sqdist<1, 16, true, 1, 4>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
     default: return set_error(FEDAVG_EMODE, "%s: unsupported unroll=%d cols=%d", what, unroll, cols);
   }
@@ -472,14 +494,16 @@ extern "C" {
 
 int64_t fedavg_client_sqdist_workspace(int64_t K, int64_t P) {
   if (K <= 0 || P <= 0) return 0;
-  return K * sqdist_waves_for(P, 4);  // enough for every variant (cols = 4 has the most waves)
+  return K * sqdist_waves_for(P, dist_cols(P) < 4 ? dist_cols(P) : 4);  // production; any variant of >= 4 slices
 }
 
 int fedavg_client_sqdist_f32(const float* clients, int64_t K, int64_t P, int64_t ld, const float* glob,
                              double* workspace, int64_t workspace_elems, double* sumsq, void* stream) {
-  return sqdist_buf_impl(clients, K, P, ld, glob, workspace, workspace_elems, sumsq,
-                         kDistBufChains * 10000 + kDistBufRows, kDistBufCols,
-                         0, stream, "fedavg_client_sqdist_f32");
+  // unroll codes: chains x 10000 + rows per batch (4 chains, at most one per slice)
+  const int cols = P > 0 ? dist_cols(P) : kDistBufCols;
+  const int rows = cols == 16 ? kDistBufRows : (cols == 4 ? 4 : 8);
+  return sqdist_buf_impl(clients, K, P, ld, glob, workspace, workspace_elems, sumsq, kDistBufChains * 10000 + rows,
+                         cols, 0, stream, "fedavg_client_sqdist_f32");
 }
 
 int64_t fedavg_client_sqdist_workspace_elems(int64_t K, int64_t P, int64_t elem_size) {

@@ -45,7 +45,7 @@ def main():
     for k in range(K):
         x[k].normal_(0, 0.05)
     glob = x[:, :P].mean(0).contiguous()
-    n_ws = lib.fedavg_client_sqdist_workspace(K, P)
+    n_ws = K * 4 * (((P + 3) // 4 + 255) // 256)  # per-wave partials at one 16-B slice per thread (the most)
     work = torch.empty(n_ws, dtype=torch.float64, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
     ap_glob = [tuple(int(t) for t in v.split(",")) for v in args.glob]
