@@ -135,6 +135,19 @@ int fedavg_reduce_segments_f32_variant(const int64_t* client_ptrs, const int64_t
                                        float* out, void* host_ws, void* dev_ws, int64_t ws_bytes, int unroll, int cols,
                                        int blocks_per_cu, void* stream);
 
+/*
+ * :291 on device-resident clients (fedavg_client_sqdist_segments_f32, same
+ * tables and workspaces) with an explicit schedule: unroll client rows per
+ * load batch x cols 16-B slices per thread, (U, C) in {(1,4), (2,4), (4,4),
+ * (8,4), (4,1), (8,1), (4,2), (8,2), (2,8), (4,8)}; units of 1,024 x cols
+ * columns; partials: K x units x 4 doubles for that unit size.
+ */
+int fedavg_client_sqdist_segments_f32_variant(const int64_t* client_ptrs, const int64_t* key_numel,
+                                              const int64_t* key_offset, const int64_t* key_kind, int64_t n_keys,
+                                              int64_t K, const float* glob, double* partials, int64_t partial_elems,
+                                              double* sumsq, void* host_ws, void* dev_ws, int64_t ws_bytes,
+                                              int unroll, int cols, void* stream);
+
 /* The exact fp32 row reduce through buffer descriptors (one per client row
  * and column group, base in SGPRs, 32-bit lane offsets) in launch_split's
  * round-split schedule, workgroups of `block` threads (64, 128 or 256).

@@ -66,6 +66,8 @@ TUNING_SIGNATURES = {
     "fedavg_reduce_f32_buf": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _vp]),
     "fedavg_reduce_segments_f32_variant": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _c_i64,
                                                     _c_int, _c_int, _c_int, _vp]),
+    "fedavg_client_sqdist_segments_f32_variant": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_i64, _vp, _vp, _c_i64, _vp,
+                                                           _vp, _vp, _c_i64, _c_int, _c_int, _vp]),
     "fedavg_fpf_index_workspace": (_c_i64, [_c_i64, _c_i64]),
     "fedavg_fpf_index_variant": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _c_i64, _c_int, _c_int,
                                           _c_int, _vp]),

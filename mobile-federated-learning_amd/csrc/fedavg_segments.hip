@@ -43,6 +43,16 @@ constexpr int kSegBlocksPerCU = 3;
 constexpr int kSegSmallC = 1;
 constexpr int kSegSmallBlocksPerCU = 8;
 constexpr int64_t kSegSmallUnitsPerCU = 4;
+constexpr int64_t kSegSmallSpan = static_cast<int64_t>(kBlock) * kSegSmallC * 4;
+// :291 on device-resident clients: U4 client rows per load batch; units of
+// 8,192 columns (C8), or the small-model units of 1,024 (C1).  rocprofv3
+// kernel time (scripts/segments_dist_probe.py, profiles/r02/sweeps/
+// segments_dist.json): flat 100 x 25M 1,638 us at U4 x C8 vs 1,656 for the
+// round-1 form (one client at a time, C4) and 1,681 at U4 x C4; resnet56 x 100
+// 84.5 us at U4 x C1 vs 100.8 (one client at a time, C4); FEMNIST 13.8 vs 14.5.
+constexpr int kSegDistU = 4;
+constexpr int kSegDistC = 8;
+constexpr int64_t kSegDistSpan = static_cast<int64_t>(kBlock) * kSegDistC * 4;
 constexpr int64_t kSegSpanMaxBytes = static_cast<int64_t>(kBlock) * 16 * 16;  // widest unit (C = 16), bytes
 
 enum : int64_t { kRaw = 0, kI64 = 1, kI32 = 2, kI16 = 3, kI8 = 4, kU8 = 5, kBool = 6 };
@@ -264,45 +274,83 @@ __device__ __forceinline__ double sq4_add(double acc, f32x4 d) {
   return __builtin_fma(w, w, acc);
 }
 
-__device__ __forceinline__ double wave_sum(double v) {
+// one fp32 unit of :291 for U client rows per batch: the unit's model slice
+// stays in registers, each batch loads U rows x C slices before any square is
+// summed (full units through one buffer descriptor per client, the key's last
+// unit masked), and every row's wave sum goes through DPP lane moves
+template <int U, int C, bool FULL>
+__device__ __forceinline__ void sqdist_raw_unit(const int64_t* __restrict__ P, int K, int64_t c0, int64_t n,
+                                                const float* __restrict__ g, double* __restrict__ partials,
+                                                int64_t nparts, int64_t part) {
+  uint32_t off[C];
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  for (int s = 0; s < C; ++s) off[s] = 16u * (threadIdx.x + s * kBlock);
+  f32x4 gv[C];
+#pragma unroll
+  for (int s = 0; s < C; ++s) gv[s] = load_slice(g, 4 * (threadIdx.x + s * kBlock), n);
+  const bool lane0 = (threadIdx.x & 63u) == 0;
+  int k = 0;
+  for (; k + U <= K; k += U) {
+    f32x4 xs[U][C];
+#pragma unroll
+    for (int r = 0; r < U; ++r) {
+      const float* xr = reinterpret_cast<const float*>(P[k + r]) + c0;
+      if constexpr (FULL) {
+        const __amdgpu_buffer_rsrc_t rr = unit_rsrc(xr);
+#pragma unroll
+        for (int s = 0; s < C; ++s) xs[r][s] = ldb(rr, off[s]);
+      } else {
+#pragma unroll
+        for (int s = 0; s < C; ++s) xs[r][s] = load_slice(xr, 4 * (threadIdx.x + s * kBlock), n);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < U; ++r) {
+      double acc = 0.0;
+#pragma unroll
+      for (int s = 0; s < C; ++s) acc = sq4_add(acc, xs[r][s] - gv[s]);  // fp32 difference, as the reference
+      acc = wave_sum_dpp(acc);
+      if (lane0) partials[static_cast<int64_t>(k + r) * nparts + part] = acc;
+    }
+  }
+  for (; k < K; ++k) {
+    const float* xk = reinterpret_cast<const float*>(P[k]) + c0;
+    double acc = 0.0;
+#pragma unroll
+    for (int s = 0; s < C; ++s) acc = sq4_add(acc, load_slice(xk, 4 * (threadIdx.x + s * kBlock), n) - gv[s]);
+    acc = wave_sum_dpp(acc);
+    if (lane0) partials[static_cast<int64_t>(k) * nparts + part] = acc;
+  }
 }
 
 // :291 on the same units: per client, sum over the unit's columns of
 // fl32(x - g)^2 in fp64 (fused square-adds, as client_sqdist_f32x4_kernel),
 // one partial per wave: partials[k][unit * 4 + wave].  Lanes past the unit's
-// end contribute exactly 0 (x and g both read as 0 there).
-template <int C>
+// end contribute exactly 0 (x and g both read as 0 there).  Units are
+// kBlock x C x 4 columns (the same table staging as the reduce with that span).
+template <int U, int C>
 __global__ __launch_bounds__(kBlock) void sqdist_segments_f32_kernel(const SegKey* __restrict__ keys,
                                                                      const int64_t* __restrict__ ptrs, int64_t n_keys,
                                                                      int64_t unit0, int K, const float* __restrict__ G,
                                                                      double* __restrict__ partials, int64_t nparts) {
+  constexpr int64_t span = static_cast<int64_t>(kBlock) * C * 4;
   const int64_t u = unit0 + blockIdx.x;
   const int64_t j = find_key(keys, n_keys, u);
   const SegKey key = keys[j];
-  const int64_t c0 = (u - key.unit_start) * kSegSpan;
-  const int64_t n = key.numel - c0 < kSegSpan ? key.numel - c0 : kSegSpan;
+  const int64_t c0 = (u - key.unit_start) * span;
+  const int64_t n = key.numel - c0 < span ? key.numel - c0 : span;
   const int64_t* P = ptrs + j * K;
   const float* g = G + key.out_offset + c0;
   const int64_t part = u * (kBlock / 64) + (threadIdx.x >> 6);
-  const int lane = static_cast<int>(threadIdx.x & 63u);
   if (key.kind == kRaw) {
-    f32x4 gv[C];
-#pragma unroll
-    for (int s = 0; s < C; ++s) gv[s] = load_slice(g, 4 * (threadIdx.x + s * kBlock), n);
-    for (int k = 0; k < K; ++k) {
-      const float* xk = reinterpret_cast<const float*>(P[k]) + c0;
-      double acc = 0.0;
-#pragma unroll
-      for (int s = 0; s < C; ++s) acc = sq4_add(acc, load_slice(xk, 4 * (threadIdx.x + s * kBlock), n) - gv[s]);
-      acc = wave_sum(acc);
-      if (lane == 0) partials[static_cast<int64_t>(k) * nparts + part] = acc;
-    }
+    if (n == span)
+      sqdist_raw_unit<U, C, true>(P, K, c0, n, g, partials, nparts, part);
+    else
+      sqdist_raw_unit<1, C, false>(P, K, c0, n, g, partials, nparts, part);
     return;
   }
   constexpr int kPer = 4 * C;
+  const bool lane0 = (threadIdx.x & 63u) == 0;
   for (int k = 0; k < K; ++k) {
     const void* xk = reinterpret_cast<const void*>(P[k]);
     double acc = 0.0;
@@ -314,8 +362,8 @@ __global__ __launch_bounds__(kBlock) void sqdist_segments_f32_kernel(const SegKe
         acc = __builtin_fma(d, d, acc);
       }
     }
-    acc = wave_sum(acc);
-    if (lane == 0) partials[static_cast<int64_t>(k) * nparts + part] = acc;
+    acc = wave_sum_dpp(acc);
+    if (lane0) partials[static_cast<int64_t>(k) * nparts + part] = acc;
   }
 }
 
@@ -339,6 +387,15 @@ int64_t units_of(const int64_t* numel, int64_t n_keys, int64_t span = kSegSpan) 
   int64_t units = 0;
   for (int64_t j = 0; j < n_keys; ++j) units += (numel[j] + span - 1) / span;
   return units;
+}
+
+// a model with fewer than kSegSmallUnitsPerCU units of kSegSpan per CU takes
+// the narrow units (reduce and :291 alike)
+bool segments_small(const int64_t* numel, int64_t n_keys) {
+  if (!numel || n_keys <= 0) return false;
+  for (int64_t j = 0; j < n_keys; ++j)
+    if (numel[j] < 0) return false;  // stage_tables reports it
+  return units_of(numel, n_keys) < kSegSmallUnitsPerCU * static_cast<int64_t>(cu_count());
 }
 
 // Validate the tables, write the device tables into host_ws, copy them to
@@ -417,7 +474,8 @@ int64_t fedavg_segments_workspace(int64_t K, int64_t n_keys) {
 
 int64_t fedavg_segments_partials(const int64_t* key_numel, int64_t n_keys, int64_t K) {
   if (!key_numel || n_keys <= 0 || K <= 0) return 0;
-  return K * units_of(key_numel, n_keys) * (kBlock / 64);
+  return K * units_of(key_numel, n_keys, segments_small(key_numel, n_keys) ? kSegSmallSpan : kSegDistSpan) *
+         (kBlock / 64);
 }
 
 int fedavg_reduce_ptrs_f32(const float* const* client_ptrs, int64_t K, int64_t P, const float* weights,
@@ -454,9 +512,8 @@ int fedavg_reduce_segments_f32(const int64_t* client_ptrs, const int64_t* key_nu
   if (!weights || !out) return set_error(FEDAVG_EINVAL, "%s: null weights/out", what);
   if (!is_device_memory(out)) return set_error(FEDAVG_EINVAL, "%s: out must be device memory", what);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const bool small = key_numel && n_keys > 0 &&
-                     units_of(key_numel, n_keys) < kSegSmallUnitsPerCU * static_cast<int64_t>(cu_count());
-  const int64_t span = small ? static_cast<int64_t>(kBlock) * kSegSmallC * 4 : kSegSpan;
+  const bool small = segments_small(key_numel, n_keys);
+  const int64_t span = small ? kSegSmallSpan : kSegSpan;
   const int64_t units = stage_tables(what, client_ptrs, key_numel, key_offset, key_kind, n_keys, K, host_ws, dev_ws,
                                      ws_bytes, s, span);
   if (units <= 0) return static_cast<int>(units);
@@ -483,8 +540,9 @@ int fedavg_client_sqdist_segments_f32(const int64_t* client_ptrs, const int64_t*
   const int64_t need = fedavg_segments_partials(key_numel, n_keys, K);
   if (partial_elems < need) return set_error(FEDAVG_EINVAL, "%s: partials need %lld doubles", what, (long long)need);
   hipStream_t s = static_cast<hipStream_t>(stream);
+  const bool small = segments_small(key_numel, n_keys);
   const int64_t units = stage_tables(what, client_ptrs, key_numel, key_offset, key_kind, n_keys, K, host_ws, dev_ws,
-                                     ws_bytes, s);
+                                     ws_bytes, s, small ? kSegSmallSpan : kSegDistSpan);
   if (units < 0) return static_cast<int>(units);
   if (units == 0) {
     const hipError_t e = hipMemsetAsync(sumsq, 0, static_cast<size_t>(K) * sizeof(double), s);
@@ -494,8 +552,12 @@ int fedavg_client_sqdist_segments_f32(const int64_t* client_ptrs, const int64_t*
   const auto* ptrs = reinterpret_cast<const int64_t*>(static_cast<const char*>(dev_ws) +
                                                       n_keys * static_cast<int64_t>(sizeof(SegKey)));
   const int64_t nparts = units * (kBlock / 64);
-  hipLaunchKernelGGL((sqdist_segments_f32_kernel<kSegC>), dim3(static_cast<unsigned>(units)), dim3(kBlock), 0, s, keys,
-                     ptrs, n_keys, int64_t(0), static_cast<int>(K), glob, partials, nparts);
+  if (small)
+    hipLaunchKernelGGL((sqdist_segments_f32_kernel<kSegDistU, kSegSmallC>), dim3(static_cast<unsigned>(units)),
+                       dim3(kBlock), 0, s, keys, ptrs, n_keys, int64_t(0), static_cast<int>(K), glob, partials, nparts);
+  else
+    hipLaunchKernelGGL((sqdist_segments_f32_kernel<kSegDistU, kSegDistC>), dim3(static_cast<unsigned>(units)),
+                       dim3(kBlock), 0, s, keys, ptrs, n_keys, int64_t(0), static_cast<int>(K), glob, partials, nparts);
   int rc = launch_status(what);
   if (rc) return rc;
   hipLaunchKernelGGL(segments_finalize_kernel, dim3(static_cast<unsigned>(K)), dim3(kBlock), 0, s, partials, nparts,
@@ -504,6 +566,60 @@ int fedavg_client_sqdist_segments_f32(const int64_t* client_ptrs, const int64_t*
 }
 
 // tuning hook (fedavg_amd_tuning.h): the zero-copy reduce with an explicit
+#ifdef FEDAVG_TUNING  // probe library only (libfedavg_amd_probe.so)
+// fedavg_client_sqdist_segments_f32 with an explicit (U, C): units of
+// 1,024 x C columns; partials need K x units x 4 doubles for that span
+int fedavg_client_sqdist_segments_f32_variant(const int64_t* client_ptrs, const int64_t* key_numel,
+                                              const int64_t* key_offset, const int64_t* key_kind, int64_t n_keys,
+                                              int64_t K, const float* glob, double* partials, int64_t partial_elems,
+                                              double* sumsq, void* host_ws, void* dev_ws, int64_t ws_bytes,
+                                              int unroll, int cols, void* stream) {
+  const char* what = "fedavg_client_sqdist_segments_f32_variant";
+  if (!glob || !partials || !sumsq || !key_numel || n_keys <= 0 || K <= 0)
+    return set_error(FEDAVG_EINVAL, "%s: bad arguments", what);
+  const int uc = unroll * 100 + cols;
+  if (uc != 104 && uc != 204 && uc != 404 && uc != 804 && uc != 401 && uc != 801 && uc != 402 && uc != 802 &&
+      uc != 208 && uc != 408)
+    return set_error(FEDAVG_EMODE, "%s: unsupported (unroll, cols) = (%d, %d)", what, unroll, cols);
+  const int64_t span = static_cast<int64_t>(kBlock) * cols * 4;
+  const int64_t need = K * units_of(key_numel, n_keys, span) * (kBlock / 64);
+  if (partial_elems < need) return set_error(FEDAVG_EINVAL, "%s: partials need %lld doubles", what, (long long)need);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t units = stage_tables(what, client_ptrs, key_numel, key_offset, key_kind, n_keys, K, host_ws, dev_ws,
+                                     ws_bytes, s, span);
+  if (units <= 0) return static_cast<int>(units);
+  const auto* keys = static_cast<const SegKey*>(dev_ws);
+  const auto* ptrs = reinterpret_cast<const int64_t*>(static_cast<const char*>(dev_ws) +
+                                                      n_keys * static_cast<int64_t>(sizeof(SegKey)));
+  const int64_t nparts = units * (kBlock / 64);
+  const dim3 grid(static_cast<unsigned>(units));
+  const int k = static_cast<int>(K);
+  switch (uc) {
+#define FEDAVG_SQSEG_CASE(U, C)                                                                                      \
+  case U * 100 + C:                                                                                                  \
+    hipLaunchKernelGGL((sqdist_segments_f32_kernel<U, C>), grid, dim3(kBlock), 0, s, keys, ptrs, n_keys, int64_t(0), \
+                       k, glob, partials, nparts);                                                                   \
+    break;
+    FEDAVG_SQSEG_CASE(1, 4)
+    FEDAVG_SQSEG_CASE(2, 4)
+    FEDAVG_SQSEG_CASE(4, 4)
+    FEDAVG_SQSEG_CASE(8, 4)
+    FEDAVG_SQSEG_CASE(4, 1)
+    FEDAVG_SQSEG_CASE(8, 1)
+    FEDAVG_SQSEG_CASE(4, 2)
+    FEDAVG_SQSEG_CASE(8, 2)
+    FEDAVG_SQSEG_CASE(2, 8)
+    FEDAVG_SQSEG_CASE(4, 8)
+#undef FEDAVG_SQSEG_CASE
+  }
+  int rc = launch_status(what);
+  if (rc) return rc;
+  hipLaunchKernelGGL(segments_finalize_kernel, dim3(static_cast<unsigned>(K)), dim3(kBlock), 0, s, partials, nparts,
+                     sumsq);
+  return launch_status(what);
+}
+#endif  // FEDAVG_TUNING
+
 // (U, C) schedule -- units of 1,024 x C columns -- and launch size; same bits
 #ifdef FEDAVG_TUNING  // probe library only (libfedavg_amd_probe.so)
 int fedavg_reduce_segments_f32_variant(const int64_t* client_ptrs, const int64_t* key_numel, const int64_t* key_offset,
