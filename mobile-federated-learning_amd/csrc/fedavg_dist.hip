@@ -392,6 +392,14 @@ int sqdist_impl(const float* clients, int64_t K, int64_t P, int64_t ld, const fl
 }
 #endif  // FEDAVG_TUNING
 
+// fp64/fp16/bf16 passes: U4 x C8 while that gives ~one workgroup per CU,
+// else U8 x C2 (the fp32 pass's short-row measurements, dist_cols)
+constexpr int kDistSmallRows = 8;
+constexpr int kDistSmallCols = 2;
+int dist_vec_cols(int64_t nvec) {
+  return (nvec + kBlock * kDistCols - 1) / (kBlock * kDistCols) >= cu_count() * 9 / 10 ? kDistCols : kDistSmallCols;
+}
+
 int64_t sqdist_vec_waves(int64_t nvec, int cols) {
   const int64_t blocks = (nvec + kBlock * cols - 1) / (kBlock * cols);
   return blocks * (kBlock / 64);
@@ -409,15 +417,22 @@ int sqdist_vec_impl(const void* clients, int64_t K, int64_t P, int64_t ld, const
   if (!aligned16(clients) || !aligned16(glob) || (ld % lanes) != 0)
     return set_error(FEDAVG_EALIGN, "%s: needs 16-B aligned clients/glob and ld %% %d == 0", what, (int)lanes);
   const int64_t nvec = (P + lanes - 1) / lanes;
-  const int64_t nwaves = sqdist_vec_waves(nvec, kDistCols);
+  const int cols = dist_vec_cols(nvec);
+  const int64_t nwaves = sqdist_vec_waves(nvec, cols);
   if (!workspace || workspace_elems < K * nwaves)
     return set_error(FEDAVG_EINVAL, "%s: workspace needs %lld doubles", what, (long long)(K * nwaves));
   hipStream_t s = static_cast<hipStream_t>(stream);
   using vec = typename D::vec;
-  const int64_t blocks = (nvec + kBlock * kDistCols - 1) / (kBlock * kDistCols);
-  hipLaunchKernelGGL((client_sqdist_vec_kernel<D, kDistRows, kDistCols>), dim3(static_cast<unsigned>(blocks)),
-                     dim3(kBlock), 0, s, reinterpret_cast<const vec*>(clients), static_cast<int>(K), ld / lanes, nvec,
-                     static_cast<int>(P % lanes), reinterpret_cast<const vec*>(glob), workspace, nwaves);
+  const int64_t blocks = (nvec + kBlock * cols - 1) / (kBlock * cols);
+  if (cols == kDistCols)
+    hipLaunchKernelGGL((client_sqdist_vec_kernel<D, kDistRows, kDistCols>), dim3(static_cast<unsigned>(blocks)),
+                       dim3(kBlock), 0, s, reinterpret_cast<const vec*>(clients), static_cast<int>(K), ld / lanes, nvec,
+                       static_cast<int>(P % lanes), reinterpret_cast<const vec*>(glob), workspace, nwaves);
+  else
+    hipLaunchKernelGGL((client_sqdist_vec_kernel<D, kDistSmallRows, kDistSmallCols>),
+                       dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, s, reinterpret_cast<const vec*>(clients),
+                       static_cast<int>(K), ld / lanes, nvec, static_cast<int>(P % lanes),
+                       reinterpret_cast<const vec*>(glob), workspace, nwaves);
   rc = launch_status(what);
   if (rc) return rc;
   hipLaunchKernelGGL(client_sqdist_finalize_kernel, dim3(static_cast<unsigned>(K)), dim3(kBlock), 0, s, workspace,
@@ -509,7 +524,8 @@ int fedavg_client_sqdist_f32(const float* clients, int64_t K, int64_t P, int64_t
 int64_t fedavg_client_sqdist_workspace_elems(int64_t K, int64_t P, int64_t elem_size) {
   if (K <= 0 || P <= 0 || (elem_size != 2 && elem_size != 4 && elem_size != 8)) return 0;
   const int64_t lanes = 16 / elem_size;
-  return K * sqdist_vec_waves((P + lanes - 1) / lanes, kDistCols);
+  const int64_t nvec = (P + lanes - 1) / lanes;
+  return K * sqdist_vec_waves(nvec, dist_vec_cols(nvec));
 }
 
 int fedavg_client_sqdist_f64(const double* clients, int64_t K, int64_t P, int64_t ld, const double* glob,
