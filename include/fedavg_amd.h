@@ -115,6 +115,23 @@ int fedavg_client_sqdist_f32(const float* clients, int64_t K, int64_t P, int64_t
                              double* sumsq, void* stream);
 
 /*
+ * Aggregate and :291 in ONE pass over the client rows (fedavg_trainer.py:217
+ * then :291 of the same round read the same K x P bytes twice):
+ *   out   : fedavg_reduce_f32's result, the same bits;
+ *   sumsq : fedavg_client_sqdist_f32(clients, ..., out, ...)'s sums, the
+ *           same rounding rules (fp32 difference, fp64 squares and sum,
+ *           fixed order; not necessarily the same summation tree).
+ * K <= 128 with 16-B aligned rows and ld % 4 == 0 runs the fused kernel
+ * (K x 64-256 columns staged in LDS per workgroup); anything else runs the two
+ * passes back to back.  workspace : fedavg_reduce_sqdist_workspace(K, P)
+ * doubles of device scratch.  P == 0 writes sumsq = 0.
+ */
+int64_t fedavg_reduce_sqdist_workspace(int64_t K, int64_t P);
+int fedavg_reduce_sqdist_f32(const float* clients, int64_t K, int64_t P, int64_t ld,
+                             const float* weights, float* out, double* workspace,
+                             int64_t workspace_elems, double* sumsq, void* stream);
+
+/*
  * The same pass for fp64 / fp16 / bf16 keys (a state_dict group of that
  * dtype).  `w[para] - w_glob[para]` at :291 forms the difference in the
  * key's dtype -- fp64, or fp32 math rounded to fp16/bf16 (ATen opmath) --

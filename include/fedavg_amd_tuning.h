@@ -163,6 +163,13 @@ int fedavg_reduce_f32_buf(const float* clients, int64_t K, int64_t P, int64_t ld
  * count ends at the last float4 (lanes past it read 0); (unroll, cols) in
  * {(4,8), (8,4), (2,16), (2,8), (8,8)}; round-split launches of <= max_blocks
  * blocks (0 = one launch).  Same workspace as fedavg_client_sqdist_f32. */
+/* fedavg_reduce_sqdist_f32 with an explicit tile width (cols = 64, 128 or
+ * 256 columns) and workgroups per CU (0 = as many as LDS allows); K <= 128,
+ * workspace >= K x (blocks per CU x CUs) doubles. */
+int fedavg_reduce_sqdist_f32_variant(const float* clients, int64_t K, int64_t P, int64_t ld,
+                                     const float* weights, float* out, double* workspace,
+                                     int64_t workspace_elems, double* sumsq, int cols,
+                                     int blocks_per_cu, void* stream);
 int fedavg_client_sqdist_buf(const float* clients, int64_t K, int64_t P, int64_t ld, const float* glob,
                              double* workspace, int64_t workspace_elems, double* sumsq, int unroll, int cols,
                              int max_blocks, void* stream);

@@ -27,7 +27,7 @@ from .aggregate import (
     sample_weights,
 )
 from .layout import KeyTable, ShapeMismatchError, result_dtype
-from .reduce import ALIGN_ELEMS, client_sqdist, reduce_packed, reduce_tensors, weights_tensor
+from .reduce import ALIGN_ELEMS, client_sqdist, reduce_packed, reduce_tensors, reduce_with_sqdist, weights_tensor
 from .session import RoundSession
 from .fpf import FPFTracker
 
@@ -41,6 +41,7 @@ __all__ = [
     "client_distances",
     "estimate_delta",
     "client_sqdist",
+    "reduce_with_sqdist",
     "default_aggregator",
     "install",
     "sample_weights",

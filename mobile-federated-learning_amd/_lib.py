@@ -41,6 +41,8 @@ SIGNATURES = {
     "fedavg_client_sqdist_workspace": (_c_i64, [_c_i64, _c_i64]),
     "fedavg_client_sqdist_f32": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_i64, _vp, _vp]),
     "fedavg_client_sqdist_workspace_elems": (_c_i64, [_c_i64, _c_i64, _c_i64]),
+    "fedavg_reduce_sqdist_workspace": (_c_i64, [_c_i64, _c_i64]),
+    "fedavg_reduce_sqdist_f32": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _c_i64, _vp, _vp]),
     "fedavg_client_sqdist_f64": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_i64, _vp, _vp]),
     "fedavg_client_sqdist_f16": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_i64, _vp, _vp]),
     "fedavg_client_sqdist_bf16": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_i64, _vp, _vp]),
@@ -82,6 +84,8 @@ TUNING_SIGNATURES = {
                                               _c_int, _vp]),
     "fedavg_client_sqdist_buf": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_i64, _vp, _c_int, _c_int,
                                           _c_int, _vp]),
+    "fedavg_reduce_sqdist_f32_variant": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _c_i64, _vp, _c_int,
+                                                  _c_int, _vp]),
     "fedavg_reduce_vec_buf": (_c_int, [_c_int, _vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_int, _c_int, _c_int, _vp]),
     "fedavg_probe_busy_copy": (_c_int, [_vp, _vp, _c_i64, _c_int, _c_int, _vp]),
     "fedavg_stream_create_masked": (_c_int, [_c_int, _c_int, _vp]),

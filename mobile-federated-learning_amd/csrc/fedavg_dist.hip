@@ -295,6 +295,256 @@ __global__ __launch_bounds__(kBlock) void client_sqdist_finalize_kernel(const do
   if (threadIdx.x == 0) out[k] = red[0];
 }
 
+// ---------------------------------------------------------------------------
+// Aggregate (:450-457) and :291 in ONE pass over the client rows.  The
+// reference reads every client's update twice per round: once to average it
+// (:217) and once to measure ||w_i - w_glob|| (:291).  Both passes are
+// HBM-read bound on the same K x P bytes, so fusing them halves the round's
+// traffic -- if every column's K values are still on chip when that column's
+// average is known.  A workgroup therefore owns tiles of S columns x all K
+// rows staged in LDS (K x S x 4 bytes: 25.6 KB for K = 100, S = 64):
+//   1. every row segment lands in LDS by LDS-DMA (global_load_lds_dwordx4,
+//      1 KiB per wave instruction, no VGPR round trip).  The 16-B slots of
+//      row r are XOR-swizzled by (r & 7): slot j holds the row's slice
+//      j ^ (r & 7) (the swizzle is in the per-lane GLOBAL address; LDS stays
+//      linear, as LDS-DMA requires), so threads reading one slice of 8
+//      consecutive rows hit 8 different bank groups;
+//   2. one thread per column runs the reference's sequential chain over the
+//      K rows (fl32 products and sums in client order: the bits of
+//      fedavg_reduce_f32) and stores the average to `out` and to LDS;
+//   3. thread t owns row t % K and the slices t / K, t / K + q, ... (q =
+//      256 / K threads per row), and adds fl32(x - g)^2 in fp64 to ONE
+//      register accumulator that lives across all of the workgroup's tiles.
+//      At the end the q accumulators of a row are added in a fixed order.
+// A thread keeps one fp64 accumulator instead of one per row, so the kernel
+// is LDS-bound, not register-bound: K = 100 x 64 columns runs 6 workgroups
+// per CU.  Workgroups are persistent (grid = resident workgroups) and walk the
+// tiles with a grid stride, so the running workgroups sweep one compact
+// window of every row, as the round-split row reduce does.
+// partials[k][workgroup], then the fixed-order finalize: deterministic.
+// K <= 128 (q >= 2).
+// ---------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef const __attribute__((address_space(1))) void* gbl_ptr_t;
+
+// rows -> LDS for the tile at column c0: slot i = row * V + j (LDS byte
+// 16 i from `buf`) holds slice j ^ (row & 7) of the row segment
+template <int S>
+__device__ __forceinline__ void fused_load_tile(const float* __restrict__ X, int K, int64_t ld, int64_t P, int64_t c0,
+                                                float* buf) {
+  constexpr int V = S / 4;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nload = K * V;
+  const int ncols = P - c0 < S ? static_cast<int>(P - c0) : S;
+  const int nv4 = (ncols + 3) >> 2;  // slices holding valid columns (the last may run into the row padding)
+  for (int i0 = wave * 64; i0 < nload; i0 += kBlock) {
+    const int i = i0 + lane;
+    const int row = i / V;
+    const int c = (i % V) ^ (row & 7);
+    if (i < nload && c < nv4)
+      __builtin_amdgcn_global_load_lds((gbl_ptr_t)(X + static_cast<int64_t>(row) * ld + c0 + 4 * c),
+                                       (lds_ptr_t)(buf + 4 * i0), 16, 0, 2 /* nt */);
+  }
+}
+
+// Barriers without the compiler's vmcnt(0) drain: a plain __syncthreads()
+// would also wait for the NEXT tile's LDS-DMA loads in flight.
+__device__ __forceinline__ void barrier_lds() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+__device__ __forceinline__ void barrier_loads() {
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+template <int S, bool DB, int RW = 0, bool LOADS_ONLY = false>
+__global__ __launch_bounds__(kBlock) void reduce_sqdist_f32_kernel(const float* __restrict__ X, int K, int64_t ld,
+                                                                   int64_t P, int64_t ntiles,
+                                                                   const float* __restrict__ W,
+                                                                   float* __restrict__ out,
+                                                                   double* __restrict__ partials) {
+  static_assert(S == 64 || S == 128 || S == 256, "tile widths: 64, 128 or 256 columns");
+  // one tile buffer [K][S] (swizzled slots) -- two when DB -- then the tile's average [S]
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int V = S / 4;  // 16-B slots per row segment
+  const int tile_floats = K * S;
+  float* gs = lds + (DB ? 2 : 1) * tile_floats;
+  const int q = kBlock / K;            // threads per row in phase 3
+  const int my_row = threadIdx.x % K;  // phase 3: this thread's row ...
+  const int my_sub = threadIdx.x / K;  // ... and first slice (active while < q)
+  const int my_swz = my_row & 7;
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};  // one chain per lane of a 16-B slice
+  double acc_rows[RW > 0 ? RW : 1];      // RW > 0: one accumulator per row of this wave
+#pragma unroll
+  for (int r = 0; r < (RW > 0 ? RW : 1); ++r) acc_rows[r] = 0.0;
+  int cur = 0;
+  if (DB && static_cast<int64_t>(blockIdx.x) < ntiles)
+    fused_load_tile<S>(X, K, ld, P, static_cast<int64_t>(blockIdx.x) * S, lds);
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    float* tile = lds + cur * tile_floats;
+    const int64_t c0 = t * S;
+    const int ncols = P - c0 < S ? static_cast<int>(P - c0) : S;
+    if constexpr (DB) {
+      barrier_loads();  // this tile has landed; every wave is done with the other buffer
+      // 1. the next tile's rows stream into the other buffer while this one is used
+      if (t + gridDim.x < ntiles) fused_load_tile<S>(X, K, ld, P, (t + gridDim.x) * S, lds + (cur ^ 1) * tile_floats);
+    } else {
+      fused_load_tile<S>(X, K, ld, P, c0, tile);  // 1. rows -> LDS
+      barrier_loads();
+    }
+    if constexpr (LOADS_ONLY) {  // probe: the tile traffic alone (one column of each tile stored)
+      if (threadIdx.x == 0) out[c0] = tile[0];
+      barrier_lds();
+      continue;
+    }
+    // 2. the average of each column, in the reference's order (:455-457)
+    if (threadIdx.x < S) {
+      const int c = threadIdx.x;
+      const int j = c >> 2, e = c & 3;
+      float a = tile[j * 4 + e] * W[0];
+      for (int k = 1; k < K; ++k) {
+        const float term = tile[k * S + ((j ^ (k & 7)) << 2) + e] * W[k];
+        a = a + term;
+      }
+      gs[c] = a;
+      if (c < ncols) out[c0 + c] = a;
+    }
+    barrier_lds();
+    if constexpr (RW > 0) {
+      // 3'. rows wave + 4r (r < RW), S / 64 adjacent columns per lane, one
+      //     register accumulator per row
+      constexpr int PER = S / 64;
+#pragma unroll
+      for (int r = 0; r < RW; ++r) {
+        const int row = (threadIdx.x >> 6) + 4 * r;
+        if (row < K) {
+          const int c = (threadIdx.x & 63) * PER;
+          const float* x = tile + row * S + ((((c >> 2) ^ (row & 7))) << 2) + (c & 3);
+#pragma unroll
+          for (int j = 0; j < PER; ++j) {
+            const float d = x[j] - gs[c + j];  // fp32 difference, as the reference forms it
+            const double dd = c + j < ncols ? static_cast<double>(d) : 0.0;  // select: padding may hold NaN/inf
+            acc_rows[r] = __builtin_fma(dd, dd, acc_rows[r]);
+          }
+        }
+      }
+    } else {
+      // 3. :291 squares of this thread's row over its slices
+      if (my_sub < q) {
+        const f32x4* my_x = reinterpret_cast<const f32x4*>(tile) + my_row * V;
+        for (int c = my_sub; c < V; c += q) {
+          const f32x4 x = my_x[c ^ my_swz];
+          const f32x4 g = reinterpret_cast<const f32x4*>(gs)[c];
+          const f32x4 d = x - g;  // fp32 difference, as the reference forms it
+          const int n = ncols - 4 * c;  // valid columns of this slice (select, not multiply: padding may hold NaN/inf)
+          if (n > 0) {
+            const double dx = d.x, dy = n > 1 ? d.y : 0.f, dz = n > 2 ? d.z : 0.f, dw = n > 3 ? d.w : 0.f;
+            acc[0] = __builtin_fma(dx, dx, acc[0]);
+            acc[1] = __builtin_fma(dy, dy, acc[1]);
+            acc[2] = __builtin_fma(dz, dz, acc[2]);
+            acc[3] = __builtin_fma(dw, dw, acc[3]);
+          }
+        }
+      }
+    }
+    if constexpr (DB)
+      cur ^= 1;
+    else
+      barrier_lds();  // the tile is read out before the next one lands
+  }
+  if constexpr (RW > 0) {
+#pragma unroll
+    for (int r = 0; r < RW; ++r) {
+      const int row = (threadIdx.x >> 6) + 4 * r;
+      if (row < K) {
+        const double sr = wave_sum_dpp(acc_rows[r]);
+        if ((threadIdx.x & 63) == 0) partials[static_cast<int64_t>(row) * gridDim.x + blockIdx.x] = sr;
+      }
+    }
+    return;
+  }
+  // the q accumulators of each row, added in a fixed order
+  barrier_loads();
+  double* red = reinterpret_cast<double*>(lds);
+  red[threadIdx.x] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  barrier_lds();
+  if (threadIdx.x < K) {
+    double s = red[threadIdx.x];
+    for (int u = 1; u < q; ++u) s += red[threadIdx.x + u * K];
+    partials[static_cast<int64_t>(threadIdx.x) * gridDim.x + blockIdx.x] = s;
+  }
+}
+
+constexpr int kFusedMaxK = kBlock / 2;  // two threads per row at least: K <= 128
+
+// the tile + its average, and at least the 256 doubles of the final per-row sums
+inline int64_t fused_lds_bytes(int64_t K, int S, bool db = false) {
+  const int64_t b = ((db ? 2 : 1) * K + 1) * S * 4;
+  return b > kBlock * 8 ? b : kBlock * 8;
+}
+
+// Tile width for K rows (0 = K outside the fused range): 64 columns (256 B
+// per row segment) from K = 33, 128 up to 32 rows, 256 up to 16
+inline int fused_cols(int64_t K) {
+  if (K < 1 || K > kFusedMaxK) return 0;
+  if (K > 32) return 64;
+  return K > 16 ? 128 : 256;
+}
+
+// Workgroups per CU the fused kernel keeps resident at this K (LDS-bound),
+// after raising the kernel's dynamic LDS limit past 64 KiB where needed;
+// cached per (device, S, K).  0 = the LDS request cannot be granted.
+template <int S, bool DB = false, int RW = 0, bool LO = false>
+int fused_per_cu(int64_t K) {
+  static std::mutex mu;
+  static std::map<std::pair<int, int64_t>, int> cache;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find({dev, K});
+  if (it != cache.end()) return it->second;
+  const auto kern = reduce_sqdist_f32_kernel<S, DB, RW, LO>;
+  const int64_t lds = fused_lds_bytes(K, S, DB);
+  int per_cu = 0;
+  if (lds > 65536 && hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         static_cast<int>(lds)) != hipSuccess) {
+    (void)hipGetLastError();
+  } else if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kBlock, static_cast<size_t>(lds)) !=
+             hipSuccess) {
+    (void)hipGetLastError();
+    per_cu = 0;
+  }
+  cache[{dev, K}] = per_cu;
+  return per_cu;
+}
+
+template <int S, bool DB = false, int RW = 0, bool LO = false>
+int64_t fused_grid(int64_t K, int64_t P, int blocks_per_cu) {
+  const int per_cu = blocks_per_cu > 0 ? blocks_per_cu : fused_per_cu<S, DB, RW, LO>(K);
+  const int64_t ntiles = (P + S - 1) / S;
+  const int64_t g = static_cast<int64_t>(per_cu) * cu_count();
+  return ntiles < g ? ntiles : g;
+}
+
+template <int S, bool DB = false, int RW = 0, bool LO = false>
+int launch_fused(const float* clients, int64_t K, int64_t P, int64_t ld, const float* weights, float* out,
+                 double* partials, int64_t partial_elems, double* sumsq, int blocks_per_cu, hipStream_t s,
+                 const char* what) {
+  if (RW > 0 && K > 4 * RW) return set_error(FEDAVG_EMODE, "%s: %d rows per wave cover K <= %d", what, RW, 4 * RW);
+  if (fused_per_cu<S, DB, RW, LO>(K) <= 0) return set_error(FEDAVG_EMODE, "%s: the %d-column tile does not fit LDS at K = %lld",
+                                                what, S, (long long)K);
+  const int64_t ntiles = (P + S - 1) / S;
+  const int64_t grid = fused_grid<S, DB, RW, LO>(K, P, blocks_per_cu);
+  if (partial_elems < K * grid)
+    return set_error(FEDAVG_EINVAL, "%s: workspace needs %lld doubles", what, (long long)(K * grid));
+  hipLaunchKernelGGL((reduce_sqdist_f32_kernel<S, DB, RW, LO>), dim3(static_cast<unsigned>(grid)), dim3(kBlock),
+                     static_cast<unsigned>(fused_lds_bytes(K, S, DB)), s, clients, static_cast<int>(K), ld, P, ntiles,
+                     weights, out, partials);
+  int rc = launch_status(what);
+  if (rc) return rc;
+  hipLaunchKernelGGL(client_sqdist_finalize_kernel, dim3(static_cast<unsigned>(K)), dim3(kBlock), 0, s, partials, grid,
+                     sumsq);
+  return launch_status(what);
+}
+
 // Global-pointer schedule (the fp64/fp16/bf16 passes and the probe
 // variants): 32 x 16-B loads in flight per thread (U4 x C8) in one launch;
 // scripts/dist_variants.py (profiles/sweeps/r01_dist_*.jsonl) measured
@@ -560,6 +810,86 @@ int fedavg_client_sqdist_buf(const float* clients, int64_t K, int64_t P, int64_t
                              int max_blocks, void* stream) {
   return sqdist_buf_impl(clients, K, P, ld, glob, workspace, workspace_elems, sumsq, unroll, cols, max_blocks, stream,
                          "fedavg_client_sqdist_buf");
+}
+#endif  // FEDAVG_TUNING
+
+// Aggregate + :291 sums in one pass (reduce_sqdist_f32_kernel) for K <= 128
+// with 16-B aligned rows; otherwise the two production passes back to back
+// (fedavg_reduce_f32, then fedavg_client_sqdist_f32 on its output).  Either
+// way `out` holds fedavg_reduce_f32's bits and sumsq the :291 sums.
+int64_t fedavg_reduce_sqdist_workspace(int64_t K, int64_t P) {
+  if (K <= 0 || P <= 0) return 0;
+  const int S = fused_cols(K);
+  const int64_t two_pass = fedavg_client_sqdist_workspace(K, P);
+  int64_t fused = 0;
+  if (S == 64) fused = K * fused_grid<64>(K, P, 0);
+  if (S == 128) fused = K * fused_grid<128>(K, P, 0);
+  if (S == 256) fused = K * fused_grid<256>(K, P, 0);
+  return fused > two_pass ? fused : two_pass;
+}
+
+int fedavg_reduce_sqdist_f32(const float* clients, int64_t K, int64_t P, int64_t ld, const float* weights, float* out,
+                             double* workspace, int64_t workspace_elems, double* sumsq, void* stream) {
+  const char* what = "fedavg_reduce_sqdist_f32";
+  int rc = check_common(clients, K, P, ld, weights, out, what);
+  if (rc) return rc;
+  if (!sumsq || !workspace) return set_error(FEDAVG_EINVAL, "%s: null workspace/sumsq", what);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (P == 0) {
+    const hipError_t e = hipMemsetAsync(sumsq, 0, static_cast<size_t>(K) * sizeof(double), s);
+    return e == hipSuccess ? FEDAVG_OK : set_error(-static_cast<int>(e), "%s: hipMemsetAsync failed", what);
+  }
+  const int S = fused_cols(K);
+  if (S > 0 && aligned16(clients) && (ld % 4) == 0 && aligned4(out) && aligned4(weights)) {
+    if (S == 64) return launch_fused<64>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq, 0, s, what);
+    if (S == 128)
+      return launch_fused<128>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq, 0, s, what);
+    return launch_fused<256>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq, 0, s, what);
+  }
+  rc = fedavg_reduce_f32(clients, K, P, ld, weights, out, stream);
+  if (rc) return rc;
+  return fedavg_client_sqdist_f32(clients, K, P, ld, out, workspace, workspace_elems, sumsq, stream);
+}
+
+#ifdef FEDAVG_TUNING  // probe library only (libfedavg_amd_probe.so)
+// the fused pass with an explicit tile width (64 / 128 / 256 columns) and
+// workgroups per CU (0 = as many as LDS allows); workspace >= K x grid
+int fedavg_reduce_sqdist_f32_variant(const float* clients, int64_t K, int64_t P, int64_t ld, const float* weights,
+                                     float* out, double* workspace, int64_t workspace_elems, double* sumsq, int cols,
+                                     int blocks_per_cu, void* stream) {
+  const char* what = "fedavg_reduce_sqdist_f32_variant";
+  int rc = check_common(clients, K, P, ld, weights, out, what);
+  if (rc) return rc;
+  if (P == 0 || K > kFusedMaxK || !aligned16(clients) || (ld % 4) != 0 || !sumsq || !workspace)
+    return set_error(FEDAVG_EINVAL, "%s: needs 1 <= K <= %d, P >= 1, 16-B aligned rows", what, kFusedMaxK);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  // cols + 1000: double-buffered tiles (the next tile's loads in flight while
+  // one is used); + 10000: rows per wave with one register accumulator each
+  switch (cols) {
+#define FEDAVG_FUSED_CASE(C, DBUF, RWS)                                                                           \
+  case C + (DBUF ? 1000 : 0) + (RWS ? 10000 : 0):                                                                \
+    return launch_fused<C, DBUF, RWS>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq,         \
+                                      blocks_per_cu, s, what);
+    FEDAVG_FUSED_CASE(64, false, 0)
+    FEDAVG_FUSED_CASE(128, false, 0)
+    FEDAVG_FUSED_CASE(256, false, 0)
+    FEDAVG_FUSED_CASE(64, true, 0)
+    FEDAVG_FUSED_CASE(128, true, 0)
+    FEDAVG_FUSED_CASE(256, true, 0)
+    FEDAVG_FUSED_CASE(64, false, 32)
+    FEDAVG_FUSED_CASE(128, false, 32)
+    FEDAVG_FUSED_CASE(256, false, 32)
+    FEDAVG_FUSED_CASE(128, true, 32)
+#undef FEDAVG_FUSED_CASE
+    // + 100000: the tile loads alone (no average, no sums: a traffic probe, wrong results)
+    case 100064: return launch_fused<64, false, 0, true>(clients, K, P, ld, weights, out, workspace, workspace_elems,
+                                                         sumsq, blocks_per_cu, s, what);
+    case 100128: return launch_fused<128, false, 0, true>(clients, K, P, ld, weights, out, workspace, workspace_elems,
+                                                          sumsq, blocks_per_cu, s, what);
+    case 101064: return launch_fused<64, true, 0, true>(clients, K, P, ld, weights, out, workspace, workspace_elems,
+                                                        sumsq, blocks_per_cu, s, what);
+    default: return set_error(FEDAVG_EMODE, "%s: cols must be 64, 128 or 256 (+1000: double-buffered)", what);
+  }
 }
 #endif  // FEDAVG_TUNING
 

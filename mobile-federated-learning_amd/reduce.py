@@ -13,7 +13,8 @@ import torch
 
 from . import _lib
 
-__all__ = ["reduce_packed", "reduce_tensors", "weights_tensor", "client_sqdist", "ALIGN_ELEMS"]
+__all__ = ["reduce_packed", "reduce_tensors", "weights_tensor", "client_sqdist", "reduce_with_sqdist",
+           "ALIGN_ELEMS"]
 
 # Row stride granule of the packed [K, ld] layout: 64 elements (256 B for
 # fp32) keeps every client row 16-B aligned for the float4/double2/8xhalf
@@ -261,3 +262,24 @@ def client_sqdist(clients: torch.Tensor, glob: torch.Tensor, P: Optional[int] = 
                              _stream_handle(stream, clients.device))
     _lib.check(rc, entry)
     return out
+
+
+def reduce_with_sqdist(clients: torch.Tensor, weights: torch.Tensor, P: Optional[int] = None,
+                       out: Optional[torch.Tensor] = None, *, stream: Optional[torch.cuda.Stream] = None):
+    """One round's aggregate (fedavg_trainer.py:450-457) AND its :291 sums of
+    squares in one pass over fp32 rows: returns ``(out, sumsq)`` with ``out``
+    the bits of ``reduce_packed(clients, weights, P)`` and ``sumsq`` [K]
+    float64 device sums as ``client_sqdist(clients, out, P)`` forms them.
+    K <= 128 reads the rows once (fedavg_reduce_sqdist_f32); larger K runs
+    the two passes inside the same call."""
+    K, ld, P, dtype, out = _check_packed(clients, weights, P, out)
+    if dtype != torch.float32:
+        raise TypeError("reduce_with_sqdist: fp32 rows only (other dtypes: reduce_packed + client_sqdist)")
+    lib = _lib.load()
+    n_ws = lib.fedavg_reduce_sqdist_workspace(K, P)
+    work = torch.empty(max(n_ws, 1), dtype=torch.float64, device=clients.device)
+    sumsq = torch.empty(K, dtype=torch.float64, device=clients.device)
+    rc = lib.fedavg_reduce_sqdist_f32(clients.data_ptr(), K, P, ld, weights.data_ptr(), out.data_ptr(),
+                                      work.data_ptr(), n_ws, sumsq.data_ptr(), _stream_handle(stream, clients.device))
+    _lib.check(rc, "fedavg_reduce_sqdist_f32")
+    return out, sumsq

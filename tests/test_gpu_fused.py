@@ -1,0 +1,122 @@
+"""GPU parity of the fused aggregate + :291 pass (fedavg_reduce_sqdist_f32).
+
+The averaged model must carry the oracle's bits (fedavg_trainer.py:450-457,
+the same bar as fedavg_reduce_f32); the sums of squares follow :291's rule
+(fp32 difference, squared and summed in fp64), checked against fp64 sums of
+the same fp32 differences at 1e-12 relative and for run-to-run determinism.
+"""
+import numpy as np
+import pytest
+import torch
+
+import fedavg_oracle as O
+import mfl_amd
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda", 0)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu(gpu_available):
+    mfl_amd._lib.load()
+    torch.cuda.set_device(DEV)
+    yield
+
+
+def _rows(K, P, seed, pad=float("nan")):
+    ld = (P + 63) // 64 * 64
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    x = torch.full((K, ld), pad, device=DEV)
+    x[:, :P] = torch.randn((K, P), generator=g, device=DEV) * 0.05 + torch.randn((K, 1), generator=g, device=DEV) * 1e-3
+    counts = torch.randint(1, 1000, (K,), generator=torch.Generator().manual_seed(seed)).tolist()
+    weights = mfl_amd.sample_weights(counts)
+    return x, ld, weights
+
+
+def _sumsq_ref(x, out, P):
+    return torch.stack([((x[k, :P] - out[:P]).double() ** 2).sum() for k in range(x.shape[0])])
+
+
+@pytest.mark.parametrize("K,P", [(1, 1), (1, 129), (2, 3), (3, 127), (3, 128), (5, 1001), (7, 4096 * 3 + 5),
+                                 (13, 300_007), (64, 65_536), (100, 100_003), (127, 20_000), (128, 20_001)])
+def test_fused_small_vs_oracle(K, P):
+    x, ld, weights = _rows(K, P, K * 1000 + P)
+    w = mfl_amd.weights_tensor(weights, torch.float32, DEV)
+    out, sumsq = mfl_amd.reduce_with_sqdist(x, w, P)
+    exp = O.reduce_f32(x[:, :P].cpu().numpy(), np.array([np.float32(v) for v in weights], dtype=np.float32))
+    assert out.cpu().numpy().view(np.uint32).tobytes() == exp.view(np.uint32).tobytes()
+    ref = _sumsq_ref(x, out, P)
+    rel = ((sumsq - ref).abs() / ref.clamp_min(1e-300)).max().item()
+    assert rel < 1e-12, rel
+    _, again = mfl_amd.reduce_with_sqdist(x, w, P)
+    assert torch.equal(sumsq, again)  # deterministic
+
+
+@pytest.mark.parametrize("K,P", [(129, 5003), (300, 70_001)])
+def test_fused_large_k_takes_two_passes(K, P):
+    """K > 128: the same entry runs the two production passes; same bits."""
+    x, ld, weights = _rows(K, P, K + P)
+    w = mfl_amd.weights_tensor(weights, torch.float32, DEV)
+    out, sumsq = mfl_amd.reduce_with_sqdist(x, w, P)
+    assert torch.equal(out.view(torch.int32), mfl_amd.reduce_packed(x, w, P).view(torch.int32))
+    assert torch.equal(sumsq, mfl_amd.client_sqdist(x, out, P))
+
+
+def test_fused_target_size_matches_two_pass():
+    """100 x 25M (the north-star round): the reduce's bits on every column,
+    sums within 1e-12 of the two-pass sums."""
+    K, P = 100, 25_000_000 + 3
+    ld = (P + 63) // 64 * 64
+    g = torch.Generator(device=DEV).manual_seed(11)
+    x = torch.randn((K, ld), generator=g, device=DEV) * 0.05
+    w = mfl_amd.weights_tensor(mfl_amd.sample_weights(list(range(1, K + 1))), torch.float32, DEV)
+    out, sumsq = mfl_amd.reduce_with_sqdist(x, w, P)
+    ref_out = mfl_amd.reduce_packed(x, w, P)
+    assert torch.equal(out.view(torch.int32), ref_out.view(torch.int32))
+    ref = mfl_amd.client_sqdist(x, ref_out, P)
+    rel = ((sumsq - ref).abs() / ref).max().item()
+    assert rel < 1e-12, rel
+    del x
+
+
+def test_fused_variants_same_bits():
+    lib = mfl_amd._lib.load_probe()
+    K, P = 100, 600_372
+    x, ld, weights = _rows(K, P, 3)
+    w = mfl_amd.weights_tensor(weights, torch.float32, DEV)
+    out0, s0 = mfl_amd.reduce_with_sqdist(x, w, P)
+    n_ws = K * 256 * 8
+    work = torch.empty(n_ws, dtype=torch.float64, device=DEV)
+    # tile width (+1000 double-buffered, +10000 rows per wave), workgroups per CU
+    for cols, bpc in [(64, 0), (128, 0), (128, 1), (64, 2), (256, 0), (1064, 0), (10064, 0), (10128, 0), (11128, 0)]:
+        out = torch.empty(P, device=DEV)
+        s = torch.empty(K, dtype=torch.float64, device=DEV)
+        mfl_amd._lib.check(lib.fedavg_reduce_sqdist_f32_variant(x.data_ptr(), K, P, ld, w.data_ptr(), out.data_ptr(),
+                                                                work.data_ptr(), n_ws, s.data_ptr(), cols, bpc,
+                                                                None), f"cols {cols} bpc {bpc}", lib)
+        torch.cuda.synchronize()
+        assert torch.equal(out.view(torch.int32), out0.view(torch.int32)), (cols, bpc)
+        rel = ((s - s0).abs() / s0).max().item()
+        assert rel < 1e-12, (cols, bpc, rel)
+    # two 256-column tiles of 100 rows (201 KB) exceed the CU's 160 KB of LDS
+    rc = lib.fedavg_reduce_sqdist_f32_variant(x.data_ptr(), K, P, ld, w.data_ptr(), out.data_ptr(), work.data_ptr(),
+                                              n_ws, s.data_ptr(), 1256, 0, None)
+    assert rc == mfl_amd._lib.FEDAVG_EMODE
+
+
+def test_fused_nonfinite_rows():
+    """NaN/inf inside the model propagate as the reference's ops propagate
+    them; NaN in the row padding never reaches the sums."""
+    K, P = 4, 1030
+    x, ld, weights = _rows(K, P, 9)
+    x[1, 17] = float("inf")
+    x[2, 500] = float("nan")
+    w = mfl_amd.weights_tensor(weights, torch.float32, DEV)
+    out, sumsq = mfl_amd.reduce_with_sqdist(x, w, P)
+    exp = O.reduce_f32(x[:, :P].cpu().numpy(), np.array([np.float32(v) for v in weights], dtype=np.float32))
+    got = out.cpu().numpy()
+    assert np.array_equal(np.isnan(got), np.isnan(exp))
+    assert np.array_equal(got[~np.isnan(got)], exp[~np.isnan(exp)])
+    ref = _sumsq_ref(x, out, P)
+    assert torch.equal(torch.isnan(sumsq), torch.isnan(ref))
