@@ -352,6 +352,44 @@ def overlap_diagnostics(red, w_dev, steps: int, step_elapsed: float, reps: int =
             "note": "after the timed region; not part of value"}
 
 
+def fused_round(red, w_dev, reps: int = 10) -> dict:
+    """N = 1 side measurement of the round's second read: the aggregate plus
+    the :291 sums of squares (fedavg_trainer.py:217 then :291) as two passes
+    over the rows (fedavg_reduce_f32 + fedavg_client_sqdist_f32) against the
+    fused pass (fedavg_reduce_sqdist_f32), interleaved, HIP events around
+    each call; the averaged model must keep its bits."""
+    import numpy as np
+    import torch
+
+    import mfl_amd
+
+    K, P = red.clients.shape[0], red.plan.valid_local_cols()
+    rows = red.clients
+    o2, o1 = torch.empty(P, device=rows.device), torch.empty(P, device=rows.device)
+    runs = {"two_pass": lambda: mfl_amd.client_sqdist(rows, mfl_amd.reduce_packed(rows, w_dev, P, o2), P),
+            "fused": lambda: mfl_amd.reduce_with_sqdist(rows, w_dev, P, o1)[1]}
+    sums = {n: fn() for n, fn in runs.items()}
+    times = {n: [] for n in runs}
+    for _ in range(reps):
+        for n, fn in runs.items():
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            fn()
+            b.record()
+            times[n].append((a, b))
+    torch.cuda.synchronize()
+    ms = {n: float(np.median([a.elapsed_time(b) for a, b in v])) for n, v in times.items()}
+    alg = algorithmic_bytes(K, P)
+    rel = float(((sums["fused"] - sums["two_pass"]).abs() / sums["two_pass"].abs().clamp_min(1e-300)).max())
+    return {"what": "aggregate + :291 sums of squares over the same resident rows (fedavg_trainer.py:217, :291)",
+            "two_pass_ms": round(ms["two_pass"], 4), "fused_ms": round(ms["fused"], 4),
+            "speedup": round(ms["two_pass"] / ms["fused"], 3),
+            "fused_GBps_of_round_bytes": round(alg / ms["fused"] / 1e6, 1),
+            "out_bits_equal": bool(torch.equal(o1.view(torch.int32), o2.view(torch.int32))),
+            "sums_max_rel_vs_two_pass": rel,
+            "timing": f"median of {reps} interleaved calls, HIP events around each call"}
+
+
 def launch_check(args):
     """``--launch-check``: the multi-rank launch path alone, on CPU (gloo) --
     every rank joins the group and all-reduces its rank; rank 0 prints one
@@ -711,6 +749,8 @@ def main(argv=None):
         }
         if diagnostics is not None:
             out["diagnostics"] = diagnostics
+        if world == 1 and passes == 1 and plan_world == 1 and K <= 128 and red.plan.chunks == 1:
+            out["round_with_distances"] = fused_round(red, w_dev)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(min(P_global, 25_000_000))
         print(json.dumps(out), flush=True)

@@ -53,7 +53,7 @@ import torch
 from . import _lib
 from .layout import KeyTable
 from .layout import _collect_ext as layout_collect_ext
-from .reduce import client_sqdist, reduce_packed
+from .reduce import client_sqdist, reduce_packed, reduce_with_sqdist
 
 __all__ = [
     "sample_weights",
@@ -152,9 +152,36 @@ def column_chunks(P: int) -> List[Tuple[int, int]]:
     return [(c0, min(P, c0 + step)) for c0 in range(0, P, step)] or [(0, 0)]
 
 
+# An fp32 row reduce with at most this many clients also forms the round's
+# :291 sums of squares in the same pass over the rows (fedavg_reduce_sqdist_f32:
+# 100 x 25M, 1.76 ms for both against 1.42 + 1.47 ms for the two passes,
+# DESIGN.md section 3); client_distances then reads them instead of the rows.
+# The reference runs :291 after every aggregate with clients (fedavg_trainer.py
+# :289-291), so the drop-in fuses by default; FEDAVG_FUSE_DISTANCES=0 keeps
+# the reduce alone.
+FUSED_MAX_K = 128
+FUSE_DISTANCES = os.environ.get("FEDAVG_FUSE_DISTANCES", "1") != "0"
+
+
+def fuse_eligible(devbuf: torch.Tensor) -> bool:
+    return FUSE_DISTANCES and devbuf.dtype == torch.float32 and 0 < devbuf.shape[0] <= FUSED_MAX_K
+
+
+def reduce_rows(devbuf: torch.Tensor, w_dev: torch.Tensor, P: int, out: torch.Tensor,
+                sums: Optional[list] = None) -> None:
+    """``reduce_packed`` of [K, ld] rows into ``out``; with ``sums`` (a list)
+    and fused-eligible rows, the :291 sums of squares of the same columns are
+    formed in the same pass and their [K] fp64 device tensor appended."""
+    if sums is not None and fuse_eligible(devbuf):
+        sums.append(reduce_with_sqdist(devbuf, w_dev, P, out)[1])
+    else:
+        reduce_packed(devbuf, w_dev, P, out)
+
+
 def reduce_and_fetch(devbuf: torch.Tensor, w_dev: torch.Tensor, P: int, d2h_stream,
                      ready: Optional[Sequence] = None,
-                     out_host: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+                     out_host: Optional[torch.Tensor] = None,
+                     sums: Optional[dict] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """Reduce ``devbuf`` [K, ld] on the current stream in ``column_chunks(P)``
     and copy each chunk to a pinned host buffer on ``d2h_stream`` as soon as
     it is reduced.  ``ready[c]`` (optional): an event after which chunk c's
@@ -162,20 +189,28 @@ def reduce_and_fetch(devbuf: torch.Tensor, w_dev: torch.Tensor, P: int, d2h_stre
     that, so the last client's H2D, the reduce and the D2H pipeline.
     ``out_host`` (optional): a pinned [>=P] buffer allocated ahead (a fresh
     100 MB pinned allocation costs 5.6-8.6 ms); a new one
-    otherwise.  Returns ``(out_dev, out_host)``; the caller synchronizes
-    ``d2h_stream``."""
+    otherwise.  ``sums`` (optional dict): fused-eligible fp32 rows also give
+    the :291 sums of squares, ``sums[dtype]`` = their [K] fp64 device tensor
+    (the chunks' sums added in chunk order).  Returns ``(out_dev, out_host)``;
+    the caller synchronizes ``d2h_stream``."""
     dev = devbuf.device
     compute = torch.cuda.current_stream(dev)
     out_dev = torch.empty(P, dtype=devbuf.dtype, device=dev)
     if out_host is None:
         out_host = torch.empty(P, dtype=devbuf.dtype, pin_memory=True)
     chunks = column_chunks(P)
+    parts = [] if sums is not None else None
     for c, (c0, c1) in enumerate(chunks):
         if ready is not None:
             compute.wait_event(ready[c])
-        reduce_packed(devbuf[:, c0:c1] if len(chunks) > 1 else devbuf, w_dev, c1 - c0, out_dev[c0:c1])
+        reduce_rows(devbuf[:, c0:c1] if len(chunks) > 1 else devbuf, w_dev, c1 - c0, out_dev[c0:c1], parts)
         d2h_stream.wait_stream(compute)
         _fetch(out_dev[c0:c1], out_host[c0:c1], d2h_stream)
+    if parts:
+        total = parts[0]
+        for s in parts[1:]:
+            total = total + s
+        sums[devbuf.dtype] = total
     return out_dev, out_host
 
 
@@ -522,8 +557,11 @@ class DeviceAggregator:
                     if w is None or w.K < K:
                         w = self._seg_weights = _Weights(K, torch.float32, self.device)
                     out_dev = torch.empty(g.P, dtype=torch.float32, device=dev)
-                    reduce_packed(rows, w.upload(weights, compute), g.P, out_dev)
+                    sums = []
+                    reduce_rows(rows, w.upload(weights, compute), g.P, out_dev, sums)
                     self._last["dev"][g.dtype] = (rows, out_dev)  # the clients' own rows: :291 / FPF read them
+                    if sums:
+                        self._last.setdefault("sumsq", {})[g.dtype] = sums[0]
                     self.arena_rounds += 1
                 elif g.dtype == torch.float32 and self.DEVICE_SEGMENTS:
                     out_dev = self._reduce_segments(g, ptrs, weights, compute)
@@ -534,8 +572,11 @@ class DeviceAggregator:
                     self._pack_on_device(table, g, ptrs, 0, st.dev, compute)
                     w_dev = st.upload_weights(weights, compute)
                     out_dev = torch.empty(g.P, dtype=g.dtype, device=dev)
-                    reduce_packed(st.dev[:K], w_dev, g.P, out_dev)
+                    sums = []
+                    reduce_rows(st.dev[:K], w_dev, g.P, out_dev, sums)
                     self._last["dev"][g.dtype] = (st.dev[:K], out_dev)
+                    if sums:
+                        self._last.setdefault("sumsq", {})[g.dtype] = sums[0]
                 results.update(table.unpack(g, out_dev))
         self.last_profile = {"pack_issue_ms": (time.perf_counter() - t0) * 1e3, "h2d_kernel_d2h_ms": 0.0}
         return results
@@ -656,10 +697,10 @@ class DeviceAggregator:
             compute.wait_stream(copy_s)
             t1 = time.perf_counter()
             outs = []
-            self._last = {"table": table, "K": K, "dev": {}}
+            self._last = {"table": table, "K": K, "dev": {}, "sumsq": {}}
             d2h = self._d2h_stream_for()
             for g, devbuf, w_dev in staged:
-                out_dev, out_host = reduce_and_fetch(devbuf, w_dev, g.P, d2h)
+                out_dev, out_host = reduce_and_fetch(devbuf, w_dev, g.P, d2h, sums=self._last["sumsq"])
                 outs.append((g, out_host))
                 self._last["dev"][g.dtype] = (devbuf, out_dev)
             # the D2H stream waited on the compute stream after every chunk's
@@ -716,9 +757,12 @@ class DeviceAggregator:
             parts = []  # (group dtype, [K] fp64 sums on the device, the group's averaged model)
             if cached:
                 table = last["table"]
+                fused = last.get("sumsq") or {}
                 for dt, (devbuf, out_dev) in devs.items():
                     P = table.groups[dt].P
-                    if devbuf is None:  # zero-copy round: read the clients' tensors where they lie
+                    if dt in fused:  # formed by the aggregate's own pass over the rows
+                        parts.append((dt, fused[dt], out_dev[:P]))
+                    elif devbuf is None:  # zero-copy round: read the clients' tensors where they lie
                         # the dict aliased to w_glob (client 0, :449) holds the average
                         # now; its own tensors stand in (its norm is overridden below)
                         dicts = [last["seg_keep0"] if sd is w_glob else sd for _, sd in w_locals]

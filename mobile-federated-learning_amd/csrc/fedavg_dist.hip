@@ -480,11 +480,14 @@ inline int64_t fused_lds_bytes(int64_t K, int S, bool db = false) {
   return b > kBlock * 8 ? b : kBlock * 8;
 }
 
-// Tile width for K rows (0 = K outside the fused range): 64 columns (256 B
-// per row segment) from K = 33, 128 up to 32 rows, 256 up to 16
+// Tile width for K rows (0 = K outside the fused range), single-buffered
+// with one thread group per row (scripts/fused_probe.py, profiles/r02/fused/):
+// 64 columns (256 B per row segment) above 64 rows -- 100 x 25M: 1.76 ms vs
+// 1.85 at 128 columns, 2.17 double-buffered; 128 up to 64 rows (64 x 10M:
+// 0.473 vs 0.497 ms); 256 up to 16 (10 x 1.2M: 16.7 vs 17.8 us)
 inline int fused_cols(int64_t K) {
   if (K < 1 || K > kFusedMaxK) return 0;
-  if (K > 32) return 64;
+  if (K > 64) return 64;
   return K > 16 ? 128 : 256;
 }
 

@@ -191,6 +191,7 @@ class RoundSession:
             return self._finish_device(K, weights, acc_dict)
         outs = []
         dev_state = {}
+        sums = {}
         t0 = time.perf_counter()
         with torch.cuda.device(self.dev):
             d2h = self.agg._d2h_stream_for()
@@ -201,7 +202,7 @@ class RoundSession:
                 w_dev = st.upload_weights(weights, self._compute)
                 out_dev, out_host = reduce_and_fetch(st.dev[:K], w_dev, g.P,
                                                      d2h, ready=self._ready[g.dtype],
-                                                     out_host=self._out_host.get(g.dtype))
+                                                     out_host=self._out_host.get(g.dtype), sums=sums)
                 outs.append((g, out_host))
                 dev_state[g.dtype] = (st.dev[:K], out_dev)
             t1 = time.perf_counter()
@@ -215,7 +216,7 @@ class RoundSession:
         # host-side phases of the finish (ms): issuing weights/reduce/D2H, waiting for them, unpacking
         self.finish_profile = {"issue_ms": (t1 - t0) * 1e3, "wait_ms": (t2 - t1) * 1e3,
                                "unpack_ms": (time.perf_counter() - t2) * 1e3}
-        return self._close(K, dev_state, acc_dict)
+        return self._close(K, dev_state, acc_dict, sums)
 
     def _finish_small(self, K, weights, acc_dict):
         """Rows already packed by add(): weights, one kernel, result copy, in one native call."""
@@ -240,27 +241,31 @@ class RoundSession:
     def _finish_device(self, K, weights, acc_dict):
         """Device-resident clients: the averaged model stays in HBM (device
         tensors, ordered on the current stream, no host round trip)."""
-        from .reduce import reduce_packed
+        from .aggregate import reduce_rows
 
         dev_state = {}
+        sums = {}
         with torch.cuda.device(self.dev):
             self._compute.wait_stream(self._copy)  # every client's packing kernel
             for g in self.table.groups.values():
                 st = self._staging[g.dtype]
                 w_dev = st.upload_weights(weights, self._compute)
                 out_dev = torch.empty(g.P, dtype=g.dtype, device=self.dev)
-                reduce_packed(st.dev[:K], w_dev, g.P, out_dev)
+                parts = []
+                reduce_rows(st.dev[:K], w_dev, g.P, out_dev, parts)
+                if parts:
+                    sums[g.dtype] = parts[0]
                 dev_state[g.dtype] = (st.dev[:K], out_dev)
                 for name, t in self.table.unpack(g, out_dev).items():
                     acc_dict[name] = t
-        return self._close(K, dev_state, acc_dict)
+        return self._close(K, dev_state, acc_dict, sums)
 
-    def _close(self, K, dev_state, acc_dict):
+    def _close(self, K, dev_state, acc_dict, sums=None):
         self._keepalive.clear()
         self.table.forget_tensors()
         # leave the round's device rows + averaged model for client_distances (:291)
         try:
-            self.agg._last = {"table": self.table, "K": K, "dev": dev_state,
+            self.agg._last = {"table": self.table, "K": K, "dev": dev_state, "sumsq": sums or {},
                               "refs": [weakref.ref(sd) for sd in self.dicts], "acc": weakref.ref(acc_dict)}
         except TypeError:
             self.agg._last = {}

@@ -120,3 +120,54 @@ def test_fused_nonfinite_rows():
     assert np.array_equal(got[~np.isnan(got)], exp[~np.isnan(exp)])
     ref = _sumsq_ref(x, out, P)
     assert torch.equal(torch.isnan(sumsq), torch.isnan(ref))
+
+
+def _host_round(K, shapes, seed):
+    g = torch.Generator().manual_seed(seed)
+    w_locals = []
+    for i in range(K):
+        sd = {}
+        for name, shp in shapes.items():
+            if name.endswith("num_batches_tracked"):
+                sd[name] = torch.tensor(10 + i, dtype=torch.int64)
+            else:
+                sd[name] = torch.randn(shp, generator=g) * 0.05
+        w_locals.append((int(torch.randint(1, 500, (1,), generator=g)), sd))
+    return w_locals
+
+
+@pytest.mark.parametrize("K", [1, 9, 100, 128, 129])
+def test_dropin_distances_from_the_fused_pass(K):
+    """aggregate (host state_dicts) leaves the fused :291 sums; client_distances
+    returns the reference's norms (torch.norm of the fp32 differences) from
+    them -- client 0 (aliased to w_glob, :449) gets 0.  K = 129 takes the
+    two-pass route and gives the same norms."""
+    import copy
+
+    shapes = {"conv.weight": (32, 3, 5, 5), "conv.bias": (32,), "bn.num_batches_tracked": (),
+              "fc.weight": (10, 3000), "fc.bias": (10,)}
+    w_locals = _host_round(K, shapes, K)
+    ref_locals = copy.deepcopy(w_locals)
+    agg = mfl_amd.DeviceAggregator(DEV)
+    agg.SMALL_ROUND_BYTES = 0  # the pipelined host path even for a few clients (small rounds: one native call)
+    w_glob = agg.aggregate(w_locals)
+    fused = agg._last.get("sumsq", {})
+    assert (torch.float32 in fused) == (K <= 128)
+    norms = agg.client_distances(w_locals, w_glob)
+    keys = list(shapes)
+    exp = []
+    for i, (_, sd) in enumerate(ref_locals):
+        if i == 0:
+            exp.append(0.0)
+            continue
+        d = torch.cat([(sd[k].reshape(-1) - w_glob[k].reshape(-1)).double() for k in keys])
+        exp.append(float(torch.sqrt((d * d).sum()).float()))
+    np.testing.assert_allclose(norms, np.array(exp), rtol=2e-7, atol=0)
+    # the same round through the two passes (rows re-read): same fp32 norms up to one ulp
+    agg2 = mfl_amd.DeviceAggregator(DEV)
+    w_glob2 = agg2.aggregate(copy.deepcopy(ref_locals))
+    agg2._last.pop("sumsq", None)
+    locals2 = copy.deepcopy(ref_locals)
+    locals2[0] = (locals2[0][0], w_glob2)
+    norms2 = agg2.client_distances(locals2, w_glob2)
+    np.testing.assert_allclose(norms, norms2, rtol=2e-7, atol=0)
