@@ -368,6 +368,20 @@ int fedavg_client_sqdist_segments_f32(const int64_t* client_ptrs, const int64_t*
                                       const int64_t* key_kind, int64_t n_keys, int64_t K, const float* glob,
                                       double* partials, int64_t partial_elems, double* sumsq, void* host_ws,
                                       void* dev_ws, int64_t ws_bytes, void* stream);
+/*
+ * Both in ONE pass over the clients' tensors (the fused tiles of
+ * fedavg_reduce_sqdist_f32 on the same key/pointer tables): `out` with the
+ * bits of fedavg_reduce_segments_f32, sumsq the :291 sums against that out.
+ * Needs 1 <= K <= 128 and every fp32 key's client tensors 16-B aligned
+ * (FEDAVG_EALIGN / FEDAVG_EINVAL otherwise: run the two calls above).
+ * partials : fedavg_reduce_sqdist_segments_partials(K) doubles.
+ */
+int64_t fedavg_reduce_sqdist_segments_partials(int64_t K);
+int fedavg_reduce_sqdist_segments_f32(const int64_t* client_ptrs, const int64_t* key_numel,
+                                      const int64_t* key_offset, const int64_t* key_kind, int64_t n_keys,
+                                      int64_t K, const float* weights, float* out, double* partials,
+                                      int64_t partial_elems, double* sumsq, void* host_ws, void* dev_ws,
+                                      int64_t ws_bytes, void* stream);
 
 #ifdef __cplusplus
 }

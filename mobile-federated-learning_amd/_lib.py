@@ -35,6 +35,9 @@ SIGNATURES = {
     "fedavg_reduce_segments_f32": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _c_i64, _vp]),
     "fedavg_client_sqdist_segments_f32": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_i64, _vp, _vp, _c_i64, _vp, _vp,
                                                    _vp, _c_i64, _vp]),
+    "fedavg_reduce_sqdist_segments_partials": (_c_i64, [_c_i64]),
+    "fedavg_reduce_sqdist_segments_f32": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_i64, _vp, _vp, _vp, _c_i64, _vp,
+                                                   _vp, _vp, _c_i64, _vp]),
     "fedavg_pack_rows_device": (_c_int, [_vp, _c_i64, _vp, _c_i64, _vp, _vp, _c_i64, _vp]),
     "fedavg_round_f32": (_c_int, [_vp, _c_i64, _vp, _vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _c_int,
                                   _vp]),

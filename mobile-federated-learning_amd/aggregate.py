@@ -449,6 +449,39 @@ class DeviceAggregator:
         self._table_ws_done.record(stream)
         return out_dev
 
+    def _reduce_sqdist_segments(self, g, ptrs, weights, stream):
+        """The zero-copy reduce and the round's :291 sums in one pass
+        (fedavg_reduce_sqdist_segments_f32) when the round qualifies (K <= 128,
+        fused distances on, every fp32 source 16-B aligned): ``(out, sumsq)``,
+        else None."""
+        import numpy as np
+
+        K = ptrs.shape[0]
+        if not FUSE_DISTANCES or K > FUSED_MAX_K:
+            return None
+        cptrs, numel, offset, kind = self._segment_tables(g, ptrs)
+        raw = (kind == 0) & (numel > 0)
+        if bool(np.any(cptrs[:, raw] & 15)):
+            return None
+        lib = _lib.load()
+        w = self._seg_weights
+        if w is None or w.K < K:
+            w = self._seg_weights = _Weights(K, torch.float32, self.device)
+        w_dev = w.upload(weights, stream)
+        out_dev = torch.empty(g.P, dtype=torch.float32, device=self.device)
+        partials = torch.empty(max(1, lib.fedavg_reduce_sqdist_segments_partials(K)), dtype=torch.float64,
+                               device=self.device)
+        sumsq = torch.empty(K, dtype=torch.float64, device=self.device)
+        host_ws, dev_ws = self._stage_ws(lib.fedavg_segments_workspace(K, len(numel)))
+        _lib.check(lib.fedavg_reduce_sqdist_segments_f32(cptrs.ctypes.data, numel.ctypes.data, offset.ctypes.data,
+                                                         kind.ctypes.data, len(numel), K, w_dev.data_ptr(),
+                                                         out_dev.data_ptr(), partials.data_ptr(), partials.numel(),
+                                                         sumsq.data_ptr(), host_ws.data_ptr(), dev_ws.data_ptr(),
+                                                         host_ws.numel(), stream.cuda_stream),
+                   "fedavg_reduce_sqdist_segments_f32")
+        self._table_ws_done.record(stream)
+        return out_dev, sumsq
+
     def _sqdist_segments(self, table: KeyTable, dicts, glob: torch.Tensor) -> torch.Tensor:
         """:291 sums of squares straight from device-resident clients' tensors."""
         lib = _lib.load()
@@ -564,7 +597,12 @@ class DeviceAggregator:
                         self._last.setdefault("sumsq", {})[g.dtype] = sums[0]
                     self.arena_rounds += 1
                 elif g.dtype == torch.float32 and self.DEVICE_SEGMENTS:
-                    out_dev = self._reduce_segments(g, ptrs, weights, compute)
+                    fused = self._reduce_sqdist_segments(g, ptrs, weights, compute)
+                    if fused is not None:
+                        out_dev, sums = fused
+                        self._last.setdefault("sumsq", {})[g.dtype] = sums
+                    else:
+                        out_dev = self._reduce_segments(g, ptrs, weights, compute)
                     self._last["dev"][g.dtype] = (None, out_dev)  # no rows: see materialize_rows
                     self._last["segments"] = True
                 else:

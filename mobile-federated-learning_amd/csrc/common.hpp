@@ -525,4 +525,88 @@ void launch_split_buf(const float* clients, int K, int64_t ld, int64_t P, const 
   }
 }
 
+// ---------------------------------------------------------------------------
+// Fused aggregate + :291 tiles (fedavg_dist.hip: [K, ld] rows;
+// fedavg_segments.hip: device-resident clients).  A workgroup stages a tile of
+// S columns x all K rows in LDS -- row r's 16-B slot j holds the row's slice
+// j ^ (r & 7) (XOR swizzle applied to the per-lane GLOBAL address, LDS-DMA
+// keeps LDS linear) -- then:
+//   fused_average : one thread per column, the reference's sequential chain
+//                   over the K rows (:455-457, the bits of fedavg_reduce_f32),
+//                   stored to `out` and to LDS (`gs`);
+//   fused_squares : thread t owns row t % K and slices t / K, t / K + q, ...
+//                   (q = 256 / K threads per row): fl32(x - g)^2 in fp64 into
+//                   four register chains that live across all tiles;
+//   fused_finish  : the q threads of a row added in a fixed order ->
+//                   partials[row][workgroup].
+// ---------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void* fused_lds_t;
+typedef const __attribute__((address_space(1))) void* fused_gbl_t;
+
+// Barriers without the compiler's vmcnt(0) drain (a plain __syncthreads()
+// would also wait for LDS-DMA loads meant to stay in flight across it).
+__device__ __forceinline__ void barrier_lds() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+__device__ __forceinline__ void barrier_loads() {
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// LDS float index of (row, column) in a swizzled tile of S columns
+template <int S>
+__device__ __forceinline__ int fused_at(int row, int col) {
+  return row * S + ((((col >> 2) ^ (row & 7))) << 2) + (col & 3);
+}
+
+template <int S>
+__device__ __forceinline__ void fused_average(const float* tile, float* gs, int K, const float* __restrict__ W,
+                                              int ncols, float* __restrict__ out) {
+  if (threadIdx.x < S) {
+    const int c = threadIdx.x;
+    float a = tile[fused_at<S>(0, c)] * W[0];
+    for (int k = 1; k < K; ++k) {
+      const float term = tile[fused_at<S>(k, c)] * W[k];
+      a = a + term;
+    }
+    gs[c] = a;
+    if (c < ncols) out[c] = a;
+  }
+}
+
+template <int S>
+__device__ __forceinline__ void fused_squares(const float* tile, const float* gs, int K, int ncols, double (&acc)[4]) {
+  constexpr int V = S / 4;
+  const int q = kBlock / K;
+  const int my_row = threadIdx.x % K;
+  const int my_sub = threadIdx.x / K;
+  if (my_sub >= q) return;
+  const int swz = my_row & 7;
+  const f32x4* x4 = reinterpret_cast<const f32x4*>(tile) + my_row * V;
+  for (int c = my_sub; c < V; c += q) {
+    const f32x4 x = x4[c ^ swz];
+    const f32x4 g = reinterpret_cast<const f32x4*>(gs)[c];
+    const f32x4 d = x - g;        // fp32 difference, as the reference forms it
+    const int n = ncols - 4 * c;  // valid columns of this slice (select, not multiply: padding may hold NaN/inf)
+    if (n > 0) {
+      const double dx = d.x, dy = n > 1 ? d.y : 0.f, dz = n > 2 ? d.z : 0.f, dw = n > 3 ? d.w : 0.f;
+      acc[0] = __builtin_fma(dx, dx, acc[0]);
+      acc[1] = __builtin_fma(dy, dy, acc[1]);
+      acc[2] = __builtin_fma(dz, dz, acc[2]);
+      acc[3] = __builtin_fma(dw, dw, acc[3]);
+    }
+  }
+}
+
+// `lds` holds >= 256 doubles and no tile is in use or in flight any more
+__device__ __forceinline__ void fused_finish(float* lds, const double (&acc)[4], int K, double* __restrict__ partials) {
+  const int q = kBlock / K;
+  barrier_loads();
+  double* red = reinterpret_cast<double*>(lds);
+  red[threadIdx.x] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  barrier_lds();
+  if (threadIdx.x < K) {
+    double s = red[threadIdx.x];
+    for (int u = 1; u < q; ++u) s += red[threadIdx.x + u * K];
+    partials[static_cast<int64_t>(threadIdx.x) * gridDim.x + blockIdx.x] = s;
+  }
+}
+
 }  // namespace fedavg_impl

@@ -324,8 +324,6 @@ __global__ __launch_bounds__(kBlock) void client_sqdist_finalize_kernel(const do
 // partials[k][workgroup], then the fixed-order finalize: deterministic.
 // K <= 128 (q >= 2).
 // ---------------------------------------------------------------------------
-typedef __attribute__((address_space(3))) void* lds_ptr_t;
-typedef const __attribute__((address_space(1))) void* gbl_ptr_t;
 
 // rows -> LDS for the tile at column c0: slot i = row * V + j (LDS byte
 // 16 i from `buf`) holds slice j ^ (row & 7) of the row segment
@@ -342,17 +340,11 @@ __device__ __forceinline__ void fused_load_tile(const float* __restrict__ X, int
     const int row = i / V;
     const int c = (i % V) ^ (row & 7);
     if (i < nload && c < nv4)
-      __builtin_amdgcn_global_load_lds((gbl_ptr_t)(X + static_cast<int64_t>(row) * ld + c0 + 4 * c),
-                                       (lds_ptr_t)(buf + 4 * i0), 16, 0, 2 /* nt */);
+      __builtin_amdgcn_global_load_lds((fused_gbl_t)(X + static_cast<int64_t>(row) * ld + c0 + 4 * c),
+                                       (fused_lds_t)(buf + 4 * i0), 16, 0, 2 /* nt */);
   }
 }
 
-// Barriers without the compiler's vmcnt(0) drain: a plain __syncthreads()
-// would also wait for the NEXT tile's LDS-DMA loads in flight.
-__device__ __forceinline__ void barrier_lds() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-__device__ __forceinline__ void barrier_loads() {
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
 
 template <int S, bool DB, int RW = 0, bool LOADS_ONLY = false>
 __global__ __launch_bounds__(kBlock) void reduce_sqdist_f32_kernel(const float* __restrict__ X, int K, int64_t ld,
@@ -363,13 +355,8 @@ __global__ __launch_bounds__(kBlock) void reduce_sqdist_f32_kernel(const float* 
   static_assert(S == 64 || S == 128 || S == 256, "tile widths: 64, 128 or 256 columns");
   // one tile buffer [K][S] (swizzled slots) -- two when DB -- then the tile's average [S]
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  constexpr int V = S / 4;  // 16-B slots per row segment
   const int tile_floats = K * S;
   float* gs = lds + (DB ? 2 : 1) * tile_floats;
-  const int q = kBlock / K;            // threads per row in phase 3
-  const int my_row = threadIdx.x % K;  // phase 3: this thread's row ...
-  const int my_sub = threadIdx.x / K;  // ... and first slice (active while < q)
-  const int my_swz = my_row & 7;
   double acc[4] = {0.0, 0.0, 0.0, 0.0};  // one chain per lane of a 16-B slice
   double acc_rows[RW > 0 ? RW : 1];      // RW > 0: one accumulator per row of this wave
 #pragma unroll
@@ -394,18 +381,7 @@ __global__ __launch_bounds__(kBlock) void reduce_sqdist_f32_kernel(const float* 
       barrier_lds();
       continue;
     }
-    // 2. the average of each column, in the reference's order (:455-457)
-    if (threadIdx.x < S) {
-      const int c = threadIdx.x;
-      const int j = c >> 2, e = c & 3;
-      float a = tile[j * 4 + e] * W[0];
-      for (int k = 1; k < K; ++k) {
-        const float term = tile[k * S + ((j ^ (k & 7)) << 2) + e] * W[k];
-        a = a + term;
-      }
-      gs[c] = a;
-      if (c < ncols) out[c0 + c] = a;
-    }
+    fused_average<S>(tile, gs, K, W, ncols, out + c0);  // 2. the average of each column
     barrier_lds();
     if constexpr (RW > 0) {
       // 3'. rows wave + 4r (r < RW), S / 64 adjacent columns per lane, one
@@ -426,23 +402,7 @@ __global__ __launch_bounds__(kBlock) void reduce_sqdist_f32_kernel(const float* 
         }
       }
     } else {
-      // 3. :291 squares of this thread's row over its slices
-      if (my_sub < q) {
-        const f32x4* my_x = reinterpret_cast<const f32x4*>(tile) + my_row * V;
-        for (int c = my_sub; c < V; c += q) {
-          const f32x4 x = my_x[c ^ my_swz];
-          const f32x4 g = reinterpret_cast<const f32x4*>(gs)[c];
-          const f32x4 d = x - g;  // fp32 difference, as the reference forms it
-          const int n = ncols - 4 * c;  // valid columns of this slice (select, not multiply: padding may hold NaN/inf)
-          if (n > 0) {
-            const double dx = d.x, dy = n > 1 ? d.y : 0.f, dz = n > 2 ? d.z : 0.f, dw = n > 3 ? d.w : 0.f;
-            acc[0] = __builtin_fma(dx, dx, acc[0]);
-            acc[1] = __builtin_fma(dy, dy, acc[1]);
-            acc[2] = __builtin_fma(dz, dz, acc[2]);
-            acc[3] = __builtin_fma(dw, dw, acc[3]);
-          }
-        }
-      }
+      fused_squares<S>(tile, gs, K, ncols, acc);  // 3. :291 squares of this thread's row over its slices
     }
     if constexpr (DB)
       cur ^= 1;
@@ -460,16 +420,7 @@ __global__ __launch_bounds__(kBlock) void reduce_sqdist_f32_kernel(const float* 
     }
     return;
   }
-  // the q accumulators of each row, added in a fixed order
-  barrier_loads();
-  double* red = reinterpret_cast<double*>(lds);
-  red[threadIdx.x] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-  barrier_lds();
-  if (threadIdx.x < K) {
-    double s = red[threadIdx.x];
-    for (int u = 1; u < q; ++u) s += red[threadIdx.x + u * K];
-    partials[static_cast<int64_t>(threadIdx.x) * gridDim.x + blockIdx.x] = s;
-  }
+  fused_finish(lds, acc, K, partials);
 }
 
 constexpr int kFusedMaxK = kBlock / 2;  // two threads per row at least: K <= 128

@@ -383,6 +383,126 @@ __global__ __launch_bounds__(kBlock) void segments_finalize_kernel(const double*
   if (threadIdx.x == 0) sumsq[k] = red[0];
 }
 
+// Aggregate + :291 in ONE pass over device-resident clients' own tensors
+// (fedavg_dist.hip's fused tiles on the key/pointer tables): a unit is S
+// columns of one key x all K clients, staged in LDS -- full 16-B slices of
+// fp32 keys by LDS-DMA straight from each client's tensor (16-B aligned
+// sources: the host checks), the key's ragged last slice and integer/bool
+// keys element by element (converted like the packers) -- then the
+// reference's sequential average of each column and the per-row squares.
+// The running workgroup keeps its rows' client addresses of the current key
+// in registers (reloaded at a key change only).  K <= 128.
+constexpr int kSegFusedRowsPerThread = 8;  // ceil(K * S / 4 / 256) slots per thread at K <= 128, S <= 64 ... 256
+
+template <int S>
+__global__ __launch_bounds__(kBlock) void reduce_sqdist_segments_f32_kernel(const SegKey* __restrict__ keys,
+                                                                            const int64_t* __restrict__ ptrs,
+                                                                            int64_t n_keys, int64_t units, int K,
+                                                                            const float* __restrict__ W,
+                                                                            float* __restrict__ out,
+                                                                            double* __restrict__ partials) {
+  constexpr int V = S / 4;
+  extern __shared__ __attribute__((aligned(16))) float lds[];  // [K][S] swizzled tile, then the average [S]
+  float* tile = lds;
+  float* gs = lds + K * S;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nload = K * V;
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  int64_t cur_key = -1;
+  int64_t src[kSegFusedRowsPerThread];  // client address of the row of this thread's m-th load slot
+  for (int64_t u = blockIdx.x; u < units; u += gridDim.x) {
+    const int64_t j = find_key(keys, n_keys, u);
+    const SegKey key = keys[j];
+    const int64_t c0 = (u - key.unit_start) * S;
+    const int n = key.numel - c0 < S ? static_cast<int>(key.numel - c0) : S;
+    const int64_t* P = ptrs + j * K;
+    if (key.kind == kRaw) {
+      if (j != cur_key) {
+        cur_key = j;
+#pragma unroll
+        for (int m = 0; m < kSegFusedRowsPerThread; ++m) {
+          const int i = wave * 64 + m * kBlock + lane;
+          src[m] = i < nload ? P[i / V] : 0;
+        }
+      }
+      const int nfull = n >> 2;  // whole 16-B slices of this unit
+#pragma unroll
+      for (int m = 0; m < kSegFusedRowsPerThread; ++m) {
+        const int i0 = wave * 64 + m * kBlock;
+        const int i = i0 + lane;
+        const int row = i / V;
+        const int c = (i % V) ^ (row & 7);
+        if (i0 < nload && i < nload && c < nfull)
+          __builtin_amdgcn_global_load_lds((fused_gbl_t)(reinterpret_cast<const float*>(src[m]) + c0 + 4 * c),
+                                           (fused_lds_t)(tile + 4 * i0), 16, 0, 2 /* nt */);
+      }
+      if (n & 3) {  // the key's ragged last slice, element by element (never past the tensor's end)
+        for (int row = threadIdx.x; row < K; row += kBlock) {
+          const gptr<float> x = to_global<float>(reinterpret_cast<const void*>(P[row]));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int col = 4 * nfull + e;
+            tile[fused_at<S>(row, col)] = col < n ? x[c0 + col] : 0.f;
+          }
+        }
+      }
+    } else {  // integer / bool key: converted element by element, as the packers do
+      for (int idx = threadIdx.x; idx < K * S; idx += kBlock) {
+        const int row = idx / S, col = idx % S;
+        tile[fused_at<S>(row, col)] = col < n ? load_cvt(reinterpret_cast<const void*>(P[row]), key.kind, c0 + col) : 0.f;
+      }
+    }
+    barrier_loads();
+    fused_average<S>(tile, gs, K, W, n, out + key.out_offset + c0);
+    barrier_lds();
+    fused_squares<S>(tile, gs, K, n, acc);
+    barrier_lds();  // the tile is read out before the next one lands
+  }
+  fused_finish(lds, acc, K, partials);
+}
+
+constexpr int kSegFusedMaxK = kBlock / 2;
+
+// tile width: as fedavg_dist.hip's fused_cols (64 above 64 clients, 128 up to
+// 64, 256 up to 16); the widest tile keeps <= 8 load slots per thread
+inline int seg_fused_cols(int64_t K) { return K > 64 ? 64 : (K > 16 ? 128 : 256); }
+
+inline int64_t seg_fused_lds_bytes(int64_t K, int S) {
+  const int64_t b = (K + 1) * S * 4;
+  return b > kBlock * 8 ? b : kBlock * 8;
+}
+
+template <int S>
+int seg_fused_per_cu(int64_t K) {
+  static std::mutex mu;
+  static std::map<std::pair<int, int64_t>, int> cache;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find({dev, K});
+  if (it != cache.end()) return it->second;
+  const auto kern = reduce_sqdist_segments_f32_kernel<S>;
+  const int64_t lds = seg_fused_lds_bytes(K, S);
+  int per_cu = 0;
+  if (lds > 65536 && hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         static_cast<int>(lds)) != hipSuccess) {
+    (void)hipGetLastError();
+  } else if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kBlock, static_cast<size_t>(lds)) !=
+             hipSuccess) {
+    (void)hipGetLastError();
+    per_cu = 0;
+  }
+  cache[{dev, K}] = per_cu;
+  return per_cu;
+}
+
+template <int S>
+int64_t seg_fused_grid(int64_t K, int64_t units) {
+  const int64_t g = static_cast<int64_t>(seg_fused_per_cu<S>(K)) * cu_count();
+  return units < g ? units : g;
+}
+
 int64_t units_of(const int64_t* numel, int64_t n_keys, int64_t span = kSegSpan) {
   int64_t units = 0;
   for (int64_t j = 0; j < n_keys; ++j) units += (numel[j] + span - 1) / span;
@@ -561,6 +681,67 @@ int fedavg_client_sqdist_segments_f32(const int64_t* client_ptrs, const int64_t*
   int rc = launch_status(what);
   if (rc) return rc;
   hipLaunchKernelGGL(segments_finalize_kernel, dim3(static_cast<unsigned>(K)), dim3(kBlock), 0, s, partials, nparts,
+                     sumsq);
+  return launch_status(what);
+}
+
+// Aggregate + :291 sums in one pass over device-resident clients (K <= 128,
+// every fp32 key's client tensors 16-B aligned): out as
+// fedavg_reduce_segments_f32, sumsq as fedavg_client_sqdist_segments_f32 on
+// that out.  partials : fedavg_reduce_sqdist_segments_partials(K) doubles.
+int64_t fedavg_reduce_sqdist_segments_partials(int64_t K) {
+  if (K <= 0 || K > kSegFusedMaxK) return 0;
+  const int S = seg_fused_cols(K);
+  const int per_cu = S == 64 ? seg_fused_per_cu<64>(K) : (S == 128 ? seg_fused_per_cu<128>(K) : seg_fused_per_cu<256>(K));
+  return K * static_cast<int64_t>(per_cu > 0 ? per_cu : 1) * cu_count();
+}
+
+int fedavg_reduce_sqdist_segments_f32(const int64_t* client_ptrs, const int64_t* key_numel, const int64_t* key_offset,
+                                      const int64_t* key_kind, int64_t n_keys, int64_t K, const float* weights,
+                                      float* out, double* partials, int64_t partial_elems, double* sumsq,
+                                      void* host_ws, void* dev_ws, int64_t ws_bytes, void* stream) {
+  const char* what = "fedavg_reduce_sqdist_segments_f32";
+  if (!weights || !out || !partials || !sumsq) return set_error(FEDAVG_EINVAL, "%s: null weights/out/partials/sumsq", what);
+  if (K < 1 || K > kSegFusedMaxK)
+    return set_error(FEDAVG_EINVAL, "%s: K = %lld outside 1..%d (use the two passes)", what, (long long)K, kSegFusedMaxK);
+  if (!is_device_memory(out) || !is_device_memory(partials) || !is_device_memory(sumsq))
+    return set_error(FEDAVG_EINVAL, "%s: out, partials and sumsq must be device memory", what);
+  if (client_ptrs && key_kind && key_numel)
+    for (int64_t j = 0; j < n_keys; ++j)
+      for (int64_t k = 0; k < K && key_kind[j] == kRaw && key_numel[j] > 0; ++k)
+        if ((client_ptrs[k * n_keys + j] & 15) != 0)
+          return set_error(FEDAVG_EALIGN, "%s: client %lld key %lld is not 16-B aligned (use the two passes)", what,
+                           (long long)k, (long long)j);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int S = seg_fused_cols(K);
+  const int64_t units = stage_tables(what, client_ptrs, key_numel, key_offset, key_kind, n_keys, K, host_ws, dev_ws,
+                                     ws_bytes, s, S);
+  if (units < 0) return static_cast<int>(units);
+  if (units == 0) {
+    const hipError_t e = hipMemsetAsync(sumsq, 0, static_cast<size_t>(K) * sizeof(double), s);
+    return e == hipSuccess ? FEDAVG_OK : set_error(-static_cast<int>(e), "%s: hipMemsetAsync failed", what);
+  }
+  const auto* keys = static_cast<const SegKey*>(dev_ws);
+  const auto* tptrs = reinterpret_cast<const int64_t*>(static_cast<const char*>(dev_ws) +
+                                                       n_keys * static_cast<int64_t>(sizeof(SegKey)));
+  int64_t grid = 0;
+#define FEDAVG_SEG_FUSED(C)                                                                                        \
+  if (S == C) {                                                                                                    \
+    if (seg_fused_per_cu<C>(K) <= 0) return set_error(FEDAVG_EMODE, "%s: tile does not fit LDS", what);            \
+    grid = seg_fused_grid<C>(K, units);                                                                            \
+    if (partial_elems < K * grid)                                                                                  \
+      return set_error(FEDAVG_EINVAL, "%s: partials need %lld doubles", what, (long long)(K * grid));              \
+    hipLaunchKernelGGL((reduce_sqdist_segments_f32_kernel<C>), dim3(static_cast<unsigned>(grid)), dim3(kBlock),      \
+                       static_cast<unsigned>(seg_fused_lds_bytes(K, C)), s, keys, tptrs, n_keys, units,             \
+                       static_cast<int>(K), weights, out, partials);                                               \
+  }
+  FEDAVG_SEG_FUSED(64)
+  FEDAVG_SEG_FUSED(128)
+  FEDAVG_SEG_FUSED(256)
+#undef FEDAVG_SEG_FUSED
+  int rc = launch_status(what);
+  if (rc) return rc;
+  hipLaunchKernelGGL(segments_finalize_kernel, dim3(static_cast<unsigned>(K)), dim3(kBlock), 0, s, partials, grid,
                      sumsq);
   return launch_status(what);
 }

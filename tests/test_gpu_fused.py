@@ -171,3 +171,51 @@ def test_dropin_distances_from_the_fused_pass(K):
     locals2[0] = (locals2[0][0], w_glob2)
     norms2 = agg2.client_distances(locals2, w_glob2)
     np.testing.assert_allclose(norms, norms2, rtol=2e-7, atol=0)
+
+
+def _device_round(K, shapes, seed, misalign=False):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    w_locals = []
+    for i in range(K):
+        sd = {}
+        for name, shp in shapes.items():
+            if name.endswith("num_batches_tracked"):
+                sd[name] = torch.tensor(10 + i, dtype=torch.int64, device=DEV)
+            else:
+                t = torch.randn(shp, generator=g, device=DEV) * 0.05
+                if misalign and i == K - 1 and name == "fc.weight":
+                    buf = torch.empty(t.numel() + 1, device=DEV)  # a view one float into its storage
+                    buf[1:].copy_(t.reshape(-1))
+                    t = buf[1:].view(shp)
+                sd[name] = t
+        w_locals.append((int(torch.randint(1, 500, (1,), generator=torch.Generator().manual_seed(seed + i))), sd))
+    return w_locals
+
+
+@pytest.mark.parametrize("K,misalign", [(1, False), (7, False), (100, False), (128, False), (12, True), (129, False)])
+def test_device_round_fused_segments(K, misalign):
+    """Device-resident clients (separate tensors, an int64 buffer, ragged key
+    sizes): the zero-copy round's average keeps the oracle's bits and the
+    fused :291 sums give the reference's norms.  A misaligned client tensor
+    or K > 128 takes the two-pass route with the same results."""
+    import copy
+
+    shapes = {"conv.weight": (16, 3, 3, 3), "conv.bias": (16,), "bn.num_batches_tracked": (),
+              "fc.weight": (10, 3001), "fc.bias": (10,), "head.weight": (257,)}
+    w_locals = _device_round(K, shapes, 5 * K + misalign, misalign)
+    host_locals = [(n, {k: v.cpu() for k, v in sd.items()}) for n, sd in w_locals]
+    ref = O.aggregate_torch(copy.deepcopy(host_locals))
+    agg = mfl_amd.DeviceAggregator(DEV)
+    w_glob = agg.aggregate(w_locals)
+    for k in shapes:
+        got, exp = w_glob[k].cpu(), ref[k]
+        assert got.dtype == exp.dtype, k
+        assert torch.equal(got.reshape(-1).view(torch.int32), exp.reshape(-1).view(torch.int32)), k
+    assert (torch.float32 in agg._last.get("sumsq", {})) == (K <= 128 and not misalign)
+    norms = agg.client_distances(w_locals, w_glob)
+    keys = list(shapes)
+    # :291's fp32 differences (int64 buffers promote to fp32), squared and summed exactly
+    exp = [0.0] + [float(torch.sqrt(torch.cat([(sd[k].reshape(-1).float() - ref[k].reshape(-1)).double()
+                                               for k in keys]).pow(2).sum()).float())
+                   for _, sd in host_locals[1:]]
+    np.testing.assert_allclose(norms, np.array(exp), rtol=2e-7, atol=0)
