@@ -42,7 +42,9 @@ def counter_means(paths, kernel_regex="reduce_"):
     for p in paths:
         for row in read_csv(p):
             name = row.get("Kernel_Name", "")
-            if kernel_regex not in name:
+            # the reduce kernels only: bench.py's round_with_distances side measurement
+            # also runs the fused reduce_sqdist and the :291 kernels
+            if kernel_regex not in name or "sqdist" in name:
                 continue
             vals[(name, row["Counter_Name"])].append(float(row["Counter_Value"]))
             meta[name] = {k: row.get(k) for k in ("Grid_Size", "Workgroup_Size", "VGPR_Count", "SGPR_Count",
@@ -70,7 +72,7 @@ def main():
         shutil.copy(stats[0], prof / f"{tag}_kernel_stats.csv")
         rows = read_csv(stats[0])
         for r in rows:
-            if "reduce_" in r.get("Name", ""):
+            if "reduce_" in r.get("Name", "") and "sqdist" not in r.get("Name", ""):
                 print(f"[stats] {r['Name'][:90]} calls={r['Calls']} avg={float(r['AverageNs'])/1e3:.1f} us")
 
     fetch, meta, nf = counter_means(find(base / "prof_fetch", "counter_collection.csv"))
