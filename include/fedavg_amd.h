@@ -121,8 +121,8 @@ int fedavg_client_sqdist_f32(const float* clients, int64_t K, int64_t P, int64_t
  *   sumsq : fedavg_client_sqdist_f32(clients, ..., out, ...)'s sums, the
  *           same rounding rules (fp32 difference, fp64 squares and sum,
  *           fixed order; not necessarily the same summation tree).
- * K <= 128 with 16-B aligned rows and ld % 4 == 0 runs the fused kernel
- * (K x 64-256 columns staged in LDS per workgroup); anything else runs the two
+ * K <= 300 with 16-B aligned rows and ld % 4 == 0 runs the fused kernel
+ * (K x 32-256 columns staged in LDS per workgroup); anything else runs the two
  * passes back to back.  workspace : fedavg_reduce_sqdist_workspace(K, P)
  * doubles of device scratch.  P == 0 writes sumsq = 0.
  */

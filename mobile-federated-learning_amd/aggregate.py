@@ -159,7 +159,8 @@ def column_chunks(P: int) -> List[Tuple[int, int]]:
 # The reference runs :291 after every aggregate with clients (fedavg_trainer.py
 # :289-291), so the drop-in fuses by default; FEDAVG_FUSE_DISTANCES=0 keeps
 # the reduce alone.
-FUSED_MAX_K = 128
+FUSED_MAX_K = 300  # rows kernel (fedavg_reduce_sqdist_f32; more clients: the two passes are faster)
+FUSED_SEGMENTS_MAX_K = 128  # device-resident clients' own tensors (fedavg_reduce_sqdist_segments_f32)
 FUSE_DISTANCES = os.environ.get("FEDAVG_FUSE_DISTANCES", "1") != "0"
 
 
@@ -457,7 +458,7 @@ class DeviceAggregator:
         import numpy as np
 
         K = ptrs.shape[0]
-        if not FUSE_DISTANCES or K > FUSED_MAX_K:
+        if not FUSE_DISTANCES or K > FUSED_SEGMENTS_MAX_K:
             return None
         cptrs, numel, offset, kind = self._segment_tables(g, ptrs)
         raw = (kind == 0) & (numel > 0)

@@ -535,8 +535,9 @@ void launch_split_buf(const float* clients, int K, int64_t ld, int64_t P, const 
 //                   over the K rows (:455-457, the bits of fedavg_reduce_f32),
 //                   stored to `out` and to LDS (`gs`);
 //   fused_squares : thread t owns row t % K and slices t / K, t / K + q, ...
-//                   (q = 256 / K threads per row): fl32(x - g)^2 in fp64 into
-//                   four register chains that live across all tiles;
+//                   (q = 256 / K threads per row; above 256 rows, rows t,
+//                   t + 256, ... whole): fl32(x - g)^2 in fp64 into four
+//                   register chains per row that live across all tiles;
 //   fused_finish  : the q threads of a row added in a fixed order ->
 //                   partials[row][workgroup].
 // ---------------------------------------------------------------------------
@@ -571,41 +572,68 @@ __device__ __forceinline__ void fused_average(const float* tile, float* gs, int 
   }
 }
 
-template <int S>
-__device__ __forceinline__ void fused_squares(const float* tile, const float* gs, int K, int ncols, double (&acc)[4]) {
+// RM = 1: K <= 256, thread t owns row t % K and slices t / K, t / K + q, ...
+// (q = 256 / K); RM > 1: 256 < K <= 256 RM, thread t owns rows t, t + 256, ...
+// and every slice of them.  acc[m][0..3]: four fp64 chains per owned row.
+template <int S, int RM = 1>
+__device__ __forceinline__ void fused_squares(const float* tile, const float* gs, int K, int ncols,
+                                              double (&acc)[RM][4]) {
   constexpr int V = S / 4;
-  const int q = kBlock / K;
-  const int my_row = threadIdx.x % K;
-  const int my_sub = threadIdx.x / K;
-  if (my_sub >= q) return;
-  const int swz = my_row & 7;
-  const f32x4* x4 = reinterpret_cast<const f32x4*>(tile) + my_row * V;
-  for (int c = my_sub; c < V; c += q) {
-    const f32x4 x = x4[c ^ swz];
+  const auto sq = [&](double (&a)[4], f32x4 x, int c) {
     const f32x4 g = reinterpret_cast<const f32x4*>(gs)[c];
     const f32x4 d = x - g;        // fp32 difference, as the reference forms it
     const int n = ncols - 4 * c;  // valid columns of this slice (select, not multiply: padding may hold NaN/inf)
     if (n > 0) {
       const double dx = d.x, dy = n > 1 ? d.y : 0.f, dz = n > 2 ? d.z : 0.f, dw = n > 3 ? d.w : 0.f;
-      acc[0] = __builtin_fma(dx, dx, acc[0]);
-      acc[1] = __builtin_fma(dy, dy, acc[1]);
-      acc[2] = __builtin_fma(dz, dz, acc[2]);
-      acc[3] = __builtin_fma(dw, dw, acc[3]);
+      a[0] = __builtin_fma(dx, dx, a[0]);
+      a[1] = __builtin_fma(dy, dy, a[1]);
+      a[2] = __builtin_fma(dz, dz, a[2]);
+      a[3] = __builtin_fma(dw, dw, a[3]);
+    }
+  };
+  if constexpr (RM == 1) {
+    const int q = kBlock / K;
+    const int my_row = threadIdx.x % K;
+    const int my_sub = threadIdx.x / K;
+    if (my_sub >= q) return;
+    const int swz = my_row & 7;
+    const f32x4* x4 = reinterpret_cast<const f32x4*>(tile) + my_row * V;
+    for (int c = my_sub; c < V; c += q) sq(acc[0], x4[c ^ swz], c);
+  } else {
+#pragma unroll
+    for (int m = 0; m < RM; ++m) {
+      const int row = threadIdx.x + m * kBlock;
+      if (row < K) {
+        const int swz = row & 7;
+        const f32x4* x4 = reinterpret_cast<const f32x4*>(tile) + row * V;
+        for (int c = 0; c < V; ++c) sq(acc[m], x4[c ^ swz], c);
+      }
     }
   }
 }
 
 // `lds` holds >= 256 doubles and no tile is in use or in flight any more
-__device__ __forceinline__ void fused_finish(float* lds, const double (&acc)[4], int K, double* __restrict__ partials) {
-  const int q = kBlock / K;
+template <int RM = 1>
+__device__ __forceinline__ void fused_finish(float* lds, const double (&acc)[RM][4], int K,
+                                             double* __restrict__ partials) {
   barrier_loads();
-  double* red = reinterpret_cast<double*>(lds);
-  red[threadIdx.x] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-  barrier_lds();
-  if (threadIdx.x < K) {
-    double s = red[threadIdx.x];
-    for (int u = 1; u < q; ++u) s += red[threadIdx.x + u * K];
-    partials[static_cast<int64_t>(threadIdx.x) * gridDim.x + blockIdx.x] = s;
+  if constexpr (RM == 1) {
+    const int q = kBlock / K;
+    double* red = reinterpret_cast<double*>(lds);
+    red[threadIdx.x] = (acc[0][0] + acc[0][1]) + (acc[0][2] + acc[0][3]);
+    barrier_lds();
+    if (threadIdx.x < K) {
+      double s = red[threadIdx.x];
+      for (int u = 1; u < q; ++u) s += red[threadIdx.x + u * K];
+      partials[static_cast<int64_t>(threadIdx.x) * gridDim.x + blockIdx.x] = s;
+    }
+  } else {
+#pragma unroll
+    for (int m = 0; m < RM; ++m) {
+      const int row = threadIdx.x + m * kBlock;
+      if (row < K)
+        partials[static_cast<int64_t>(row) * gridDim.x + blockIdx.x] = (acc[m][0] + acc[m][1]) + (acc[m][2] + acc[m][3]);
+    }
   }
 }
 

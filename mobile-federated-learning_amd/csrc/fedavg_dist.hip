@@ -346,18 +346,20 @@ __device__ __forceinline__ void fused_load_tile(const float* __restrict__ X, int
 }
 
 
-template <int S, bool DB, int RW = 0, bool LOADS_ONLY = false>
+template <int S, bool DB, int RW = 0, bool LOADS_ONLY = false, int RM = 1>
 __global__ __launch_bounds__(kBlock) void reduce_sqdist_f32_kernel(const float* __restrict__ X, int K, int64_t ld,
                                                                    int64_t P, int64_t ntiles,
                                                                    const float* __restrict__ W,
                                                                    float* __restrict__ out,
                                                                    double* __restrict__ partials) {
-  static_assert(S == 64 || S == 128 || S == 256, "tile widths: 64, 128 or 256 columns");
+  static_assert(S == 32 || S == 64 || S == 128 || S == 256, "tile widths: 32, 64, 128 or 256 columns");
   // one tile buffer [K][S] (swizzled slots) -- two when DB -- then the tile's average [S]
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tile_floats = K * S;
   float* gs = lds + (DB ? 2 : 1) * tile_floats;
-  double acc[4] = {0.0, 0.0, 0.0, 0.0};  // one chain per lane of a 16-B slice
+  double acc[RM][4];  // four chains per row this thread owns (one per lane of a 16-B slice)
+#pragma unroll
+  for (int m = 0; m < RM; ++m) acc[m][0] = acc[m][1] = acc[m][2] = acc[m][3] = 0.0;
   double acc_rows[RW > 0 ? RW : 1];      // RW > 0: one accumulator per row of this wave
 #pragma unroll
   for (int r = 0; r < (RW > 0 ? RW : 1); ++r) acc_rows[r] = 0.0;
@@ -402,7 +404,7 @@ __global__ __launch_bounds__(kBlock) void reduce_sqdist_f32_kernel(const float* 
         }
       }
     } else {
-      fused_squares<S>(tile, gs, K, ncols, acc);  // 3. :291 squares of this thread's row over its slices
+      fused_squares<S, RM>(tile, gs, K, ncols, acc);  // 3. :291 squares of this thread's rows over its slices
     }
     if constexpr (DB)
       cur ^= 1;
@@ -420,10 +422,16 @@ __global__ __launch_bounds__(kBlock) void reduce_sqdist_f32_kernel(const float* 
     }
     return;
   }
-  fused_finish(lds, acc, K, partials);
+  fused_finish<RM>(lds, acc, K, partials);
 }
 
-constexpr int kFusedMaxK = kBlock / 2;  // two threads per row at least: K <= 128
+// Fused up to 300 clients (RM = 2 rows per thread above 256).  Beyond that
+// the K-step chain of each tile and the rows per thread make it slower than
+// the two passes (320 x 5M: 2.17 vs 2.05 ms; 500 x 11.2M: 10.8 vs 7.26 ms;
+// 1000 x 12.5M: 40.6 vs 15.6 ms), while 200 x 10M gains 2.74 -> 1.84 ms,
+// 256 x 8M 2.69 -> 2.31 and 300 x 5M 1.96 -> 1.58
+// (profiles/r02/fused/fused_many_clients*_probe.jsonl).
+constexpr int kFusedMaxK = 300;
 
 // the tile + its average, and at least the 256 doubles of the final per-row sums
 inline int64_t fused_lds_bytes(int64_t K, int S, bool db = false) {
@@ -435,9 +443,12 @@ inline int64_t fused_lds_bytes(int64_t K, int S, bool db = false) {
 // with one thread group per row (scripts/fused_probe.py, profiles/r02/fused/):
 // 64 columns (256 B per row segment) above 64 rows -- 100 x 25M: 1.76 ms vs
 // 1.85 at 128 columns, 2.17 double-buffered; 128 up to 64 rows (64 x 10M:
-// 0.473 vs 0.497 ms); 256 up to 16 (10 x 1.2M: 16.7 vs 17.8 us)
+// 0.473 vs 0.497 ms); 256 up to 16 (10 x 1.2M: 16.7 vs 17.8 us); above 224
+// rows 32 columns (256 x 8M: 2.31 vs 2.41 ms, 300 x 5M: 1.58 vs 1.80 at 64;
+// 200 x 10M: 1.90 vs 1.82)
 inline int fused_cols(int64_t K) {
   if (K < 1 || K > kFusedMaxK) return 0;
+  if (K > 224) return 32;
   if (K > 64) return 64;
   return K > 16 ? 128 : 256;
 }
@@ -445,7 +456,7 @@ inline int fused_cols(int64_t K) {
 // Workgroups per CU the fused kernel keeps resident at this K (LDS-bound),
 // after raising the kernel's dynamic LDS limit past 64 KiB where needed;
 // cached per (device, S, K).  0 = the LDS request cannot be granted.
-template <int S, bool DB = false, int RW = 0, bool LO = false>
+template <int S, bool DB = false, int RW = 0, bool LO = false, int RM = 1>
 int fused_per_cu(int64_t K) {
   static std::mutex mu;
   static std::map<std::pair<int, int64_t>, int> cache;
@@ -454,7 +465,7 @@ int fused_per_cu(int64_t K) {
   std::lock_guard<std::mutex> lk(mu);
   auto it = cache.find({dev, K});
   if (it != cache.end()) return it->second;
-  const auto kern = reduce_sqdist_f32_kernel<S, DB, RW, LO>;
+  const auto kern = reduce_sqdist_f32_kernel<S, DB, RW, LO, RM>;
   const int64_t lds = fused_lds_bytes(K, S, DB);
   int per_cu = 0;
   if (lds > 65536 && hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -470,26 +481,26 @@ int fused_per_cu(int64_t K) {
   return per_cu;
 }
 
-template <int S, bool DB = false, int RW = 0, bool LO = false>
+template <int S, bool DB = false, int RW = 0, bool LO = false, int RM = 1>
 int64_t fused_grid(int64_t K, int64_t P, int blocks_per_cu) {
-  const int per_cu = blocks_per_cu > 0 ? blocks_per_cu : fused_per_cu<S, DB, RW, LO>(K);
+  const int per_cu = blocks_per_cu > 0 ? blocks_per_cu : fused_per_cu<S, DB, RW, LO, RM>(K);
   const int64_t ntiles = (P + S - 1) / S;
   const int64_t g = static_cast<int64_t>(per_cu) * cu_count();
   return ntiles < g ? ntiles : g;
 }
 
-template <int S, bool DB = false, int RW = 0, bool LO = false>
-int launch_fused(const float* clients, int64_t K, int64_t P, int64_t ld, const float* weights, float* out,
-                 double* partials, int64_t partial_elems, double* sumsq, int blocks_per_cu, hipStream_t s,
-                 const char* what) {
+template <int S, bool DB, int RW, bool LO, int RM>
+int launch_fused_rm(const float* clients, int64_t K, int64_t P, int64_t ld, const float* weights, float* out,
+                    double* partials, int64_t partial_elems, double* sumsq, int blocks_per_cu, hipStream_t s,
+                    const char* what) {
   if (RW > 0 && K > 4 * RW) return set_error(FEDAVG_EMODE, "%s: %d rows per wave cover K <= %d", what, RW, 4 * RW);
-  if (fused_per_cu<S, DB, RW, LO>(K) <= 0) return set_error(FEDAVG_EMODE, "%s: the %d-column tile does not fit LDS at K = %lld",
-                                                what, S, (long long)K);
+  if (fused_per_cu<S, DB, RW, LO, RM>(K) <= 0)
+    return set_error(FEDAVG_EMODE, "%s: the %d-column tile does not fit LDS at K = %lld", what, S, (long long)K);
   const int64_t ntiles = (P + S - 1) / S;
-  const int64_t grid = fused_grid<S, DB, RW, LO>(K, P, blocks_per_cu);
+  const int64_t grid = fused_grid<S, DB, RW, LO, RM>(K, P, blocks_per_cu);
   if (partial_elems < K * grid)
     return set_error(FEDAVG_EINVAL, "%s: workspace needs %lld doubles", what, (long long)(K * grid));
-  hipLaunchKernelGGL((reduce_sqdist_f32_kernel<S, DB, RW, LO>), dim3(static_cast<unsigned>(grid)), dim3(kBlock),
+  hipLaunchKernelGGL((reduce_sqdist_f32_kernel<S, DB, RW, LO, RM>), dim3(static_cast<unsigned>(grid)), dim3(kBlock),
                      static_cast<unsigned>(fused_lds_bytes(K, S, DB)), s, clients, static_cast<int>(K), ld, P, ntiles,
                      weights, out, partials);
   int rc = launch_status(what);
@@ -497,6 +508,20 @@ int launch_fused(const float* clients, int64_t K, int64_t P, int64_t ld, const f
   hipLaunchKernelGGL(client_sqdist_finalize_kernel, dim3(static_cast<unsigned>(K)), dim3(kBlock), 0, s, partials, grid,
                      sumsq);
   return launch_status(what);
+}
+
+// RM = rows per thread in the squares: 1 up to 256 rows, else 2
+template <int S, bool DB = false, int RW = 0, bool LO = false>
+int launch_fused(const float* clients, int64_t K, int64_t P, int64_t ld, const float* weights, float* out,
+                 double* partials, int64_t partial_elems, double* sumsq, int blocks_per_cu, hipStream_t s,
+                 const char* what) {
+  if (K <= kBlock)
+    return launch_fused_rm<S, DB, RW, LO, 1>(clients, K, P, ld, weights, out, partials, partial_elems, sumsq,
+                                             blocks_per_cu, s, what);
+  if constexpr (RW == 0 && !LO)
+    return launch_fused_rm<S, DB, RW, LO, 2>(clients, K, P, ld, weights, out, partials, partial_elems, sumsq,
+                                             blocks_per_cu, s, what);
+  return set_error(FEDAVG_EMODE, "%s: this variant covers K <= %d", what, kBlock);
 }
 
 // Global-pointer schedule (the fp64/fp16/bf16 passes and the probe
@@ -767,7 +792,7 @@ int fedavg_client_sqdist_buf(const float* clients, int64_t K, int64_t P, int64_t
 }
 #endif  // FEDAVG_TUNING
 
-// Aggregate + :291 sums in one pass (reduce_sqdist_f32_kernel) for K <= 128
+// Aggregate + :291 sums in one pass (reduce_sqdist_f32_kernel) for K <= 300
 // with 16-B aligned rows; otherwise the two production passes back to back
 // (fedavg_reduce_f32, then fedavg_client_sqdist_f32 on its output).  Either
 // way `out` holds fedavg_reduce_f32's bits and sumsq the :291 sums.
@@ -776,7 +801,9 @@ int64_t fedavg_reduce_sqdist_workspace(int64_t K, int64_t P) {
   const int S = fused_cols(K);
   const int64_t two_pass = fedavg_client_sqdist_workspace(K, P);
   int64_t fused = 0;
-  if (S == 64) fused = K * fused_grid<64>(K, P, 0);
+  const bool wide = K > kBlock;  // two rows per thread in the squares (RM = 2)
+  if (S == 32) fused = K * (wide ? fused_grid<32, false, 0, false, 2>(K, P, 0) : fused_grid<32>(K, P, 0));
+  if (S == 64) fused = K * (wide ? fused_grid<64, false, 0, false, 2>(K, P, 0) : fused_grid<64>(K, P, 0));
   if (S == 128) fused = K * fused_grid<128>(K, P, 0);
   if (S == 256) fused = K * fused_grid<256>(K, P, 0);
   return fused > two_pass ? fused : two_pass;
@@ -795,6 +822,7 @@ int fedavg_reduce_sqdist_f32(const float* clients, int64_t K, int64_t P, int64_t
   }
   const int S = fused_cols(K);
   if (S > 0 && aligned16(clients) && (ld % 4) == 0 && aligned4(out) && aligned4(weights)) {
+    if (S == 32) return launch_fused<32>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq, 0, s, what);
     if (S == 64) return launch_fused<64>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq, 0, s, what);
     if (S == 128)
       return launch_fused<128>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq, 0, s, what);
@@ -824,6 +852,7 @@ int fedavg_reduce_sqdist_f32_variant(const float* clients, int64_t K, int64_t P,
   case C + (DBUF ? 1000 : 0) + (RWS ? 10000 : 0):                                                                \
     return launch_fused<C, DBUF, RWS>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq,         \
                                       blocks_per_cu, s, what);
+    FEDAVG_FUSED_CASE(32, false, 0)
     FEDAVG_FUSED_CASE(64, false, 0)
     FEDAVG_FUSED_CASE(128, false, 0)
     FEDAVG_FUSED_CASE(256, false, 0)
@@ -842,7 +871,7 @@ int fedavg_reduce_sqdist_f32_variant(const float* clients, int64_t K, int64_t P,
                                                           sumsq, blocks_per_cu, s, what);
     case 101064: return launch_fused<64, true, 0, true>(clients, K, P, ld, weights, out, workspace, workspace_elems,
                                                         sumsq, blocks_per_cu, s, what);
-    default: return set_error(FEDAVG_EMODE, "%s: cols must be 64, 128 or 256 (+1000: double-buffered)", what);
+    default: return set_error(FEDAVG_EMODE, "%s: cols must be 32, 64, 128 or 256 (+1000: double-buffered)", what);
   }
 }
 #endif  // FEDAVG_TUNING

@@ -407,7 +407,7 @@ __global__ __launch_bounds__(kBlock) void reduce_sqdist_segments_f32_kernel(cons
   float* gs = lds + K * S;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int nload = K * V;
-  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  double acc[1][4] = {{0.0, 0.0, 0.0, 0.0}};
   int64_t cur_key = -1;
   int64_t src[kSegFusedRowsPerThread];  // client address of the row of this thread's m-th load slot
   for (int64_t u = blockIdx.x; u < units; u += gridDim.x) {

@@ -71,7 +71,7 @@ def main():
             return run
 
         runs = {"two-pass": two_pass, "reduce-only": reduce_only}
-        if K <= 128:
+        if K <= 1024:
             runs["fused"] = fused
             for v in args.variants:
                 cols, bpc = (int(t) for t in v.split(","))

@@ -53,9 +53,23 @@ def test_fused_small_vs_oracle(K, P):
     assert torch.equal(sumsq, again)  # deterministic
 
 
-@pytest.mark.parametrize("K,P", [(129, 5003), (300, 70_001)])
+@pytest.mark.parametrize("K,P", [(129, 5003), (256, 777), (257, 2049), (300, 70_001), (301, 33_333), (500, 1001)])
+def test_fused_many_clients_vs_oracle(K, P):
+    """K > 128: 32/64-column tiles, two rows per thread in the squares above
+    256 clients; above 300 the entry runs the two passes -- same bits."""
+    x, ld, weights = _rows(K, P, K * 7 + P)
+    w = mfl_amd.weights_tensor(weights, torch.float32, DEV)
+    out, sumsq = mfl_amd.reduce_with_sqdist(x, w, P)
+    exp = O.reduce_f32(x[:, :P].cpu().numpy(), weights)
+    assert out.cpu().numpy().view(np.uint32).tobytes() == exp.view(np.uint32).tobytes()
+    ref = _sumsq_ref(x, out, P)
+    rel = ((sumsq - ref).abs() / ref.clamp_min(1e-300)).max().item()
+    assert rel < 1e-12, rel
+
+
+@pytest.mark.parametrize("K,P", [(301, 5003), (1300, 2001)])
 def test_fused_large_k_takes_two_passes(K, P):
-    """K > 128: the same entry runs the two production passes; same bits."""
+    """K > 300: the same entry runs the two production passes; same bits."""
     x, ld, weights = _rows(K, P, K + P)
     w = mfl_amd.weights_tensor(weights, torch.float32, DEV)
     out, sumsq = mfl_amd.reduce_with_sqdist(x, w, P)
@@ -136,11 +150,11 @@ def _host_round(K, shapes, seed):
     return w_locals
 
 
-@pytest.mark.parametrize("K", [1, 9, 100, 128, 129])
+@pytest.mark.parametrize("K", [1, 9, 100, 128, 300, 301])
 def test_dropin_distances_from_the_fused_pass(K):
     """aggregate (host state_dicts) leaves the fused :291 sums; client_distances
     returns the reference's norms (torch.norm of the fp32 differences) from
-    them -- client 0 (aliased to w_glob, :449) gets 0.  K = 129 takes the
+    them -- client 0 (aliased to w_glob, :449) gets 0.  K = 301 takes the
     two-pass route and gives the same norms."""
     import copy
 
@@ -152,7 +166,7 @@ def test_dropin_distances_from_the_fused_pass(K):
     agg.SMALL_ROUND_BYTES = 0  # the pipelined host path even for a few clients (small rounds: one native call)
     w_glob = agg.aggregate(w_locals)
     fused = agg._last.get("sumsq", {})
-    assert (torch.float32 in fused) == (K <= 128)
+    assert (torch.float32 in fused) == (K <= 300)
     norms = agg.client_distances(w_locals, w_glob)
     keys = list(shapes)
     exp = []
