@@ -552,10 +552,30 @@ constexpr int kDistBufChains = 4;
 // (10 x 1.2M).  rocprofv3 kernel time (profiles/r02/sweeps/dist_small_models.json):
 // resnet56 275 -> 72 us (U8 x C2), FEMNIST 30.8 -> 12.7 us (U4 x C4),
 // cfg4 500 x 1M 1,383 -> 391 us (U4 x C4), 100 x 3.125M 309 -> 197 us (U4 x C4).
+//
+// Between them, U4 x C8 when the 16-slice launch would end in a partly
+// filled round of workgroups: a launch of g groups on r resident slots runs
+// ceil(g / r) rounds, so 685 groups (cfg4, 500 x 11.2M) on 512 slots of the
+// 16-slice kernel (2 per CU) fill 67 %, against 89 % for the 1,371 8-slice
+// groups on its 768 slots (3 per CU).  scripts/dist_variants.py
+// (profiles/r02/sweeps/dist_many_clients*.jsonl): 500 x 11.2M 4.10 -> 3.69 ms,
+// 1000 x 12.5M 8.49 -> 8.03, 200 x 10M 1.52 -> 1.26; 100 x 25M keeps 16
+// slices (1,526 groups, 99 %; 1.467 vs 1.600 ms at 8).
+double round_fill(int64_t groups, int64_t slots) {
+  if (slots <= 0) return 0.0;
+  const int64_t rounds = (groups + slots - 1) / slots;
+  return static_cast<double>(groups) / static_cast<double>(rounds * slots);
+}
+
 int dist_cols(int64_t P) {
   const int64_t nvec = (P + 3) / 4;
   const int64_t cus = cu_count();
-  if ((nvec + kBlock * 16 - 1) / (kBlock * 16) >= 2 * cus) return 16;
+  const int64_t g16 = (nvec + kBlock * 16 - 1) / (kBlock * 16);
+  const int64_t g8 = (nvec + kBlock * 8 - 1) / (kBlock * 8);
+  const int64_t slots16 = resident_blocks(client_sqdist_buf_kernel<2, 16, 1, 4>);
+  const int64_t slots8 = resident_blocks(client_sqdist_buf_kernel<4, 8, 1, 4>);
+  if (g16 >= 2 * cus) return round_fill(g8, slots8) > round_fill(g16, slots16) + 0.05 ? 8 : 16;
+  if (g8 >= slots8) return 8;
   if ((nvec + kBlock * 4 - 1) / (kBlock * 4) >= cus * 9 / 10) return 4;
   return 2;
 }
@@ -745,7 +765,7 @@ int fedavg_client_sqdist_f32(const float* clients, int64_t K, int64_t P, int64_t
                              double* workspace, int64_t workspace_elems, double* sumsq, void* stream) {
   // unroll codes: chains x 10000 + rows per batch (4 chains, at most one per slice)
   const int cols = P > 0 ? dist_cols(P) : kDistBufCols;
-  const int rows = cols == 16 ? kDistBufRows : (cols == 4 ? 4 : 8);
+  const int rows = cols == 16 ? kDistBufRows : (cols == 8 || cols == 4 ? 4 : 8);
   return sqdist_buf_impl(clients, K, P, ld, glob, workspace, workspace_elems, sumsq, kDistBufChains * 10000 + rows,
                          cols, 0, stream, "fedavg_client_sqdist_f32");
 }

@@ -233,3 +233,20 @@ def test_device_round_fused_segments(K, misalign):
                                                for k in keys]).pow(2).sum()).float())
                    for _, sd in host_locals[1:]]
     np.testing.assert_allclose(norms, np.array(exp), rtol=2e-7, atol=0)
+
+
+@pytest.mark.parametrize("P", [10_000_003, 11_227_812, 5_000_001, 25_000_003])
+def test_client_sqdist_round_fill_schedules(P):
+    """The :291 pass's 16- / 8- / 4-slice choice (round fill of the launch):
+    every schedule within 1e-12 of fp64 sums of the fp32 differences."""
+    K = 3
+    ld = (P + 63) // 64 * 64
+    g = torch.Generator(device=DEV).manual_seed(P)
+    x = torch.full((K, ld), float("nan"), device=DEV)
+    x[:, :P] = torch.randn((K, P), generator=g, device=DEV) * 0.05
+    glob = torch.randn(ld, generator=g, device=DEV) * 0.05
+    got = mfl_amd.client_sqdist(x, glob, P)
+    ref = torch.stack([((x[k, :P] - glob[:P]).double() ** 2).sum() for k in range(K)])
+    rel = ((got - ref).abs() / ref).max().item()
+    assert rel < 1e-12, rel
+    assert torch.equal(got, mfl_amd.client_sqdist(x, glob, P))
