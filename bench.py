@@ -749,7 +749,7 @@ def main(argv=None):
         }
         if diagnostics is not None:
             out["diagnostics"] = diagnostics
-        if world == 1 and passes == 1 and plan_world == 1 and K <= 128 and red.plan.chunks == 1:
+        if world == 1 and passes == 1 and plan_world == 1 and K <= 300 and red.plan.chunks == 1:
             out["round_with_distances"] = fused_round(red, w_dev)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(min(P_global, 25_000_000))
