@@ -372,7 +372,7 @@ int fedavg_client_sqdist_segments_f32(const int64_t* client_ptrs, const int64_t*
  * Both in ONE pass over the clients' tensors (the fused tiles of
  * fedavg_reduce_sqdist_f32 on the same key/pointer tables): `out` with the
  * bits of fedavg_reduce_segments_f32, sumsq the :291 sums against that out.
- * Needs 1 <= K <= 128 and every fp32 key's client tensors 16-B aligned
+ * Needs 1 <= K <= 256 and every fp32 key's client tensors 16-B aligned
  * (FEDAVG_EALIGN / FEDAVG_EINVAL otherwise: run the two calls above).
  * partials : fedavg_reduce_sqdist_segments_partials(K) doubles.
  */

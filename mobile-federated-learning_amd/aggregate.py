@@ -160,7 +160,7 @@ def column_chunks(P: int) -> List[Tuple[int, int]]:
 # :289-291), so the drop-in fuses by default; FEDAVG_FUSE_DISTANCES=0 keeps
 # the reduce alone.
 FUSED_MAX_K = 300  # rows kernel (fedavg_reduce_sqdist_f32; more clients: the two passes are faster)
-FUSED_SEGMENTS_MAX_K = 128  # device-resident clients' own tensors (fedavg_reduce_sqdist_segments_f32)
+FUSED_SEGMENTS_MAX_K = 256  # device-resident clients' own tensors (fedavg_reduce_sqdist_segments_f32)
 FUSE_DISTANCES = os.environ.get("FEDAVG_FUSE_DISTANCES", "1") != "0"
 
 
@@ -452,7 +452,7 @@ class DeviceAggregator:
 
     def _reduce_sqdist_segments(self, g, ptrs, weights, stream):
         """The zero-copy reduce and the round's :291 sums in one pass
-        (fedavg_reduce_sqdist_segments_f32) when the round qualifies (K <= 128,
+        (fedavg_reduce_sqdist_segments_f32) when the round qualifies (K <= 256,
         fused distances on, every fp32 source 16-B aligned): ``(out, sumsq)``,
         else None."""
         import numpy as np

@@ -391,7 +391,7 @@ __global__ __launch_bounds__(kBlock) void segments_finalize_kernel(const double*
 // keys element by element (converted like the packers) -- then the
 // reference's sequential average of each column and the per-row squares.
 // The running workgroup keeps its rows' client addresses of the current key
-// in registers (reloaded at a key change only).  K <= 128.
+// in registers (reloaded at a key change only).  K <= 256.
 constexpr int kSegFusedRowsPerThread = 8;  // ceil(K * S / 4 / 256) slots per thread at K <= 128, S <= 64 ... 256
 
 template <int S>
@@ -461,11 +461,11 @@ __global__ __launch_bounds__(kBlock) void reduce_sqdist_segments_f32_kernel(cons
   fused_finish(lds, acc, K, partials);
 }
 
-constexpr int kSegFusedMaxK = kBlock / 2;
+constexpr int kSegFusedMaxK = kBlock;
 
-// tile width: as fedavg_dist.hip's fused_cols (64 above 64 clients, 128 up to
-// 64, 256 up to 16); the widest tile keeps <= 8 load slots per thread
-inline int seg_fused_cols(int64_t K) { return K > 64 ? 64 : (K > 16 ? 128 : 256); }
+// tile width: as fedavg_dist.hip's fused_cols (32 above 128 clients, 64 above
+// 64, 128 up to 64, 256 up to 16); every width keeps <= 8 load slots per thread
+inline int seg_fused_cols(int64_t K) { return K > 128 ? 32 : (K > 64 ? 64 : (K > 16 ? 128 : 256)); }
 
 inline int64_t seg_fused_lds_bytes(int64_t K, int S) {
   const int64_t b = (K + 1) * S * 4;
@@ -685,14 +685,15 @@ int fedavg_client_sqdist_segments_f32(const int64_t* client_ptrs, const int64_t*
   return launch_status(what);
 }
 
-// Aggregate + :291 sums in one pass over device-resident clients (K <= 128,
+// Aggregate + :291 sums in one pass over device-resident clients (K <= 256,
 // every fp32 key's client tensors 16-B aligned): out as
 // fedavg_reduce_segments_f32, sumsq as fedavg_client_sqdist_segments_f32 on
 // that out.  partials : fedavg_reduce_sqdist_segments_partials(K) doubles.
 int64_t fedavg_reduce_sqdist_segments_partials(int64_t K) {
   if (K <= 0 || K > kSegFusedMaxK) return 0;
   const int S = seg_fused_cols(K);
-  const int per_cu = S == 64 ? seg_fused_per_cu<64>(K) : (S == 128 ? seg_fused_per_cu<128>(K) : seg_fused_per_cu<256>(K));
+  const int per_cu = S == 32 ? seg_fused_per_cu<32>(K)
+                     : (S == 64 ? seg_fused_per_cu<64>(K) : (S == 128 ? seg_fused_per_cu<128>(K) : seg_fused_per_cu<256>(K)));
   return K * static_cast<int64_t>(per_cu > 0 ? per_cu : 1) * cu_count();
 }
 
@@ -735,6 +736,7 @@ int fedavg_reduce_sqdist_segments_f32(const int64_t* client_ptrs, const int64_t*
                        static_cast<unsigned>(seg_fused_lds_bytes(K, C)), s, keys, tptrs, n_keys, units,             \
                        static_cast<int>(K), weights, out, partials);                                               \
   }
+  FEDAVG_SEG_FUSED(32)
   FEDAVG_SEG_FUSED(64)
   FEDAVG_SEG_FUSED(128)
   FEDAVG_SEG_FUSED(256)

@@ -31,6 +31,8 @@ A = sys.modules[mfl_amd.DeviceAggregator.__module__]  # the module (mfl_amd.aggr
 def clients_for(name, dev):
     if name == "flat":
         K, shapes = 100, [("w", (25_000_000,))]
+    elif name == "flat200":
+        K, shapes = 200, [("w", (10_000_000,))]
     else:
         from model_shapes import CONFIGS
         K, shapes = CONFIGS[name]

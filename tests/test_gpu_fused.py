@@ -206,12 +206,13 @@ def _device_round(K, shapes, seed, misalign=False):
     return w_locals
 
 
-@pytest.mark.parametrize("K,misalign", [(1, False), (7, False), (100, False), (128, False), (12, True), (129, False)])
+@pytest.mark.parametrize("K,misalign", [(1, False), (7, False), (100, False), (129, False), (256, False), (12, True),
+                                       (257, False)])
 def test_device_round_fused_segments(K, misalign):
     """Device-resident clients (separate tensors, an int64 buffer, ragged key
     sizes): the zero-copy round's average keeps the oracle's bits and the
     fused :291 sums give the reference's norms.  A misaligned client tensor
-    or K > 128 takes the two-pass route with the same results."""
+    or K > 256 takes the two-pass route with the same results."""
     import copy
 
     shapes = {"conv.weight": (16, 3, 3, 3), "conv.bias": (16,), "bn.num_batches_tracked": (),
@@ -225,7 +226,7 @@ def test_device_round_fused_segments(K, misalign):
         got, exp = w_glob[k].cpu(), ref[k]
         assert got.dtype == exp.dtype, k
         assert torch.equal(got.reshape(-1).view(torch.int32), exp.reshape(-1).view(torch.int32)), k
-    assert (torch.float32 in agg._last.get("sumsq", {})) == (K <= 128 and not misalign)
+    assert (torch.float32 in agg._last.get("sumsq", {})) == (K <= 256 and not misalign)
     norms = agg.client_distances(w_locals, w_glob)
     keys = list(shapes)
     # :291's fp32 differences (int64 buffers promote to fp32), squared and summed exactly
