@@ -750,7 +750,10 @@ def main(argv=None):
         if diagnostics is not None:
             out["diagnostics"] = diagnostics
         if world == 1 and passes == 1 and plan_world == 1 and K <= 300 and red.plan.chunks == 1:
-            out["round_with_distances"] = fused_round(red, w_dev)
+            try:  # a side measurement: never the reason the bench line is missing
+                out["round_with_distances"] = fused_round(red, w_dev)
+            except Exception as e:  # noqa: BLE001
+                out["round_with_distances"] = {"error": f"{type(e).__name__}: {e}"}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(min(P_global, 25_000_000))
         print(json.dumps(out), flush=True)
