@@ -575,10 +575,22 @@ __device__ __forceinline__ void fused_average(const float* tile, float* gs, int 
 // RM = 1: K <= 256, thread t owns row t % K and slices t / K, t / K + q, ...
 // (q = 256 / K); RM > 1: 256 < K <= 256 RM, thread t owns rows t, t + 256, ...
 // and every slice of them.  acc[m][0..3]: four fp64 chains per owned row.
-template <int S, int RM = 1>
+// UNMASKED: full tiles skip the padding selects (the rows kernel; the
+// segments kernel keeps one masked path, which holds it to 6 workgroups/CU)
+template <int S, int RM = 1, bool UNMASKED = true>
 __device__ __forceinline__ void fused_squares(const float* tile, const float* gs, int K, int ncols,
                                               double (&acc)[RM][4]) {
   constexpr int V = S / 4;
+  // a full tile (every column valid: all but a key's / the model's last) takes
+  // no masks at all; the ragged one selects the padding out
+  const auto sq_full = [&](double (&a)[4], f32x4 x, int c) {
+    const f32x4 d = x - reinterpret_cast<const f32x4*>(gs)[c];  // fp32 difference, as the reference forms it
+    const double dx = d.x, dy = d.y, dz = d.z, dw = d.w;
+    a[0] = __builtin_fma(dx, dx, a[0]);
+    a[1] = __builtin_fma(dy, dy, a[1]);
+    a[2] = __builtin_fma(dz, dz, a[2]);
+    a[3] = __builtin_fma(dw, dw, a[3]);
+  };
   const auto sq = [&](double (&a)[4], f32x4 x, int c) {
     const f32x4 g = reinterpret_cast<const f32x4*>(gs)[c];
     const f32x4 d = x - g;        // fp32 difference, as the reference forms it
@@ -591,6 +603,7 @@ __device__ __forceinline__ void fused_squares(const float* tile, const float* gs
       a[3] = __builtin_fma(dw, dw, a[3]);
     }
   };
+  const bool full = UNMASKED && ncols == S;
   if constexpr (RM == 1) {
     const int q = kBlock / K;
     const int my_row = threadIdx.x % K;
@@ -598,7 +611,11 @@ __device__ __forceinline__ void fused_squares(const float* tile, const float* gs
     if (my_sub >= q) return;
     const int swz = my_row & 7;
     const f32x4* x4 = reinterpret_cast<const f32x4*>(tile) + my_row * V;
-    for (int c = my_sub; c < V; c += q) sq(acc[0], x4[c ^ swz], c);
+    if (full) {
+      for (int c = my_sub; c < V; c += q) sq_full(acc[0], x4[c ^ swz], c);
+    } else {
+      for (int c = my_sub; c < V; c += q) sq(acc[0], x4[c ^ swz], c);
+    }
   } else {
 #pragma unroll
     for (int m = 0; m < RM; ++m) {
@@ -606,7 +623,11 @@ __device__ __forceinline__ void fused_squares(const float* tile, const float* gs
       if (row < K) {
         const int swz = row & 7;
         const f32x4* x4 = reinterpret_cast<const f32x4*>(tile) + row * V;
-        for (int c = 0; c < V; ++c) sq(acc[m], x4[c ^ swz], c);
+        if (full) {
+          for (int c = 0; c < V; ++c) sq_full(acc[m], x4[c ^ swz], c);
+        } else {
+          for (int c = 0; c < V; ++c) sq(acc[m], x4[c ^ swz], c);
+        }
       }
     }
   }

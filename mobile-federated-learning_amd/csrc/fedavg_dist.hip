@@ -327,6 +327,53 @@ __global__ __launch_bounds__(kBlock) void client_sqdist_finalize_kernel(const do
 
 // rows -> LDS for the tile at column c0: slot i = row * V + j (LDS byte
 // 16 i from `buf`) holds slice j ^ (row & 7) of the row segment
+// Load slots per thread at the widest K each tile width serves (fused_cols):
+// 300 x 32, 128 x 64, 64 x 128, 32 x 256 columns
+template <int S>
+constexpr int fused_slots() {
+  return S == 32 ? 10 : 8;
+}
+
+// The byte offset (row * ld + slice) of each of this thread's load slots,
+// the same for every tile: computed once per workgroup, so a tile's loads
+// cost one 64-bit add each instead of the row / slice / swizzle arithmetic
+template <int S>
+struct FusedSlots {
+  int64_t off[fused_slots<S>()];
+};
+
+template <int S>
+__device__ __forceinline__ FusedSlots<S> fused_slots_of(int K, int64_t ld) {
+  constexpr int V = S / 4;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  FusedSlots<S> sl;
+#pragma unroll
+  for (int m = 0; m < fused_slots<S>(); ++m) {
+    const int i = wave * 64 + m * kBlock + lane;
+    const int row = i / V;
+    const int c = (i % V) ^ (row & 7);
+    sl.off[m] = (static_cast<int64_t>(row) * ld + 4 * c) * 4;
+  }
+  return sl;
+}
+
+// a full tile's loads through the precomputed slots (the ragged last tile
+// takes fused_load_tile, which masks slices past the model's end)
+template <int S>
+__device__ __forceinline__ void fused_load_full(const float* __restrict__ X, int K, int64_t c0,
+                                                const FusedSlots<S>& sl, float* buf) {
+  constexpr int V = S / 4;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nload = K * V;
+  const char* base = reinterpret_cast<const char*>(X + c0);
+#pragma unroll
+  for (int m = 0; m < fused_slots<S>(); ++m) {
+    const int i0 = wave * 64 + m * kBlock;
+    if (i0 < nload && i0 + lane < nload)
+      __builtin_amdgcn_global_load_lds((fused_gbl_t)(base + sl.off[m]), (fused_lds_t)(buf + 4 * i0), 16, 0, 2 /* nt */);
+  }
+}
+
 template <int S>
 __device__ __forceinline__ void fused_load_tile(const float* __restrict__ X, int K, int64_t ld, int64_t P, int64_t c0,
                                                 float* buf) {
@@ -363,6 +410,7 @@ __global__ __launch_bounds__(kBlock) void reduce_sqdist_f32_kernel(const float* 
   double acc_rows[RW > 0 ? RW : 1];      // RW > 0: one accumulator per row of this wave
 #pragma unroll
   for (int r = 0; r < (RW > 0 ? RW : 1); ++r) acc_rows[r] = 0.0;
+  const FusedSlots<S> slots = fused_slots_of<S>(K, ld);
   int cur = 0;
   if (DB && static_cast<int64_t>(blockIdx.x) < ntiles)
     fused_load_tile<S>(X, K, ld, P, static_cast<int64_t>(blockIdx.x) * S, lds);
@@ -375,7 +423,10 @@ __global__ __launch_bounds__(kBlock) void reduce_sqdist_f32_kernel(const float* 
       // 1. the next tile's rows stream into the other buffer while this one is used
       if (t + gridDim.x < ntiles) fused_load_tile<S>(X, K, ld, P, (t + gridDim.x) * S, lds + (cur ^ 1) * tile_floats);
     } else {
-      fused_load_tile<S>(X, K, ld, P, c0, tile);  // 1. rows -> LDS
+      if (ncols == S && !RW && K * (S / 4) <= fused_slots<S>() * kBlock)  // 1. rows -> LDS
+        fused_load_full<S>(X, K, c0, slots, tile);
+      else
+        fused_load_tile<S>(X, K, ld, P, c0, tile);
       barrier_loads();
     }
     if constexpr (LOADS_ONLY) {  // probe: the tile traffic alone (one column of each tile stored)
@@ -443,14 +494,16 @@ inline int64_t fused_lds_bytes(int64_t K, int S, bool db = false) {
 // with one thread group per row (scripts/fused_probe.py, profiles/r02/fused/):
 // 64 columns (256 B per row segment) above 64 rows -- 100 x 25M: 1.76 ms vs
 // 1.85 at 128 columns, 2.17 double-buffered; 128 up to 64 rows (64 x 10M:
-// 0.473 vs 0.497 ms); 256 up to 16 (10 x 1.2M: 16.7 vs 17.8 us); above 224
+// 0.473 vs 0.497 ms); 256 up to 16 (10 x 1.2M: 16.7 vs 17.8 us); above 128
 // rows 32 columns (256 x 8M: 2.31 vs 2.41 ms, 300 x 5M: 1.58 vs 1.80 at 64;
-// 200 x 10M: 1.90 vs 1.82)
+// 200 x 10M: 1.90 vs 1.82 -- kept at 32 so that 64-column tiles need only 8
+// precomputed load slots per thread: the register budget of 6 workgroups/CU);
+// 256 up to 32 rows (20 x 25M: 0.40 vs 0.49 ms at 128, 32 x 20M: 0.48 vs 0.58)
 inline int fused_cols(int64_t K) {
   if (K < 1 || K > kFusedMaxK) return 0;
-  if (K > 224) return 32;
+  if (K > 128) return 32;
   if (K > 64) return 64;
-  return K > 16 ? 128 : 256;
+  return K > 32 ? 128 : 256;
 }
 
 // Workgroups per CU the fused kernel keeps resident at this K (LDS-bound),

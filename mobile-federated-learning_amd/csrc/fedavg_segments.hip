@@ -455,7 +455,7 @@ __global__ __launch_bounds__(kBlock) void reduce_sqdist_segments_f32_kernel(cons
     barrier_loads();
     fused_average<S>(tile, gs, K, W, n, out + key.out_offset + c0);
     barrier_lds();
-    fused_squares<S>(tile, gs, K, n, acc);
+    fused_squares<S, 1, false>(tile, gs, K, n, acc);
     barrier_lds();  // the tile is read out before the next one lands
   }
   fused_finish(lds, acc, K, partials);
