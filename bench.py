@@ -699,7 +699,7 @@ def main(argv=None):
             except (ValueError, OSError, KeyError):
                 pass
         if red.gather:
-            exchange = "rccl all_gather_into_tensor, overlapped per chunk"
+            exchange = ("rccl" if backend == "nccl" else backend) + " all_gather_into_tensor, overlapped per chunk"
         elif host_out is not None:
             exchange = "none: each rank D2Hs its shard chunks into pinned host memory (host consumer)"
         else:
