@@ -563,6 +563,10 @@ __device__ __forceinline__ void fused_average(const float* tile, float* gs, int 
   if (threadIdx.x < S) {
     const int c = threadIdx.x;
     float a = tile[fused_at<S>(0, c)] * W[0];
+    // 16 rows per batch: one s_load_dwordx16 of weights and 16 LDS reads per
+    // wait (interleaved A/B, profiles/r02/fused/ab_chain_unroll16.jsonl:
+    // 200 x 10M 1.693 -> 1.624 ms, 20 x 25M 0.428 -> 0.406, K = 100 equal)
+#pragma unroll 16
     for (int k = 1; k < K; ++k) {
       const float term = tile[fused_at<S>(k, c)] * W[k];
       a = a + term;
