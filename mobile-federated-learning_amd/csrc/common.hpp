@@ -565,8 +565,11 @@ __device__ __forceinline__ void fused_average(const float* tile, float* gs, int 
     float a = tile[fused_at<S>(0, c)] * W[0];
     // 16 rows per batch: one s_load_dwordx16 of weights and 16 LDS reads per
     // wait (interleaved A/B, profiles/r02/fused/ab_chain_unroll16.jsonl:
-    // 200 x 10M 1.693 -> 1.624 ms, 20 x 25M 0.428 -> 0.406, K = 100 equal)
-#pragma unroll 16
+    // 200 x 10M 1.693 -> 1.624 ms, 20 x 25M 0.428 -> 0.406, K = 100 equal);
+    // 32 for the 64-column tiles of 65-128 clients (ab_chain_unroll32*.jsonl:
+    // 100 x 25M 1.760 -> 1.668 ms; slower for the other widths)
+    constexpr int kChainUnroll = S == 64 ? 32 : 16;
+#pragma unroll kChainUnroll
     for (int k = 1; k < K; ++k) {
       const float term = tile[fused_at<S>(k, c)] * W[k];
       a = a + term;
