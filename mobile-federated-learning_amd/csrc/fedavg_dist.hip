@@ -577,6 +577,197 @@ int launch_fused(const float* clients, int64_t K, int64_t P, int64_t ld, const f
   return set_error(FEDAVG_EMODE, "%s: this variant covers K <= %d", what, kBlock);
 }
 
+// ---------------------------------------------------------------------------
+// Register-staged fused tiles (round 3).  The LDS-DMA form above fills a
+// tile straight into LDS and has nothing in flight while a tile is averaged
+// and squared; LDS-DMA also tops out near 6.5-6.8 TB/s chip-wide where
+// register loads reach the row reduce's 7.1.  Here the tile goes through
+// registers:
+//   slot m of thread t holds row r0 + m R, 16-B slice sl of the tile
+//   (V = S / 4 slices per row segment, R = 256 / V rows per slot round,
+//   r0 = t / V, sl = t % V), so a wave instruction reads 64 / V row segments
+//   of S x 4 bytes and the slot's LDS image is the linear 16 (t + 256 m);
+// per tile:
+//   1. the staged slots (loaded one tile earlier) are written to LDS,
+//   2. the NEXT tile's loads are issued into the same registers -- they stay
+//      in flight while this tile is averaged and squared,
+//   3. the reference's sequential chain, one thread per column (S threads),
+//   4. every thread squares its own slots against the tile's average; slot m
+//      always belongs to the same row, so one fp64 accumulator per slot lives
+//      across all tiles, and the V threads of a row (one per slice) are added
+//      in a fixed order at the end: partials[row][workgroup].
+// MODE 1 / 2 are traffic probes (1: loads only; 2: loads + LDS writes).
+// ---------------------------------------------------------------------------
+template <int S, int SLOTS, int MODE = 0>
+__global__ __launch_bounds__(kBlock) void reduce_sqdist_rs_kernel(const float* __restrict__ X, int K, int64_t ld,
+                                                                  int64_t P, int64_t ntiles,
+                                                                  const float* __restrict__ W,
+                                                                  float* __restrict__ out,
+                                                                  double* __restrict__ partials) {
+  static_assert(S == 32 || S == 64 || S == 128 || S == 256, "tile widths: 32, 64, 128 or 256 columns");
+  constexpr int V = S / 4;
+  constexpr int R = kBlock / V;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* gs = lds + K * S;
+  const int t = threadIdx.x;
+  const int r0 = t / V, sl = t % V;
+  const int nslot = r0 < K ? (K - r0 + R - 1) / R : 0;  // slots of this thread that hold a row
+  const char* p0 = reinterpret_cast<const char*>(X) + (static_cast<int64_t>(r0) * ld + 4 * sl) * 4;
+  const int64_t mstride = static_cast<int64_t>(R) * ld * 4;
+  f32x4* tile4 = reinterpret_cast<f32x4*>(lds);
+  f32x4 xs[SLOTS];
+  double acc[SLOTS];
+#pragma unroll
+  for (int m = 0; m < SLOTS; ++m) acc[m] = 0.0;
+
+  // this thread's slots of tile `tt` into registers (slices past the model's
+  // end are not loaded: the last row's would run off the allocation)
+  const auto issue = [&](int64_t tt) {
+    const int64_t c0 = tt * S;
+    const char* p = p0 + c0 * 4;
+    const bool slice_ok = c0 + 4 * sl < P;
+#pragma unroll
+    for (int m = 0; m < SLOTS; ++m)
+      if (m < nslot && slice_ok) xs[m] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p + m * mstride));
+  };
+
+  if (static_cast<int64_t>(blockIdx.x) < ntiles) issue(blockIdx.x);
+  for (int64_t tt = blockIdx.x; tt < ntiles; tt += gridDim.x) {
+    const int64_t c0 = tt * S;
+    const int ncols = P - c0 < S ? static_cast<int>(P - c0) : S;
+    barrier_lds();  // every wave is done with the previous tile
+    if constexpr (MODE != 1) {
+#pragma unroll
+      for (int m = 0; m < SLOTS; ++m)
+        if (m < nslot) tile4[t + kBlock * m] = xs[m];  // 1. (a ragged slice keeps stale data: never used)
+    } else {
+#pragma unroll
+      for (int m = 0; m < SLOTS; ++m)
+        if (m < nslot) asm volatile("" ::"v"(xs[m]));  // probe: consume the loads
+    }
+    barrier_lds();
+    if (tt + gridDim.x < ntiles) issue(tt + gridDim.x);  // 2. next tile in flight
+    if constexpr (MODE != 0) {
+      if (t == 0) out[c0] = lds[0];
+      continue;
+    }
+    if (t < S) {  // 3. the average of column t, in the reference's order
+      float a = lds[t] * W[0];
+      constexpr int kUnroll = S == 64 ? 32 : 16;
+#pragma unroll kUnroll
+      for (int k = 1; k < K; ++k) {
+        const float term = lds[k * S + t] * W[k];
+        a = a + term;
+      }
+      gs[t] = a;
+      if (t < ncols) out[c0 + t] = a;
+    }
+    barrier_lds();
+    // 4. squares of this thread's slots: fl32(x - g) as the reference forms it, fp64 square-adds
+    const f32x4 g = reinterpret_cast<const f32x4*>(gs)[sl];
+    const int nv = ncols - 4 * sl;  // valid columns of this slice
+    if (nv >= 4) {
+#pragma unroll
+      for (int m = 0; m < SLOTS; ++m)
+        if (m < nslot) {
+          const f32x4 d = tile4[t + kBlock * m] - g;
+          const double dx = d.x, dy = d.y, dz = d.z, dw = d.w;
+          acc[m] = __builtin_fma(dx, dx, acc[m]);
+          acc[m] = __builtin_fma(dy, dy, acc[m]);
+          acc[m] = __builtin_fma(dz, dz, acc[m]);
+          acc[m] = __builtin_fma(dw, dw, acc[m]);
+        }
+    } else if (nv > 0) {  // ragged slice: select (not multiply) -- padding may hold NaN/inf
+#pragma unroll
+      for (int m = 0; m < SLOTS; ++m)
+        if (m < nslot) {
+          const f32x4 d = tile4[t + kBlock * m] - g;
+          const double dx = d.x, dy = nv > 1 ? d.y : 0.f, dz = nv > 2 ? d.z : 0.f;
+          acc[m] = __builtin_fma(dx, dx, acc[m]);
+          acc[m] = __builtin_fma(dy, dy, acc[m]);
+          acc[m] = __builtin_fma(dz, dz, acc[m]);
+        }
+    }
+  }
+  if constexpr (MODE != 0) return;
+  // the V slot sums of a row are contiguous in red[]: row * V + slice = t + 256 m
+  barrier_loads();
+  double* red = reinterpret_cast<double*>(lds);
+#pragma unroll
+  for (int m = 0; m < SLOTS; ++m)
+    if (m < nslot) red[t + kBlock * m] = acc[m];
+  barrier_lds();
+  for (int row = t; row < K; row += kBlock) {
+    double s = red[row * V];
+#pragma unroll
+    for (int j = 1; j < V; ++j) s += red[row * V + j];
+    partials[static_cast<int64_t>(row) * gridDim.x + blockIdx.x] = s;
+  }
+}
+
+// LDS of a register-staged tile: [K][S] + the average [S]; the final per-row
+// sums need K * V doubles (= K * S * 2 bytes, inside the tile)
+inline int64_t fused_rs_lds_bytes(int64_t K, int S) { return (K + 1) * S * 4; }
+
+template <int S, int SLOTS, int MODE>
+int fused_rs_per_cu(int64_t K) {
+  static std::mutex mu;
+  static std::map<std::pair<int, int64_t>, int> cache;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find({dev, K});
+  if (it != cache.end()) return it->second;
+  const auto kern = reduce_sqdist_rs_kernel<S, SLOTS, MODE>;
+  const int64_t lds = fused_rs_lds_bytes(K, S);
+  int per_cu = 0;
+  if (lds > 65536 && hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         static_cast<int>(lds)) != hipSuccess) {
+    (void)hipGetLastError();
+  } else if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kBlock, static_cast<size_t>(lds)) !=
+             hipSuccess) {
+    (void)hipGetLastError();
+    per_cu = 0;
+  }
+  cache[{dev, K}] = per_cu;
+  return per_cu;
+}
+
+template <int S, int SLOTS, int MODE>
+int64_t fused_rs_grid(int64_t K, int64_t P, int blocks_per_cu) {
+  const int per_cu = blocks_per_cu > 0 ? blocks_per_cu : fused_rs_per_cu<S, SLOTS, MODE>(K);
+  const int64_t ntiles = (P + S - 1) / S;
+  const int64_t g = static_cast<int64_t>(per_cu) * cu_count();
+  return ntiles < g ? ntiles : g;
+}
+
+template <int S, int SLOTS, int MODE = 0>
+int launch_fused_rs(const float* clients, int64_t K, int64_t P, int64_t ld, const float* weights, float* out,
+                    double* partials, int64_t partial_elems, double* sumsq, int blocks_per_cu, hipStream_t s,
+                    const char* what) {
+  if ((K * S + 1023) / 1024 > SLOTS)
+    return set_error(FEDAVG_EMODE, "%s: %d slots per thread cover K <= %d at %d columns", what, SLOTS,
+                     SLOTS * 1024 / S, S);
+  const int per_cu = fused_rs_per_cu<S, SLOTS, MODE>(K);
+  if (per_cu <= 0)
+    return set_error(FEDAVG_EMODE, "%s: the %d-column tile does not fit LDS at K = %lld", what, S, (long long)K);
+  if (blocks_per_cu > per_cu)
+    return set_error(FEDAVG_EMODE, "%s: %d workgroups per CU requested, %d resident", what, blocks_per_cu, per_cu);
+  const int64_t ntiles = (P + S - 1) / S;
+  const int64_t grid = fused_rs_grid<S, SLOTS, MODE>(K, P, blocks_per_cu);
+  if (partial_elems < K * grid)
+    return set_error(FEDAVG_EINVAL, "%s: workspace needs %lld doubles", what, (long long)(K * grid));
+  hipLaunchKernelGGL((reduce_sqdist_rs_kernel<S, SLOTS, MODE>), dim3(static_cast<unsigned>(grid)), dim3(kBlock),
+                     static_cast<unsigned>(fused_rs_lds_bytes(K, S)), s, clients, static_cast<int>(K), ld, P, ntiles,
+                     weights, out, partials);
+  int rc = launch_status(what);
+  if (rc || MODE != 0) return rc;
+  hipLaunchKernelGGL(client_sqdist_finalize_kernel, dim3(static_cast<unsigned>(K)), dim3(kBlock), 0, s, partials, grid,
+                     sumsq);
+  return launch_status(what);
+}
+
 // Global-pointer schedule (the fp64/fp16/bf16 passes and the probe
 // variants): 32 x 16-B loads in flight per thread (U4 x C8) in one launch;
 // scripts/dist_variants.py (profiles/sweeps/r01_dist_*.jsonl) measured
@@ -944,6 +1135,26 @@ int fedavg_reduce_sqdist_f32_variant(const float* clients, int64_t K, int64_t P,
                                                           sumsq, blocks_per_cu, s, what);
     case 101064: return launch_fused<64, true, 0, true>(clients, K, P, ld, weights, out, workspace, workspace_elems,
                                                         sumsq, blocks_per_cu, s, what);
+    // register-staged tiles (reduce_sqdist_rs_kernel): 200000 + S; 210000 + S
+    // with the slots of K = 100 at 128 / 256 columns; + 100000: loads only,
+    // + 200000: loads + LDS writes (traffic probes, wrong results)
+#define FEDAVG_RS_CASE(CODE, C, SL, MODE)                                                                         \
+  case CODE:                                                                                                     \
+    return launch_fused_rs<C, SL, MODE>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq,      \
+                                        blocks_per_cu, s, what);
+    FEDAVG_RS_CASE(200032, 32, 10, 0)
+    FEDAVG_RS_CASE(200064, 64, 8, 0)
+    FEDAVG_RS_CASE(200128, 128, 8, 0)
+    FEDAVG_RS_CASE(200256, 256, 8, 0)
+    FEDAVG_RS_CASE(210128, 128, 13, 0)
+    FEDAVG_RS_CASE(210256, 256, 25, 0)
+    FEDAVG_RS_CASE(300064, 64, 8, 1)
+    FEDAVG_RS_CASE(310128, 128, 13, 1)
+    FEDAVG_RS_CASE(310256, 256, 25, 1)
+    FEDAVG_RS_CASE(400064, 64, 8, 2)
+    FEDAVG_RS_CASE(410128, 128, 13, 2)
+    FEDAVG_RS_CASE(410256, 256, 25, 2)
+#undef FEDAVG_RS_CASE
     default: return set_error(FEDAVG_EMODE, "%s: cols must be 32, 64, 128 or 256 (+1000: double-buffered)", what);
   }
 }

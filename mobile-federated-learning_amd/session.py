@@ -194,12 +194,16 @@ class RoundSession:
         sums = {}
         t0 = time.perf_counter()
         with torch.cuda.device(self.dev):
+            # weights, reduce and the staging's release all on the stream
+            # current at finish() (reduce_and_fetch launches there), which
+            # need not be the one current at begin_round
+            cur = torch.cuda.current_stream(self.dev)
             d2h = self.agg._d2h_stream_for()
             for g in self.table.groups.values():
                 st = self._staging[g.dtype]
                 # the staging's own pinned weight buffer: no pinned allocation
                 # inside finish (a fresh one costs milliseconds to issue)
-                w_dev = st.upload_weights(weights, self._compute)
+                w_dev = st.upload_weights(weights, cur)
                 out_dev, out_host = reduce_and_fetch(st.dev[:K], w_dev, g.P,
                                                      d2h, ready=self._ready[g.dtype],
                                                      out_host=self._out_host.get(g.dtype), sums=sums)
@@ -207,8 +211,8 @@ class RoundSession:
                 dev_state[g.dtype] = (st.dev[:K], out_dev)
             t1 = time.perf_counter()
             d2h.synchronize()
-            self._compute.synchronize()
-            self._compute.wait_stream(self._copy)  # nothing else may reuse the staging before its copies end
+            cur.synchronize()
+            cur.wait_stream(self._copy)  # nothing else may reuse the staging before its copies end
         t2 = time.perf_counter()
         for g, out_host in outs:
             for name, t in self.table.unpack(g, out_host).items():
@@ -226,14 +230,15 @@ class RoundSession:
         st = self._staging[torch.float32]
         w64 = np.array([float(w) for w in weights], dtype=np.float64)
         with torch.cuda.device(self.dev):
-            self._compute.wait_stream(self._copy)  # earlier users of the device staging are done
+            cur = torch.cuda.current_stream(self.dev)
+            cur.wait_stream(self._copy)  # earlier users of the device staging are done
             st._w_done.synchronize()  # the native call rewrites w_host: an async device round may still read it
             out_dev = torch.empty(g.P, dtype=torch.float32, device=self.dev)
             out_host = torch.empty(g.P, dtype=torch.float32, pin_memory=True)
             _lib.check(self._lib.fedavg_round_f32(None, 0, st.host.data_ptr(), st.dev.data_ptr(), K, g.P, g.ld,
                                                   w64.ctypes.data, st.w_host.data_ptr(), st.w_dev.data_ptr(),
                                                   out_dev.data_ptr(), out_host.data_ptr(), self._threads,
-                                                  self._compute.cuda_stream), "fedavg_round_f32")
+                                                  cur.cuda_stream), "fedavg_round_f32")
         for name, t in self.table.unpack(g, out_host).items():
             acc_dict[name] = t
         return self._close(K, {torch.float32: (st.dev[:K], out_dev)}, acc_dict)
@@ -246,10 +251,11 @@ class RoundSession:
         dev_state = {}
         sums = {}
         with torch.cuda.device(self.dev):
-            self._compute.wait_stream(self._copy)  # every client's packing kernel
+            cur = torch.cuda.current_stream(self.dev)  # the reduce runs here, so the weights go here too
+            cur.wait_stream(self._copy)  # every client's packing kernel
             for g in self.table.groups.values():
                 st = self._staging[g.dtype]
-                w_dev = st.upload_weights(weights, self._compute)
+                w_dev = st.upload_weights(weights, cur)
                 out_dev = torch.empty(g.P, dtype=g.dtype, device=self.dev)
                 parts = []
                 reduce_rows(st.dev[:K], w_dev, g.P, out_dev, parts)

@@ -35,7 +35,7 @@ def _run_bench(*args, timeout=180):
                           timeout=timeout, env=env, cwd=str(ROOT))
 
 
-@pytest.mark.parametrize("n", [2, 3])
+@pytest.mark.parametrize("n", [2, 3, 8])
 def test_self_launch_starts_n_ranks_and_relays_one_json_line(n):
     r = _run_bench("--gpus", str(n), "--launch-check")
     assert r.returncode == 0, r.stderr[-2000:]
@@ -124,7 +124,7 @@ def _parity_worker(rank, ws, port, K, P, chunks, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("ws,K,P,chunks", [(2, 5, 10_007, 3), (2, 12, 4_099, 1)])
+@pytest.mark.parametrize("ws,K,P,chunks", [(2, 5, 10_007, 3), (2, 12, 4_099, 1), (8, 4, 60_013, 3)])
 def test_bench_parity_and_reassembly_checks_gloo(ws, K, P, chunks):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -132,7 +132,7 @@ def test_bench_parity_and_reassembly_checks_gloo(ws, K, P, chunks):
     procs = [ctx.Process(target=_parity_worker, args=(r, ws, port, K, P, chunks, q)) for r in range(ws)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=180) for _ in range(ws)]
+    res = [q.get(timeout=300) for _ in range(ws)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0

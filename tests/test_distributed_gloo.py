@@ -55,7 +55,9 @@ def _worker(rank, ws, port, K, P, chunks, seed, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("ws,K,P,chunks", [(2, 5, 1001, 1), (2, 7, 4096, 3), (3, 4, 777, 2), (2, 1, 65, 1)])
+@pytest.mark.parametrize("ws,K,P,chunks", [(2, 5, 1001, 1), (2, 7, 4096, 3), (3, 4, 777, 2), (2, 1, 65, 1),
+                                            # the driver's 8-GPU shape: 8 ranks, uneven last block, 3 and 5 chunks
+                                            (8, 5, 100_003, 3), (8, 3, 40_961, 5), (8, 2, 130, 1)])
 def test_sharded_reduce_allgather_matches_oracle(ws, K, P, chunks):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -63,7 +65,7 @@ def test_sharded_reduce_allgather_matches_oracle(ws, K, P, chunks):
     procs = [ctx.Process(target=_worker, args=(r, ws, port, K, P, chunks, 11 + P, q)) for r in range(ws)]
     for p in procs:
         p.start()
-    results = [q.get(timeout=120) for _ in range(ws)]
+    results = [q.get(timeout=240) for _ in range(ws)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -107,7 +109,7 @@ def _worker_host_out(rank, ws, port, K, P, chunks, seed, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("ws,K,P,chunks", [(2, 5, 1001, 1), (3, 4, 4099, 3)])
+@pytest.mark.parametrize("ws,K,P,chunks", [(2, 5, 1001, 1), (3, 4, 4099, 3), (8, 3, 50_001, 3)])
 def test_sharded_reduce_host_out_matches_oracle(ws, K, P, chunks):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -116,7 +118,7 @@ def test_sharded_reduce_host_out_matches_oracle(ws, K, P, chunks):
     procs = [ctx.Process(target=_worker_host_out, args=(r, ws, port, K, P, chunks, seed, q)) for r in range(ws)]
     for p in procs:
         p.start()
-    parts = dict(q.get(timeout=120) for _ in range(ws))
+    parts = dict(q.get(timeout=240) for _ in range(ws))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0

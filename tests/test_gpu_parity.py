@@ -677,6 +677,58 @@ def test_round_session_streaming_matches_golden(small_bytes):
     assert small_seen >= (4 if small_bytes is None else 0)
 
 
+@pytest.mark.parametrize("small_bytes", [None, 0])
+def test_round_session_finish_under_side_stream(small_bytes):
+    """begin_round on the default stream, finish() under another one: the
+    weights must be uploaded on the stream the reduce runs on (a previous
+    round's weights, or the warm-up's 1/K, would otherwise be read).  Several
+    rounds with different sample counts on one aggregator, the weight copy
+    held back by a busy side stream."""
+    _, w_locals, expected = load_case("mnist_lr_k10")
+    for big in (False, True):
+        agg = mfl_amd.DeviceAggregator(DEV)
+        if small_bytes is not None:
+            agg.SMALL_ROUND_BYTES = small_bytes
+        if big:  # a multi-chunk row (reduce_and_fetch path): one 4.2M-column key
+            g = torch.Generator().manual_seed(5)
+            base = torch.randn(4_194_304 + 5, generator=g) * 0.05
+            rounds = []
+            for r in range(3):
+                counts = [int(c) for c in torch.randint(1, 1000, (4,), generator=g)]
+                dl = [(n, {"w": base + 1e-3 * torch.randn(base.numel(), generator=g)}) for n in counts]
+                exp = torch.from_numpy(O.reduce_f32(np.stack([d["w"].numpy() for _, d in dl]),
+                                                    O.sample_weights(counts)))
+                rounds.append((dl, {"w": exp}))
+        else:
+            rounds = []
+            for r in range(3):  # same rows, permuted sample counts: different weights per round
+                perm = np.random.default_rng(r).permutation(len(w_locals))
+                dl = [(w_locals[int(p)][0], {k: v.clone() for k, v in w_locals[i][1].items()})
+                      for i, p in enumerate(perm)]
+                counts = [n for n, _ in dl]
+                flat_keys = list(expected)
+                rows = np.stack([np.concatenate([d[k].reshape(-1).numpy().astype(np.float32) for k in flat_keys])
+                                 for _, d in dl])
+                ref = O.reduce_f32(rows, O.sample_weights(counts))
+                exp, off = {}, 0
+                for k in flat_keys:
+                    n = expected[k].numel()
+                    exp[k] = torch.from_numpy(ref[off:off + n].copy()).reshape(expected[k].shape)
+                    off += n
+                rounds.append((dl, exp))
+        side = torch.cuda.Stream(DEV)
+        for dl, exp in rounds:
+            sess = agg.begin_round(dl[0][1], len(dl))
+            for n, sd in dl:
+                sess.add(n, sd)
+            with torch.cuda.stream(side):
+                torch.cuda._sleep(2_000_000)  # the side stream is busy when finish() enqueues on it
+                out = sess.finish(dl)
+            torch.cuda.synchronize(DEV)
+            for k, e in exp.items():
+                assert_bits(out[k], e, f"side-stream finish {k}")
+
+
 def test_round_session_checks_w_locals():
     _, w_locals, _ = load_case("mnist_lr_k10")
     agg = mfl_amd.DeviceAggregator(DEV)
