@@ -128,25 +128,30 @@ def auto_chunks(K: int, shard_cols: int, world: int, host_out: bool) -> int:
 
 
 def _thread_count():
-    """Host threads for the CPU baseline: the CPUs this process may run on
-    (sched_getaffinity), capped by OMP_NUM_THREADS when the box sets it (the
-    GPU box gives each 1-GPU job a 16-CPU share of a larger machine)."""
+    """Host threads for the CPU baseline: BASELINE.md's plan times the
+    reference loop with torch.set_num_threads(len(os.sched_getaffinity(0)));
+    the GPU box also sets OMP_NUM_THREADS (its 1-GPU job share of a larger
+    machine), timed as a second, labelled entry.  Returns (affinity CPUs,
+    OMP-capped count or None when there is no cap below the affinity)."""
     n_aff = len(os.sched_getaffinity(0))
     omp = env_int("OMP_NUM_THREADS", 0)
-    return (min(n_aff, omp) if omp > 0 else n_aff), n_aff
+    return n_aff, (omp if 0 < omp < n_aff else None)
 
 
-def cpu_baseline(P: int, flat_seconds: float = 10.0, model_seconds: float = 5.0):
+def cpu_baseline(K: int, P: int, flat_seconds: float = 8.0, model_seconds: float = 4.0):
     """The reference's torch CPU loop (fedavg_trainer.py:444-458, restated in
-    oracle/fedavg_oracle.py) on bounded samples, with as many torch threads
-    as the host gives this process:
+    oracle/fedavg_oracle.py) on the GPU box's host cores, per BASELINE.md's
+    CPU-baseline plan:
 
-    * flat: a K-slice -- 10 clients with the workload's full P-element key
-      (1 GB at P = 25M), so every tensor has the workload's size and cache
-      behaviour; repeated for ~flat_seconds.  This is ``value``.
-    * model-shaped: cfg3's resnet56 state_dict (350 keys, 58 int64
+    * flat: the workload itself -- K clients with one P-element fp32 key
+      (100 x 25M = 10 GB of host tensors at the target), best of a few reps,
+      ``torch.set_num_threads(len(os.sched_getaffinity(0)))``.  This is
+      ``value``; the same with the OMP_NUM_THREADS cap the box sets is a
+      second entry (``layouts``).
+    * model-shaped: cfg3's resnet56 state_dicts (350 keys, 58 int64
       num_batches_tracked buffers), all 100 clients -- the per-key dispatch
-      cost the reference pays on real models (slowest layout)."""
+      cost the reference pays on real models (slowest layout), at
+      the affinity thread count."""
     import torch
 
     sys.path.insert(0, str(ROOT / "oracle"))
@@ -154,8 +159,8 @@ def cpu_baseline(P: int, flat_seconds: float = 10.0, model_seconds: float = 5.0)
     import fedavg_oracle as O
     from model_shapes import CONFIGS, numel
 
-    threads, n_aff = _thread_count()
-    torch.set_num_threads(threads)
+    n_aff, n_omp = _thread_count()
+    torch.set_num_threads(n_omp or n_aff)  # generation at the box's own share
 
     def timed(w_locals_factory, seconds):
         times = []
@@ -171,42 +176,53 @@ def cpu_baseline(P: int, flat_seconds: float = 10.0, model_seconds: float = 5.0)
 
     from mfl_amd.synthetic import sample_counts
 
-    K = 10
     g = torch.Generator().manual_seed(0)
     base = torch.randn(P, generator=g) * 0.05
-    clients = [base + torch.randn(P, generator=g) * 1e-3 for _ in range(K)]
+    shift = 7919
+    noise = torch.randn(P + K * shift, generator=g) * 1e-3
+    rows = torch.empty((K, P))  # client i = base + a shifted window of one noise vector (timing data)
+    for i in range(K):
+        torch.add(base, noise[i * shift:i * shift + P], out=rows[i])
+    del noise
     counts = sample_counts(K)
-    best, reps = timed(lambda: [(counts[i], {"w": clients[i]}) for i in range(K)], flat_seconds)
-    del clients, base
-    flat = {"layout": "flat", "value": round(algorithmic_bytes(K, P) / best / 1e9, 3), "unit": "GB/s",
-            "sample": f"K-slice: K={K} x P={P} fp32, one flat key; best of {reps} reps after 1 warm-up, "
-                      f"{best * 1e3:.1f} ms/reduce"}
-
+    layouts = []
+    for label, n in (("affinity", n_aff), ("OMP_NUM_THREADS", n_omp)):
+        if n is None:
+            continue
+        torch.set_num_threads(n)
+        best, reps = timed(lambda: [(counts[i], {"w": rows[i]}) for i in range(K)], flat_seconds)
+        layouts.append({"layout": "flat", "threads": n, "threads_from": label,
+                        "value": round(algorithmic_bytes(K, P) / best / 1e9, 3), "unit": "GB/s",
+                        "sample": f"the workload: K={K} x P={P} fp32, one flat key per client; best of {reps} "
+                                  f"reps after 1 warm-up, {best * 1e3:.1f} ms/reduce, {n} torch threads"})
+    del rows, base
+    torch.set_num_threads(n_aff)
     Km, shapes = CONFIGS["resnet56"]
     Pm = numel(shapes)
-    base = {k: torch.randn(s, generator=g) * 0.05 for k, s in shapes}
+    mbase = {k: torch.randn(s, generator=g) * 0.05 for k, s in shapes}
     dicts = []
     for i in range(Km):
         sd = {}
         for k, s in shapes:
             sd[k] = (torch.tensor(1000 + i, dtype=torch.int64) if k.endswith("num_batches_tracked")
-                     else base[k] + torch.randn(s, generator=g) * 1e-3)
+                     else mbase[k] + torch.randn(s, generator=g) * 1e-3)
         dicts.append(sd)
     mcounts = sample_counts(Km)
     best_m, reps_m = timed(lambda: [(mcounts[0], dict(dicts[0]))] + list(zip(mcounts[1:], dicts[1:])), model_seconds)
-    model = {"layout": "model-shaped (resnet56)", "value": round(algorithmic_bytes(Km, Pm) / best_m / 1e9, 3),
-             "unit": "GB/s",
-             "sample": f"cfg3 resnet56 state_dicts: K={Km} x P={Pm}, {len(shapes)} keys; best of {reps_m} reps "
-                       f"after 1 warm-up, {best_m * 1e3:.1f} ms/reduce"}
+    layouts.append({"layout": "model-shaped (resnet56)", "threads": n_aff, "threads_from": "affinity",
+                    "value": round(algorithmic_bytes(Km, Pm) / best_m / 1e9, 3), "unit": "GB/s",
+                    "sample": f"cfg3 resnet56 state_dicts: K={Km} x P={Pm}, {len(shapes)} keys; best of {reps_m} "
+                              f"reps after 1 warm-up, {best_m * 1e3:.1f} ms/reduce, {n_aff} torch threads"})
+    flat = layouts[0]
     return {
         "value": flat["value"],
         "unit": "GB/s",
-        "cores": threads,
+        "cores": n_aff,
         "kind": "port",
-        "sample": flat["sample"] + " (value); reference torch CPU loop restated (oracle/fedavg_oracle.py "
-                                   "aggregate_torch)",
+        "sample": flat["sample"] + " (value; torch.set_num_threads(len(os.sched_getaffinity(0))), BASELINE.md); "
+                                   "reference torch CPU loop restated (oracle/fedavg_oracle.py aggregate_torch)",
         "affinity_cpus": n_aff,
-        "layouts": [flat, model],
+        "layouts": layouts,
     }
 
 
@@ -755,7 +771,9 @@ def main(argv=None):
             except Exception as e:  # noqa: BLE001
                 out["round_with_distances"] = {"error": f"{type(e).__name__}: {e}"}
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(min(P_global, 25_000_000))
+            # the workload's own K x P while its rows fit a bounded host sample
+            # (<= 10 GB: the target); cfg5's 400 GB is timed on a P-slice
+            out["cpu_baseline"] = cpu_baseline(K, min(P_global, 10_000_000_000 // (4 * K)))
         print(json.dumps(out), flush=True)
     if use_pg:
         dist.barrier()

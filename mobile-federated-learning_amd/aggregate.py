@@ -964,13 +964,74 @@ class FedAvgAggregateMixin:
         return aggregate(w_locals, getattr(self, "model_global", None), self.fedavg_device)
 
 
-def install(trainer_cls, device: Optional[torch.device] = None):
-    """Patch ``trainer_cls.aggregate`` (e.g. the reference ``FedAvgTrainer``) in place."""
+def _feed_of(trainer, device):
+    """The trainer's ClientFeed (autostream), created on first use."""
+    from .autostream import ClientFeed
+
+    feed = trainer.__dict__.get("_mfl_feed")
+    if feed is None:
+        clients = getattr(trainer, "client_list", None)  # fedavg_trainer.py:88: the Client objects of a round
+        max_clients = len(clients) if clients else 128
+        feed = ClientFeed(lambda: default_aggregator(device), max_clients)
+        trainer.__dict__["_mfl_feed"] = feed
+    return feed
+
+
+def install(trainer_cls, device: Optional[torch.device] = None, client_cls=None, stream_clients: Optional[bool] = None):
+    """Patch ``trainer_cls.aggregate`` (e.g. the reference ``FedAvgTrainer``) in place.
+
+    With ``stream_clients`` (default: on unless ``FEDAVG_STREAM_CLIENTS=0``)
+    also wrap ``trainer_cls.train`` (the round loop, fedavg_trainer.py:95) and
+    ``client_cls.train`` (client.py:38; default: the ``Client`` that
+    ``trainer_cls``'s module imported) so each valid client result is packed
+    and uploaded while the loop goes on, and ``aggregate`` at :217 only
+    reduces (autostream.py; falls back to the plain path whenever
+    ``w_locals`` is not what was streamed)."""
+    from . import autostream
+
+    if stream_clients is None:
+        stream_clients = autostream.enabled()
+    if client_cls is None:
+        import sys
+
+        client_cls = getattr(sys.modules.get(trainer_cls.__module__), "Client", None)
+    streaming = bool(stream_clients) and client_cls is not None and hasattr(trainer_cls, "train")
 
     def aggregate_method(self, w_locals):
+        feed = self.__dict__.get("_mfl_feed") if streaming else None
+        if feed is not None and autostream.active_trainer() is self:
+            out = feed.take(w_locals)
+            if out is not None:
+                return out
         return aggregate(w_locals, getattr(self, "model_global", None), device)
 
     aggregate_method.__doc__ = FedAvgAggregateMixin.aggregate.__doc__
     aggregate_method.__wrapped_reference__ = getattr(trainer_cls, "aggregate", None)
     trainer_cls.aggregate = aggregate_method
+    if not streaming or getattr(trainer_cls.train, "__mfl_stream__", False):
+        return trainer_cls
+    loop = trainer_cls.train
+
+    def train_method(self, *args, **kwargs):  # fedavg_trainer.py:95, the round loop
+        with autostream.trainer_scope(self):
+            return loop(self, *args, **kwargs)
+
+    train_method.__doc__ = loop.__doc__
+    train_method.__mfl_stream__ = True
+    train_method.__wrapped_reference__ = loop
+    trainer_cls.train = train_method
+    if not getattr(client_cls.train, "__mfl_stream__", False):
+        client_train = client_cls.train
+
+        def client_train_method(self, *args, **kwargs):  # client.py:38
+            res = client_train(self, *args, **kwargs)
+            trainer = autostream.active_trainer()
+            if trainer is not None and autostream.valid_train_result(res):  # fedavg_trainer.py:190
+                _feed_of(trainer, device).feed(self.get_sample_number(), res[0])
+            return res
+
+        client_train_method.__doc__ = client_train.__doc__
+        client_train_method.__mfl_stream__ = True
+        client_train_method.__wrapped_reference__ = client_train
+        client_cls.train = client_train_method
     return trainer_cls

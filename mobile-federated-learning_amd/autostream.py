@@ -1,0 +1,239 @@
+"""Zero-edit streaming: each client's upload overlaps the round loop.
+
+The reference trains the selected clients one after another
+(fedavg_trainer.py:172-214): ``client.train`` at :189 returns
+``net.cpu().state_dict()`` (client.py:96), a valid result (:190) is appended
+as ``(client.get_sample_number(), copy.deepcopy(w))`` at :199, and only at
+:217 does ``self.aggregate(w_locals)`` see the round.  A drop-in that patches
+``aggregate`` alone therefore packs and uploads all K clients at :217: at
+100 clients x 25M parameters that is 10 GB over PCIe on the round's critical
+path (178.8 ms).
+
+``install`` (aggregate.py) also wraps ``Client.train`` and
+``FedAvgTrainer.train``, so the unchanged loop streams:
+
+* while ``FedAvgTrainer.train`` runs, every valid ``Client.train`` result --
+  the same validity test as :190 -- is handed to a per-trainer
+  :class:`ClientFeed` together with ``client.get_sample_number()``; a
+  background thread packs it into pinned staging and starts its H2D
+  (``RoundSession.add``) while the loop deep-copies it (:199) and the next
+  client trains;
+* the patched ``aggregate(w_locals)`` waits for the feed to drain, checks
+  that ``w_locals`` is what was fed -- same count, the same sample numbers in
+  order, the same key set, and bit-identical values at sampled positions of
+  the largest, first and last keys (compared while the reduce runs) -- and
+  then only the weights, the kernel and the result's D2H remain.
+
+Anything else falls back to the plain drop-in on ``w_locals`` (same bits,
+the reference's exceptions): a count or sample-number mismatch, a retried
+client the loop did not append, a key-table change, device-resident
+clients, more clients than the trainer's ``client_list``, any error inside
+the feed, or ``FEDAVG_STREAM_CLIENTS=0``.
+"""
+from __future__ import annotations
+
+import os
+import queue
+import threading
+from typing import Optional
+
+import torch
+
+__all__ = ["ClientFeed", "enabled", "valid_train_result", "active_trainer", "trainer_scope"]
+
+_tls = threading.local()
+
+
+def enabled() -> bool:
+    return os.environ.get("FEDAVG_STREAM_CLIENTS", "1") != "0"
+
+
+def valid_train_result(res) -> bool:
+    """fedavg_trainer.py:190: ``loss``, ``local_beta``, ``local_rho`` and
+    ``local_acc`` all not None (a diverged client returns Nones, client.py:71-73)."""
+    try:
+        _, loss, beta, rho, acc = res[0], res[1], res[2], res[3], res[4]
+    except (TypeError, IndexError, KeyError):
+        return False
+    return loss is not None and beta is not None and rho is not None and acc is not None
+
+
+def active_trainer():
+    """The trainer whose ``train()`` (the round loop) is running on this thread."""
+    return getattr(_tls, "trainer", None)
+
+
+class trainer_scope:
+    """``with trainer_scope(trainer):`` -- Client.train results on this thread feed ``trainer``."""
+
+    def __init__(self, trainer):
+        self.trainer = trainer
+
+    def __enter__(self):
+        self.prev = getattr(_tls, "trainer", None)
+        _tls.trainer = self.trainer
+        return self.trainer
+
+    def __exit__(self, *exc):
+        _tls.trainer = self.prev
+        feed = self.trainer.__dict__.get("_mfl_feed")
+        if feed is not None:
+            feed.close()
+        return False
+
+
+def _bits(t: torch.Tensor):
+    """The elements of a host tensor as a flat integer numpy view (bit patterns)."""
+    size = t.element_size()
+    ity = {1: torch.uint8, 2: torch.int16, 4: torch.int32, 8: torch.int64}[size]
+    flat = t.reshape(-1)
+    if t.dtype == torch.bool:
+        flat = flat.view(torch.uint8)
+    elif t.dtype != ity:
+        flat = flat.view(ity)
+    return flat.numpy()
+
+
+class ClientFeed:
+    """One trainer's streaming state: at most one open ``RoundSession`` (the
+    round being fed), filled by a background thread."""
+
+    SAMPLE_KEYS = 4  # keys compared per client (largest, first, last, middle)
+
+    def __init__(self, aggregator_fn, max_clients: int):
+        self._aggregator_fn = aggregator_fn  # () -> DeviceAggregator (created lazily, on first use)
+        self.max_clients = max(1, int(max_clients))
+        self.session = None
+        self.broken = False
+        self.fed = []  # (sample_num, dict) in feed order, as the worker received them
+        self._q: Optional[queue.Queue] = None
+        self._worker: Optional[threading.Thread] = None
+        self._err: Optional[BaseException] = None
+        self.stats = {"rounds_streamed": 0, "rounds_fallback": 0, "last_fallback": ""}
+
+    # -- producer side (Client.train wrapper) ---------------------------------
+    def feed(self, sample_num, state_dict) -> None:
+        if self.broken:
+            return
+        if len(self.fed) >= self.max_clients or not self._host_dict(state_dict):
+            self._break("more clients than max_clients" if len(self.fed) >= self.max_clients
+                        else "not a host state_dict")
+            return
+        self.fed.append((sample_num, state_dict))
+        if self._worker is None:
+            self._q = queue.Queue()
+            self._worker = threading.Thread(target=self._run, name="mfl-client-feed", daemon=True)
+            self._worker.start()
+        self._q.put((sample_num, state_dict))
+
+    @staticmethod
+    def _host_dict(sd) -> bool:
+        try:
+            return all(isinstance(v, torch.Tensor) and v.device.type == "cpu" for v in sd.values())
+        except AttributeError:
+            return False
+
+    def _run(self):
+        while True:
+            item = self._q.get()
+            if item is None:
+                self._q.task_done()
+                return
+            try:
+                if not self.broken and self._err is None:
+                    n, sd = item
+                    if self.session is None:
+                        self.session = self._aggregator_fn().begin_round(sd, self.max_clients)
+                    self.session.add(n, sd)
+            except BaseException as e:  # noqa: BLE001 -- any failure means: fall back at aggregate
+                self._err = e
+            finally:
+                self._q.task_done()
+
+    def _drain(self):
+        if self._q is not None:
+            self._q.join()
+
+    def _break(self, why: str):
+        self.broken = True
+        self.stats["last_fallback"] = why
+
+    # -- consumer side (patched aggregate) --------------------------------------
+    def take(self, w_locals):
+        """The streamed result for ``w_locals``, or None (the caller runs the
+        plain drop-in).  Always leaves the feed empty for the next round."""
+        try:
+            self._drain()
+            sess = self.session
+            why = self._mismatch(w_locals, sess)
+            if why:
+                self.stats["last_fallback"] = why
+                self.stats["rounds_fallback"] += 1
+                return None
+            out = sess.finish(w_locals, verify=lambda: self._same_values(w_locals))
+            if out is None:
+                self.stats["last_fallback"] = "sampled values differ from the fed clients"
+                self.stats["rounds_fallback"] += 1
+            else:
+                self.stats["rounds_streamed"] += 1
+            return out
+        finally:
+            self._reset()
+
+    def _mismatch(self, w_locals, sess) -> str:
+        if self.broken:
+            return self.stats["last_fallback"] or "feed broken"
+        if self._err is not None:
+            return f"feed error: {self._err!r}"
+        if sess is None:
+            return "nothing fed"
+        if type(w_locals) is not list or len(w_locals) != len(self.fed) or len(sess.counts) != len(self.fed):
+            return "client count differs from the fed clients"
+        for (n, _), (n2, _) in zip(w_locals, self.fed):
+            if n != n2:
+                return "sample numbers differ from the fed clients"
+        return ""
+
+    def _same_values(self, w_locals) -> bool:
+        """Key sets equal and sampled element bits equal, client by client."""
+        fed0 = self.fed[0][1]
+        names = list(fed0.keys())
+        if not names:
+            return False
+        big = max(names, key=lambda k: fed0[k].numel())
+        picks = list(dict.fromkeys([big, names[0], names[-1], names[len(names) // 2]]))[:self.SAMPLE_KEYS]
+        pos = {}
+        for k in picks:
+            n = fed0[k].numel()
+            pos[k] = sorted({0, n - 1, n // 2, (n * 7) // 13, (n * 5) // 11})
+        for (_, sd), (_, fd) in zip(w_locals, self.fed):
+            if sd.keys() != fd.keys():
+                return False
+            for k in picks:
+                a, b = sd[k], fd[k]
+                if not isinstance(a, torch.Tensor) or a.dtype != b.dtype or a.shape != b.shape or a.is_cuda:
+                    return False
+                if not (_bits(a)[pos[k]] == _bits(b)[pos[k]]).all():
+                    return False
+        return True
+
+    def _reset(self):
+        sess = self.session
+        if sess is not None and not sess._finished:
+            sess.abandon()
+        self.session = None
+        self.fed = []
+        self.broken = False
+        self._err = None
+
+    def close(self):
+        """End of the round loop: abandon an open round, stop the worker."""
+        try:
+            self._drain()
+        finally:
+            self._reset()
+            if self._worker is not None:
+                self._q.put(None)
+                self._worker.join(timeout=60)
+                self._worker = None
+                self._q = None

@@ -598,7 +598,12 @@ int launch_fused(const float* clients, int64_t K, int64_t P, int64_t ld, const f
 //      in a fixed order at the end: partials[row][workgroup].
 // MODE 1 / 2 are traffic probes (1: loads only; 2: loads + LDS writes).
 // ---------------------------------------------------------------------------
-template <int S, int SLOTS, int MODE = 0>
+// FLAGS (probes): 1 = TILED buffer [ntiles][K][S] (each tile's rows contiguous);
+// 2 = the workgroups of one XCD take contiguous tiles of a sweep (dispatch
+// puts workgroup b on XCD b % 8); 4 = and the workgroups of one CU too
+// (b, b + 256, ... share a CU).  Both remaps are bijections of the sweep: a
+// different placement only changes the speed.
+template <int S, int SLOTS, int MODE = 0, int FLAGS = 0>
 __global__ __launch_bounds__(kBlock) void reduce_sqdist_rs_kernel(const float* __restrict__ X, int K, int64_t ld,
                                                                   int64_t P, int64_t ntiles,
                                                                   const float* __restrict__ W,
@@ -612,8 +617,10 @@ __global__ __launch_bounds__(kBlock) void reduce_sqdist_rs_kernel(const float* _
   const int t = threadIdx.x;
   const int r0 = t / V, sl = t % V;
   const int nslot = r0 < K ? (K - r0 + R - 1) / R : 0;  // slots of this thread that hold a row
-  const char* p0 = reinterpret_cast<const char*>(X) + (static_cast<int64_t>(r0) * ld + 4 * sl) * 4;
-  const int64_t mstride = static_cast<int64_t>(R) * ld * 4;
+  constexpr bool TILED = (FLAGS & 1) != 0;
+  const int64_t rstride = TILED ? S : ld;  // TILED: ld unused
+  const char* p0 = reinterpret_cast<const char*>(X) + (static_cast<int64_t>(r0) * rstride + 4 * sl) * 4;
+  const int64_t mstride = static_cast<int64_t>(R) * rstride * 4;
   f32x4* tile4 = reinterpret_cast<f32x4*>(lds);
   f32x4 xs[SLOTS];
   double acc[SLOTS];
@@ -624,15 +631,25 @@ __global__ __launch_bounds__(kBlock) void reduce_sqdist_rs_kernel(const float* _
   // end are not loaded: the last row's would run off the allocation)
   const auto issue = [&](int64_t tt) {
     const int64_t c0 = tt * S;
-    const char* p = p0 + c0 * 4;
+    const char* p = p0 + (TILED ? tt * K * S : c0) * 4;
     const bool slice_ok = c0 + 4 * sl < P;
 #pragma unroll
     for (int m = 0; m < SLOTS; ++m)
       if (m < nslot && slice_ok) xs[m] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p + m * mstride));
   };
 
-  if (static_cast<int64_t>(blockIdx.x) < ntiles) issue(blockIdx.x);
-  for (int64_t tt = blockIdx.x; tt < ntiles; tt += gridDim.x) {
+  int64_t first = blockIdx.x;  // this workgroup's position in every sweep of gridDim.x tiles
+  if constexpr ((FLAGS & 6) != 0) {
+    const int64_t b = blockIdx.x, per_xcd = gridDim.x / 8;
+    if constexpr ((FLAGS & 4) != 0) {
+      const int64_t j = b / 8, per_cu = per_xcd / 32;
+      first = (b % 8) * per_xcd + (j % 32) * per_cu + j / 32;
+    } else {
+      first = (b % 8) * per_xcd + b / 8;
+    }
+  }
+  if (first < ntiles) issue(first);
+  for (int64_t tt = first; tt < ntiles; tt += gridDim.x) {
     const int64_t c0 = tt * S;
     const int ncols = P - c0 < S ? static_cast<int>(P - c0) : S;
     barrier_lds();  // every wave is done with the previous tile
@@ -709,7 +726,7 @@ __global__ __launch_bounds__(kBlock) void reduce_sqdist_rs_kernel(const float* _
 // sums need K * V doubles (= K * S * 2 bytes, inside the tile)
 inline int64_t fused_rs_lds_bytes(int64_t K, int S) { return (K + 1) * S * 4; }
 
-template <int S, int SLOTS, int MODE>
+template <int S, int SLOTS, int MODE, int FLAGS = 0>
 int fused_rs_per_cu(int64_t K) {
   static std::mutex mu;
   static std::map<std::pair<int, int64_t>, int> cache;
@@ -718,7 +735,7 @@ int fused_rs_per_cu(int64_t K) {
   std::lock_guard<std::mutex> lk(mu);
   auto it = cache.find({dev, K});
   if (it != cache.end()) return it->second;
-  const auto kern = reduce_sqdist_rs_kernel<S, SLOTS, MODE>;
+  const auto kern = reduce_sqdist_rs_kernel<S, SLOTS, MODE, FLAGS>;
   const int64_t lds = fused_rs_lds_bytes(K, S);
   int per_cu = 0;
   if (lds > 65536 && hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -734,31 +751,33 @@ int fused_rs_per_cu(int64_t K) {
   return per_cu;
 }
 
-template <int S, int SLOTS, int MODE>
+template <int S, int SLOTS, int MODE, int FLAGS = 0>
 int64_t fused_rs_grid(int64_t K, int64_t P, int blocks_per_cu) {
-  const int per_cu = blocks_per_cu > 0 ? blocks_per_cu : fused_rs_per_cu<S, SLOTS, MODE>(K);
+  const int per_cu = blocks_per_cu > 0 ? blocks_per_cu : fused_rs_per_cu<S, SLOTS, MODE, FLAGS>(K);
   const int64_t ntiles = (P + S - 1) / S;
   const int64_t g = static_cast<int64_t>(per_cu) * cu_count();
   return ntiles < g ? ntiles : g;
 }
 
-template <int S, int SLOTS, int MODE = 0>
+template <int S, int SLOTS, int MODE = 0, int FLAGS = 0>
 int launch_fused_rs(const float* clients, int64_t K, int64_t P, int64_t ld, const float* weights, float* out,
                     double* partials, int64_t partial_elems, double* sumsq, int blocks_per_cu, hipStream_t s,
                     const char* what) {
   if ((K * S + 1023) / 1024 > SLOTS)
     return set_error(FEDAVG_EMODE, "%s: %d slots per thread cover K <= %d at %d columns", what, SLOTS,
                      SLOTS * 1024 / S, S);
-  const int per_cu = fused_rs_per_cu<S, SLOTS, MODE>(K);
+  const int per_cu = fused_rs_per_cu<S, SLOTS, MODE, FLAGS>(K);
   if (per_cu <= 0)
     return set_error(FEDAVG_EMODE, "%s: the %d-column tile does not fit LDS at K = %lld", what, S, (long long)K);
   if (blocks_per_cu > per_cu)
     return set_error(FEDAVG_EMODE, "%s: %d workgroups per CU requested, %d resident", what, blocks_per_cu, per_cu);
   const int64_t ntiles = (P + S - 1) / S;
-  const int64_t grid = fused_rs_grid<S, SLOTS, MODE>(K, P, blocks_per_cu);
+  const int64_t grid = fused_rs_grid<S, SLOTS, MODE, FLAGS>(K, P, blocks_per_cu);
+  if ((FLAGS & 6) != 0 && (cu_count() != 256 || grid != (blocks_per_cu > 0 ? blocks_per_cu : per_cu) * 256LL))
+    return set_error(FEDAVG_EMODE, "%s: the XCD / CU remaps need a full grid on 256 CUs", what);
   if (partial_elems < K * grid)
     return set_error(FEDAVG_EINVAL, "%s: workspace needs %lld doubles", what, (long long)(K * grid));
-  hipLaunchKernelGGL((reduce_sqdist_rs_kernel<S, SLOTS, MODE>), dim3(static_cast<unsigned>(grid)), dim3(kBlock),
+  hipLaunchKernelGGL((reduce_sqdist_rs_kernel<S, SLOTS, MODE, FLAGS>), dim3(static_cast<unsigned>(grid)), dim3(kBlock),
                      static_cast<unsigned>(fused_rs_lds_bytes(K, S)), s, clients, static_cast<int>(K), ld, P, ntiles,
                      weights, out, partials);
   int rc = launch_status(what);
@@ -1155,6 +1174,25 @@ int fedavg_reduce_sqdist_f32_variant(const float* clients, int64_t K, int64_t P,
     FEDAVG_RS_CASE(410128, 128, 13, 2)
     FEDAVG_RS_CASE(410256, 256, 25, 2)
 #undef FEDAVG_RS_CASE
+    // + 1000000: the same over a TILED buffer [ceil(P / S)][K][S] (probe: is the
+    // row-major tile walk limited by the spread of its K row segments?)
+    case 1200064: return launch_fused_rs<64, 8, 0, 1>(clients, K, P, ld, weights, out, workspace, workspace_elems,
+                                                         sumsq, blocks_per_cu, s, what);
+    case 1300064: return launch_fused_rs<64, 8, 1, 1>(clients, K, P, ld, weights, out, workspace, workspace_elems,
+                                                         sumsq, blocks_per_cu, s, what);
+    case 1310128: return launch_fused_rs<128, 13, 1, 1>(clients, K, P, ld, weights, out, workspace,
+                                                         workspace_elems, sumsq, blocks_per_cu, s, what);
+    // + 2000000 / 4000000: XCD-contiguous / XCD- and CU-contiguous tile sweeps
+    case 2200064: return launch_fused_rs<64, 8, 0, 2>(clients, K, P, ld, weights, out, workspace, workspace_elems,
+                                                      sumsq, blocks_per_cu, s, what);
+    case 2300064: return launch_fused_rs<64, 8, 1, 2>(clients, K, P, ld, weights, out, workspace, workspace_elems,
+                                                      sumsq, blocks_per_cu, s, what);
+    case 4200064: return launch_fused_rs<64, 8, 0, 4>(clients, K, P, ld, weights, out, workspace, workspace_elems,
+                                                      sumsq, blocks_per_cu, s, what);
+    case 4300064: return launch_fused_rs<64, 8, 1, 4>(clients, K, P, ld, weights, out, workspace, workspace_elems,
+                                                      sumsq, blocks_per_cu, s, what);
+    case 4200032: return launch_fused_rs<32, 10, 0, 4>(clients, K, P, ld, weights, out, workspace, workspace_elems,
+                                                       sumsq, blocks_per_cu, s, what);
     default: return set_error(FEDAVG_EMODE, "%s: cols must be 32, 64, 128 or 256 (+1000: double-buffered)", what);
   }
 }

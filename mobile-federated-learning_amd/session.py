@@ -54,6 +54,7 @@ class RoundSession:
         self.dicts = []
         self._keepalive = []
         self._finished = False
+        self._verify = None
         self.dev = aggregator.device
         self._lib = _lib.load()
         self._threads = max(1, torch.get_num_threads())
@@ -167,8 +168,26 @@ class RoundSession:
                     events.append(ev)
             self._ready[g.dtype] = events  # the copy stream is FIFO: covers earlier rows too
 
-    def finish(self, w_locals=None):
-        """Reduce the added clients; ``aggregate``'s contract (fedavg_trainer.py:441-458)."""
+    def abandon(self) -> None:
+        """Close the session without a result (its staging is free once the
+        uploads already issued have ended)."""
+        if self._finished:
+            return
+        self._finished = True
+        with torch.cuda.device(self.dev):
+            self._copy.synchronize()
+        self._keepalive.clear()
+        self.table.forget_tensors()
+
+    def finish(self, w_locals=None, verify=None):
+        """Reduce the added clients; ``aggregate``'s contract (fedavg_trainer.py:441-458).
+
+        ``verify`` (optional, for callers whose ``w_locals`` holds COPIES of
+        the added dicts, e.g. the reference's ``copy.deepcopy(w)`` at :199):
+        replaces the identity check of each dict; it is called once the GPU
+        work is issued, while it runs, and a False answer makes finish()
+        return None without touching ``w_locals`` (the caller then takes the
+        plain path)."""
         if self._finished:
             raise RuntimeError("session already finished")
         self._finished = True
@@ -176,8 +195,9 @@ class RoundSession:
             if len(w_locals) != len(self.counts):
                 raise ValueError(f"w_locals has {len(w_locals)} clients, session has {len(self.counts)}")
             for i, ((n, sd), n2, sd2) in enumerate(zip(w_locals, self.counts, self.dicts)):
-                if sd is not sd2 or n != n2:
+                if (verify is None and sd is not sd2) or n != n2:
                     raise ValueError(f"w_locals[{i}] is not the client added as #{i}")
+        self._verify = verify
         if not self.counts:
             raise ValueError("no clients added (the reference returns the global model then: use aggregate([]))")
         K = len(self.counts)
@@ -210,10 +230,15 @@ class RoundSession:
                 outs.append((g, out_host))
                 dev_state[g.dtype] = (st.dev[:K], out_dev)
             t1 = time.perf_counter()
+            ok = self._verify() if self._verify is not None else True  # overlaps the GPU work just issued
             d2h.synchronize()
             cur.synchronize()
             cur.wait_stream(self._copy)  # nothing else may reuse the staging before its copies end
         t2 = time.perf_counter()
+        if not ok:
+            self._keepalive.clear()
+            self.table.forget_tensors()
+            return None
         for g, out_host in outs:
             for name, t in self.table.unpack(g, out_host).items():
                 acc_dict[name] = t
@@ -239,6 +264,10 @@ class RoundSession:
                                                   w64.ctypes.data, st.w_host.data_ptr(), st.w_dev.data_ptr(),
                                                   out_dev.data_ptr(), out_host.data_ptr(), self._threads,
                                                   cur.cuda_stream), "fedavg_round_f32")
+        if self._verify is not None and not self._verify():
+            self._keepalive.clear()
+            self.table.forget_tensors()
+            return None
         for name, t in self.table.unpack(g, out_host).items():
             acc_dict[name] = t
         return self._close(K, {torch.float32: (st.dev[:K], out_dev)}, acc_dict)
@@ -262,7 +291,12 @@ class RoundSession:
                 if parts:
                     sums[g.dtype] = parts[0]
                 dev_state[g.dtype] = (st.dev[:K], out_dev)
-                for name, t in self.table.unpack(g, out_dev).items():
+            if self._verify is not None and not self._verify():
+                self._keepalive.clear()
+                self.table.forget_tensors()
+                return None
+            for g in self.table.groups.values():
+                for name, t in self.table.unpack(g, dev_state[g.dtype][1]).items():
                     acc_dict[name] = t
         return self._close(K, dev_state, acc_dict, sums)
 

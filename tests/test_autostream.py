@@ -1,0 +1,163 @@
+"""Zero-edit streaming (mfl_amd.install wraps Client.train and the round loop)
+on CPU: the feed/fallback decisions, with a stand-in aggregator that records
+what the patched loop hands it.  The GPU runs of the same harness are in
+test_gpu_autostream.py."""
+import sys
+from collections import OrderedDict
+
+import pytest
+import torch
+
+import mfl_amd
+from loop_replay import fresh_classes
+
+AGG_MOD = sys.modules["mfl_amd.aggregate"]
+
+
+class _FakeSession:
+    def __init__(self, template, max_clients):
+        self.keys = list(template.keys())
+        self.max_clients = max_clients
+        self.counts, self.dicts = [], []
+        self._finished = False
+        self.verified = None
+
+    def add(self, n, sd):
+        assert list(sd.keys()) == self.keys
+        self.counts.append(n)
+        self.dicts.append(sd)
+
+    def finish(self, w_locals, verify=None):
+        self._finished = True
+        assert [n for n, _ in w_locals] == self.counts
+        self.verified = verify()
+        if not self.verified:
+            return None
+        out = w_locals[0][1]
+        out["__streamed__"] = torch.tensor(len(self.counts))
+        return out
+
+    def abandon(self):
+        self._finished = True
+
+
+class _FakeAgg:
+    def __init__(self):
+        self.sessions = []
+
+    def begin_round(self, template, max_clients):
+        s = _FakeSession(template, max_clients)
+        self.sessions.append(s)
+        return s
+
+
+def _rounds(n_rounds=2, K=4, P=10, fail_first=()):
+    g = torch.Generator().manual_seed(0)
+    rounds = []
+    for r in range(n_rounds):
+        specs = []
+        for i in range(K):
+            sd = OrderedDict(w=torch.randn(P, generator=g), b=torch.randn(3, generator=g),
+                             nbt=torch.tensor(7 + i, dtype=torch.int64))
+            attempts = [None, sd] if i in fail_first else [sd]
+            specs.append((10 * (i + 1) + r, attempts))
+        rounds.append(specs)
+    return rounds
+
+
+@pytest.fixture
+def plain_calls(monkeypatch):
+    calls = []
+
+    def fake_plain(w_locals, model_global=None, device=None):
+        calls.append([n for n, _ in w_locals])
+        out = w_locals[0][1]
+        out["__plain__"] = torch.tensor(1)
+        return out
+
+    monkeypatch.setattr(AGG_MOD, "aggregate", fake_plain)
+    return calls
+
+
+def _run(rounds, after_append=None, stream=None):
+    T, C = fresh_classes()
+    mfl_amd.install(T, stream_clients=stream)
+    tr = T({"w": torch.zeros(10)}, rounds, after_append=after_append)
+    agg = _FakeAgg()
+    from mfl_amd.autostream import ClientFeed
+
+    tr.__dict__["_mfl_feed"] = ClientFeed(lambda: agg, len(tr.client_list))
+    tr.train()
+    return tr, agg
+
+
+def test_every_round_streams(plain_calls):
+    rounds = _rounds(3, fail_first=(1,))  # client 1 diverges once and is retried (:181-195)
+    tr, agg = _run(rounds)
+    assert plain_calls == []
+    assert len(agg.sessions) == 3
+    for r, s in enumerate(agg.sessions):
+        assert s.counts == [n for n, _ in rounds[r]] and s.verified
+        assert s.max_clients == 4
+    assert all("__streamed__" in res for res in tr.results)
+    feed = tr.__dict__["_mfl_feed"]
+    assert feed.stats["rounds_streamed"] == 3 and feed._worker is None  # the loop's end stopped the worker
+
+
+def test_sampled_value_change_falls_back(plain_calls):
+    def mutate(r, w_locals):
+        if r == 1:  # the largest key's first element, a sampled position
+            w_locals[2][1]["w"][0] += 1.0
+
+    tr, agg = _run(_rounds(2), after_append=mutate)
+    assert "__streamed__" in tr.results[0] and "__plain__" in tr.results[1]
+    assert agg.sessions[1].verified is False
+    assert len(plain_calls) == 1
+
+
+def test_extra_client_falls_back(plain_calls):
+    def extra(r, w_locals):
+        if r == 0:
+            w_locals.append(w_locals[-1])
+
+    tr, agg = _run(_rounds(2), after_append=extra)
+    assert "__plain__" in tr.results[0] and "__streamed__" in tr.results[1]
+    assert agg.sessions[0]._finished  # abandoned: the staging is free for the plain path
+
+
+def test_sample_number_change_falls_back(plain_calls):
+    def renumber(r, w_locals):
+        w_locals[0] = (w_locals[0][0] + 1, w_locals[0][1])
+
+    tr, _ = _run(_rounds(1), after_append=renumber)
+    assert "__plain__" in tr.results[0]
+
+
+def test_key_set_change_falls_back(plain_calls):
+    def drop(r, w_locals):
+        del w_locals[1][1]["b"]
+
+    tr, _ = _run(_rounds(1), after_append=drop)
+    assert "__plain__" in tr.results[0]
+
+
+def test_streaming_off(plain_calls, monkeypatch):
+    monkeypatch.setenv("FEDAVG_STREAM_CLIENTS", "0")
+    T, C = fresh_classes()
+    mfl_amd.install(T)
+    assert not getattr(T.train, "__mfl_stream__", False)
+    tr = T({"w": torch.zeros(10)}, _rounds(1))
+    tr.train()
+    assert "__plain__" in tr.results[0]
+
+
+def test_valid_train_result_mirrors_reference_check():
+    from mfl_amd.autostream import valid_train_result
+
+    assert valid_train_result(({}, 0.1, 0.2, 0.3, 0.4, 1.0))
+    assert valid_train_result(({}, 0.0, 0.0, 0.0, 0.0, None))  # cycles are not part of :190
+    for i in range(1, 5):
+        r = [{}, 0.1, 0.2, 0.3, 0.4, 1.0]
+        r[i] = None
+        assert not valid_train_result(tuple(r))
+    assert not valid_train_result(None)
