@@ -21,7 +21,7 @@ path (178.8 ms).
 * the patched ``aggregate(w_locals)`` waits for the feed to drain, checks
   that ``w_locals`` is what was fed -- same count, the same sample numbers in
   order, the same key set, and bit-identical values at sampled positions of
-  the largest, first and last keys (compared while the reduce runs) -- and
+  the largest and a middle key (compared while the reduce runs) -- and
   then only the weights, the kernel and the result's D2H remain.
 
 Anything else falls back to the plain drop-in on ``w_locals`` (same bits,
@@ -35,6 +35,7 @@ from __future__ import annotations
 import os
 import queue
 import threading
+import time
 from typing import Optional
 
 import torch
@@ -94,22 +95,30 @@ def _bits(t: torch.Tensor):
     return flat.numpy()
 
 
+class _Release(list):
+    """Host tensors a finished round displaced, for the feed worker to drop."""
+
+
 class ClientFeed:
     """One trainer's streaming state: at most one open ``RoundSession`` (the
     round being fed), filled by a background thread."""
 
-    SAMPLE_KEYS = 4  # keys compared per client (largest, first, last, middle)
+    SAMPLE_KEYS = 2  # keys compared per client (the largest and the middle one)
 
     def __init__(self, aggregator_fn, max_clients: int):
         self._aggregator_fn = aggregator_fn  # () -> DeviceAggregator (created lazily, on first use)
         self.max_clients = max(1, int(max_clients))
         self.session = None
         self.broken = False
-        self.fed = []  # (sample_num, dict) in feed order, as the worker received them
+        self.fed = []  # sample numbers in feed order
+        self._prints = []  # per fed client: what _compare checks (worker-made, see _fingerprint)
+        self._picks = ([], {})
         self._q: Optional[queue.Queue] = None
         self._worker: Optional[threading.Thread] = None
         self._err: Optional[BaseException] = None
-        self.stats = {"rounds_streamed": 0, "rounds_fallback": 0, "last_fallback": ""}
+        self._add_ms = []
+        self._t_fed = self._t_done = 0.0
+        self.stats = {"rounds_streamed": 0, "rounds_fallback": 0, "last_fallback": "", "last_round": {}}
 
     # -- producer side (Client.train wrapper) ---------------------------------
     def feed(self, sample_num, state_dict) -> None:
@@ -119,11 +128,12 @@ class ClientFeed:
             self._break("more clients than max_clients" if len(self.fed) >= self.max_clients
                         else "not a host state_dict")
             return
-        self.fed.append((sample_num, state_dict))
+        self.fed.append(sample_num)  # the dict itself goes to the worker only (no round-long reference)
         if self._worker is None:
             self._q = queue.Queue()
             self._worker = threading.Thread(target=self._run, name="mfl-client-feed", daemon=True)
             self._worker.start()
+        self._t_fed = time.perf_counter()
         self._q.put((sample_num, state_dict))
 
     @staticmethod
@@ -139,16 +149,34 @@ class ClientFeed:
             if item is None:
                 self._q.task_done()
                 return
+            if type(item) is _Release:  # displaced tensors of a finished round: freed here, off :217
+                item = None
+                self._q.task_done()
+                continue
+            t0 = time.perf_counter()
             try:
                 if not self.broken and self._err is None:
                     n, sd = item
                     if self.session is None:
                         self.session = self._aggregator_fn().begin_round(sd, self.max_clients)
+                        self.session.keep_dicts = False
+                        self.session.defer_release = self._defer_release
+                        self._picks = self._sample_plan(sd)
                     self.session.add(n, sd)
+                    self._prints.append(self._fingerprint(sd))
             except BaseException as e:  # noqa: BLE001 -- any failure means: fall back at aggregate
                 self._err = e
             finally:
+                item = n = sd = None  # drop the client's tensors now (the loop holds its own copy)
+                t1 = time.perf_counter()
+                self._add_ms.append((t1 - t0) * 1e3)
+                self._t_done = t1
                 self._q.task_done()
+
+    def _defer_release(self, objs):
+        q = self._q
+        if q is not None:
+            q.put(_Release(objs))
 
     def _drain(self):
         if self._q is not None:
@@ -163,14 +191,24 @@ class ClientFeed:
         """The streamed result for ``w_locals``, or None (the caller runs the
         plain drop-in).  Always leaves the feed empty for the next round."""
         try:
+            t_call = time.perf_counter()
             self._drain()
+            if self._add_ms:  # the worker's per-client cost and how far it trailed the loop
+                self.stats["last_round"] = {
+                    "clients": len(self._add_ms), "add_ms_median": sorted(self._add_ms)[len(self._add_ms) // 2],
+                    "add_ms_max": max(self._add_ms), "drain_wait_ms": (time.perf_counter() - t_call) * 1e3,
+                    "worker_done_after_last_feed_ms": (self._t_done - self._t_fed) * 1e3,
+                    "session_add_profile": dict(getattr(self.session, "add_profile", {}))}
             sess = self.session
             why = self._mismatch(w_locals, sess)
             if why:
                 self.stats["last_fallback"] = why
                 self.stats["rounds_fallback"] += 1
                 return None
+            t_f = time.perf_counter()
             out = sess.finish(w_locals, verify=lambda: self._same_values(w_locals))
+            self.stats["last_round"]["finish_ms"] = (time.perf_counter() - t_f) * 1e3
+            self.stats["last_round"]["finish_profile"] = dict(getattr(sess, "finish_profile", {}))
             if out is None:
                 self.stats["last_fallback"] = "sampled values differ from the fed clients"
                 self.stats["rounds_fallback"] += 1
@@ -189,31 +227,56 @@ class ClientFeed:
             return "nothing fed"
         if type(w_locals) is not list or len(w_locals) != len(self.fed) or len(sess.counts) != len(self.fed):
             return "client count differs from the fed clients"
-        for (n, _), (n2, _) in zip(w_locals, self.fed):
+        for (n, _), n2 in zip(w_locals, self.fed):
             if n != n2:
                 return "sample numbers differ from the fed clients"
+        if len(self._prints) != len(self.fed):
+            return "a fed client was not recorded"
         return ""
 
     def _same_values(self, w_locals) -> bool:
-        """Key sets equal and sampled element bits equal, client by client."""
-        fed0 = self.fed[0][1]
-        names = list(fed0.keys())
-        if not names:
+        """Key sets equal and sampled element bits equal, client by client.
+        Never raises (it runs while the round's GPU work is in flight)."""
+        try:
+            return self._compare(w_locals)
+        except Exception:  # noqa: BLE001 -- anything unexpected: not the fed round
             return False
-        big = max(names, key=lambda k: fed0[k].numel())
-        picks = list(dict.fromkeys([big, names[0], names[-1], names[len(names) // 2]]))[:self.SAMPLE_KEYS]
+
+    def _sample_plan(self, sd):
+        """(keys, {key: positions}) compared per client: the largest and the
+        middle key with at least one element, five positions each."""
+        names = [k for k in sd.keys() if sd[k].numel() > 0]
+        if not names:
+            return list(sd), {}
+        big = max(names, key=lambda k: sd[k].numel())
+        picks = list(dict.fromkeys([big, names[len(names) // 2]]))[:self.SAMPLE_KEYS]
         pos = {}
         for k in picks:
-            n = fed0[k].numel()
+            n = sd[k].numel()
             pos[k] = sorted({0, n - 1, n // 2, (n * 7) // 13, (n * 5) // 11})
-        for (_, sd), (_, fd) in zip(w_locals, self.fed):
-            if sd.keys() != fd.keys():
+        return list(sd), pos
+
+    def _fingerprint(self, sd):
+        """What ``_compare`` checks of one fed client, taken when it was fed:
+        its key tuple and, per sampled key, (dtype, shape, element bits)."""
+        keys, pos = self._picks
+        if list(sd) != keys:
+            return None
+        return {k: (sd[k].dtype, tuple(sd[k].shape), _bits(sd[k])[p].copy()) for k, p in pos.items()}
+
+    def _compare(self, w_locals) -> bool:
+        keys, pos = self._picks
+        if not pos:
+            return False
+        for (_, sd), fp in zip(w_locals, self._prints):
+            if fp is None or list(sd) != keys:
                 return False
-            for k in picks:
-                a, b = sd[k], fd[k]
-                if not isinstance(a, torch.Tensor) or a.dtype != b.dtype or a.shape != b.shape or a.is_cuda:
+            for k, p in pos.items():
+                a = sd[k]
+                dt, shape, bits = fp[k]
+                if not isinstance(a, torch.Tensor) or a.dtype != dt or tuple(a.shape) != shape or a.is_cuda:
                     return False
-                if not (_bits(a)[pos[k]] == _bits(b)[pos[k]]).all():
+                if not (_bits(a)[p] == bits).all():
                     return False
         return True
 
@@ -223,8 +286,10 @@ class ClientFeed:
             sess.abandon()
         self.session = None
         self.fed = []
+        self._prints = []
         self.broken = False
         self._err = None
+        self._add_ms = []
 
     def close(self):
         """End of the round loop: abandon an open round, stop the worker."""

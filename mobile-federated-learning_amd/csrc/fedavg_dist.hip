@@ -603,13 +603,17 @@ int launch_fused(const float* clients, int64_t K, int64_t P, int64_t ld, const f
 // puts workgroup b on XCD b % 8); 4 = and the workgroups of one CU too
 // (b, b + 256, ... share a CU).  Both remaps are bijections of the sweep: a
 // different placement only changes the speed.
-template <int S, int SLOTS, int MODE = 0, int FLAGS = 0>
-__global__ __launch_bounds__(kBlock) void reduce_sqdist_rs_kernel(const float* __restrict__ X, int K, int64_t ld,
+// DEPTH 2: two tiles' loads in flight per workgroup (two register stages,
+// the tile in LDS a third).  MODE 3: loads only with no LDS at all (probe:
+// the tile walk at the occupancy registers alone allow).
+template <int S, int SLOTS, int MODE = 0, int FLAGS = 0, int DEPTH = 1>
+__global__ __launch_bounds__(kBlock, DEPTH == 2 ? 4 : 1) void reduce_sqdist_rs_kernel(const float* __restrict__ X, int K, int64_t ld,
                                                                   int64_t P, int64_t ntiles,
                                                                   const float* __restrict__ W,
                                                                   float* __restrict__ out,
                                                                   double* __restrict__ partials) {
   static_assert(S == 32 || S == 64 || S == 128 || S == 256, "tile widths: 32, 64, 128 or 256 columns");
+  static_assert(DEPTH == 1 || DEPTH == 2, "one or two tiles in flight");
   constexpr int V = S / 4;
   constexpr int R = kBlock / V;
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -622,14 +626,13 @@ __global__ __launch_bounds__(kBlock) void reduce_sqdist_rs_kernel(const float* _
   const char* p0 = reinterpret_cast<const char*>(X) + (static_cast<int64_t>(r0) * rstride + 4 * sl) * 4;
   const int64_t mstride = static_cast<int64_t>(R) * rstride * 4;
   f32x4* tile4 = reinterpret_cast<f32x4*>(lds);
-  f32x4 xs[SLOTS];
   double acc[SLOTS];
 #pragma unroll
   for (int m = 0; m < SLOTS; ++m) acc[m] = 0.0;
 
   // this thread's slots of tile `tt` into registers (slices past the model's
   // end are not loaded: the last row's would run off the allocation)
-  const auto issue = [&](int64_t tt) {
+  const auto issue = [&](f32x4 (&xs)[SLOTS], int64_t tt) {
     const int64_t c0 = tt * S;
     const char* p = p0 + (TILED ? tt * K * S : c0) * 4;
     const bool slice_ok = c0 + 4 * sl < P;
@@ -638,35 +641,28 @@ __global__ __launch_bounds__(kBlock) void reduce_sqdist_rs_kernel(const float* _
       if (m < nslot && slice_ok) xs[m] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p + m * mstride));
   };
 
-  int64_t first = blockIdx.x;  // this workgroup's position in every sweep of gridDim.x tiles
-  if constexpr ((FLAGS & 6) != 0) {
-    const int64_t b = blockIdx.x, per_xcd = gridDim.x / 8;
-    if constexpr ((FLAGS & 4) != 0) {
-      const int64_t j = b / 8, per_cu = per_xcd / 32;
-      first = (b % 8) * per_xcd + (j % 32) * per_cu + j / 32;
-    } else {
-      first = (b % 8) * per_xcd + b / 8;
-    }
-  }
-  if (first < ntiles) issue(first);
-  for (int64_t tt = first; tt < ntiles; tt += gridDim.x) {
+  // one tile: staged slots -> LDS, refill the stage with tile `next`, average, squares
+  const auto body = [&](f32x4 (&xs)[SLOTS], int64_t tt, int64_t next) {
     const int64_t c0 = tt * S;
     const int ncols = P - c0 < S ? static_cast<int>(P - c0) : S;
-    barrier_lds();  // every wave is done with the previous tile
-    if constexpr (MODE != 1) {
+    if constexpr (MODE == 1 || MODE == 3) {
+      float probe = 0.f;
 #pragma unroll
       for (int m = 0; m < SLOTS; ++m)
-        if (m < nslot) tile4[t + kBlock * m] = xs[m];  // 1. (a ragged slice keeps stale data: never used)
-    } else {
-#pragma unroll
-      for (int m = 0; m < SLOTS; ++m)
-        if (m < nslot) asm volatile("" ::"v"(xs[m]));  // probe: consume the loads
+        if (m < nslot) probe += xs[m].x;  // consume the loads
+      if (next < ntiles) issue(xs, next);
+      if (t == 0) out[c0] = probe;
+      return;
     }
+    barrier_lds();  // every wave is done with the previous tile
+#pragma unroll
+    for (int m = 0; m < SLOTS; ++m)
+      if (m < nslot) tile4[t + kBlock * m] = xs[m];  // 1. (a ragged slice keeps stale data: never used)
     barrier_lds();
-    if (tt + gridDim.x < ntiles) issue(tt + gridDim.x);  // 2. next tile in flight
-    if constexpr (MODE != 0) {
+    if (next < ntiles) issue(xs, next);  // 2. that stage's next tile in flight
+    if constexpr (MODE == 2) {
       if (t == 0) out[c0] = lds[0];
-      continue;
+      return;
     }
     if (t < S) {  // 3. the average of column t, in the reference's order
       float a = lds[t] * W[0];
@@ -705,6 +701,31 @@ __global__ __launch_bounds__(kBlock) void reduce_sqdist_rs_kernel(const float* _
           acc[m] = __builtin_fma(dz, dz, acc[m]);
         }
     }
+  };
+
+  int64_t first = blockIdx.x;  // this workgroup's position in every sweep of gridDim.x tiles
+  if constexpr ((FLAGS & 6) != 0) {
+    const int64_t b = blockIdx.x, per_xcd = gridDim.x / 8;
+    if constexpr ((FLAGS & 4) != 0) {
+      const int64_t j = b / 8, per_cu = per_xcd / 32;
+      first = (b % 8) * per_xcd + (j % 32) * per_cu + j / 32;
+    } else {
+      first = (b % 8) * per_xcd + b / 8;
+    }
+  }
+  const int64_t G = gridDim.x;
+  f32x4 xa[SLOTS];
+  if (first < ntiles) issue(xa, first);
+  if constexpr (DEPTH == 1) {
+    for (int64_t tt = first; tt < ntiles; tt += G) body(xa, tt, tt + G);
+  } else {
+    f32x4 xb[SLOTS];
+    if (first + G < ntiles) issue(xb, first + G);
+    for (int64_t tt = first; tt < ntiles; tt += 2 * G) {
+      body(xa, tt, tt + 2 * G);
+      if (tt + G >= ntiles) break;
+      body(xb, tt + G, tt + 3 * G);
+    }
   }
   if constexpr (MODE != 0) return;
   // the V slot sums of a row are contiguous in red[]: row * V + slice = t + 256 m
@@ -724,9 +745,9 @@ __global__ __launch_bounds__(kBlock) void reduce_sqdist_rs_kernel(const float* _
 
 // LDS of a register-staged tile: [K][S] + the average [S]; the final per-row
 // sums need K * V doubles (= K * S * 2 bytes, inside the tile)
-inline int64_t fused_rs_lds_bytes(int64_t K, int S) { return (K + 1) * S * 4; }
+inline int64_t fused_rs_lds_bytes(int64_t K, int S, int mode = 0) { return mode == 3 ? 0 : (K + 1) * S * 4; }
 
-template <int S, int SLOTS, int MODE, int FLAGS = 0>
+template <int S, int SLOTS, int MODE, int FLAGS = 0, int DEPTH = 1>
 int fused_rs_per_cu(int64_t K) {
   static std::mutex mu;
   static std::map<std::pair<int, int64_t>, int> cache;
@@ -735,8 +756,8 @@ int fused_rs_per_cu(int64_t K) {
   std::lock_guard<std::mutex> lk(mu);
   auto it = cache.find({dev, K});
   if (it != cache.end()) return it->second;
-  const auto kern = reduce_sqdist_rs_kernel<S, SLOTS, MODE, FLAGS>;
-  const int64_t lds = fused_rs_lds_bytes(K, S);
+  const auto kern = reduce_sqdist_rs_kernel<S, SLOTS, MODE, FLAGS, DEPTH>;
+  const int64_t lds = fused_rs_lds_bytes(K, S, MODE);
   int per_cu = 0;
   if (lds > 65536 && hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                          hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -751,34 +772,34 @@ int fused_rs_per_cu(int64_t K) {
   return per_cu;
 }
 
-template <int S, int SLOTS, int MODE, int FLAGS = 0>
+template <int S, int SLOTS, int MODE, int FLAGS = 0, int DEPTH = 1>
 int64_t fused_rs_grid(int64_t K, int64_t P, int blocks_per_cu) {
-  const int per_cu = blocks_per_cu > 0 ? blocks_per_cu : fused_rs_per_cu<S, SLOTS, MODE, FLAGS>(K);
+  const int per_cu = blocks_per_cu > 0 ? blocks_per_cu : fused_rs_per_cu<S, SLOTS, MODE, FLAGS, DEPTH>(K);
   const int64_t ntiles = (P + S - 1) / S;
   const int64_t g = static_cast<int64_t>(per_cu) * cu_count();
   return ntiles < g ? ntiles : g;
 }
 
-template <int S, int SLOTS, int MODE = 0, int FLAGS = 0>
+template <int S, int SLOTS, int MODE = 0, int FLAGS = 0, int DEPTH = 1>
 int launch_fused_rs(const float* clients, int64_t K, int64_t P, int64_t ld, const float* weights, float* out,
                     double* partials, int64_t partial_elems, double* sumsq, int blocks_per_cu, hipStream_t s,
                     const char* what) {
   if ((K * S + 1023) / 1024 > SLOTS)
     return set_error(FEDAVG_EMODE, "%s: %d slots per thread cover K <= %d at %d columns", what, SLOTS,
                      SLOTS * 1024 / S, S);
-  const int per_cu = fused_rs_per_cu<S, SLOTS, MODE, FLAGS>(K);
+  const int per_cu = fused_rs_per_cu<S, SLOTS, MODE, FLAGS, DEPTH>(K);
   if (per_cu <= 0)
     return set_error(FEDAVG_EMODE, "%s: the %d-column tile does not fit LDS at K = %lld", what, S, (long long)K);
   if (blocks_per_cu > per_cu)
     return set_error(FEDAVG_EMODE, "%s: %d workgroups per CU requested, %d resident", what, blocks_per_cu, per_cu);
   const int64_t ntiles = (P + S - 1) / S;
-  const int64_t grid = fused_rs_grid<S, SLOTS, MODE, FLAGS>(K, P, blocks_per_cu);
+  const int64_t grid = fused_rs_grid<S, SLOTS, MODE, FLAGS, DEPTH>(K, P, blocks_per_cu);
   if ((FLAGS & 6) != 0 && (cu_count() != 256 || grid != (blocks_per_cu > 0 ? blocks_per_cu : per_cu) * 256LL))
     return set_error(FEDAVG_EMODE, "%s: the XCD / CU remaps need a full grid on 256 CUs", what);
   if (partial_elems < K * grid)
     return set_error(FEDAVG_EINVAL, "%s: workspace needs %lld doubles", what, (long long)(K * grid));
-  hipLaunchKernelGGL((reduce_sqdist_rs_kernel<S, SLOTS, MODE, FLAGS>), dim3(static_cast<unsigned>(grid)), dim3(kBlock),
-                     static_cast<unsigned>(fused_rs_lds_bytes(K, S)), s, clients, static_cast<int>(K), ld, P, ntiles,
+  hipLaunchKernelGGL((reduce_sqdist_rs_kernel<S, SLOTS, MODE, FLAGS, DEPTH>), dim3(static_cast<unsigned>(grid)),
+                     dim3(kBlock), static_cast<unsigned>(fused_rs_lds_bytes(K, S, MODE)), s, clients, static_cast<int>(K), ld, P, ntiles,
                      weights, out, partials);
   int rc = launch_status(what);
   if (rc || MODE != 0) return rc;
@@ -1193,6 +1214,20 @@ int fedavg_reduce_sqdist_f32_variant(const float* clients, int64_t K, int64_t P,
                                                       sumsq, blocks_per_cu, s, what);
     case 4200032: return launch_fused_rs<32, 10, 0, 4>(clients, K, P, ld, weights, out, workspace, workspace_elems,
                                                        sumsq, blocks_per_cu, s, what);
+    // + 10000000: two tiles in flight per workgroup; 5300064 / 5310128: loads
+    // only, no LDS (occupancy from registers alone)
+    case 10200064: return launch_fused_rs<64, 8, 0, 0, 2>(clients, K, P, ld, weights, out, workspace,
+                                                          workspace_elems, sumsq, blocks_per_cu, s, what);
+    case 10200032: return launch_fused_rs<32, 10, 0, 0, 2>(clients, K, P, ld, weights, out, workspace,
+                                                           workspace_elems, sumsq, blocks_per_cu, s, what);
+    case 10200128: return launch_fused_rs<128, 8, 0, 0, 2>(clients, K, P, ld, weights, out, workspace,
+                                                           workspace_elems, sumsq, blocks_per_cu, s, what);
+    case 10300064: return launch_fused_rs<64, 8, 1, 0, 2>(clients, K, P, ld, weights, out, workspace,
+                                                          workspace_elems, sumsq, blocks_per_cu, s, what);
+    case 5300064: return launch_fused_rs<64, 8, 3>(clients, K, P, ld, weights, out, workspace, workspace_elems,
+                                                   sumsq, blocks_per_cu, s, what);
+    case 15300064: return launch_fused_rs<64, 8, 3, 0, 2>(clients, K, P, ld, weights, out, workspace,
+                                                          workspace_elems, sumsq, blocks_per_cu, s, what);
     default: return set_error(FEDAVG_EMODE, "%s: cols must be 32, 64, 128 or 256 (+1000: double-buffered)", what);
   }
 }

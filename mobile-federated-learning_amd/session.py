@@ -74,6 +74,9 @@ class RoundSession:
         self._out_host = {}
         self.finish_profile = {}
         self.add_ms = 0.0
+        self.add_profile = {}  # host ms per phase of add(), summed over the round's clients
+        self.keep_dicts = True
+        self.defer_release = None  # callable(list): where displaced host tensors are dropped
         # a round whose fp32 rows fit in SMALL_ROUND_BYTES finishes in ONE
         # native call (fedavg_round_f32 over the rows add() already packed):
         # its kernel reads them from pinned memory, so add() skips the H2D
@@ -107,12 +110,15 @@ class RoundSession:
             self._copy.wait_stream(torch.cuda.current_stream(self.dev))
             for g in self.table.groups.values():
                 self.agg._pack_on_device(self.table, g, ptrs, i, self._staging[g.dtype].dev, self._copy)
+            if keep:
+                self._keepalive.append(keep)  # until the packing kernel has read them
         else:
-            self._add_host(i, ptrs)
+            self._add_host(i, ptrs)  # packed synchronously: contiguous copies may go now
         self.counts.append(sample_num)
-        self.dicts.append(state_dict)
-        if keep:
-            self._keepalive.append(keep)
+        # the dicts are kept for finish()'s identity check; a caller that
+        # verifies copies instead (autostream) sets keep_dicts = False so that
+        # a round's client tensors are not all held until finish
+        self.dicts.append(state_dict if self.keep_dicts else None)
         self.add_ms += (time.perf_counter() - t0) * 1e3
 
     # The first finish() of a process paid ~10 ms of one-time runtime work on
@@ -154,9 +160,12 @@ class RoundSession:
         """Pack host client ``i`` into its pinned row and start its H2D (unless the round is small)."""
         for g in self.table.groups.values():
             st = self._staging[g.dtype]
+            t0 = time.perf_counter()
             items = self.table.pack_items(g, ptrs, i, g.ld)
             _lib.check(self._lib.fedavg_pack_rows(items.ctypes.data, items.shape[0], st.host.data_ptr(),
                                                   st.host.element_size(), self._threads), "fedavg_pack_rows")
+            t1 = time.perf_counter()
+            self.add_profile["pack_ms"] = self.add_profile.get("pack_ms", 0.0) + (t1 - t0) * 1e3
             if self._small:
                 continue
             events = []
@@ -167,6 +176,8 @@ class RoundSession:
                     ev.record(self._copy)
                     events.append(ev)
             self._ready[g.dtype] = events  # the copy stream is FIFO: covers earlier rows too
+            self.add_profile["h2d_issue_ms"] = (self.add_profile.get("h2d_issue_ms", 0.0)
+                                                + (time.perf_counter() - t1) * 1e3)
 
     def abandon(self) -> None:
         """Close the session without a result (its staging is free once the
@@ -177,7 +188,7 @@ class RoundSession:
         with torch.cuda.device(self.dev):
             self._copy.synchronize()
         self._keepalive.clear()
-        self.table.forget_tensors()
+        self._forget_table()
 
     def finish(self, w_locals=None, verify=None):
         """Reduce the added clients; ``aggregate``'s contract (fedavg_trainer.py:441-458).
@@ -198,6 +209,8 @@ class RoundSession:
                 if (verify is None and sd is not sd2) or n != n2:
                     raise ValueError(f"w_locals[{i}] is not the client added as #{i}")
         self._verify = verify
+        if verify is not None and w_locals is not None:
+            self.dicts = [sd for _, sd in w_locals]  # the round _close() leaves for :291 reuse
         if not self.counts:
             raise ValueError("no clients added (the reference returns the global model then: use aggregate([]))")
         K = len(self.counts)
@@ -231,19 +244,20 @@ class RoundSession:
                 dev_state[g.dtype] = (st.dev[:K], out_dev)
             t1 = time.perf_counter()
             ok = self._verify() if self._verify is not None else True  # overlaps the GPU work just issued
+            t_v = time.perf_counter()
             d2h.synchronize()
             cur.synchronize()
             cur.wait_stream(self._copy)  # nothing else may reuse the staging before its copies end
         t2 = time.perf_counter()
+        self.finish_profile = {"issue_ms": (t1 - t0) * 1e3, "verify_ms": (t_v - t1) * 1e3, "wait_ms": (t2 - t_v) * 1e3}
         if not ok:
             self._keepalive.clear()
-            self.table.forget_tensors()
+            self._forget_table()
             return None
         for g, out_host in outs:
-            for name, t in self.table.unpack(g, out_host).items():
-                acc_dict[name] = t
+            self._set_results(acc_dict, self.table.unpack(g, out_host))
         # host-side phases of the finish (ms): issuing weights/reduce/D2H, waiting for them, unpacking
-        self.finish_profile = {"issue_ms": (t1 - t0) * 1e3, "wait_ms": (t2 - t1) * 1e3,
+        self.finish_profile = {"issue_ms": (t1 - t0) * 1e3, "verify_ms": (t_v - t1) * 1e3, "wait_ms": (t2 - t_v) * 1e3,
                                "unpack_ms": (time.perf_counter() - t2) * 1e3}
         return self._close(K, dev_state, acc_dict, sums)
 
@@ -266,10 +280,9 @@ class RoundSession:
                                                   cur.cuda_stream), "fedavg_round_f32")
         if self._verify is not None and not self._verify():
             self._keepalive.clear()
-            self.table.forget_tensors()
+            self._forget_table()
             return None
-        for name, t in self.table.unpack(g, out_host).items():
-            acc_dict[name] = t
+        self._set_results(acc_dict, self.table.unpack(g, out_host))
         return self._close(K, {torch.float32: (st.dev[:K], out_dev)}, acc_dict)
 
     def _finish_device(self, K, weights, acc_dict):
@@ -293,16 +306,34 @@ class RoundSession:
                 dev_state[g.dtype] = (st.dev[:K], out_dev)
             if self._verify is not None and not self._verify():
                 self._keepalive.clear()
-                self.table.forget_tensors()
+                self._forget_table()
                 return None
             for g in self.table.groups.values():
-                for name, t in self.table.unpack(g, dev_state[g.dtype][1]).items():
-                    acc_dict[name] = t
+                self._set_results(acc_dict, self.table.unpack(g, dev_state[g.dtype][1]))
         return self._close(K, dev_state, acc_dict, sums)
+
+    def _release(self, objs) -> None:
+        """Drop references to a round's displaced host tensors -- freeing
+        100 MB of host memory costs ~10 ms of munmap -- on the caller's
+        release hook (autostream: its worker thread) when one is set."""
+        if self.defer_release is not None and objs:
+            self.defer_release(objs)
+
+    def _forget_table(self) -> None:
+        self._release(list(self.table._template))  # client 0's tensors, held for the native walk's checks
+        self.table.forget_tensors()
+
+    def _set_results(self, acc_dict, results) -> None:
+        """acc_dict[name] = result (fedavg_trainer.py:455 replaces client 0's values)."""
+        old = []
+        for name, t in results.items():
+            old.append(acc_dict.get(name))
+            acc_dict[name] = t
+        self._release(old)
 
     def _close(self, K, dev_state, acc_dict, sums=None):
         self._keepalive.clear()
-        self.table.forget_tensors()
+        self._forget_table()
         # leave the round's device rows + averaged model for client_distances (:291)
         try:
             self.agg._last = {"table": self.table, "K": K, "dev": dev_state, "sumsq": sums or {},

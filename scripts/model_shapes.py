@@ -38,6 +38,26 @@ def resnet56_shapes(num_classes=10):
     return shapes
 
 
+def resnet18_gn_shapes(num_classes=100):
+    """FedML resnet18_gn for fed_cifar100 (BasicBlock [2, 2, 2, 2], 7x7 stem,
+    GroupNorm: weight + bias, no running statistics): 62 keys, 11,227,812
+    elements."""
+    shapes = [("conv1.weight", (64, 3, 7, 7)), ("bn1.weight", (64,)), ("bn1.bias", (64,))]
+    inplanes = 64
+    for li, (planes, stride) in enumerate([(64, 1), (128, 2), (256, 2), (512, 2)], 1):
+        for b in range(2):
+            p = f"layer{li}.{b}"
+            shapes += [(f"{p}.conv1.weight", (planes, inplanes, 3, 3)), (f"{p}.bn1.weight", (planes,)),
+                       (f"{p}.bn1.bias", (planes,)), (f"{p}.conv2.weight", (planes, planes, 3, 3)),
+                       (f"{p}.bn2.weight", (planes,)), (f"{p}.bn2.bias", (planes,))]
+            if b == 0 and (stride != 1 or inplanes != planes):
+                shapes += [(f"{p}.downsample.0.weight", (planes, inplanes, 1, 1)),
+                           (f"{p}.downsample.1.weight", (planes,)), (f"{p}.downsample.1.bias", (planes,))]
+            inplanes = planes
+    shapes += [("fc.weight", (num_classes, 512)), ("fc.bias", (num_classes,))]
+    return shapes
+
+
 CONFIGS = {
     "mnist_lr": (10, [("linear.weight", (10, 784)), ("linear.bias", (10,))]),
     "femnist_cnn": (10, [("conv2d_1.weight", (32, 1, 3, 3)), ("conv2d_1.bias", (32,)),
@@ -45,6 +65,7 @@ CONFIGS = {
                          ("linear_1.weight", (128, 9216)), ("linear_1.bias", (128,)),
                          ("linear_2.weight", (62, 128)), ("linear_2.bias", (62,))]),
     "resnet56": (100, resnet56_shapes()),
+    "resnet18_gn": (500, resnet18_gn_shapes()),
     "target_flat": (100, [("w", (25_000_000,))]),
 }
 

@@ -3,7 +3,7 @@ cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 O=gpurun_out/r03/g2
 mkdir -p $O
-timeout -k 10 300 python -u -m pytest tests/test_gpu_autostream.py tests/test_gpu_parity.py -k "autostream or side_stream or session or golden" -x -q --timeout 120 --timeout-method thread > $O/pytest_new.log 2>&1
+timeout -k 10 400 python -u -m pytest tests/test_gpu_autostream.py tests/test_gpu_model_shapes.py tests/test_gpu_parity.py -k "autostream or side_stream or session or golden or model" -x -v --timeout 150 --timeout-method thread > $O/pytest_new.log 2>&1
 echo tests ok
 timeout -k 10 300 python -u scripts/fused_tiled_probe.py > $O/tiled.jsonl 2> $O/tiled.err
 echo tiled ok

@@ -62,16 +62,29 @@ def main():
     for leg, stream in (("streaming", True), ("plain", False)):
         T, C = fresh_classes()
         mfl_amd.install(T, device=dev, client_cls=C, stream_clients=stream)
+        round_stats = []
+
         tr = T(OrderedDict((k, torch.zeros_like(v)) for k, v in clients[0].items()), rounds,
                train_delay_s=args.delay_ms / 1e3)
+        orig_agg = T.aggregate
+
+        def agg_and_snap(self, w_locals, _orig=orig_agg, _rs=round_stats):
+            out = _orig(self, w_locals)
+            f = self.__dict__.get("_mfl_feed")
+            _rs.append(dict(f.stats["last_round"]) if f is not None else None)
+            return out
+
+        T.aggregate = agg_and_snap
         tr.train()
         legs[leg] = tr
         feed = tr.__dict__.get("_mfl_feed")
         for r, tm in enumerate(tr.timings):
+            if feed is not None and r < len(round_stats):
+                tm = dict(tm, feed=round_stats[r])
             print(json.dumps({"leg": leg, "K": K, "P": P, "keys": args.keys, "round": r,
                               "aggregate_ms": round(tm["aggregate_ms"], 3),
                               "last_train_to_model_ms": round(tm["last_train_to_model_ms"], 3),
-                              "delay_ms": args.delay_ms}), flush=True)
+                              "delay_ms": args.delay_ms, "feed": tm.get("feed")}), flush=True)
         if feed is not None:
             print(json.dumps({"leg": leg, "feed_stats": feed.stats}), flush=True)
     same = all(torch.equal(a[k].view(-1).view(torch.int32), b[k].view(-1).view(torch.int32))

@@ -21,6 +21,7 @@ class _FakeSession:
         self.counts, self.dicts = [], []
         self._finished = False
         self.verified = None
+        self.keep_dicts = True
 
     def add(self, n, sd):
         assert list(sd.keys()) == self.keys

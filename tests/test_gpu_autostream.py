@@ -75,7 +75,7 @@ def test_changed_w_locals_falls_back_to_reference_bits(where):
     def change(r, wl):
         if r == 1:
             if where == "sampled":
-                wl[3][1]["weight"].view(-1)[0] += 0.5  # first element of the largest key: a sampled position
+                wl[3][1]["linear.weight"].view(-1)[0] += 0.5  # first element of the largest key: a sampled position
             else:
                 wl.append((wl[0][0], copy.deepcopy(wl[0][1])))
         expect.append(O.aggregate_torch(copy.deepcopy(wl)))
