@@ -765,7 +765,7 @@ def main(argv=None):
         }
         if diagnostics is not None:
             out["diagnostics"] = diagnostics
-        if world == 1 and passes == 1 and plan_world == 1 and K <= 300 and red.plan.chunks == 1:
+        if world == 1 and passes == 1 and plan_world == 1 and K <= 512 and red.plan.chunks == 1:
             try:  # a side measurement: never the reason the bench line is missing
                 out["round_with_distances"] = fused_round(red, w_dev)
             except Exception as e:  # noqa: BLE001

@@ -159,13 +159,18 @@ def column_chunks(P: int) -> List[Tuple[int, int]]:
 # The reference runs :291 after every aggregate with clients (fedavg_trainer.py
 # :289-291), so the drop-in fuses by default; FEDAVG_FUSE_DISTANCES=0 keeps
 # the reduce alone.
-FUSED_MAX_K = 300  # rows kernel (fedavg_reduce_sqdist_f32; more clients: the two passes are faster)
+FUSED_MAX_K = 512  # rows kernels (fedavg_reduce_sqdist_f32's fused_plan; more clients: the two passes are faster)
 FUSED_SEGMENTS_MAX_K = 256  # device-resident clients' own tensors (fedavg_reduce_sqdist_segments_f32)
 FUSE_DISTANCES = os.environ.get("FEDAVG_FUSE_DISTANCES", "1") != "0"
 
 
 def fuse_eligible(devbuf: torch.Tensor) -> bool:
-    return FUSE_DISTANCES and devbuf.dtype == torch.float32 and 0 < devbuf.shape[0] <= FUSED_MAX_K
+    """fp32 rows the one-read aggregate + :291 pass takes: K <= FUSED_MAX_K,
+    16-B aligned rows (its loads are 16-B slices; the reduce alone also
+    serves unaligned rows)."""
+    return (FUSE_DISTANCES and devbuf.dtype == torch.float32 and 0 < devbuf.shape[0] <= FUSED_MAX_K
+            and devbuf.data_ptr() % 16 == 0 and (devbuf.shape[0] == 1 or devbuf.stride(0) % 4 == 0)
+            and devbuf.stride(-1) == 1)
 
 
 def reduce_rows(devbuf: torch.Tensor, w_dev: torch.Tensor, P: int, out: torch.Tensor,

@@ -113,6 +113,7 @@ class ClientFeed:
         self.fed = []  # sample numbers in feed order
         self._prints = []  # per fed client: what _compare checks (worker-made, see _fingerprint)
         self._picks = ([], {})
+        self._graveyard = []  # _Release lists waiting for the next round (worker thread only)
         self._q: Optional[queue.Queue] = None
         self._worker: Optional[threading.Thread] = None
         self._err: Optional[BaseException] = None
@@ -149,10 +150,17 @@ class ClientFeed:
             if item is None:
                 self._q.task_done()
                 return
-            if type(item) is _Release:  # displaced tensors of a finished round: freed here, off :217
+            if type(item) is _Release:
+                # displaced tensors of a finished round: kept until the next
+                # round's first client arrives and dropped then, while the loop
+                # trains -- dropping them now would hold the GIL through ~10 ms
+                # of munmap per 100 MB right after :217, beside the caller
+                self._graveyard.append(item)
                 item = None
                 self._q.task_done()
                 continue
+            if self._graveyard:
+                self._graveyard.clear()
             t0 = time.perf_counter()
             try:
                 if not self.broken and self._err is None:
@@ -302,3 +310,4 @@ class ClientFeed:
                 self._worker.join(timeout=60)
                 self._worker = None
                 self._q = None
+            self._graveyard.clear()

@@ -476,34 +476,15 @@ __global__ __launch_bounds__(kBlock) void reduce_sqdist_f32_kernel(const float* 
   fused_finish<RM>(lds, acc, K, partials);
 }
 
-// Fused up to 300 clients (RM = 2 rows per thread above 256).  Beyond that
-// the K-step chain of each tile and the rows per thread make it slower than
-// the two passes (320 x 5M: 2.17 vs 2.05 ms; 500 x 11.2M: 10.8 vs 7.26 ms;
-// 1000 x 12.5M: 40.6 vs 15.6 ms), while 200 x 10M gains 2.74 -> 1.84 ms,
-// 256 x 8M 2.69 -> 2.31 and 300 x 5M 1.96 -> 1.58
-// (profiles/r02/fused/fused_many_clients*_probe.jsonl).
-constexpr int kFusedMaxK = 300;
+// (The LDS-DMA kernel serves 17-128 rows in production, fused_plan below.
+// Round 2 ran it up to 300 clients with two rows per thread above 256:
+// 200 x 10M 2.74 -> 1.84 ms, 300 x 5M 1.96 -> 1.58, but 500 x 11.2M 10.8 vs
+// 7.26 ms for the two passes; profiles/r02/fused/fused_many_clients*_probe.jsonl.)
 
 // the tile + its average, and at least the 256 doubles of the final per-row sums
 inline int64_t fused_lds_bytes(int64_t K, int S, bool db = false) {
   const int64_t b = ((db ? 2 : 1) * K + 1) * S * 4;
   return b > kBlock * 8 ? b : kBlock * 8;
-}
-
-// Tile width for K rows (0 = K outside the fused range), single-buffered
-// with one thread group per row (scripts/fused_probe.py, profiles/r02/fused/):
-// 64 columns (256 B per row segment) above 64 rows -- 100 x 25M: 1.76 ms vs
-// 1.85 at 128 columns, 2.17 double-buffered; 128 up to 64 rows (64 x 10M:
-// 0.473 vs 0.497 ms); 256 up to 16 (10 x 1.2M: 16.7 vs 17.8 us); above 128
-// rows 32 columns (256 x 8M: 2.31 vs 2.41 ms, 300 x 5M: 1.58 vs 1.80 at 64;
-// 200 x 10M: 1.90 vs 1.82 -- kept at 32 so that 64-column tiles need only 8
-// precomputed load slots per thread: the register budget of 6 workgroups/CU);
-// 256 up to 32 rows (20 x 25M: 0.40 vs 0.49 ms at 128, 32 x 20M: 0.48 vs 0.58)
-inline int fused_cols(int64_t K) {
-  if (K < 1 || K > kFusedMaxK) return 0;
-  if (K > 128) return 32;
-  if (K > 64) return 64;
-  return K > 32 ? 128 : 256;
 }
 
 // Workgroups per CU the fused kernel keeps resident at this K (LDS-bound),
@@ -808,6 +789,41 @@ int launch_fused_rs(const float* clients, int64_t K, int64_t P, int64_t ld, cons
   return launch_status(what);
 }
 
+// Which one-read kernel serves K rows (production), from interleaved
+// measurements of every candidate against the others and the two passes on
+// ~4 GB of rows (scripts/fused_probe.py, profiles/r03/fused_rule/*.jsonl; ms):
+//   K <= 16    register-staged, 256-column tiles (8 x 125M 0.896 vs 0.880
+//              LDS-DMA; FEMNIST 10 x 1.2M 16.6 vs 22.2 us)
+//   K <= 32    LDS-DMA, 128 columns (24 x 41.7M 0.733 vs 0.738 register-staged)
+//   K <= 48    LDS-DMA, 256 columns (48 x 20.8M 0.737 vs 0.758 at 128)
+//   K <= 64    LDS-DMA, 128 columns (64 x 10M 0.472 vs 0.486 register-staged)
+//   K <= 128   LDS-DMA, 64 columns (100 x 25M 1.654 vs 1.753 register-staged)
+//   K <= 192   register-staged, 64 columns, 16 slots (192 x 5.2M 0.778 vs
+//              0.857 at 32 columns; the LDS-DMA kernel 0.829)
+//   K <= 320   register-staged, 32 columns, 10 slots (224 x 4.5M 0.728 vs
+//              1.03 at 64; 300 x 5M 1.08 vs 1.41 LDS-DMA vs 1.98 two passes)
+//   K <= 512   register-staged, 32 columns, 16 slots (500 x 11.2M 5.41 vs
+//              6.88 ms for the two passes; 512 x 5M 2.58 vs 3.22)
+// Beyond 512 rows the two passes are faster (640 x 3M: 2.37 vs 3.32 ms;
+// 1000 x 12.5M: 15.2 vs 20.0): each tile's K-step chain grows with K.
+constexpr int kFusedNone = 0, kFusedLds = 1, kFusedRs = 2;
+constexpr int64_t kFusedRowsMaxK = 512;
+struct FusedPlan {
+  int kind, S, slots;
+};
+
+inline FusedPlan fused_plan(int64_t K) {
+  if (K < 1 || K > kFusedRowsMaxK) return {kFusedNone, 0, 0};
+  if (K <= 16) return {kFusedRs, 256, 8};
+  if (K <= 32) return {kFusedLds, 128, 0};
+  if (K <= 48) return {kFusedLds, 256, 0};
+  if (K <= 64) return {kFusedLds, 128, 0};
+  if (K <= 128) return {kFusedLds, 64, 0};
+  if (K <= 192) return {kFusedRs, 64, 16};
+  if (K <= 320) return {kFusedRs, 32, 10};
+  return {kFusedRs, 32, 16};
+}
+
 // Global-pointer schedule (the fp64/fp16/bf16 passes and the probe
 // variants): 32 x 16-B loads in flight per thread (U4 x C8) in one launch;
 // scripts/dist_variants.py (profiles/sweeps/r01_dist_*.jsonl) measured
@@ -1096,20 +1112,29 @@ int fedavg_client_sqdist_buf(const float* clients, int64_t K, int64_t P, int64_t
 }
 #endif  // FEDAVG_TUNING
 
-// Aggregate + :291 sums in one pass (reduce_sqdist_f32_kernel) for K <= 300
-// with 16-B aligned rows; otherwise the two production passes back to back
-// (fedavg_reduce_f32, then fedavg_client_sqdist_f32 on its output).  Either
-// way `out` holds fedavg_reduce_f32's bits and sumsq the :291 sums.
+// Aggregate + :291 sums in one pass for K <= kFusedRowsMaxK with 16-B
+// aligned rows (fused_plan picks the kernel and tile); otherwise the two
+// production passes back to back (fedavg_reduce_f32, then
+// fedavg_client_sqdist_f32 on its output).  Either way `out` holds
+// fedavg_reduce_f32's bits and sumsq the :291 sums.
 int64_t fedavg_reduce_sqdist_workspace(int64_t K, int64_t P) {
   if (K <= 0 || P <= 0) return 0;
-  const int S = fused_cols(K);
+  const FusedPlan pl = fused_plan(K);
   const int64_t two_pass = fedavg_client_sqdist_workspace(K, P);
   int64_t fused = 0;
-  const bool wide = K > kBlock;  // two rows per thread in the squares (RM = 2)
-  if (S == 32) fused = K * (wide ? fused_grid<32, false, 0, false, 2>(K, P, 0) : fused_grid<32>(K, P, 0));
-  if (S == 64) fused = K * (wide ? fused_grid<64, false, 0, false, 2>(K, P, 0) : fused_grid<64>(K, P, 0));
-  if (S == 128) fused = K * fused_grid<128>(K, P, 0);
-  if (S == 256) fused = K * fused_grid<256>(K, P, 0);
+  if (pl.kind == kFusedLds) {
+    if (pl.S == 64) fused = K * fused_grid<64>(K, P, 0);
+    if (pl.S == 128) fused = K * fused_grid<128>(K, P, 0);
+    if (pl.S == 256) fused = K * fused_grid<256>(K, P, 0);
+  } else if (pl.kind == kFusedRs) {
+    switch (pl.S * 100 + pl.slots) {
+      case 25608: fused = K * fused_rs_grid<256, 8, 0>(K, P, 0); break;
+      case 6416: fused = K * fused_rs_grid<64, 16, 0>(K, P, 0); break;
+      case 3210: fused = K * fused_rs_grid<32, 10, 0>(K, P, 0); break;
+      case 3216: fused = K * fused_rs_grid<32, 16, 0>(K, P, 0); break;
+      default: break;
+    }
+  }
   return fused > two_pass ? fused : two_pass;
 }
 
@@ -1119,18 +1144,35 @@ int fedavg_reduce_sqdist_f32(const float* clients, int64_t K, int64_t P, int64_t
   int rc = check_common(clients, K, P, ld, weights, out, what);
   if (rc) return rc;
   if (!sumsq || !workspace) return set_error(FEDAVG_EINVAL, "%s: null workspace/sumsq", what);
+  // both forms read the rows as 16-B slices (the two-pass fallback's distance
+  // pass too): refuse unaligned rows up front rather than after the reduce
+  if (!aligned16(clients) || (ld % 4) != 0)
+    return set_error(FEDAVG_EALIGN, "%s: needs 16-B aligned rows and ld %% 4 == 0 (reduce alone: fedavg_reduce_f32)",
+                     what);
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (P == 0) {
     const hipError_t e = hipMemsetAsync(sumsq, 0, static_cast<size_t>(K) * sizeof(double), s);
     return e == hipSuccess ? FEDAVG_OK : set_error(-static_cast<int>(e), "%s: hipMemsetAsync failed", what);
   }
-  const int S = fused_cols(K);
-  if (S > 0 && aligned16(clients) && (ld % 4) == 0 && aligned4(out) && aligned4(weights)) {
-    if (S == 32) return launch_fused<32>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq, 0, s, what);
-    if (S == 64) return launch_fused<64>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq, 0, s, what);
-    if (S == 128)
+  const FusedPlan pl = fused_plan(K);
+  if (pl.kind != kFusedNone && aligned4(out) && aligned4(weights)) {
+    if (pl.kind == kFusedLds) {
+      if (pl.S == 64)
+        return launch_fused<64>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq, 0, s, what);
+      if (pl.S == 256)
+        return launch_fused<256>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq, 0, s, what);
       return launch_fused<128>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq, 0, s, what);
-    return launch_fused<256>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq, 0, s, what);
+    }
+    switch (pl.S * 100 + pl.slots) {
+      case 25608:
+        return launch_fused_rs<256, 8>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq, 0, s, what);
+      case 6416:
+        return launch_fused_rs<64, 16>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq, 0, s, what);
+      case 3210:
+        return launch_fused_rs<32, 10>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq, 0, s, what);
+      default:
+        return launch_fused_rs<32, 16>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq, 0, s, what);
+    }
   }
   rc = fedavg_reduce_f32(clients, K, P, ld, weights, out, stream);
   if (rc) return rc;
@@ -1146,8 +1188,8 @@ int fedavg_reduce_sqdist_f32_variant(const float* clients, int64_t K, int64_t P,
   const char* what = "fedavg_reduce_sqdist_f32_variant";
   int rc = check_common(clients, K, P, ld, weights, out, what);
   if (rc) return rc;
-  if (P == 0 || K > kFusedMaxK || !aligned16(clients) || (ld % 4) != 0 || !sumsq || !workspace)
-    return set_error(FEDAVG_EINVAL, "%s: needs 1 <= K <= %d, P >= 1, 16-B aligned rows", what, kFusedMaxK);
+  if (P == 0 || K > 1024 || !aligned16(clients) || (ld % 4) != 0 || !sumsq || !workspace)
+    return set_error(FEDAVG_EINVAL, "%s: needs 1 <= K <= 1024, P >= 1, 16-B aligned rows", what);
   hipStream_t s = static_cast<hipStream_t>(stream);
   // cols + 1000: double-buffered tiles (the next tile's loads in flight while
   // one is used); + 10000: rows per wave with one register accumulator each
@@ -1224,6 +1266,13 @@ int fedavg_reduce_sqdist_f32_variant(const float* clients, int64_t K, int64_t P,
                                                            workspace_elems, sumsq, blocks_per_cu, s, what);
     case 10300064: return launch_fused_rs<64, 8, 1, 0, 2>(clients, K, P, ld, weights, out, workspace,
                                                           workspace_elems, sumsq, blocks_per_cu, s, what);
+    // many clients: S = 32 with 16 / 32 slots per thread (K <= 512 / 1024), S = 64 with 16 (K <= 256)
+    case 200032 + 1600000: return launch_fused_rs<32, 16>(clients, K, P, ld, weights, out, workspace,
+                                                         workspace_elems, sumsq, blocks_per_cu, s, what);
+    case 200032 + 3200000: return launch_fused_rs<32, 32>(clients, K, P, ld, weights, out, workspace,
+                                                         workspace_elems, sumsq, blocks_per_cu, s, what);
+    case 200064 + 1600000: return launch_fused_rs<64, 16>(clients, K, P, ld, weights, out, workspace,
+                                                         workspace_elems, sumsq, blocks_per_cu, s, what);
     case 5300064: return launch_fused_rs<64, 8, 3>(clients, K, P, ld, weights, out, workspace, workspace_elems,
                                                    sumsq, blocks_per_cu, s, what);
     case 15300064: return launch_fused_rs<64, 8, 3, 0, 2>(clients, K, P, ld, weights, out, workspace,

@@ -9,3 +9,5 @@ timeout -k 10 400 python -u scripts/stream_install_probe.py --rounds 4 > $O/stre
 echo stream ok
 timeout -k 10 400 python -u scripts/stream_install_probe.py --rounds 3 --keys 350 --P 600372 > $O/stream_install_resnet56like.jsonl 2> $O/stream_install_r56.err
 echo stream2 ok
+timeout -k 10 500 python -u scripts/fused_probe.py --shapes 500x11227812 1000x12500000 320x5000000 256x8000000 150x10000000 --variants 200032,0 1800032,0 3400032,0 1800064,0 --rounds 2 --reps 4 > $O/many_clients.jsonl 2> $O/many_clients.err
+echo many ok

@@ -53,10 +53,11 @@ def test_fused_small_vs_oracle(K, P):
     assert torch.equal(sumsq, again)  # deterministic
 
 
-@pytest.mark.parametrize("K,P", [(129, 5003), (256, 777), (257, 2049), (300, 70_001), (301, 33_333), (500, 1001)])
+@pytest.mark.parametrize("K,P", [(129, 5003), (256, 777), (257, 2049), (300, 70_001), (301, 33_333), (500, 1001),
+                                 (512, 4099), (400, 300_001)])
 def test_fused_many_clients_vs_oracle(K, P):
-    """K > 128: 32/64-column tiles, two rows per thread in the squares above
-    256 clients; above 300 the entry runs the two passes -- same bits."""
+    """K > 128: register-staged tiles of 64 / 32 columns (16 / 10 / 16 slots
+    per thread), up to 512 clients -- the reduce's bits."""
     x, ld, weights = _rows(K, P, K * 7 + P)
     w = mfl_amd.weights_tensor(weights, torch.float32, DEV)
     out, sumsq = mfl_amd.reduce_with_sqdist(x, w, P)
@@ -67,14 +68,50 @@ def test_fused_many_clients_vs_oracle(K, P):
     assert rel < 1e-12, rel
 
 
-@pytest.mark.parametrize("K,P", [(301, 5003), (1300, 2001)])
+@pytest.mark.parametrize("K,P", [(513, 5003), (1300, 2001)])
 def test_fused_large_k_takes_two_passes(K, P):
-    """K > 300: the same entry runs the two production passes; same bits."""
+    """K > 512: the same entry runs the two production passes; same bits."""
     x, ld, weights = _rows(K, P, K + P)
     w = mfl_amd.weights_tensor(weights, torch.float32, DEV)
     out, sumsq = mfl_amd.reduce_with_sqdist(x, w, P)
     assert torch.equal(out.view(torch.int32), mfl_amd.reduce_packed(x, w, P).view(torch.int32))
     assert torch.equal(sumsq, mfl_amd.client_sqdist(x, out, P))
+
+
+@pytest.mark.parametrize("K", [16, 17, 32, 33, 64, 65, 128, 129, 192, 193, 320, 321, 512])
+def test_fused_plan_boundaries_bit_exact(K):
+    """Both sides of every switch of fused_plan (register-staged 256 / 128
+    columns, LDS-DMA 128 / 64, register-staged 64 / 32 columns with 16 / 10 /
+    16 slots): the reduce's bits, sums within 1e-12 of the two-pass sums, on
+    a ragged P (NaN padding) and a P that leaves some workgroups no tile."""
+    for P in (64 * 1000 + 3, 12_345):
+        x, ld, weights = _rows(K, P, K * 31 + P)
+        w = mfl_amd.weights_tensor(weights, torch.float32, DEV)
+        out, sumsq = mfl_amd.reduce_with_sqdist(x, w, P)
+        ref_out = mfl_amd.reduce_packed(x, w, P)
+        assert torch.equal(out.view(torch.int32), ref_out.view(torch.int32)), (K, P)
+        ref = mfl_amd.client_sqdist(x, ref_out, P)
+        rel = ((sumsq - ref).abs() / ref).max().item()
+        assert rel < 1e-12, (K, P, rel)
+
+
+def test_fused_rejects_unaligned_rows():
+    """Unaligned rows: fedavg_reduce_sqdist_f32 refuses them up front (its
+    distance pass reads 16-B slices) and the drop-in never sends them there."""
+    K, P = 5, 1001
+    x, ld, weights = _rows(K, P + 8, 9)
+    w = mfl_amd.weights_tensor(weights, torch.float32, DEV)
+    lib = mfl_amd._lib.load()
+    view = x[:, 1:]  # 4-B aligned rows
+    out = torch.empty(P, device=DEV)
+    s = torch.empty(K, dtype=torch.float64, device=DEV)
+    ws = torch.empty(max(1, lib.fedavg_reduce_sqdist_workspace(K, P)), dtype=torch.float64, device=DEV)
+    rc = lib.fedavg_reduce_sqdist_f32(view.data_ptr(), K, P, ld, w.data_ptr(), out.data_ptr(), ws.data_ptr(),
+                                      ws.numel(), s.data_ptr(), None)
+    assert rc == mfl_amd._lib.FEDAVG_EALIGN
+    from mfl_amd.aggregate import fuse_eligible
+
+    assert not fuse_eligible(view) and fuse_eligible(x)
 
 
 def test_fused_target_size_matches_two_pass():
@@ -103,7 +140,11 @@ def test_fused_variants_same_bits():
     n_ws = K * 256 * 8
     work = torch.empty(n_ws, dtype=torch.float64, device=DEV)
     # tile width (+1000 double-buffered, +10000 rows per wave), workgroups per CU
-    for cols, bpc in [(64, 0), (128, 0), (128, 1), (64, 2), (256, 0), (1064, 0), (10064, 0), (10128, 0), (11128, 0)]:
+    # register-staged (200000 + S, 1800000 + S: 16 slots), two tiles in flight
+    # (+ 10000000), XCD / CU-contiguous sweeps (2200064, 4200064)
+    for cols, bpc in [(64, 0), (128, 0), (128, 1), (64, 2), (256, 0), (1064, 0), (10064, 0), (10128, 0), (11128, 0),
+                      (200064, 0), (200032, 0), (1800064, 0), (1800032, 0), (10200064, 0), (2200064, 0), (4200064, 0),
+                      (200064, 3)]:
         out = torch.empty(P, device=DEV)
         s = torch.empty(K, dtype=torch.float64, device=DEV)
         mfl_amd._lib.check(lib.fedavg_reduce_sqdist_f32_variant(x.data_ptr(), K, P, ld, w.data_ptr(), out.data_ptr(),
@@ -150,11 +191,11 @@ def _host_round(K, shapes, seed):
     return w_locals
 
 
-@pytest.mark.parametrize("K", [1, 9, 100, 128, 300, 301])
+@pytest.mark.parametrize("K", [1, 9, 100, 128, 300, 512, 513])
 def test_dropin_distances_from_the_fused_pass(K):
     """aggregate (host state_dicts) leaves the fused :291 sums; client_distances
     returns the reference's norms (torch.norm of the fp32 differences) from
-    them -- client 0 (aliased to w_glob, :449) gets 0.  K = 301 takes the
+    them -- client 0 (aliased to w_glob, :449) gets 0.  K = 513 takes the
     two-pass route and gives the same norms."""
     import copy
 
@@ -166,7 +207,7 @@ def test_dropin_distances_from_the_fused_pass(K):
     agg.SMALL_ROUND_BYTES = 0  # the pipelined host path even for a few clients (small rounds: one native call)
     w_glob = agg.aggregate(w_locals)
     fused = agg._last.get("sumsq", {})
-    assert (torch.float32 in fused) == (K <= 300)
+    assert (torch.float32 in fused) == (K <= 512)
     norms = agg.client_distances(w_locals, w_glob)
     keys = list(shapes)
     exp = []
