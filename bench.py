@@ -111,16 +111,35 @@ def self_launch(argv) -> "int | None":
     return subprocess.call(cmd, env=env)
 
 
+def one_group_per_cu(K: int, cols: int, cus: int = 256) -> bool:
+    """Does the production fp32 schedule give (nearly) one column group per
+    CU on a chunk of ``cols`` columns?  The bands of choose_f32_schedule
+    (fedavg_reduce.hip): 6 slices per thread (1,536 float4 per group) for
+    K >= 64, 3 slices for K >= 256, at 3/4 to 1 group per CU.  Those are the
+    chunk shapes the kernel streams best: K = 100 x 1.56M at 85.5-86 % of
+    peak against 81.5-82 % for 781K / 1.04M chunks (profiles/r03/shard8/,
+    profiles/r03/chunk_schedules/)."""
+    nvec = -(-cols // 4)
+    if K >= 64 and cus * 3 // 4 * 256 * 6 <= nvec <= cus * 256 * 6:
+        return True
+    return K >= 256 and cus * 3 // 4 * 256 * 3 <= nvec <= cus * 256 * 3
+
+
 def auto_chunks(K: int, shard_cols: int, world: int, host_out: bool) -> int:
     """All-gather pipeline depth.  One chunk at N = 1 (no exchange; the
-    host-out consumer overlaps 4 D2H chunks).  At N > 1 the deepest of
-    8/4/2/1 whose chunks keep >= MIN_CHUNK_COLS columns: the gather of chunk
-    c overlaps the reduce of chunk c + 1, and each chunk launch still fills
-    the chip."""
+    host-out consumer overlaps 4 D2H chunks).  At N > 1 the most chunks (up
+    to 8) whose width lands in a one-group-per-CU band of the kernel (the
+    gather of chunk c overlaps the reduce of chunk c + 1); failing that the
+    deepest of 8/4/2/1 whose chunks keep >= MIN_CHUNK_COLS columns, so each
+    chunk launch still fills the chip."""
     if host_out:
         return 4
     if world == 1:
         return 1
+    for c in range(MAX_CHUNKS, 0, -1):
+        width = -(-shard_cols // c)
+        if one_group_per_cu(K, -(-width // 64) * 64):
+            return c
     c = MAX_CHUNKS
     while c > 1 and shard_cols // c < MIN_CHUNK_COLS:
         c //= 2

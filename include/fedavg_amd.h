@@ -209,7 +209,10 @@ int fedavg_fpf_index_lru(const float* lru_itr, const float* g_mat, int64_t n_row
  * end_round_promoted (:316-319): rows with keep_rows[r] == 0 get
  *   fl32(row - gdiff) computed in promote(fp32, T); A_mat EMA in T's arithmetic
  *   (t_kind 0 fp32 / 1 fp64 / 2 fp16 / 3 bf16; a_mat is fp64 [P] when t_kind
- *   is 1, else fp32) with the mean of gdiff (fp64 [P], T values) rounded to T.
+ *   is 1 or 4, else fp32) with the mean of gdiff (fp64 [P], T values) rounded
+ *   to T.  t_kind 4: the first fp64 round, whose A_mat is still the
+ *   reference's fp32 tensor: a_mat holds its values widened, and the
+ *   A_mat * (1 - 1/G2) product is formed in fp32 as ATen does.
  * index_f64 (:272 once A_mat is fp64): fpf[r] = norm(diffs[r] * a_mat) /
  *   g_mat[r] in fp64, NaN/inf replaced by 0.  fpf is DEVICE fp64.
  */

@@ -566,6 +566,10 @@ class DeviceAggregator:
         st = first.untyped_storage()
         if last.untyped_storage().data_ptr() != st.data_ptr() or (base - st.data_ptr()) % 4:
             return None
+        # the row kernels read whole 16-B slices: the last row's final slice may
+        # run up to 12 B past P, which as_strided's own check does not cover
+        if (base - st.data_ptr()) + (K - 1) * pitch + (g.P + 3) // 4 * 16 > st.nbytes():
+            return None
         try:
             return first.as_strided((K, g.P), (pitch // 4, 1), (base - st.data_ptr()) // 4)
         except RuntimeError:  # outside the storage

@@ -298,6 +298,9 @@ struct FpfGroups {  // = fedavg_fpf_groups (include/fedavg_amd.h)
   int32_t kind[4];
 };
 enum : int { kF32 = 0, kF64 = 1, kF16 = 2, kBF16 = 3 };
+// end_round_promoted only: the first fp64 round of a model whose A_mat is
+// still the reference's fp32 tensor (a_mat holds its values widened exactly)
+constexpr int kF64FromF32 = 4;
 constexpr int kFpfKeyFields = 5;  // numel, cat_off, grp, grp_off, rnd
 
 __device__ __forceinline__ float opaque1(float v) {
@@ -390,12 +393,14 @@ __global__ __launch_bounds__(kBlock) void fpf_end_round_promoted_kernel(
   s = block_sum(s, red);
   if (threadIdx.x == 0) {
     const double m = s / static_cast<double>(P);
-    mean_s = T == kF64 ? m : (T == kF32 ? static_cast<double>(static_cast<float>(m)) : rnd16(static_cast<float>(m), T));
+    mean_s = (T == kF64 || T == kF64FromF32) ? m
+             : (T == kF32 ? static_cast<double>(static_cast<float>(m)) : rnd16(static_cast<float>(m), T));
   }
   __syncthreads();
   const double mean = mean_s;
   const float meanf = static_cast<float>(mean);
   const float g2f = static_cast<float>(g2), c2f = static_cast<float>(c2);
+  constexpr bool F64 = T == kF64 || T == kF64FromF32;
   const int64_t r0 = static_cast<int64_t>(blockIdx.y) * kFpfRowsPerBlock;
   const int64_t r1 = r0 + kFpfRowsPerBlock < n_rows ? r0 + kFpfRowsPerBlock : n_rows;
   for (int64_t c = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; c < P;
@@ -405,6 +410,12 @@ __global__ __launch_bounds__(kBlock) void fpf_end_round_promoted_kernel(
       if constexpr (T == kF64) {
         double* a = static_cast<double*>(A);
         a[c] = a[c] * c2 + (g / g2) / mean;
+      } else if constexpr (T == kF64FromF32) {
+        // the reference's first promoted round: A_mat (fp32) * (1 - 1/G2) is an
+        // fp32 product (the Python float cast to fp32), widened exactly when the
+        // fp64 term is added -- fp64 A_mat from then on
+        double* a = static_cast<double*>(A);
+        a[c] = static_cast<double>(static_cast<float>(a[c]) * c2f) + (g / g2) / mean;
       } else if constexpr (T == kF32) {
         float* a = static_cast<float*>(A);
         a[c] = a[c] * c2f + (static_cast<float>(g) / g2f) / meanf;
@@ -417,7 +428,7 @@ __global__ __launch_bounds__(kBlock) void fpf_end_round_promoted_kernel(
     for (int64_t r = r0; r < r1; ++r) {
       if (keep_rows[r]) continue;
       float* p = D + r * ld + c;
-      if constexpr (T == kF64)
+      if constexpr (F64)
         *p = static_cast<float>(static_cast<double>(*p) - g);
       else
         *p = *p - static_cast<float>(g);
@@ -628,6 +639,10 @@ int fedavg_fpf_end_round_promoted(float* diffs, int64_t n_rows, int64_t ld, cons
       hipLaunchKernelGGL(fpf_end_round_promoted_kernel<kF64>, grid, dim3(kBlock), 0, s, diffs, ld, n_rows, keep_rows,
                          a_mat, gdiff, P, workspace, np, static_cast<double>(g2), c2);
       break;
+    case kF64FromF32:
+      hipLaunchKernelGGL(fpf_end_round_promoted_kernel<kF64FromF32>, grid, dim3(kBlock), 0, s, diffs, ld, n_rows,
+                         keep_rows, a_mat, gdiff, P, workspace, np, static_cast<double>(g2), c2);
+      break;
     case kF16:
       hipLaunchKernelGGL(fpf_end_round_promoted_kernel<kF16>, grid, dim3(kBlock), 0, s, diffs, ld, n_rows, keep_rows,
                          a_mat, gdiff, P, workspace, np, static_cast<double>(g2), c2);
@@ -636,7 +651,7 @@ int fedavg_fpf_end_round_promoted(float* diffs, int64_t n_rows, int64_t ld, cons
       hipLaunchKernelGGL(fpf_end_round_promoted_kernel<kBF16>, grid, dim3(kBlock), 0, s, diffs, ld, n_rows, keep_rows,
                          a_mat, gdiff, P, workspace, np, static_cast<double>(g2), c2);
       break;
-    default: return set_error(FEDAVG_EINVAL, "%s: t_kind must be 0..3 (got %d)", what, t_kind);
+    default: return set_error(FEDAVG_EINVAL, "%s: t_kind must be 0..4 (got %d)", what, t_kind);
   }
   return launch_status(what);
 }

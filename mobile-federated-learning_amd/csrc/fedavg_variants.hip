@@ -594,6 +594,16 @@ int fedavg_reduce_f32_buf(const float* clients, int64_t K, int64_t P, int64_t ld
     FEDAVG_BUF_CASE(16, 4, 256)
     FEDAVG_BUF_CASE(8, 2, 256)
     FEDAVG_BUF_CASE(8, 1, 256)
+    // 6 / 3 / 12 slices: 1,536- / 768-float4 column groups, one per CU for the
+    // 1.56M / 781K-column chunks of the N = 8 (and N = 4) all-gather pipeline
+    FEDAVG_BUF_CASE(4, 6, 256)
+    FEDAVG_BUF_CASE(2, 6, 256)
+    FEDAVG_BUF_CASE(8, 6, 256)
+    FEDAVG_BUF_CASE(8, 3, 256)
+    FEDAVG_BUF_CASE(4, 3, 256)
+    FEDAVG_BUF_CASE(16, 3, 256)
+    FEDAVG_BUF_CASE(2, 12, 128)
+    FEDAVG_BUF_CASE(4, 6, 128)
     FEDAVG_BUF_CASE(8, 1, 128)
     FEDAVG_BUF_CASE(8, 2, 128)
     FEDAVG_BUF_CASE(8, 4, 128)

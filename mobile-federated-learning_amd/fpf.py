@@ -69,6 +69,7 @@ G2 = 2  # config.py:75
 THRESHOLD_WEIGHT_SIZE = 100000  # config.py:83
 
 _KIND = {torch.float32: 0, torch.float64: 1, torch.float16: 2, torch.bfloat16: 3}  # fedavg_fpf_groups.kind
+_KIND_F64_FROM_F32 = 4  # fedavg_fpf_end_round_promoted: the first fp64 round (A_mat still fp32)
 
 
 class FPFTracker:
@@ -297,11 +298,17 @@ class FPFTracker:
             self._keys.data_ptr(), self._keys.shape[0], self.P, ctypes.addressof(cur), 1, ctypes.addressof(lastg),
             None, 1, self._gd.data_ptr(), self.ld, 1, s), "fedavg_fpf_cat_diff")
         a = self._a64 if self.T == torch.float64 else self._a
+        kind = _KIND[self.T]
+        if self.T == torch.float64 and not self._a_is64:
+            # the reference's A_mat is still fp32 here (:114): its product with
+            # (1 - 1/G2) is an fp32 one, the sum with the fp64 term promotes
+            self._a64.copy_(self._a)  # exact widening, on the current stream (= s)
+            kind = _KIND_F64_FROM_F32
         _lib.check(self._lib.fedavg_fpf_end_round_promoted(
             self._diffs.data_ptr(), self.n, self.ld, keep_dev.data_ptr(), a.data_ptr(), self._gd.data_ptr(), self.P,
-            _KIND[self.T], self.g2, self._ws.data_ptr(), self._ws.numel(), s), "fedavg_fpf_end_round_promoted")
+            kind, self.g2, self._ws.data_ptr(), self._ws.numel(), s), "fedavg_fpf_end_round_promoted")
         if self.T == torch.float64:
-            self._a_is64 = True  # A_mat * 0.5 (fp32) + fp64 term -> fp64 from now on
+            self._a_is64 = True  # fl32(A_mat * c2) + fp64 term -> fp64 from now on
 
     def _check_bool(self):
         if self._has_bool:

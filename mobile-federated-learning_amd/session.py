@@ -139,8 +139,7 @@ class RoundSession:
         if getattr(agg, "_finish_warm", False) or not self.FINISH_WARMUP:
             return
         agg._finish_warm = True
-        from .aggregate import _fetch
-        from .reduce import reduce_packed
+        from .aggregate import _fetch, reduce_rows
 
         with torch.cuda.device(self.dev):
             d2h = agg._d2h_stream_for()
@@ -152,7 +151,9 @@ class RoundSession:
                 w = st.upload_weights([1.0 / K] * K, d2h)
                 scratch = torch.empty(c1 - c0, dtype=g.dtype, device=self.dev)
                 with torch.cuda.stream(d2h):
-                    reduce_packed(st.dev[:K, c0:c1], w, c1 - c0, scratch)
+                    # the finish's own kernel: the fused aggregate + :291 pass when
+                    # the rows qualify (its own code object), else the row reduce
+                    reduce_rows(st.dev[:K, c0:c1], w, c1 - c0, scratch, [])
                 _fetch(scratch, self._out_host[g.dtype][c0:c1], d2h)
                 scratch.record_stream(d2h)
 

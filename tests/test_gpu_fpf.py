@@ -29,9 +29,9 @@ RTOL = 1e-5
 
 
 class _TrackerImpl:
-    def __init__(self, meta, init):
+    def __init__(self, meta, init, g2=FO.G2):
         self.t = mfl_amd.FPFTracker(meta["client_num_in_total"], init, meta["comm_round"], device=DEV,
-                                    threshold=meta["threshold"])
+                                    threshold=meta["threshold"], g2=g2)
 
     def begin_round(self, last_w):
         self.t.begin_round(last_w)
@@ -85,9 +85,9 @@ class _DeviceTrackerImpl(_TrackerImpl):
 
 
 class _OracleImpl(_TrackerImpl):
-    def __init__(self, meta, init):
+    def __init__(self, meta, init, g2=FO.G2):
         weight_size = sum(v.numel() for v in init.values())
-        self.o = FO.FPFOracle(meta["client_num_in_total"], weight_size, meta["comm_round"], meta["threshold"])
+        self.o = FO.FPFOracle(meta["client_num_in_total"], weight_size, meta["comm_round"], meta["threshold"], g2=g2)
 
     def begin_round(self, last_w):
         pass
@@ -163,9 +163,9 @@ def _random_case(n_total, P, rounds, seed, threshold=FO.THRESHOLD_WEIGHT_SIZE, b
     return fpf_replay.FPFCase(meta, init, states, None)
 
 
-def _replay_both(case, after):
-    tr = _TrackerImpl(case.meta, case.init)
-    orc = _OracleImpl(case.meta, case.init)
+def _replay_both(case, after, g2=FO.G2):
+    tr = _TrackerImpl(case.meta, case.init, g2)
+    orc = _OracleImpl(case.meta, case.init, g2)
     rows_t = fpf_replay.replay(case, tr, record_after_aggregate=after)
     rows_o = fpf_replay.replay(case, orc)
     return tr.t, orc.o, rows_t, rows_o
@@ -327,6 +327,24 @@ def test_fpf_promoted_device_clients(name):
         got = fpf_replay.replay(case, _DeviceTrackerImpl(case.meta, case.init), record_after_aggregate=after)
         host = fpf_replay.replay(case, _TrackerImpl(case.meta, case.init), record_after_aggregate=after)
         assert np.array_equal(got.view(np.uint32), host.view(np.uint32))
+
+
+@pytest.mark.parametrize("name", ["f32w_f64b", "f64_only", "f32w_f16b"])
+def test_fpf_g2_not_a_power_of_two(name):
+    """G2 = 3: (1 - 1/G2) is not an fp32 number.  The reference's first
+    end_round multiplies its fp32 A_mat (:114) by it in fp32 and only then
+    promotes (:319) -- A_mat after every round of the fp64 models within
+    1e-12 of the oracle, the fp32 model within the fp32 tolerance."""
+    (wdt, bdt, int_key), T = MIXED[name]
+    case = _mixed_case(30, 700, ROUNDS[:4], seed=29, wdt=wdt, bdt=bdt, int_key=int_key)
+    for r_end in range(1, 5):
+        sub = fpf_replay.FPFCase(dict(case.meta, rounds=case.meta["rounds"][:r_end], comm_round=r_end), case.init,
+                                 case.client_states[:r_end], None)
+        t, o, _, _ = _replay_both(sub, False, g2=3)
+        assert t.A_mat.dtype == o.A_mat.dtype
+        rtol = MIXED_RTOL[T]
+        a_t, a_o = t.A_mat.cpu().double().numpy(), o.A_mat.double().numpy()
+        np.testing.assert_allclose(a_t, a_o, rtol=rtol, atol=rtol * np.abs(a_o).max(), err_msg=f"round {r_end}")
 
 
 def test_fpf_promoted_first_round_index_is_fp32():
