@@ -115,14 +115,14 @@ def one_group_per_cu(K: int, cols: int, cus: int = 256) -> bool:
     """Does the production fp32 schedule give (nearly) one column group per
     CU on a chunk of ``cols`` columns?  The bands of choose_f32_schedule
     (fedavg_reduce.hip): 6 slices per thread (1,536 float4 per group) for
-    K >= 64, 3 slices for K >= 256, at 3/4 to 1 group per CU.  Those are the
-    chunk shapes the kernel streams best: K = 100 x 1.56M at 85.5-86 % of
-    peak against 81.5-82 % for 781K / 1.04M chunks (profiles/r03/shard8/,
-    profiles/r03/chunk_schedules/)."""
+    K >= 64, 3 slices for K >= 256, at 0.9 to 1 group per CU.  Those are the
+    chunk shapes the kernel streams best: K = 100 x 1.56M (254 groups) at
+    85-86 % of peak against 81.5-82 % for 781K / 1.04M chunks and 83.5 % for
+    1.25M (0.8 groups per CU) (profiles/r03/shard8/, profiles/r03/chunk_schedules/)."""
     nvec = -(-cols // 4)
-    if K >= 64 and cus * 3 // 4 * 256 * 6 <= nvec <= cus * 256 * 6:
+    if K >= 64 and cus * 9 // 10 * 256 * 6 <= nvec <= cus * 256 * 6:
         return True
-    return K >= 256 and cus * 3 // 4 * 256 * 3 <= nvec <= cus * 256 * 3
+    return K >= 256 and cus * 9 // 10 * 256 * 3 <= nvec <= cus * 256 * 3
 
 
 def auto_chunks(K: int, shard_cols: int, world: int, host_out: bool) -> int:
@@ -157,20 +157,23 @@ def _thread_count():
     return n_aff, (omp if 0 < omp < n_aff else None)
 
 
-def cpu_baseline(K: int, P: int, flat_seconds: float = 8.0, model_seconds: float = 4.0):
+def cpu_baseline(K: int, P: int, flat_seconds: float = 6.0, model_seconds: float = 4.0, rep_budget_s: float = 2.5):
     """The reference's torch CPU loop (fedavg_trainer.py:444-458, restated in
     oracle/fedavg_oracle.py) on the GPU box's host cores, per BASELINE.md's
     CPU-baseline plan:
 
-    * flat: the workload itself -- K clients with one P-element fp32 key
-      (100 x 25M = 10 GB of host tensors at the target), best of a few reps,
-      ``torch.set_num_threads(len(os.sched_getaffinity(0)))``.  This is
-      ``value``; the same with the OMP_NUM_THREADS cap the box sets is a
-      second entry (``layouts``).
+    * flat: the workload's own K x P (100 x 25M = 10 GB of host tensors at
+      the target) with ``torch.set_num_threads(len(os.sched_getaffinity(0)))``
+      -- ``value`` -- and again at the OMP_NUM_THREADS cap the box sets (a
+      second, labelled entry).  When one full-K reduce at a thread count would
+      take longer than ``rep_budget_s`` (estimated from a timed 10-client
+      slice: the affinity count of a shared box can be many times its CPU
+      share), that entry times the 10-client K-slice instead and says so.
     * model-shaped: cfg3's resnet56 state_dicts (350 keys, 58 int64
       num_batches_tracked buffers), all 100 clients -- the per-key dispatch
-      cost the reference pays on real models (slowest layout), at
-      the affinity thread count."""
+      cost the reference pays on real models (slowest layout) -- at
+      the box's own thread share.
+    Progress goes to stderr (a long silent CPU phase looks like a hang)."""
     import torch
 
     sys.path.insert(0, str(ROOT / "oracle"))
@@ -178,10 +181,13 @@ def cpu_baseline(K: int, P: int, flat_seconds: float = 8.0, model_seconds: float
     import fedavg_oracle as O
     from model_shapes import CONFIGS, numel
 
+    def note(msg):
+        print(f"[cpu_baseline] {msg}", file=sys.stderr, flush=True)
+
     n_aff, n_omp = _thread_count()
     torch.set_num_threads(n_omp or n_aff)  # generation at the box's own share
 
-    def timed(w_locals_factory, seconds):
+    def timed(w_locals_factory, seconds, max_reps=50):
         times = []
         t_end = time.perf_counter() + seconds
         while time.perf_counter() < t_end or len(times) < 3:
@@ -189,7 +195,7 @@ def cpu_baseline(K: int, P: int, flat_seconds: float = 8.0, model_seconds: float
             t0 = time.perf_counter()
             O.aggregate_torch(w_locals)
             times.append(time.perf_counter() - t0)
-            if len(times) >= 50:
+            if len(times) >= max_reps:
                 break
         return min(times[1:]), len(times) - 1
 
@@ -202,20 +208,29 @@ def cpu_baseline(K: int, P: int, flat_seconds: float = 8.0, model_seconds: float
     rows = torch.empty((K, P))  # client i = base + a shifted window of one noise vector (timing data)
     for i in range(K):
         torch.add(base, noise[i * shift:i * shift + P], out=rows[i])
-    del noise
+    del noise, base
     counts = sample_counts(K)
+    note(f"flat rows ready: K={K} x P={P} ({4 * K * P / 1e9:.1f} GB); affinity {n_aff} CPUs, OMP cap {n_omp}")
     layouts = []
+    k_slice = min(K, 10)
     for label, n in (("affinity", n_aff), ("OMP_NUM_THREADS", n_omp)):
         if n is None:
             continue
         torch.set_num_threads(n)
-        best, reps = timed(lambda: [(counts[i], {"w": rows[i]}) for i in range(K)], flat_seconds)
-        layouts.append({"layout": "flat", "threads": n, "threads_from": label,
-                        "value": round(algorithmic_bytes(K, P) / best / 1e9, 3), "unit": "GB/s",
-                        "sample": f"the workload: K={K} x P={P} fp32, one flat key per client; best of {reps} "
-                                  f"reps after 1 warm-up, {best * 1e3:.1f} ms/reduce, {n} torch threads"})
-    del rows, base
-    torch.set_num_threads(n_aff)
+        t0 = time.perf_counter()
+        O.aggregate_torch([(counts[i], {"w": rows[i]}) for i in range(k_slice)])  # warm-up + estimate
+        est_full = (time.perf_counter() - t0) * K / k_slice
+        Kt = K if est_full <= rep_budget_s else k_slice
+        best, reps = timed(lambda: [(counts[i], {"w": rows[i]}) for i in range(Kt)], flat_seconds)
+        why = ("the workload" if Kt == K else
+               f"K-slice of the workload: one full K={K} reduce at {n} threads would take ~{est_full:.1f} s")
+        layouts.append({"layout": "flat", "threads": n, "threads_from": label, "K": Kt,
+                        "value": round(algorithmic_bytes(Kt, P) / best / 1e9, 3), "unit": "GB/s",
+                        "sample": f"{why}: K={Kt} x P={P} fp32, one flat key per client; best of {reps} reps after "
+                                  f"1 warm-up, {best * 1e3:.1f} ms/reduce, {n} torch threads"})
+        note(f"flat at {n} threads ({label}): {layouts[-1]['value']} GB/s (K={Kt})")
+    del rows
+    torch.set_num_threads(n_omp or n_aff)
     Km, shapes = CONFIGS["resnet56"]
     Pm = numel(shapes)
     mbase = {k: torch.randn(s, generator=g) * 0.05 for k, s in shapes}
@@ -227,11 +242,19 @@ def cpu_baseline(K: int, P: int, flat_seconds: float = 8.0, model_seconds: float
                      else mbase[k] + torch.randn(s, generator=g) * 1e-3)
         dicts.append(sd)
     mcounts = sample_counts(Km)
-    best_m, reps_m = timed(lambda: [(mcounts[0], dict(dicts[0]))] + list(zip(mcounts[1:], dicts[1:])), model_seconds)
-    layouts.append({"layout": "model-shaped (resnet56)", "threads": n_aff, "threads_from": "affinity",
+    # 35,000 small ops per reduce: at the box's own share of threads (an
+    # oversubscribed team per op would time the scheduler, not the loop)
+    n_m = n_omp or n_aff
+    torch.set_num_threads(n_m)
+    best_m, reps_m = timed(lambda: [(mcounts[0], dict(dicts[0]))] + list(zip(mcounts[1:], dicts[1:])), model_seconds,
+                           max_reps=20)
+    layouts.append({"layout": "model-shaped (resnet56)", "threads": n_m,
+                    "threads_from": "OMP_NUM_THREADS" if n_omp else "affinity",
                     "value": round(algorithmic_bytes(Km, Pm) / best_m / 1e9, 3), "unit": "GB/s",
                     "sample": f"cfg3 resnet56 state_dicts: K={Km} x P={Pm}, {len(shapes)} keys; best of {reps_m} "
-                              f"reps after 1 warm-up, {best_m * 1e3:.1f} ms/reduce, {n_aff} torch threads"})
+                              f"reps after 1 warm-up, {best_m * 1e3:.1f} ms/reduce, {n_m} torch threads"})
+    note(f"model-shaped: {layouts[-1]['value']} GB/s")
+    torch.set_num_threads(n_omp or n_aff)
     flat = layouts[0]
     return {
         "value": flat["value"],

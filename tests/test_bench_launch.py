@@ -63,7 +63,7 @@ def test_no_self_launch_under_torchrun(monkeypatch):
 @pytest.mark.parametrize("K,P,world,expect", [
     (100, 25_000_000, 1, 1),          # N = 1: no exchange, one chunk
     (100, 25_000_000, 8, 2),          # target at 8 GPUs: 3.125M columns -> 2 x 1.56M (one group per CU)
-    (100, 25_000_000, 4, 5),          # 6.25M -> 5 x 1.25M (0.8 groups per CU)
+    (100, 25_000_000, 4, 4),          # 6.25M -> 4 x 1.56M (5 x 1.25M would give 0.8 groups per CU)
     (100, 25_000_000, 2, 8),          # 12.5M -> 8 x 1.56M
     (500, 11_227_812, 8, 2),          # cfg4: 1.4M -> 2 x 702K (3-slice band, K >= 256)
     (1000, 100_000_000, 8, 8),        # cfg5: 12.5M -> 8 x 1.56M
@@ -80,7 +80,8 @@ def test_auto_chunks(K, P, world, expect):
 def test_one_group_per_cu_bands():
     assert bench.one_group_per_cu(100, 1_562_560) and not bench.one_group_per_cu(100, 781_312)
     assert not bench.one_group_per_cu(63, 1_562_560)  # the 6-slice band starts at K = 64
-    assert bench.one_group_per_cu(500, 701_760) and not bench.one_group_per_cu(100, 701_760)
+    assert bench.one_group_per_cu(500, 760_000) and not bench.one_group_per_cu(100, 760_000)
+    assert not bench.one_group_per_cu(100, 1_250_000)  # 0.8 groups per CU
 
 
 def test_strong_and_weak_workloads():
