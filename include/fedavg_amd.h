@@ -121,10 +121,12 @@ int fedavg_client_sqdist_f32(const float* clients, int64_t K, int64_t P, int64_t
  *   sumsq : fedavg_client_sqdist_f32(clients, ..., out, ...)'s sums, the
  *           same rounding rules (fp32 difference, fp64 squares and sum,
  *           fixed order; not necessarily the same summation tree).
- * K <= 300 with 16-B aligned rows and ld % 4 == 0 runs the fused kernel
- * (K x 32-256 columns staged in LDS per workgroup); anything else runs the two
- * passes back to back.  workspace : fedavg_reduce_sqdist_workspace(K, P)
- * doubles of device scratch.  P == 0 writes sumsq = 0.
+ * Needs 16-B aligned rows and ld % 4 == 0 (FEDAVG_EALIGN otherwise, before
+ * any work: fedavg_reduce_f32 alone takes unaligned rows).  K <= 512 runs a
+ * fused kernel (tiles of K rows x 32-256 columns staged in LDS per
+ * workgroup, by LDS-DMA or through registers); K > 512 runs the two passes
+ * back to back.  workspace : fedavg_reduce_sqdist_workspace(K, P) doubles of
+ * device scratch.  P == 0 writes sumsq = 0.
  */
 int64_t fedavg_reduce_sqdist_workspace(int64_t K, int64_t P);
 int fedavg_reduce_sqdist_f32(const float* clients, int64_t K, int64_t P, int64_t ld,

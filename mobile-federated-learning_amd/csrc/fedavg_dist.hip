@@ -587,14 +587,18 @@ int launch_fused(const float* clients, int64_t K, int64_t P, int64_t ld, const f
 // DEPTH 2: two tiles' loads in flight per workgroup (two register stages,
 // the tile in LDS a third).  MODE 3: loads only with no LDS at all (probe:
 // the tile walk at the occupancy registers alone allow).
+constexpr int rs_min_waves(int S, int DEPTH) {
+  return DEPTH == 1 || S == 256 ? 1 : (S <= 64 ? 4 : (DEPTH == 2 ? 3 : 2));
+}
+
 template <int S, int SLOTS, int MODE = 0, int FLAGS = 0, int DEPTH = 1>
-__global__ __launch_bounds__(kBlock, DEPTH == 2 ? 4 : 1) void reduce_sqdist_rs_kernel(const float* __restrict__ X, int K, int64_t ld,
+__global__ __launch_bounds__(kBlock, rs_min_waves(S, DEPTH)) void reduce_sqdist_rs_kernel(const float* __restrict__ X, int K, int64_t ld,
                                                                   int64_t P, int64_t ntiles,
                                                                   const float* __restrict__ W,
                                                                   float* __restrict__ out,
                                                                   double* __restrict__ partials) {
   static_assert(S == 32 || S == 64 || S == 128 || S == 256, "tile widths: 32, 64, 128 or 256 columns");
-  static_assert(DEPTH == 1 || DEPTH == 2, "one or two tiles in flight");
+  static_assert(DEPTH >= 1 && DEPTH <= 3, "one to three tiles in flight");
   constexpr int V = S / 4;
   constexpr int R = kBlock / V;
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -699,13 +703,24 @@ __global__ __launch_bounds__(kBlock, DEPTH == 2 ? 4 : 1) void reduce_sqdist_rs_k
   if (first < ntiles) issue(xa, first);
   if constexpr (DEPTH == 1) {
     for (int64_t tt = first; tt < ntiles; tt += G) body(xa, tt, tt + G);
-  } else {
+  } else if constexpr (DEPTH == 2) {
     f32x4 xb[SLOTS];
     if (first + G < ntiles) issue(xb, first + G);
     for (int64_t tt = first; tt < ntiles; tt += 2 * G) {
       body(xa, tt, tt + 2 * G);
       if (tt + G >= ntiles) break;
       body(xb, tt + G, tt + 3 * G);
+    }
+  } else {
+    f32x4 xb[SLOTS], xc[SLOTS];
+    if (first + G < ntiles) issue(xb, first + G);
+    if (first + 2 * G < ntiles) issue(xc, first + 2 * G);
+    for (int64_t tt = first; tt < ntiles; tt += 3 * G) {
+      body(xa, tt, tt + 3 * G);
+      if (tt + G >= ntiles) break;
+      body(xb, tt + G, tt + 4 * G);
+      if (tt + 2 * G >= ntiles) break;
+      body(xc, tt + 2 * G, tt + 5 * G);
     }
   }
   if constexpr (MODE != 0) return;
@@ -1275,6 +1290,20 @@ int fedavg_reduce_sqdist_f32_variant(const float* clients, int64_t K, int64_t P,
                                                          workspace_elems, sumsq, blocks_per_cu, s, what);
     case 5300064: return launch_fused_rs<64, 8, 3>(clients, K, P, ld, weights, out, workspace, workspace_elems,
                                                    sumsq, blocks_per_cu, s, what);
+    // wide tiles with 2-3 tiles in flight (registers) beside the one in LDS:
+    // 20000000 + DEPTH * 1000000 + S (K = 100: 13 slots at 128, 25 at 256)
+    case 22000128: return launch_fused_rs<128, 13, 0, 0, 2>(clients, K, P, ld, weights, out, workspace,
+                                                            workspace_elems, sumsq, blocks_per_cu, s, what);
+    case 23000128: return launch_fused_rs<128, 13, 0, 0, 3>(clients, K, P, ld, weights, out, workspace,
+                                                            workspace_elems, sumsq, blocks_per_cu, s, what);
+    case 22000256: return launch_fused_rs<256, 25, 0, 0, 2>(clients, K, P, ld, weights, out, workspace,
+                                                            workspace_elems, sumsq, blocks_per_cu, s, what);
+    case 23000256: return launch_fused_rs<256, 25, 0, 0, 3>(clients, K, P, ld, weights, out, workspace,
+                                                            workspace_elems, sumsq, blocks_per_cu, s, what);
+    case 5310128: return launch_fused_rs<128, 13, 3>(clients, K, P, ld, weights, out, workspace, workspace_elems,
+                                                     sumsq, blocks_per_cu, s, what);
+    case 5310256: return launch_fused_rs<256, 25, 3>(clients, K, P, ld, weights, out, workspace, workspace_elems,
+                                                     sumsq, blocks_per_cu, s, what);
     case 15300064: return launch_fused_rs<64, 8, 3, 0, 2>(clients, K, P, ld, weights, out, workspace,
                                                           workspace_elems, sumsq, blocks_per_cu, s, what);
     default: return set_error(FEDAVG_EMODE, "%s: cols must be 32, 64, 128 or 256 (+1000: double-buffered)", what);
