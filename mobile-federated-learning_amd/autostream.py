@@ -110,6 +110,7 @@ class ClientFeed:
         self.max_clients = max(1, int(max_clients))
         self.session = None
         self.broken = False
+        self._small = False  # this round fits SMALL_ROUND_BYTES: left to the plain path
         self.fed = []  # sample numbers in feed order
         self._prints = []  # per fed client: what _compare checks (worker-made, see _fingerprint)
         self._picks = ([], {})
@@ -119,15 +120,24 @@ class ClientFeed:
         self._err: Optional[BaseException] = None
         self._add_ms = []
         self._t_fed = self._t_done = 0.0
-        self.stats = {"rounds_streamed": 0, "rounds_fallback": 0, "last_fallback": "", "last_round": {}}
+        self.stats = {"rounds_streamed": 0, "rounds_fallback": 0, "rounds_small": 0, "last_fallback": "", "last_round": {}}
 
     # -- producer side (Client.train wrapper) ---------------------------------
+    # A round whose rows fit this many bytes is not streamed: the plain drop-in
+    # finishes it in ONE native call (fedavg_round_f32, ~45 us for MNIST-LR x 10),
+    # where a feed thread would only add hand-offs (MNIST-LR x 10: 1.25 vs
+    # 0.29 ms at :217 in the loop-replay probe, profiles/r03/stream/).
+    SMALL_ROUND_BYTES = 4 << 20
+
     def feed(self, sample_num, state_dict) -> None:
         if self.broken:
             return
         if len(self.fed) >= self.max_clients or not self._host_dict(state_dict):
             self._break("more clients than max_clients" if len(self.fed) >= self.max_clients
                         else "not a host state_dict")
+            return
+        if not self.fed and self._row_bytes(state_dict) * self.max_clients <= self.SMALL_ROUND_BYTES:
+            self.broken = self._small = True  # by design: not counted as a fallback
             return
         self.fed.append(sample_num)  # the dict itself goes to the worker only (no round-long reference)
         if self._worker is None:
@@ -136,6 +146,10 @@ class ClientFeed:
             self._worker.start()
         self._t_fed = time.perf_counter()
         self._q.put((sample_num, state_dict))
+
+    @staticmethod
+    def _row_bytes(sd) -> int:
+        return sum(4 * v.numel() for v in sd.values())  # the packed fp32 row (wider dtypes: more)
 
     @staticmethod
     def _host_dict(sd) -> bool:
@@ -199,6 +213,9 @@ class ClientFeed:
         """The streamed result for ``w_locals``, or None (the caller runs the
         plain drop-in).  Always leaves the feed empty for the next round."""
         try:
+            if self._small:
+                self.stats["rounds_small"] += 1
+                return None
             t_call = time.perf_counter()
             self._drain()
             if self._add_ms:  # the worker's per-client cost and how far it trailed the loop
@@ -295,7 +312,7 @@ class ClientFeed:
         self.session = None
         self.fed = []
         self._prints = []
-        self.broken = False
+        self.broken = self._small = False
         self._err = None
         self._add_ms = []
 

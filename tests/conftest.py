@@ -13,6 +13,7 @@ for p in (str(REPO), str(REPO / "oracle"), str(REPO / "tests")):
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (runs on the GPU box)")
     config.addinivalue_line("markers", "slow: larger CPU cases")
+    config.addinivalue_line("markers", "default_threshold: keep the feed's small-round threshold (test_gpu_autostream)")
 
 
 @pytest.fixture(scope="session")

@@ -80,14 +80,16 @@ def plain_calls(monkeypatch):
     return calls
 
 
-def _run(rounds, after_append=None, stream=None):
+def _run(rounds, after_append=None, stream=None, small_round_bytes=0):
     T, C = fresh_classes()
     mfl_amd.install(T, stream_clients=stream)
     tr = T({"w": torch.zeros(10)}, rounds, after_append=after_append)
     agg = _FakeAgg()
     from mfl_amd.autostream import ClientFeed
 
-    tr.__dict__["_mfl_feed"] = ClientFeed(lambda: agg, len(tr.client_list))
+    feed = ClientFeed(lambda: agg, len(tr.client_list))
+    feed.SMALL_ROUND_BYTES = small_round_bytes  # the toy dicts here are tiny: stream them anyway
+    tr.__dict__["_mfl_feed"] = feed
     tr.train()
     return tr, agg
 
@@ -103,6 +105,20 @@ def test_every_round_streams(plain_calls):
     assert all("__streamed__" in res for res in tr.results)
     feed = tr.__dict__["_mfl_feed"]
     assert feed.stats["rounds_streamed"] == 3 and feed._worker is None  # the loop's end stopped the worker
+
+
+def test_small_round_left_to_plain_path(plain_calls):
+    # K x row bytes <= SMALL_ROUND_BYTES: the plain drop-in's one native call wins
+    rounds = _rounds(2, K=4, P=10)
+    row = 4 * (10 + 3 + 1)
+    tr, agg = _run(rounds, small_round_bytes=4 * row)
+    assert agg.sessions == [] and len(plain_calls) == 2
+    assert all("__plain__" in res for res in tr.results)
+    feed = tr.__dict__["_mfl_feed"]
+    assert feed.stats["rounds_small"] == 2 and feed.stats["rounds_fallback"] == 0
+    assert feed._worker is None  # never started
+    tr, agg = _run(_rounds(1, K=4, P=10), small_round_bytes=4 * row - 1)
+    assert len(agg.sessions) == 1 and "__streamed__" in tr.results[0]
 
 
 def test_sampled_value_change_falls_back(plain_calls):

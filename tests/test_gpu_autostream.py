@@ -28,6 +28,14 @@ def _gpu(gpu_available):
     yield
 
 
+@pytest.fixture(autouse=True)
+def _stream_small_rounds(request, monkeypatch):
+    # the golden cases are small rounds, which the feed leaves to the plain
+    # path by default; stream them here so the streamed path is what is checked
+    if "default_threshold" not in request.keywords:
+        monkeypatch.setattr("mfl_amd.autostream.ClientFeed.SMALL_ROUND_BYTES", 0)
+
+
 def _trainer(rounds, **kw):
     T, C = fresh_classes()
     mfl_amd.install(T, device=DEV, client_cls=C, stream_clients=True)
@@ -100,3 +108,15 @@ def test_plain_round_after_streamed_round():
     for k, e in expected.items():
         assert_bits(out[k], e, k)
         assert_bits(tr.results[0][k], e, k)
+
+
+@pytest.mark.default_threshold
+def test_small_rounds_take_the_plain_path():
+    _, w_locals, expected = load_case("mnist_lr_k10")
+    tr = _trainer([[(n, [sd]) for n, sd in w_locals]] * 3, n_clients=100)
+    tr.train()
+    stats = tr.__dict__["_mfl_feed"].stats
+    assert stats["rounds_small"] == 3 and stats["rounds_streamed"] == 0 and stats["rounds_fallback"] == 0, stats
+    for res in tr.results:
+        for k, e in expected.items():
+            assert_bits(res[k], e, k)
