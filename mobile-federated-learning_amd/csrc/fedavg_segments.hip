@@ -130,7 +130,11 @@ __device__ __forceinline__ float load_cvt(const void* base, int64_t kind, int64_
 // one unit of an fp32 key: FULL units (all kSegSpan columns) take the
 // unconditional 16-B path with U rows per batch; the last unit of a key
 // masks its tail slice element by element
-template <int U, int C, bool FULL>
+// STYLE 1: the row reduce's loop shape (reduce_f32x4_buf_kernel): each
+// batch's client addresses read from the table as the batch starts, the
+// batch's loads then consume_batch -- the compiler interleaves loads and
+// products as it does there (probe variants)
+template <int U, int C, bool FULL, int STYLE = 0>
 __device__ __forceinline__ void reduce_raw_unit(const int64_t* __restrict__ P, int K, int64_t c0, int64_t n,
                                                 const float* __restrict__ W, float* __restrict__ o) {
   f32x4 acc[C];
@@ -146,6 +150,69 @@ __device__ __forceinline__ void reduce_raw_unit(const int64_t* __restrict__ P, i
   }
   const int nb = (K - 1) / U;
   int k = 1;
+  if constexpr (FULL && STYLE >= 2) {
+    // STYLE 2/3/4: loads and products interleaved in (row, slice) order with
+    // at most L = 2/4/8 loads of this wave in flight (sched_barrier keeps the
+    // compiler from hoisting the batch's loads into one burst)
+    constexpr int L = STYLE == 2 ? 2 : (STYLE == 3 ? 4 : 8);
+    constexpr int N = U * C;
+    for (int b = 0; b < nb; ++b, k += U) {
+      __amdgpu_buffer_rsrc_t rr[U];
+      float w[U];
+#pragma unroll
+      for (int r = 0; r < U; ++r) {
+        rr[r] = unit_rsrc(reinterpret_cast<const float*>(P[k + r]) + c0);
+        w[r] = W[k + r];
+      }
+      f32x4 x[N];
+#pragma unroll
+      for (int i = 0; i < N + L; ++i) {
+        if (i < N) x[i] = ldb(rr[i / C], off[i % C]);
+        if (i >= L) {
+          const int j = i - L;
+          const f32x4 term = x[j] * w[j / C];
+          acc[j % C] = acc[j % C] + term;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    for (; k < K; ++k) {
+      const __amdgpu_buffer_rsrc_t rr = unit_rsrc(reinterpret_cast<const float*>(P[k]) + c0);
+      const float w = W[k];
+#pragma unroll
+      for (int s = 0; s < C; ++s) {
+        const f32x4 term = ldb(rr, off[s]) * w;
+        acc[s] = acc[s] + term;
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < C; ++s) *reinterpret_cast<f32x4_a4*>(o + 4 * (threadIdx.x + s * kBlock)) = acc[s];
+    return;
+  }
+  if constexpr (FULL && STYLE == 1) {
+    for (int b = 0; b < nb; ++b, k += U) {
+      f32x4 xs[U][C];
+#pragma unroll
+      for (int r = 0; r < U; ++r) {
+        const __amdgpu_buffer_rsrc_t rr = unit_rsrc(reinterpret_cast<const float*>(P[k + r]) + c0);
+#pragma unroll
+        for (int s = 0; s < C; ++s) xs[r][s] = ldb(rr, off[s]);
+      }
+      consume_batch<U, C>(acc, xs, W, k);
+    }
+    for (; k < K; ++k) {
+      const __amdgpu_buffer_rsrc_t rr = unit_rsrc(reinterpret_cast<const float*>(P[k]) + c0);
+      const float w = W[k];
+#pragma unroll
+      for (int s = 0; s < C; ++s) {
+        const f32x4 term = ldb(rr, off[s]) * w;
+        acc[s] = acc[s] + term;
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < C; ++s) *reinterpret_cast<f32x4_a4*>(o + 4 * (threadIdx.x + s * kBlock)) = acc[s];
+    return;
+  }
   // the next batch's client addresses are loaded one batch ahead, so the
   // pointer-table latency overlaps the current batch's data loads
   int64_t nxt[U];
@@ -202,7 +269,7 @@ __device__ __forceinline__ void reduce_raw_unit(const int64_t* __restrict__ P, i
   }
 }
 
-template <int U, int C>
+template <int U, int C, int STYLE = 0>
 __global__ __launch_bounds__(kBlock) void reduce_segments_f32_kernel(const SegKey* __restrict__ keys,
                                                                      const int64_t* __restrict__ ptrs, int64_t n_keys,
                                                                      int64_t unit0, int K, const float* __restrict__ W,
@@ -217,7 +284,7 @@ __global__ __launch_bounds__(kBlock) void reduce_segments_f32_kernel(const SegKe
   float* o = out + key.out_offset + c0;
   if (key.kind == kRaw) {
     if (n == span)
-      reduce_raw_unit<U, C, true>(P, K, c0, n, W, o);
+      reduce_raw_unit<U, C, true, STYLE>(P, K, c0, n, W, o);
     else
       reduce_raw_unit<1, C, false>(P, K, c0, n, W, o);
     return;
@@ -570,7 +637,7 @@ int64_t stage_tables(const char* what, const int64_t* client_ptrs, const int64_t
 
 // round-split: equal launches of at most `cap` workgroups (production: 3 x
 // CUs, the reduce's schedule); cap <= 0 = one launch
-template <int U, int C>
+template <int U, int C, int STYLE = 0>
 void launch_reduce_segments(const SegKey* keys, const int64_t* ptrs, int64_t n_keys, int64_t units, int64_t K,
                             const float* weights, float* out, int64_t cap, hipStream_t s) {
   if (cap <= 0) cap = units;
@@ -578,7 +645,7 @@ void launch_reduce_segments(const SegKey* keys, const int64_t* ptrs, int64_t n_k
   const int64_t per = (units + nl - 1) / nl;
   for (int64_t u0 = 0; u0 < units; u0 += per) {
     const int64_t nb = units - u0 < per ? units - u0 : per;
-    hipLaunchKernelGGL((reduce_segments_f32_kernel<U, C>), dim3(static_cast<unsigned>(nb)), dim3(kBlock), 0, s, keys,
+    hipLaunchKernelGGL((reduce_segments_f32_kernel<U, C, STYLE>), dim3(static_cast<unsigned>(nb)), dim3(kBlock), 0, s, keys,
                        ptrs, n_keys, u0, static_cast<int>(K), weights, out);
   }
 }
@@ -812,9 +879,13 @@ int fedavg_reduce_segments_f32_variant(const int64_t* client_ptrs, const int64_t
   const char* what = "fedavg_reduce_segments_f32_variant";
   if (!weights || !out) return set_error(FEDAVG_EINVAL, "%s: null weights/out", what);
   if (!is_device_memory(out)) return set_error(FEDAVG_EINVAL, "%s: out must be device memory", what);
+  // unroll >= 100: STYLE unroll / 100 (1: the row reduce's loop shape; 2-4:
+  // interleaved with 2 / 4 / 8 loads in flight) at unroll % 100
   const int uc = unroll * 100 + cols;
   if (uc != 408 && uc != 804 && uc != 208 && uc != 404 && uc != 802 && uc != 1602 && uc != 216 && uc != 116 &&
-      uc != 801 && uc != 401 && uc != 1601 && uc != 402)
+      uc != 801 && uc != 401 && uc != 1601 && uc != 402 && uc != 10216 && uc != 10404 && uc != 10408 &&
+      uc != 10208 && uc != 10804 && uc != 20216 && uc != 30216 && uc != 40216 && uc != 20404 && uc != 30404 &&
+      uc != 30408 && uc != 40408)
     return set_error(FEDAVG_EMODE, "%s: unsupported (unroll, cols) = (%d, %d)", what, unroll, cols);
   if (blocks_per_cu < 0) return set_error(FEDAVG_EINVAL, "%s: blocks_per_cu < 0", what);
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -834,6 +905,18 @@ int fedavg_reduce_segments_f32_variant(const int64_t* client_ptrs, const int64_t
     case 802: launch_reduce_segments<8, 2>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;
     case 1602: launch_reduce_segments<16, 2>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;
     case 216: launch_reduce_segments<2, 16>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;
+    case 10216: launch_reduce_segments<2, 16, 1>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;
+    case 10404: launch_reduce_segments<4, 4, 1>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;
+    case 10408: launch_reduce_segments<4, 8, 1>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;
+    case 10208: launch_reduce_segments<2, 8, 1>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;
+    case 10804: launch_reduce_segments<8, 4, 1>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;
+    case 20216: launch_reduce_segments<2, 16, 2>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;
+    case 30216: launch_reduce_segments<2, 16, 3>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;
+    case 40216: launch_reduce_segments<2, 16, 4>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;
+    case 20404: launch_reduce_segments<4, 4, 2>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;
+    case 30404: launch_reduce_segments<4, 4, 3>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;
+    case 30408: launch_reduce_segments<4, 8, 3>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;
+    case 40408: launch_reduce_segments<4, 8, 4>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;
     case 801: launch_reduce_segments<8, 1>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;
     case 401: launch_reduce_segments<4, 1>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;
     case 1601: launch_reduce_segments<16, 1>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;

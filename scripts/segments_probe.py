@@ -10,7 +10,12 @@ Three variants, interleaved in one process, all bit-identical:
                tensors (the device-resident drop-in's case),
   *-pow2-pitch the first two on rows at a power-of-two pitch (128 MiB),
   ptrs-*       fedavg_reduce_ptrs_f32 (device pointer array) on the rows and
-               on the separate tensors.
+               on the separate tensors,
+  seg-skewed-tensors  K separate allocations whose client starts are skewed
+               by k * 37 mod 64 x 256 B (the allocator's 2 MiB-congruent
+               starts broken, the allocations -- and their translations -- kept),
+  seg-2mib-pitch  one buffer, rows at a 2 MiB-multiple pitch (congruent
+               starts, one allocation); with --names pick a subset.
 Separates the kernel's own cost from where the clients' memory lies.  One
 JSON line per variant: median ms per call (HIP events) and GB/s.
 """
@@ -107,6 +112,7 @@ def main():
     ap.add_argument("--model", default="", help="multi-key mode: a scripts/bench_e2e.py config name")
     ap.add_argument("--sched", nargs="*", default=[], help="multi-key mode: U,C,blocks_per_cu variants to time")
     ap.add_argument("--only", default="", help="time only 'rows' and this variant (for per-kernel PMC passes)")
+    ap.add_argument("--names", nargs="*", default=[], help="time only these variants ('rows' is always timed)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -129,21 +135,39 @@ def main():
     ld2 = 1 << max(0, (P - 1).bit_length())
     rows2 = torch.empty((K, ld2), device=dev)
     rows2[:, :P].copy_(rows[:, :P])
-    names = ["rows", "rows-pow2-pitch", "seg-rows", "seg-pow2-pitch", "seg-tensors", "ptrs-rows", "ptrs-tensors"]
+    # separate allocations with skewed starts (each padded by up to 16 KiB)
+    skew = [(k * 37 % 64) * 64 for k in range(K)]  # floats: multiples of 256 B
+    skewed = []
+    for k in range(K):
+        buf = torch.empty(P + 64 * 64, device=dev)
+        buf[skew[k]:skew[k] + P].copy_(tensors[k])
+        skewed.append(buf[skew[k]:skew[k] + P])
+    # one buffer, pitch rounded up to 2 MiB (every row start congruent mod 2 MiB)
+    ld3 = (P * 4 + (2 << 20) - 1) // (2 << 20) * (2 << 20) // 4
+    rows3 = torch.empty((K, ld3), device=dev)
+    rows3[:, :P].copy_(rows[:, :P])
+    names = ["rows", "rows-pow2-pitch", "seg-rows", "seg-pow2-pitch", "seg-tensors", "ptrs-rows", "ptrs-tensors",
+             "seg-skewed-tensors", "seg-2mib-pitch"]
     sched = [(4, 8, 3), (4, 8, 0), (4, 8, 2), (4, 8, 4), (4, 8, 6), (8, 4, 3), (8, 4, 6), (2, 8, 3), (2, 8, 6),
              (4, 4, 3), (4, 4, 6), (8, 2, 6), (16, 2, 3), (2, 16, 3), (1, 16, 3), (1, 16, 6)]
     if args.sweep:
-        names += [f"var-{src}-U{u}C{c}b{b}" for src in ("tensors", "rows") for u, c, b in sched]
+        names += [f"var-{src}-U{u}C{c}b{b}" for src in ("tensors", "rows", "skewed") for u, c, b in sched]
     if args.only:
         names = ["rows", args.only]
+    if args.names:
+        names = ["rows"] + [n for n in args.names if n != "rows"]
     outs = {n: torch.empty(P, device=dev) for n in names}
     meta = [np.array([v], dtype=np.int64) for v in (P, 0, 0)]
     ptr_rows = np.array([[rows[k].data_ptr()] for k in range(K)], dtype=np.int64)
     ptr_tens = np.array([[t.data_ptr()] for t in tensors], dtype=np.int64)
     ptr_pow2 = np.array([[rows2[k].data_ptr()] for k in range(K)], dtype=np.int64)
+    ptr_skew = np.array([[t.data_ptr()] for t in skewed], dtype=np.int64)
+    ptr_2mib = np.array([[rows3[k].data_ptr()] for k in range(K)], dtype=np.int64)
     starts = [int(t.data_ptr()) for t in tensors]
     print(json.dumps({"tensor_start_alignment_log2": [min(31, (a & -a).bit_length() - 1) for a in starts[:8]],
-                      "pitch_bytes_rows": ld * 4, "pitch_bytes_pow2": ld2 * 4}), flush=True)
+                      "skewed_start_mod_2mib": [int(t.data_ptr()) % (2 << 20) for t in skewed[:8]],
+                      "pitch_bytes_rows": ld * 4, "pitch_bytes_pow2": ld2 * 4, "pitch_bytes_2mib": ld3 * 4}),
+          flush=True)
     dptrs = {"ptrs-rows": torch.from_numpy(ptr_rows[:, 0].copy()).to(dev),
              "ptrs-tensors": torch.from_numpy(ptr_tens[:, 0].copy()).to(dev)}
     need = lib.fedavg_segments_workspace(K, 1)
@@ -167,12 +191,13 @@ def main():
             _, src, uc = n.split("-")
             u, rest = uc[1:].split("C")
             c, b = rest.split("b")
-            ptrs = ptr_tens if src == "tensors" else ptr_rows
+            ptrs = {"tensors": ptr_tens, "rows": ptr_rows, "skewed": ptr_skew}[src]
             mfl_amd._lib.check(lib.fedavg_reduce_segments_f32_variant(
                 ptrs.ctypes.data, meta[0].ctypes.data, meta[1].ctypes.data, meta[2].ctypes.data, 1, K, w.data_ptr(),
                 outs[n].data_ptr(), h.data_ptr(), d.data_ptr(), need, int(u), int(c), int(b), stream.cuda_stream), n)
             return
-        ptrs = {"seg-rows": ptr_rows, "seg-pow2-pitch": ptr_pow2, "seg-tensors": ptr_tens}[n]
+        ptrs = {"seg-rows": ptr_rows, "seg-pow2-pitch": ptr_pow2, "seg-tensors": ptr_tens,
+                "seg-skewed-tensors": ptr_skew, "seg-2mib-pitch": ptr_2mib}[n]
         mfl_amd._lib.check(lib.fedavg_reduce_segments_f32(ptrs.ctypes.data, meta[0].ctypes.data, meta[1].ctypes.data,
                                                           meta[2].ctypes.data, 1, K, w.data_ptr(), outs[n].data_ptr(),
                                                           h.data_ptr(), d.data_ptr(), need, stream.cuda_stream), n)
