@@ -165,11 +165,20 @@ int fedavg_reduce_f32_buf(const float* clients, int64_t K, int64_t P, int64_t ld
  * blocks (0 = one launch).  Same workspace as fedavg_client_sqdist_f32. */
 /* fedavg_reduce_sqdist_f32 with an explicit tile width (cols = 64, 128 or
  * 256 columns) and workgroups per CU (0 = as many as LDS allows); K <= 128,
- * workspace >= K x (blocks per CU x CUs) doubles. */
+ * workspace >= K x (blocks per CU x CUs) doubles.  Other codes select the
+ * probe kernels listed at the switch in fedavg_dist.hip, among them the
+ * wave-owned windows: 70000000 + KMAX x 100 + 40 + VEC (K <= KMAX; KMAX x
+ * VEC in 16 x 4, 32 x 4, 48 x 4, 64 x 2, 80 x 2, 100 x 2, 128 x 1; workspace
+ * >= K x 4 x workgroups). */
 int fedavg_reduce_sqdist_f32_variant(const float* clients, int64_t K, int64_t P, int64_t ld,
                                      const float* weights, float* out, double* workspace,
                                      int64_t workspace_elems, double* sumsq, int cols,
                                      int blocks_per_cu, void* stream);
+/* fedavg_reduce_sqdist_f32's kernel choice for K x P: kind x 1000000 + S x 100
+ * + slots (kind 0: two passes, 1: LDS-DMA tiles of S columns, 2:
+ * register-staged tiles of S columns and `slots` slots, 3: wave-owned
+ * windows of KMAX = S rows and VEC = slots columns per lane). */
+int64_t fedavg_fused_plan_of(int64_t K, int64_t P);
 int fedavg_client_sqdist_buf(const float* clients, int64_t K, int64_t P, int64_t ld, const float* glob,
                              double* workspace, int64_t workspace_elems, double* sumsq, int unroll, int cols,
                              int max_blocks, void* stream);

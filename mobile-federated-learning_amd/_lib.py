@@ -87,6 +87,7 @@ TUNING_SIGNATURES = {
                                               _c_int, _vp]),
     "fedavg_client_sqdist_buf": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_i64, _vp, _c_int, _c_int,
                                           _c_int, _vp]),
+    "fedavg_fused_plan_of": (_c_i64, [_c_i64, _c_i64]),
     "fedavg_reduce_sqdist_f32_variant": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _c_i64, _vp, _c_int,
                                                   _c_int, _vp]),
     "fedavg_reduce_vec_buf": (_c_int, [_c_int, _vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_int, _c_int, _c_int, _vp]),

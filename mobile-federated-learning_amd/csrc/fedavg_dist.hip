@@ -804,9 +804,294 @@ int launch_fused_rs(const float* clients, int64_t K, int64_t P, int64_t ld, cons
   return launch_status(what);
 }
 
+// ---------------------------------------------------------------------------
+// Wave-owned windows (round 3).  The tile kernels above share a tile between
+// the 4 waves of a workgroup: one thread per COLUMN runs the chain from LDS,
+// so every tile crosses LDS and a barrier, and each workgroup asks for K row
+// segments of only S x 4 bytes at a time.  Here one WAVE owns a window of
+// 64 x VEC columns and ALL K rows of it in registers (lane l: columns
+// l*VEC .. l*VEC + VEC - 1 of every row; K x VEC VGPRs), so
+//   - the chain is per lane, straight from registers (packed fp32 mul/add:
+//     the bits of fedavg_reduce_f32), no LDS, no barrier;
+//   - the squares are per lane as well, and row i's registers are reloaded
+//     with the NEXT window's row i right after row i is squared: the next
+//     window's K loads are issued during this window's squares (the
+//     hardware's 63-load vmcnt cap throttles the issue, nothing else does),
+//     so one register image serves both windows with no double buffer;
+//   - a workgroup's NW waves take adjacent windows: NW x 64 x VEC x 4 bytes
+//     of every row in flight together (2 KiB at VEC 2, NW 4).
+// Row sums: a lane's fp64 partial of row i covers VEC columns; each batch of
+// 8 rows is folded across the wave with v_permlane32_swap (8 rows -> 4
+// registers, each row over 32 lanes), v_permlane16_swap (-> 2 registers, 16
+// lanes per row) and one row_ror:8 exchange (-> 1 register: row 4h + [0, 2,
+// 1, 3][l >> 4] in the 8 lanes l with (l >> 3) & 1 = h), added into one fp64
+// accumulator per batch that lives across all windows; the 8-lane groups are
+// summed once at the end (quad_perm / half-mirror DPP) -> partials[row][wave]
+// -> the fixed-order finalize.  Deterministic; windows are read through one
+// SGPR buffer descriptor per row whose range ends at the model's last 16-B
+// slice (num_records 0 past the last window: the tail's reloads are dropped
+// in the address unit, no traffic), columns past P inside the last slice are
+// zeroed before the chain.
+// MODE 1: loads only (a traffic probe: wrong results).
+// ---------------------------------------------------------------------------
+template <int VEC>
+struct WinVec {
+  typedef float T __attribute__((ext_vector_type(VEC)));
+};
+
+// lanes 0-31: a's two halves added (lane l: a[l] + a[l + 32]); lanes 32-63: b's
+__device__ __forceinline__ double fold32(double a, double b) {
+  const uint64_t ua = __builtin_bit_cast(uint64_t, a), ub = __builtin_bit_cast(uint64_t, b);
+  const auto lo = __builtin_amdgcn_permlane32_swap(static_cast<uint32_t>(ua), static_cast<uint32_t>(ub), false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap(static_cast<uint32_t>(ua >> 32), static_cast<uint32_t>(ub >> 32),
+                                                   false, false);
+  const double na = __builtin_bit_cast(double, (static_cast<uint64_t>(hi[0]) << 32) | lo[0]);
+  const double nb = __builtin_bit_cast(double, (static_cast<uint64_t>(hi[1]) << 32) | lo[1]);
+  return na + nb;
+}
+
+// 16-lane rows [a.r0 + a.r1, b.r0 + b.r1, a.r2 + a.r3, b.r2 + b.r3]
+__device__ __forceinline__ double fold16(double a, double b) {
+  const uint64_t ua = __builtin_bit_cast(uint64_t, a), ub = __builtin_bit_cast(uint64_t, b);
+  const auto lo = __builtin_amdgcn_permlane16_swap(static_cast<uint32_t>(ua), static_cast<uint32_t>(ub), false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap(static_cast<uint32_t>(ua >> 32), static_cast<uint32_t>(ub >> 32),
+                                                   false, false);
+  const double na = __builtin_bit_cast(double, (static_cast<uint64_t>(hi[0]) << 32) | lo[0]);
+  const double nb = __builtin_bit_cast(double, (static_cast<uint64_t>(hi[1]) << 32) | lo[1]);
+  return na + nb;
+}
+
+// lanes with bit 3 clear keep a's value + the lane 8 above; set: b's + the lane 8 below
+__device__ __forceinline__ double fold8(double a, double b, bool upper) {
+  const double send = upper ? a : b;
+  const double keep = upper ? b : a;
+  return keep + dpp_move_f64<0x128, 0xF>(send);  // row_ror:8 = lane xor 8 within a 16-lane row
+}
+
+// batch row held by lane l after fold32 / fold16 / fold8
+__device__ __forceinline__ int win_batch_row(int lane) {
+  const int r = lane >> 4;
+  return 4 * ((lane >> 3) & 1) + (((r & 1) << 1) | (r >> 1));
+}
+
+template <int VEC>
+__device__ __forceinline__ typename WinVec<VEC>::T win_load(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  typedef typename WinVec<VEC>::T V;
+  if constexpr (VEC == 1)
+    return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b32(r, static_cast<int>(off), 0, 2));
+  else if constexpr (VEC == 2)
+    return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b64(r, static_cast<int>(off), 0, 2));
+  else
+    return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(off), 0, 2));
+}
+
+template <int VEC>
+__device__ __forceinline__ double win_sq(typename WinVec<VEC>::T d) {
+  double s = static_cast<double>(d[0]) * static_cast<double>(d[0]);
+#pragma unroll
+  for (int v = 1; v < VEC; ++v) s = __builtin_fma(static_cast<double>(d[v]), static_cast<double>(d[v]), s);
+  return s;
+}
+
+// __launch_bounds__'s second argument is waves per SIMD: the window's KMAX x
+// VEC registers (+ a quarter more at VEC 1: one square per row per lane
+// before the folds) and ~40 others within 512 / waves
+constexpr int win_min_waves(int kmax, int vec) {
+  const int regs = kmax * vec + (vec == 1 ? kmax / 4 : 0);
+  return regs <= 88 ? 4 : (regs <= 128 ? 3 : (regs <= 216 ? 2 : 1));
+}
+
+template <int KMAX, int VEC, int NW, int MODE = 0, int MINW = win_min_waves(KMAX, VEC)>
+__global__ __launch_bounds__(64 * NW, MINW) void reduce_sqdist_win_kernel(
+    const float* __restrict__ X, int K, int64_t ld, int64_t P, int64_t nwin, const float* __restrict__ W,
+    float* __restrict__ out, double* __restrict__ partials) {
+  typedef typename WinVec<VEC>::T V;
+  constexpr int WC = 64 * VEC;
+  constexpr int NB = (KMAX + 7) / 8;
+  const int lane = threadIdx.x & 63;
+  const int64_t GW = static_cast<int64_t>(gridDim.x) * NW;
+  const int64_t gw = static_cast<int64_t>(blockIdx.x) * NW + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t voff = static_cast<uint32_t>(lane) * VEC * 4;
+  const int64_t P4 = (P + 3) & ~static_cast<int64_t>(3);  // rows are read up to their last 16-B slice
+  const int64_t row_bytes = ld * 4;
+  const bool upper = (lane & 8) != 0;
+
+  // window w's bytes per row (0: no such window -- its loads return 0 and move nothing)
+  const auto win_bytes = [&](int64_t w) -> int {
+    if (w >= nwin) return 0;
+    const int64_t n = P4 - w * WC;
+    return static_cast<int>((n < WC ? n : WC) * 4);
+  };
+  // Rows K..KMAX-1 are padding: loaded through an empty descriptor (0, no
+  // traffic) and weighted -0.0 in the chain (x + (+0 * -0) == x for every x,
+  // -0 and NaN included); their sums are never written.  Every row bound is
+  // computed per window from an opaque copy of K: hoisted out of the window
+  // loop the KMAX row masks would not fit the SGPRs.  Row i's descriptor base
+  // advances one row per load through an opaque pointer for the same reason.
+  // The LDS accumulators are per lane: no other lane touches them, no barrier.
+  // LDS: the weights padded to KMAX with -0.0 (read as uniform 16-B
+  // broadcasts in the chain), then each wave's per-batch row accumulators
+  // [NB][64] (one fp64 per lane per batch: registers are the window's)
+  __shared__ __attribute__((aligned(16))) float wl[(KMAX + 3) & ~3];
+  __shared__ double accl[NW][NB][64];
+  for (int i = threadIdx.x; i < ((KMAX + 3) & ~3); i += 64 * NW) wl[i] = i < K ? W[i] : -0.0f;
+  double* acc = &accl[threadIdx.x >> 6][0][lane];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) acc[64 * b] = 0.0;
+  __syncthreads();
+  V x[KMAX];
+  {
+    int Kw = K;
+    asm volatile("" : "+s"(Kw));
+    const int nb = win_bytes(gw);
+    const char* rp = reinterpret_cast<const char*>(X + gw * WC);
+#pragma unroll
+    for (int i = 0; i < KMAX; ++i) {
+      asm volatile("" : "+s"(rp));
+      x[i] = win_load<VEC>(__builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(rp), 0, i < Kw ? nb : 0, 0x00020000),
+                           voff);
+      rp += row_bytes;
+    }
+  }
+  float probe = 0.f;
+  for (int64_t w = gw; w < nwin; w += GW) {
+    int Kw = K;
+    asm volatile("" : "+s"(Kw));
+    const int64_t c0 = w * WC;
+    const int64_t cl = c0 + lane * VEC;  // this lane's first column
+    const int nbn = win_bytes(w + GW);
+    const char* rp = reinterpret_cast<const char*>(X + (w + GW) * WC);
+    const auto reload = [&](int i) {  // row i of the next window into x[i]
+      asm volatile("" : "+s"(rp));
+      x[i] = win_load<VEC>(__builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(rp), 0, i < Kw ? nbn : 0, 0x00020000),
+                           voff);
+      rp += row_bytes;
+    };
+    if constexpr (MODE == 1) {
+#pragma unroll
+      for (int i = 0; i < KMAX; ++i) {
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) probe += x[i][v];
+        reload(i);
+      }
+      continue;
+    }
+    const bool ragged = c0 + WC > P;
+    if (ragged) {  // columns past P (the last slice's padding) are zeroed: never NaN in the squares
+#pragma unroll
+      for (int i = 0; i < KMAX; ++i) {
+#pragma unroll
+        for (int v = 0; v < VEC; ++v)
+          if (cl + v >= P) x[i][v] = 0.f;
+      }
+    }
+    // the reference's chain, per lane: fl32(x_0 w_0), then + fl32(x_i w_i) in client order
+    int wo = 0;  // re-read per window (an opaque LDS offset): not held in registers across windows
+    asm volatile("" : "+v"(wo));
+    V a;
+#pragma unroll
+    for (int q = 0; q < (KMAX + 3) / 4; ++q) {
+      const f32x4 w4 = *reinterpret_cast<const f32x4*>(&wl[wo + 4 * q]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int i = 4 * q + j;
+        if (i == 0) {
+          a = x[0] * w4[0];
+        } else if (i < KMAX) {
+          const V t = x[i] * w4[j];
+          a = a + t;
+        }
+      }
+    }
+    if (!ragged) {
+      __builtin_nontemporal_store(a, reinterpret_cast<V*>(out + cl));
+    } else {
+#pragma unroll
+      for (int v = 0; v < VEC; ++v)
+        if (cl + v < P) out[cl + v] = a[v];
+    }
+    // squares of fl32(x - g), each row reloaded with the next window's row as soon as it is squared
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      double p[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = 8 * b + j;
+        p[j] = 0.0;
+        if (i < KMAX) {
+          p[j] = win_sq<VEC>(x[i] - a);
+          reload(i);
+        }
+      }
+      const double q01 = fold32(p[0], p[1]), q23 = fold32(p[2], p[3]);
+      const double q45 = fold32(p[4], p[5]), q67 = fold32(p[6], p[7]);
+      acc[64 * b] += fold8(fold16(q01, q23), fold16(q45, q67), upper);
+    }
+  }
+  if constexpr (MODE == 1) {
+    if (probe == 12345.f) out[0] = probe;  // keep the loads
+    return;
+  }
+  const int row_in = win_batch_row(lane);
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    double s = acc[64 * b];
+    s += dpp_move_f64<0xB1, 0xF>(s);   // quad_perm [1,0,3,2]
+    s += dpp_move_f64<0x4E, 0xF>(s);   // quad_perm [2,3,0,1]
+    s += dpp_move_f64<0x141, 0xF>(s);  // row_half_mirror: the other quad of the 8-lane group
+    const int row = 8 * b + row_in;
+    if ((lane & 7) == 0 && row < K) partials[static_cast<int64_t>(row) * GW + gw] = s;
+  }
+}
+
+// waves of a window launch: every resident workgroup (persistent), or one
+// per NW windows when the model has fewer
+template <int KMAX, int VEC, int NW, int MODE = 0, int MINW = win_min_waves(KMAX, VEC)>
+int64_t fused_win_waves(int64_t P, int blocks_per_cu) {
+  const auto kern = reduce_sqdist_win_kernel<KMAX, VEC, NW, MODE, MINW>;
+  const int64_t per_cu = blocks_per_cu > 0 ? blocks_per_cu : resident_blocks(kern, 64 * NW) / cu_count();
+  const int64_t nwin = (P + 64 * VEC - 1) / (64 * VEC);
+  const int64_t need = (nwin + NW - 1) / NW;
+  const int64_t grid = per_cu * cu_count();
+  return (grid < need ? grid : need) * NW;
+}
+
+template <int KMAX, int VEC, int NW, int MODE = 0, int MINW = win_min_waves(KMAX, VEC)>
+int launch_fused_win(const float* clients, int64_t K, int64_t P, int64_t ld, const float* weights, float* out,
+                     double* partials, int64_t partial_elems, double* sumsq, int blocks_per_cu, hipStream_t s,
+                     const char* what) {
+  if (K > KMAX) return set_error(FEDAVG_EMODE, "%s: this window kernel covers K <= %d", what, KMAX);
+  const int64_t waves = fused_win_waves<KMAX, VEC, NW, MODE, MINW>(P, blocks_per_cu);
+  if (waves <= 0) return set_error(FEDAVG_EMODE, "%s: the window kernel is not resident", what);
+  if (partial_elems < K * waves)
+    return set_error(FEDAVG_EINVAL, "%s: workspace needs %lld doubles", what, (long long)(K * waves));
+  const int64_t nwin = (P + 64 * VEC - 1) / (64 * VEC);
+  hipLaunchKernelGGL((reduce_sqdist_win_kernel<KMAX, VEC, NW, MODE, MINW>), dim3(static_cast<unsigned>(waves / NW)),
+                     dim3(64 * NW), 0, s, clients, static_cast<int>(K), ld, P, nwin, weights, out, partials);
+  int rc = launch_status(what);
+  if (rc || MODE != 0) return rc;
+  hipLaunchKernelGGL(client_sqdist_finalize_kernel, dim3(static_cast<unsigned>(K)), dim3(kBlock), 0, s, partials,
+                     waves, sumsq);
+  return launch_status(what);
+}
+
 // Which one-read kernel serves K rows (production), from interleaved
 // measurements of every candidate against the others and the two passes on
-// ~4 GB of rows (scripts/fused_probe.py, profiles/r03/fused_rule/*.jsonl; ms):
+// ~4 GB of rows (scripts/fused_probe.py, profiles/r03/fused_rule/*.jsonl and
+// profiles/r03/win/*.jsonl; ms):
+//   long rows (>= 16 windows per wave), 17 <= K <= 128: the wave-owned
+//   windows (reduce_sqdist_win_kernel), KMAX x VEC by K:
+//     K <= 48   48 x 4 (1 KiB per wave per row; 24 x 41.7M 0.675 vs 0.697
+//               LDS-DMA 128 and 0.687 at 32 x 4; 32 x 31.3M 0.715 vs 0.736;
+//               48 x 20.8M 0.652 vs 0.687 LDS-DMA 256)
+//     K <= 64   64 x 2 (64 x 10M 0.449 vs 0.464; 56 x 20M 0.841 vs 0.867)
+//     K <= 80   80 x 2 (72 x 25M 1.311 vs 1.915 LDS-DMA 64; 80 x 25M 1.397
+//               vs 2.124 -- the LDS-DMA tiles at 65-90 rows run far below
+//               their K = 100 rate)
+//     K <= 100  100 x 2 (100 x 25M 1.531-1.665 vs 1.601-1.797 by box; 90 x
+//               25M 1.578 vs 2.440; 100 x 6.25M 0.431 vs 0.451)
+//     K <= 128  128 x 1 (128 x 8M 0.693 vs 0.879; 112 x 8M 0.610 vs 0.640)
+//   shorter rows (100 x 3.1M: window 0.230 vs 0.218), other K:
 //   K <= 16    register-staged, 256-column tiles (8 x 125M 0.896 vs 0.880
 //              LDS-DMA; FEMNIST 10 x 1.2M 16.6 vs 22.2 us)
 //   K <= 32    LDS-DMA, 128 columns (24 x 41.7M 0.733 vs 0.738 register-staged)
@@ -821,14 +1106,40 @@ int launch_fused_rs(const float* clients, int64_t K, int64_t P, int64_t ld, cons
 //              6.88 ms for the two passes; 512 x 5M 2.58 vs 3.22)
 // Beyond 512 rows the two passes are faster (640 x 3M: 2.37 vs 3.32 ms;
 // 1000 x 12.5M: 15.2 vs 20.0): each tile's K-step chain grows with K.
-constexpr int kFusedNone = 0, kFusedLds = 1, kFusedRs = 2;
+constexpr int kFusedNone = 0, kFusedLds = 1, kFusedRs = 2, kFusedWin = 3;
 constexpr int64_t kFusedRowsMaxK = 512;
+constexpr int64_t kWinMinPerWave = 16;  // windows per wave below which the tile kernels keep the round
 struct FusedPlan {
-  int kind, S, slots;
+  int kind, S, slots;  // kFusedWin: S = KMAX, slots = VEC
 };
 
-inline FusedPlan fused_plan(int64_t K) {
+// the window kernel instance for K rows ({kFusedNone} outside 17..128)
+inline FusedPlan win_plan(int64_t K) {
+  if (K <= 16 || K > 128) return {kFusedNone, 0, 0};
+  if (K <= 48) return {kFusedWin, 48, 4};
+  if (K <= 64) return {kFusedWin, 64, 2};
+  if (K <= 80) return {kFusedWin, 80, 2};
+  if (K <= 100) return {kFusedWin, 100, 2};
+  return {kFusedWin, 128, 1};
+}
+
+// waves of the production window launch for plan `pl` (0: not a window plan)
+inline int64_t win_waves(const FusedPlan& pl, int64_t P) {
+  if (pl.kind != kFusedWin) return 0;
+  switch (pl.S) {
+    case 48: return fused_win_waves<48, 4, 4>(P, 0);
+    case 64: return fused_win_waves<64, 2, 4>(P, 0);
+    case 80: return fused_win_waves<80, 2, 4>(P, 0);
+    case 100: return fused_win_waves<100, 2, 4>(P, 0);
+    default: return fused_win_waves<128, 1, 4>(P, 0);
+  }
+}
+
+inline FusedPlan fused_plan(int64_t K, int64_t P) {
   if (K < 1 || K > kFusedRowsMaxK) return {kFusedNone, 0, 0};
+  const FusedPlan win = win_plan(K);
+  if (win.kind == kFusedWin && (P + 64 * win.slots - 1) / (64 * win.slots) >= kWinMinPerWave * win_waves(win, P))
+    return win;
   if (K <= 16) return {kFusedRs, 256, 8};
   if (K <= 32) return {kFusedLds, 128, 0};
   if (K <= 48) return {kFusedLds, 256, 0};
@@ -1134,10 +1445,12 @@ int fedavg_client_sqdist_buf(const float* clients, int64_t K, int64_t P, int64_t
 // fedavg_reduce_f32's bits and sumsq the :291 sums.
 int64_t fedavg_reduce_sqdist_workspace(int64_t K, int64_t P) {
   if (K <= 0 || P <= 0) return 0;
-  const FusedPlan pl = fused_plan(K);
+  const FusedPlan pl = fused_plan(K, P);
   const int64_t two_pass = fedavg_client_sqdist_workspace(K, P);
   int64_t fused = 0;
-  if (pl.kind == kFusedLds) {
+  if (pl.kind == kFusedWin) {
+    fused = K * win_waves(pl, P);
+  } else if (pl.kind == kFusedLds) {
     if (pl.S == 64) fused = K * fused_grid<64>(K, P, 0);
     if (pl.S == 128) fused = K * fused_grid<128>(K, P, 0);
     if (pl.S == 256) fused = K * fused_grid<256>(K, P, 0);
@@ -1169,8 +1482,27 @@ int fedavg_reduce_sqdist_f32(const float* clients, int64_t K, int64_t P, int64_t
     const hipError_t e = hipMemsetAsync(sumsq, 0, static_cast<size_t>(K) * sizeof(double), s);
     return e == hipSuccess ? FEDAVG_OK : set_error(-static_cast<int>(e), "%s: hipMemsetAsync failed", what);
   }
-  const FusedPlan pl = fused_plan(K);
+  const FusedPlan pl = fused_plan(K, P);
   if (pl.kind != kFusedNone && aligned4(out) && aligned4(weights)) {
+    if (pl.kind == kFusedWin) {
+      switch (pl.S) {
+        case 48:
+          return launch_fused_win<48, 4, 4>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq, 0, s,
+                                            what);
+        case 64:
+          return launch_fused_win<64, 2, 4>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq, 0, s,
+                                            what);
+        case 80:
+          return launch_fused_win<80, 2, 4>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq, 0, s,
+                                            what);
+        case 100:
+          return launch_fused_win<100, 2, 4>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq, 0, s,
+                                             what);
+        default:
+          return launch_fused_win<128, 1, 4>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq, 0, s,
+                                             what);
+      }
+    }
     if (pl.kind == kFusedLds) {
       if (pl.S == 64)
         return launch_fused<64>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq, 0, s, what);
@@ -1195,6 +1527,14 @@ int fedavg_reduce_sqdist_f32(const float* clients, int64_t K, int64_t P, int64_t
 }
 
 #ifdef FEDAVG_TUNING  // probe library only (libfedavg_amd_probe.so)
+// the production plan of fedavg_reduce_sqdist_f32 for K x P (tests): kind x
+// 1000000 + S x 100 + slots (kind 0 two passes, 1 LDS-DMA tiles, 2
+// register-staged tiles, 3 wave-owned windows with S = KMAX, slots = VEC)
+int64_t fedavg_fused_plan_of(int64_t K, int64_t P) {
+  const FusedPlan pl = fused_plan(K, P);
+  return static_cast<int64_t>(pl.kind) * 1000000 + pl.S * 100 + pl.slots;
+}
+
 // the fused pass with an explicit tile width (64 / 128 / 256 columns) and
 // workgroups per CU (0 = as many as LDS allows); workspace >= K x grid
 int fedavg_reduce_sqdist_f32_variant(const float* clients, int64_t K, int64_t P, int64_t ld, const float* weights,
@@ -1306,6 +1646,27 @@ int fedavg_reduce_sqdist_f32_variant(const float* clients, int64_t K, int64_t P,
                                                      sumsq, blocks_per_cu, s, what);
     case 15300064: return launch_fused_rs<64, 8, 3, 0, 2>(clients, K, P, ld, weights, out, workspace,
                                                           workspace_elems, sumsq, blocks_per_cu, s, what);
+    // wave-owned windows (reduce_sqdist_win_kernel): 60000000 + MODE *
+    // 1000000 + NW * 10 + VEC at K <= 100; 70000000 + KMAX * 100 + NW * 10 + VEC
+#define FEDAVG_WIN_CASE(VEC, NW, MODE)                                                                            \
+  case 60000000 + MODE * 1000000 + NW * 10 + VEC:                                                                \
+    return launch_fused_win<100, VEC, NW, MODE>(clients, K, P, ld, weights, out, workspace, workspace_elems,     \
+                                                sumsq, blocks_per_cu, s, what);
+    FEDAVG_WIN_CASE(2, 4, 1)
+    FEDAVG_WIN_CASE(4, 4, 1)
+#define FEDAVG_WINK_CASE(KMAX, VEC, MINW)                                                                         \
+  case 70000000 + KMAX * 100 + 40 + VEC:                                                                         \
+    return launch_fused_win<KMAX, VEC, 4, 0, MINW>(clients, K, P, ld, weights, out, workspace, workspace_elems,  \
+                                                   sumsq, blocks_per_cu, s, what);
+    FEDAVG_WINK_CASE(100, 2, 2)
+    FEDAVG_WINK_CASE(80, 2, 2)
+    FEDAVG_WINK_CASE(64, 2, 3)
+    FEDAVG_WINK_CASE(32, 4, 3)
+    FEDAVG_WINK_CASE(48, 4, 2)
+    FEDAVG_WINK_CASE(16, 4, 4)
+    FEDAVG_WINK_CASE(128, 1, 2)
+#undef FEDAVG_WINK_CASE
+#undef FEDAVG_WIN_CASE
     default: return set_error(FEDAVG_EMODE, "%s: cols must be 32, 64, 128 or 256 (+1000: double-buffered)", what);
   }
 }

@@ -1,0 +1,127 @@
+"""GPU parity of the wave-owned window kernels (reduce_sqdist_win_kernel):
+the fused aggregate + :291 pass for 17-128 clients on long rows.
+
+Every instance (KMAX rows x VEC columns per lane) is driven through the probe
+entry at small shapes -- one window, ragged windows, K below KMAX (padding
+rows weighted -0.0), NaN row padding -- and must give the oracle's bits
+(fedavg_trainer.py:450-457) and :291 sums (fp32 difference, fp64 squares) of
+the same fp32 differences within 1e-12; the production plan is then checked
+on both sides of each K band at a length that selects the windows.
+"""
+import numpy as np
+import pytest
+import torch
+
+import fedavg_oracle as O
+import mfl_amd
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda", 0)
+INSTANCES = [(16, 4), (32, 4), (48, 4), (64, 2), (80, 2), (100, 2), (128, 1)]
+KIND_WIN = 3
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu(gpu_available):
+    mfl_amd._lib.load()
+    torch.cuda.set_device(DEV)
+    yield
+
+
+def _rows(K, P, seed, pad=float("nan")):
+    ld = (P + 63) // 64 * 64
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    x = torch.full((K, ld), pad, device=DEV)
+    x[:, :P] = torch.randn((K, P), generator=g, device=DEV) * 0.05 + torch.randn((K, 1), generator=g, device=DEV) * 1e-3
+    counts = torch.randint(1, 1000, (K,), generator=torch.Generator().manual_seed(seed)).tolist()
+    return x, ld, mfl_amd.sample_weights(counts)
+
+
+def _sumsq_ref(x, out, P):
+    return torch.stack([((x[k, :P] - out[:P]).double() ** 2).sum() for k in range(x.shape[0])])
+
+
+def _win(x, K, P, ld, w, kmax, vec):
+    lib = mfl_amd._lib.load_probe()
+    n_ws = K * 4 * 2048
+    work = torch.empty(n_ws, dtype=torch.float64, device=DEV)
+    out = torch.empty(P, device=DEV)
+    s = torch.empty(K, dtype=torch.float64, device=DEV)
+    code = 70000000 + kmax * 100 + 40 + vec
+    mfl_amd._lib.check(lib.fedavg_reduce_sqdist_f32_variant(x.data_ptr(), K, P, ld, w.data_ptr(), out.data_ptr(),
+                                                            work.data_ptr(), n_ws, s.data_ptr(), code, 0, None),
+                       f"window {kmax}x{vec}", lib)
+    return out, s
+
+
+@pytest.mark.parametrize("kmax,vec", INSTANCES)
+def test_window_instances_vs_oracle(kmax, vec):
+    for K in sorted({1, 2, kmax // 2 + 1, kmax - 1, kmax}):
+        for P in (1, 3, 64 * vec + 5, 100_003):
+            x, ld, weights = _rows(K, P, kmax * 7919 + K * 131 + P)
+            w = mfl_amd.weights_tensor(weights, torch.float32, DEV)
+            out, s = _win(x, K, P, ld, w, kmax, vec)
+            exp = O.reduce_f32(x[:, :P].cpu().numpy(), np.array([np.float32(v) for v in weights], dtype=np.float32))
+            assert out.cpu().numpy().view(np.uint32).tobytes() == exp.view(np.uint32).tobytes(), (kmax, vec, K, P)
+            ref = _sumsq_ref(x, out, P)
+            rel = ((s - ref).abs() / ref.clamp_min(1e-300)).max().item()
+            assert rel < 1e-12, (kmax, vec, K, P, rel)
+            _, again = _win(x, K, P, ld, w, kmax, vec)
+            assert torch.equal(s, again)  # deterministic
+
+
+@pytest.mark.parametrize("kmax,vec", [(48, 4), (100, 2), (128, 1)])
+def test_window_negative_zero_and_nonfinite(kmax, vec):
+    """-0.0 everywhere keeps -0.0 through the padding rows' (+0 x -0.0) terms;
+    inf / NaN inside the model propagate as the reference's ops do."""
+    K, P = kmax - 3, 64 * vec * 3 + 1
+    x, ld, weights = _rows(K, P, 5)
+    x[:, :P] = -0.0
+    w = mfl_amd.weights_tensor(weights, torch.float32, DEV)
+    out, s = _win(x, K, P, ld, w, kmax, vec)
+    assert torch.all(out.view(torch.int32) == torch.tensor(-0.0).view(torch.int32).item())
+    assert torch.all(s == 0)
+    x, ld, weights = _rows(K, P, 6)
+    x[1, 17] = float("inf")
+    x[2, P - 1] = float("nan")
+    out, s = _win(x, K, P, ld, w, kmax, vec)
+    exp = O.reduce_f32(x[:, :P].cpu().numpy(), np.array([np.float32(v) for v in weights], dtype=np.float32))
+    got = out.cpu().numpy()
+    assert np.array_equal(np.isnan(got), np.isnan(exp))
+    assert np.array_equal(got[~np.isnan(got)], exp[~np.isnan(exp)])
+    ref = _sumsq_ref(x, out, P)
+    assert torch.equal(torch.isnan(s), torch.isnan(ref))
+
+
+@pytest.mark.parametrize("K", [17, 48, 49, 64, 65, 80, 81, 100, 101, 128])
+def test_window_plan_bands_bit_exact(K):
+    """Long rows: the production plan takes the window instance of K's band;
+    the reduce's bits, sums within 1e-12 of the two production passes."""
+    lib = mfl_amd._lib.load_probe()
+    P = 8_400_000 + 3
+    plan = lib.fedavg_fused_plan_of(K, P)
+    assert plan // 1000000 == KIND_WIN, plan
+    kmax, vec = (plan // 100) % 10000, plan % 100
+    assert K <= kmax and (kmax, vec) in INSTANCES
+    x, ld, weights = _rows(K, P, K * 31)
+    w = mfl_amd.weights_tensor(weights, torch.float32, DEV)
+    out, sumsq = mfl_amd.reduce_with_sqdist(x, w, P)
+    ref_out = mfl_amd.reduce_packed(x, w, P)
+    assert torch.equal(out.view(torch.int32), ref_out.view(torch.int32)), K
+    ref = mfl_amd.client_sqdist(x, ref_out, P)
+    rel = ((sumsq - ref).abs() / ref).max().item()
+    assert rel < 1e-12, (K, rel)
+    del x
+
+
+def test_window_plan_short_rows_and_other_k():
+    """Short rows keep the tile kernels (resnet56 x 100, 100 x 3M); K <= 16 and
+    K > 128 never take the windows; the target (100 x 25M) does."""
+    lib = mfl_amd._lib.load_probe()
+    assert lib.fedavg_fused_plan_of(100, 600_372) // 1000000 != KIND_WIN
+    assert lib.fedavg_fused_plan_of(100, 3_125_000) // 1000000 != KIND_WIN
+    assert lib.fedavg_fused_plan_of(100, 25_000_000) == KIND_WIN * 1000000 + 100 * 100 + 2
+    for K in (1, 16, 129, 300, 512):
+        assert lib.fedavg_fused_plan_of(K, 25_000_000) // 1000000 != KIND_WIN
+    assert lib.fedavg_fused_plan_of(513, 25_000_000) == 0
