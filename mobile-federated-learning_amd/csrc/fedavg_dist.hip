@@ -875,14 +875,14 @@ __device__ __forceinline__ int win_batch_row(int lane) {
 }
 
 template <int VEC>
-__device__ __forceinline__ typename WinVec<VEC>::T win_load(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+__device__ __forceinline__ typename WinVec<VEC>::T win_load(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t soff = 0) {
   typedef typename WinVec<VEC>::T V;
   if constexpr (VEC == 1)
-    return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b32(r, static_cast<int>(off), 0, 2));
+    return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b32(r, static_cast<int>(off), static_cast<int>(soff), 2));
   else if constexpr (VEC == 2)
-    return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b64(r, static_cast<int>(off), 0, 2));
+    return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b64(r, static_cast<int>(off), static_cast<int>(soff), 2));
   else
-    return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(off), 0, 2));
+    return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(off), static_cast<int>(soff), 2));
 }
 
 template <int VEC>
@@ -961,7 +961,17 @@ __global__ __launch_bounds__(64 * NW, MINW) void reduce_sqdist_win_kernel(
     const int64_t cl = c0 + lane * VEC;  // this lane's first column
     const int nbn = win_bytes(w + GW);
     const char* rp = reinterpret_cast<const char*>(X + (w + GW) * WC);
+    __amdgpu_buffer_rsrc_t rb;
     const auto reload = [&](int i) {  // row i of the next window into x[i]
+      if constexpr ((MODE & 4) != 0) {  // probe: one descriptor per 8 rows, the row by soffset (K == KMAX only)
+        if ((i & 7) == 0) {
+          asm volatile("" : "+s"(rp));
+          rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(rp), 0, nbn, 0x00020000);
+          rp += 8 * row_bytes;
+        }
+        x[i] = win_load<VEC>(rb, voff, static_cast<uint32_t>((i & 7) * row_bytes));
+        return;
+      }
       asm volatile("" : "+s"(rp));
       x[i] = win_load<VEC>(__builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(rp), 0, i < Kw ? nbn : 0, 0x00020000),
                            voff);
@@ -1011,6 +1021,8 @@ __global__ __launch_bounds__(64 * NW, MINW) void reduce_sqdist_win_kernel(
         if (cl + v < P) out[cl + v] = a[v];
     }
     // squares of fl32(x - g), each row reloaded with the next window's row as soon as it is squared
+    if constexpr ((MODE & 2) != 0) __builtin_amdgcn_s_setprio(2);  // probe: the reload issue first
+    if constexpr ((MODE & 16) != 0) __builtin_amdgcn_s_barrier();  // probe: the workgroup's waves reload in step
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       double p[8];
@@ -1019,14 +1031,28 @@ __global__ __launch_bounds__(64 * NW, MINW) void reduce_sqdist_win_kernel(
         const int i = 8 * b + j;
         p[j] = 0.0;
         if (i < KMAX) {
-          p[j] = win_sq<VEC>(x[i] - a);
+          if constexpr ((MODE & 32) != 0) {  // probe: squares summed in fp32 (not the :291 rule)
+            const V d = x[i] - a;
+            const V d2 = d * d;
+            float q = d2[0];
+#pragma unroll
+            for (int v = 1; v < VEC; ++v) q += d2[v];
+            p[j] = q;
+          } else {
+            p[j] = win_sq<VEC>(x[i] - a);
+          }
           reload(i);
         }
+      }
+      if constexpr ((MODE & 8) != 0) {  // probe: no folds (rows mixed: timing only)
+        acc[64 * b] += ((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7]));
+        continue;
       }
       const double q01 = fold32(p[0], p[1]), q23 = fold32(p[2], p[3]);
       const double q45 = fold32(p[4], p[5]), q67 = fold32(p[6], p[7]);
       acc[64 * b] += fold8(fold16(q01, q23), fold16(q45, q67), upper);
     }
+    if constexpr ((MODE & 2) != 0) __builtin_amdgcn_s_setprio(0);
   }
   if constexpr (MODE == 1) {
     if (probe == 12345.f) out[0] = probe;  // keep the loads
@@ -1069,7 +1095,7 @@ int launch_fused_win(const float* clients, int64_t K, int64_t P, int64_t ld, con
   hipLaunchKernelGGL((reduce_sqdist_win_kernel<KMAX, VEC, NW, MODE, MINW>), dim3(static_cast<unsigned>(waves / NW)),
                      dim3(64 * NW), 0, s, clients, static_cast<int>(K), ld, P, nwin, weights, out, partials);
   int rc = launch_status(what);
-  if (rc || MODE != 0) return rc;
+  if (rc || MODE == 1) return rc;
   hipLaunchKernelGGL(client_sqdist_finalize_kernel, dim3(static_cast<unsigned>(K)), dim3(kBlock), 0, s, partials,
                      waves, sumsq);
   return launch_status(what);
@@ -1654,6 +1680,15 @@ int fedavg_reduce_sqdist_f32_variant(const float* clients, int64_t K, int64_t P,
                                                 sumsq, blocks_per_cu, s, what);
     FEDAVG_WIN_CASE(2, 4, 1)
     FEDAVG_WIN_CASE(4, 4, 1)
+    FEDAVG_WIN_CASE(2, 4, 2)
+    FEDAVG_WIN_CASE(2, 4, 4)
+    FEDAVG_WIN_CASE(2, 4, 8)
+    FEDAVG_WIN_CASE(2, 4, 6)
+    FEDAVG_WIN_CASE(2, 4, 16)
+    FEDAVG_WIN_CASE(2, 8, 16)
+    FEDAVG_WIN_CASE(2, 8, 0)
+    FEDAVG_WIN_CASE(2, 4, 32)
+    FEDAVG_WIN_CASE(2, 4, 40)
 #define FEDAVG_WINK_CASE(KMAX, VEC, MINW)                                                                         \
   case 70000000 + KMAX * 100 + 40 + VEC:                                                                         \
     return launch_fused_win<KMAX, VEC, 4, 0, MINW>(clients, K, P, ld, weights, out, workspace, workspace_elems,  \

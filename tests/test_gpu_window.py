@@ -85,6 +85,7 @@ def test_window_negative_zero_and_nonfinite(kmax, vec):
     x, ld, weights = _rows(K, P, 6)
     x[1, 17] = float("inf")
     x[2, P - 1] = float("nan")
+    w = mfl_amd.weights_tensor(weights, torch.float32, DEV)
     out, s = _win(x, K, P, ld, w, kmax, vec)
     exp = O.reduce_f32(x[:, :P].cpu().numpy(), np.array([np.float32(v) for v in weights], dtype=np.float32))
     got = out.cpu().numpy()
