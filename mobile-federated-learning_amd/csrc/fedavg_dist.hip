@@ -935,10 +935,30 @@ __global__ __launch_bounds__(64 * NW, MINW) void reduce_sqdist_win_kernel(
   __shared__ __attribute__((aligned(16))) float wl[(KMAX + 3) & ~3];
   __shared__ double accl[NW][NB][64];
   for (int i = threadIdx.x; i < ((KMAX + 3) & ~3); i += 64 * NW) wl[i] = i < K ? W[i] : -0.0f;
+  float wv0 = lane < K ? W[lane] : -0.0f, wv1 = 64 + lane < K ? W[64 + lane] : -0.0f;  // LROWS: lane l = W[l], W[64 + l]
   double* acc = &accl[threadIdx.x >> 6][0][lane];
 #pragma unroll
   for (int b = 0; b < NB; ++b) acc[64 * b] = 0.0;
   __syncthreads();
+  // MODE 64 (probe): rows 0..E-1 of the next window are staged in LDS by
+  // LDS-DMA before this window's chain (the VGPR rows free up only in the
+  // squares), so E rows stay in flight through the chain; K > E
+  constexpr bool LROWS = (MODE & 64) != 0;
+  constexpr int E = LROWS ? 24 : 0;
+  static_assert(!LROWS || VEC == 2, "LDS rows: 512-B row segments (2 x 64 lanes x 4 B)");
+  __shared__ __attribute__((aligned(16))) float rowl[LROWS ? NW : 1][LROWS ? E : 1][LROWS ? WC : 1];
+  float* myrows = &rowl[LROWS ? (threadIdx.x >> 6) : 0][0][0];
+  // the wave's LDS slot base as a wave-uniform (SGPR) value: M0 for every DMA
+  const uint32_t lds_base = __builtin_amdgcn_readfirstlane(
+      static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)myrows)));
+  const auto dma_row = [&](int i, const char* rp, int bytes) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(rp), 0, bytes, 0x00020000);
+    // two dword DMAs of 256 B (all 64 lanes: no exec branch around them)
+    typedef __attribute__((address_space(3))) void* lds_ptr_t;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)(uintptr_t)(lds_base + i * WC * 4), 4, lane * 4, 0, 0, 2);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)(uintptr_t)(lds_base + i * WC * 4 + 256), 4, lane * 4 + 256,
+                                             0, 0, 2);
+  };
   V x[KMAX];
   {
     int Kw = K;
@@ -947,6 +967,12 @@ __global__ __launch_bounds__(64 * NW, MINW) void reduce_sqdist_win_kernel(
     const char* rp = reinterpret_cast<const char*>(X + gw * WC);
 #pragma unroll
     for (int i = 0; i < KMAX; ++i) {
+      if (i < E) {
+        asm volatile("" : "+s"(rp));
+        dma_row(i, rp, nb);
+        rp += row_bytes;
+        continue;
+      }
       asm volatile("" : "+s"(rp));
       x[i] = win_load<VEC>(__builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(rp), 0, i < Kw ? nb : 0, 0x00020000),
                            voff);
@@ -961,17 +987,23 @@ __global__ __launch_bounds__(64 * NW, MINW) void reduce_sqdist_win_kernel(
     const int64_t cl = c0 + lane * VEC;  // this lane's first column
     const int nbn = win_bytes(w + GW);
     const char* rp = reinterpret_cast<const char*>(X + (w + GW) * WC);
-    __amdgpu_buffer_rsrc_t rb;
-    const auto reload = [&](int i) {  // row i of the next window into x[i]
-      if constexpr ((MODE & 4) != 0) {  // probe: one descriptor per 8 rows, the row by soffset (K == KMAX only)
-        if ((i & 7) == 0) {
-          asm volatile("" : "+s"(rp));
-          rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(rp), 0, nbn, 0x00020000);
-          rp += 8 * row_bytes;
-        }
-        x[i] = win_load<VEC>(rb, voff, static_cast<uint32_t>((i & 7) * row_bytes));
-        return;
+    if constexpr (LROWS) {
+      // this window's LDS rows have landed (the E oldest loads in flight:
+      // at most the KMAX - E VGPR rows issued after them are outstanding)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(KMAX - E < 63 ? KMAX - E : 63) : "memory");  // (2 DMAs per LDS row)
+#pragma unroll
+      for (int i = 0; i < E; ++i) x[i] = *reinterpret_cast<const V*>(myrows + i * WC + lane * VEC);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read out before the next window's DMA lands
+      const char* rq = reinterpret_cast<const char*>(X + (w + GW) * WC);
+#pragma unroll
+      for (int i = 0; i < E; ++i) {
+        asm volatile("" : "+s"(rq));
+        dma_row(i, rq, nbn);
+        rq += row_bytes;
       }
+      rp += E * row_bytes;  // the VGPR rows start at row E
+    }
+    const auto reload = [&](int i) {  // row i of the next window into x[i]
       asm volatile("" : "+s"(rp));
       x[i] = win_load<VEC>(__builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(rp), 0, i < Kw ? nbn : 0, 0x00020000),
                            voff);
@@ -996,9 +1028,24 @@ __global__ __launch_bounds__(64 * NW, MINW) void reduce_sqdist_win_kernel(
       }
     }
     // the reference's chain, per lane: fl32(x_0 w_0), then + fl32(x_i w_i) in client order
+    V a;
+    if constexpr (LROWS) {
+      // weights from VGPR lanes (v_readlane): an LDS read here would wait for
+      // the LDS-DMA just issued (the compiler cannot tell the arrays apart)
+      asm volatile("" : "+v"(wv0), "+v"(wv1));  // re-read per window: not hoisted into SGPRs
+#pragma unroll
+      for (int i = 0; i < KMAX; ++i) {
+        const float wi = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(i < 64 ? wv0 : wv1), i & 63));
+        if (i == 0) {
+          a = x[0] * wi;
+        } else {
+          const V t = x[i] * wi;
+          a = a + t;
+        }
+      }
+    } else {
     int wo = 0;  // re-read per window (an opaque LDS offset): not held in registers across windows
     asm volatile("" : "+v"(wo));
-    V a;
 #pragma unroll
     for (int q = 0; q < (KMAX + 3) / 4; ++q) {
       const f32x4 w4 = *reinterpret_cast<const f32x4*>(&wl[wo + 4 * q]);
@@ -1013,6 +1060,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void reduce_sqdist_win_kernel(
         }
       }
     }
+    }
     if (!ragged) {
       __builtin_nontemporal_store(a, reinterpret_cast<V*>(out + cl));
     } else {
@@ -1021,7 +1069,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void reduce_sqdist_win_kernel(
         if (cl + v < P) out[cl + v] = a[v];
     }
     // squares of fl32(x - g), each row reloaded with the next window's row as soon as it is squared
-    if constexpr ((MODE & 2) != 0) __builtin_amdgcn_s_setprio(2);  // probe: the reload issue first
+    if constexpr ((MODE & 2) != 0) __builtin_amdgcn_s_setprio(2);  // probe: the reload issue first (no effect)
     if constexpr ((MODE & 16) != 0) __builtin_amdgcn_s_barrier();  // probe: the workgroup's waves reload in step
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
@@ -1031,17 +1079,8 @@ __global__ __launch_bounds__(64 * NW, MINW) void reduce_sqdist_win_kernel(
         const int i = 8 * b + j;
         p[j] = 0.0;
         if (i < KMAX) {
-          if constexpr ((MODE & 32) != 0) {  // probe: squares summed in fp32 (not the :291 rule)
-            const V d = x[i] - a;
-            const V d2 = d * d;
-            float q = d2[0];
-#pragma unroll
-            for (int v = 1; v < VEC; ++v) q += d2[v];
-            p[j] = q;
-          } else {
-            p[j] = win_sq<VEC>(x[i] - a);
-          }
-          reload(i);
+          p[j] = win_sq<VEC>(x[i] - a);
+          if (i >= E) reload(i);
         }
       }
       if constexpr ((MODE & 8) != 0) {  // probe: no folds (rows mixed: timing only)
@@ -1087,6 +1126,7 @@ int launch_fused_win(const float* clients, int64_t K, int64_t P, int64_t ld, con
                      double* partials, int64_t partial_elems, double* sumsq, int blocks_per_cu, hipStream_t s,
                      const char* what) {
   if (K > KMAX) return set_error(FEDAVG_EMODE, "%s: this window kernel covers K <= %d", what, KMAX);
+  if ((MODE & 64) != 0 && K <= 24) return set_error(FEDAVG_EMODE, "%s: LDS rows need K > 24", what);
   const int64_t waves = fused_win_waves<KMAX, VEC, NW, MODE, MINW>(P, blocks_per_cu);
   if (waves <= 0) return set_error(FEDAVG_EMODE, "%s: the window kernel is not resident", what);
   if (partial_elems < K * waves)
@@ -1139,6 +1179,11 @@ struct FusedPlan {
   int kind, S, slots;  // kFusedWin: S = KMAX, slots = VEC
 };
 
+// The 81-100 band stages rows 0..23 of the next window in LDS (MODE 64):
+// 100 x 25M 1.652 -> 1.646 ms, 100 x 25M+3 1.700 -> 1.690, 90 x 25M 1.607 ->
+// 1.547 (profiles/r03/win/ldsrows.jsonl); every band has K > 24 rows
+constexpr int kWin100Mode = 64;
+
 // the window kernel instance for K rows ({kFusedNone} outside 17..128)
 inline FusedPlan win_plan(int64_t K) {
   if (K <= 16 || K > 128) return {kFusedNone, 0, 0};
@@ -1156,7 +1201,7 @@ inline int64_t win_waves(const FusedPlan& pl, int64_t P) {
     case 48: return fused_win_waves<48, 4, 4>(P, 0);
     case 64: return fused_win_waves<64, 2, 4>(P, 0);
     case 80: return fused_win_waves<80, 2, 4>(P, 0);
-    case 100: return fused_win_waves<100, 2, 4>(P, 0);
+    case 100: return fused_win_waves<100, 2, 4, kWin100Mode>(P, 0);
     default: return fused_win_waves<128, 1, 4>(P, 0);
   }
 }
@@ -1522,8 +1567,8 @@ int fedavg_reduce_sqdist_f32(const float* clients, int64_t K, int64_t P, int64_t
           return launch_fused_win<80, 2, 4>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq, 0, s,
                                             what);
         case 100:
-          return launch_fused_win<100, 2, 4>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq, 0, s,
-                                             what);
+          return launch_fused_win<100, 2, 4, kWin100Mode>(clients, K, P, ld, weights, out, workspace, workspace_elems,
+                                                          sumsq, 0, s, what);
         default:
           return launch_fused_win<128, 1, 4>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq, 0, s,
                                              what);
@@ -1681,14 +1726,11 @@ int fedavg_reduce_sqdist_f32_variant(const float* clients, int64_t K, int64_t P,
     FEDAVG_WIN_CASE(2, 4, 1)
     FEDAVG_WIN_CASE(4, 4, 1)
     FEDAVG_WIN_CASE(2, 4, 2)
-    FEDAVG_WIN_CASE(2, 4, 4)
     FEDAVG_WIN_CASE(2, 4, 8)
-    FEDAVG_WIN_CASE(2, 4, 6)
     FEDAVG_WIN_CASE(2, 4, 16)
     FEDAVG_WIN_CASE(2, 8, 16)
     FEDAVG_WIN_CASE(2, 8, 0)
-    FEDAVG_WIN_CASE(2, 4, 32)
-    FEDAVG_WIN_CASE(2, 4, 40)
+    FEDAVG_WIN_CASE(2, 4, 64)
 #define FEDAVG_WINK_CASE(KMAX, VEC, MINW)                                                                         \
   case 70000000 + KMAX * 100 + 40 + VEC:                                                                         \
     return launch_fused_win<KMAX, VEC, 4, 0, MINW>(clients, K, P, ld, weights, out, workspace, workspace_elems,  \

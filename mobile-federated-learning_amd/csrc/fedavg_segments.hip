@@ -33,7 +33,18 @@ typedef f32x4 f32x4_a4 __attribute__((aligned(4)));  // dword-aligned 16-B vecto
 constexpr int kSegU = 4;
 constexpr int kSegC = 4;
 constexpr int64_t kSegSpan = static_cast<int64_t>(kBlock) * kSegC * 4;  // columns per unit
-constexpr int kSegBlocksPerCU = 3;
+// Round 3: full units run reduce_raw_unit's STYLE 2 -- loads and products
+// interleaved in (row, slice) order with two loads of the wave in flight
+// (a sched_barrier keeps the compiler from bunching a batch's loads) -- in
+// launches of 2 workgroups per CU.  Interleaved against the round-2 schedule
+// (U4 x C4, batch loads, 3 per CU) on separately allocated client tensors
+// (scripts/segments_probe.py --model, profiles/r03/seg/models.jsonl): flat
+// 100 x 25M 1.580 -> 1.444 ms (6,393 -> 6,996 GB/s), resnet18_gn x 500
+// (62 keys) 3.683 -> 3.285 ms, resnet56 x 100 (small units, 8 per CU)
+// 101.8 -> 94.6 us, FEMNIST x 10 17.4 -> 17.2 us; 3 per CU 1.479 ms, 4 loads
+// in flight 1.498 ms, 64 KiB units (U2 x C16, 1 per CU) 1.473 ms.
+constexpr int kSegStyle = 2;
+constexpr int kSegBlocksPerCU = 2;
 // Small models (fewer than 4 units of 4,096 columns per CU): units of 1,024
 // columns (U4 x C1), up to 8 blocks per CU per launch -- 4x the workgroups.
 // rocprofv3 kernel time per call (scripts/segments_probe.py --model,
@@ -320,7 +331,7 @@ __global__ __launch_bounds__(kBlock) void reduce_segments_f32_kernel(const SegKe
 
 // fedavg_reduce_ptrs_f32: one key of P columns whose client addresses are
 // already a device array [K] -- the same units, no table staging
-template <int U, int C>
+template <int U, int C, int STYLE = kSegStyle>
 __global__ __launch_bounds__(kBlock) void reduce_ptrs_f32_kernel(const int64_t* __restrict__ ptrs, int64_t P,
                                                                  int64_t unit0, int K, const float* __restrict__ W,
                                                                  float* __restrict__ out) {
@@ -328,7 +339,7 @@ __global__ __launch_bounds__(kBlock) void reduce_ptrs_f32_kernel(const int64_t* 
   const int64_t c0 = (unit0 + blockIdx.x) * span;
   const int64_t n = P - c0 < span ? P - c0 : span;
   if (n == span)
-    reduce_raw_unit<U, C, true>(ptrs, K, c0, n, W, out + c0);
+    reduce_raw_unit<U, C, true, STYLE>(ptrs, K, c0, n, W, out + c0);
   else
     reduce_raw_unit<1, C, false>(ptrs, K, c0, n, W, out + c0);
 }
@@ -708,11 +719,11 @@ int fedavg_reduce_segments_f32(const int64_t* client_ptrs, const int64_t* key_nu
   const auto* ptrs = reinterpret_cast<const int64_t*>(static_cast<const char*>(dev_ws) +
                                                       n_keys * static_cast<int64_t>(sizeof(SegKey)));
   if (small)
-    launch_reduce_segments<kSegU, kSegSmallC>(keys, ptrs, n_keys, units, K, weights, out,
-                                              static_cast<int64_t>(kSegSmallBlocksPerCU) * cu_count(), s);
+    launch_reduce_segments<kSegU, kSegSmallC, kSegStyle>(keys, ptrs, n_keys, units, K, weights, out,
+                                                         static_cast<int64_t>(kSegSmallBlocksPerCU) * cu_count(), s);
   else
-    launch_reduce_segments<kSegU, kSegC>(keys, ptrs, n_keys, units, K, weights, out,
-                                         static_cast<int64_t>(kSegBlocksPerCU) * cu_count(), s);
+    launch_reduce_segments<kSegU, kSegC, kSegStyle>(keys, ptrs, n_keys, units, K, weights, out,
+                                                    static_cast<int64_t>(kSegBlocksPerCU) * cu_count(), s);
   return launch_status(what);
 }
 
@@ -885,7 +896,7 @@ int fedavg_reduce_segments_f32_variant(const int64_t* client_ptrs, const int64_t
   if (uc != 408 && uc != 804 && uc != 208 && uc != 404 && uc != 802 && uc != 1602 && uc != 216 && uc != 116 &&
       uc != 801 && uc != 401 && uc != 1601 && uc != 402 && uc != 10216 && uc != 10404 && uc != 10408 &&
       uc != 10208 && uc != 10804 && uc != 20216 && uc != 30216 && uc != 40216 && uc != 20404 && uc != 30404 &&
-      uc != 30408 && uc != 40408)
+      uc != 30408 && uc != 40408 && uc != 20401 && uc != 30401 && uc != 20408)
     return set_error(FEDAVG_EMODE, "%s: unsupported (unroll, cols) = (%d, %d)", what, unroll, cols);
   if (blocks_per_cu < 0) return set_error(FEDAVG_EINVAL, "%s: blocks_per_cu < 0", what);
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -917,6 +928,9 @@ int fedavg_reduce_segments_f32_variant(const int64_t* client_ptrs, const int64_t
     case 30404: launch_reduce_segments<4, 4, 3>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;
     case 30408: launch_reduce_segments<4, 8, 3>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;
     case 40408: launch_reduce_segments<4, 8, 4>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;
+    case 20408: launch_reduce_segments<4, 8, 2>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;
+    case 20401: launch_reduce_segments<4, 1, 2>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;
+    case 30401: launch_reduce_segments<4, 1, 3>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;
     case 801: launch_reduce_segments<8, 1>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;
     case 401: launch_reduce_segments<4, 1>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;
     case 1601: launch_reduce_segments<16, 1>(keys, ptrs, n_keys, units, K, weights, out, cap, s); break;

@@ -42,13 +42,13 @@ def _sumsq_ref(x, out, P):
     return torch.stack([((x[k, :P] - out[:P]).double() ** 2).sum() for k in range(x.shape[0])])
 
 
-def _win(x, K, P, ld, w, kmax, vec):
+def _win(x, K, P, ld, w, kmax, vec, code=None):
     lib = mfl_amd._lib.load_probe()
     n_ws = K * 4 * 2048
     work = torch.empty(n_ws, dtype=torch.float64, device=DEV)
     out = torch.empty(P, device=DEV)
     s = torch.empty(K, dtype=torch.float64, device=DEV)
-    code = 70000000 + kmax * 100 + 40 + vec
+    code = code or 70000000 + kmax * 100 + 40 + vec
     mfl_amd._lib.check(lib.fedavg_reduce_sqdist_f32_variant(x.data_ptr(), K, P, ld, w.data_ptr(), out.data_ptr(),
                                                             work.data_ptr(), n_ws, s.data_ptr(), code, 0, None),
                        f"window {kmax}x{vec}", lib)
@@ -69,6 +69,31 @@ def test_window_instances_vs_oracle(kmax, vec):
             assert rel < 1e-12, (kmax, vec, K, P, rel)
             _, again = _win(x, K, P, ld, w, kmax, vec)
             assert torch.equal(s, again)  # deterministic
+
+
+def test_window_lds_rows_vs_oracle():
+    """The 81-100 band's production form (rows 0..23 of the next window staged
+    in LDS by LDS-DMA, weights read with v_readlane): oracle bits and sums at
+    K = 25 .. 100, including a K whose padding rows start inside a batch."""
+    lib = mfl_amd._lib.load_probe()
+    for K in (25, 81, 97, 100):
+        for P in (3, 133, 100_003):
+            x, ld, weights = _rows(K, P, K * 7 + P)
+            w = mfl_amd.weights_tensor(weights, torch.float32, DEV)
+            out, s = _win(x, K, P, ld, w, 100, 2, code=124000042)
+            exp = O.reduce_f32(x[:, :P].cpu().numpy(), np.array([np.float32(v) for v in weights], dtype=np.float32))
+            assert out.cpu().numpy().view(np.uint32).tobytes() == exp.view(np.uint32).tobytes(), (K, P)
+            ref = _sumsq_ref(x, out, P)
+            rel = ((s - ref).abs() / ref.clamp_min(1e-300)).max().item()
+            assert rel < 1e-12, (K, P, rel)
+    x, ld, weights = _rows(24, 1000, 1)
+    w = mfl_amd.weights_tensor(weights, torch.float32, DEV)
+    work = torch.empty(24 * 8192, dtype=torch.float64, device=DEV)
+    out = torch.empty(1000, device=DEV)
+    s = torch.empty(24, dtype=torch.float64, device=DEV)
+    rc = lib.fedavg_reduce_sqdist_f32_variant(x.data_ptr(), 24, 1000, ld, w.data_ptr(), out.data_ptr(), work.data_ptr(),
+                                              work.numel(), s.data_ptr(), 124000042, 0, None)
+    assert rc == mfl_amd._lib.FEDAVG_EMODE  # K <= 24: the LDS rows would hold padding rows
 
 
 @pytest.mark.parametrize("kmax,vec", [(48, 4), (100, 2), (128, 1)])
