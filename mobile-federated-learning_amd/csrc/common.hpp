@@ -665,4 +665,78 @@ __device__ __forceinline__ void fused_finish(float* lds, const double (&acc)[RM]
   }
 }
 
+// ---------------------------------------------------------------------------
+// Wave-owned windows (fedavg_dist.hip's reduce_sqdist_win_kernel and
+// fedavg_segments.hip's zero-copy form): a wave holds 64 x VEC columns of all
+// K rows in registers; each batch of 8 rows' fp64 partials is folded across
+// the wave by v_permlane32_swap / v_permlane16_swap / one row_ror:8 exchange
+// into one register (8 lanes per row, win_batch_row).
+// ---------------------------------------------------------------------------
+template <int VEC>
+struct WinVec {
+  typedef float T __attribute__((ext_vector_type(VEC)));
+};
+
+// lanes 0-31: a's two halves added (lane l: a[l] + a[l + 32]); lanes 32-63: b's
+__device__ __forceinline__ double fold32(double a, double b) {
+  const uint64_t ua = __builtin_bit_cast(uint64_t, a), ub = __builtin_bit_cast(uint64_t, b);
+  const auto lo = __builtin_amdgcn_permlane32_swap(static_cast<uint32_t>(ua), static_cast<uint32_t>(ub), false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap(static_cast<uint32_t>(ua >> 32), static_cast<uint32_t>(ub >> 32),
+                                                   false, false);
+  const double na = __builtin_bit_cast(double, (static_cast<uint64_t>(hi[0]) << 32) | lo[0]);
+  const double nb = __builtin_bit_cast(double, (static_cast<uint64_t>(hi[1]) << 32) | lo[1]);
+  return na + nb;
+}
+
+// 16-lane rows [a.r0 + a.r1, b.r0 + b.r1, a.r2 + a.r3, b.r2 + b.r3]
+__device__ __forceinline__ double fold16(double a, double b) {
+  const uint64_t ua = __builtin_bit_cast(uint64_t, a), ub = __builtin_bit_cast(uint64_t, b);
+  const auto lo = __builtin_amdgcn_permlane16_swap(static_cast<uint32_t>(ua), static_cast<uint32_t>(ub), false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap(static_cast<uint32_t>(ua >> 32), static_cast<uint32_t>(ub >> 32),
+                                                   false, false);
+  const double na = __builtin_bit_cast(double, (static_cast<uint64_t>(hi[0]) << 32) | lo[0]);
+  const double nb = __builtin_bit_cast(double, (static_cast<uint64_t>(hi[1]) << 32) | lo[1]);
+  return na + nb;
+}
+
+// lanes with bit 3 clear keep a's value + the lane 8 above; set: b's + the lane 8 below
+__device__ __forceinline__ double fold8(double a, double b, bool upper) {
+  const double send = upper ? a : b;
+  const double keep = upper ? b : a;
+  return keep + dpp_move_f64<0x128, 0xF>(send);  // row_ror:8 = lane xor 8 within a 16-lane row
+}
+
+// batch row held by lane l after fold32 / fold16 / fold8
+__device__ __forceinline__ int win_batch_row(int lane) {
+  const int r = lane >> 4;
+  return 4 * ((lane >> 3) & 1) + (((r & 1) << 1) | (r >> 1));
+}
+
+template <int VEC>
+__device__ __forceinline__ typename WinVec<VEC>::T win_load(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t soff = 0) {
+  typedef typename WinVec<VEC>::T V;
+  if constexpr (VEC == 1)
+    return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b32(r, static_cast<int>(off), static_cast<int>(soff), 2));
+  else if constexpr (VEC == 2)
+    return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b64(r, static_cast<int>(off), static_cast<int>(soff), 2));
+  else
+    return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(off), static_cast<int>(soff), 2));
+}
+
+template <int VEC>
+__device__ __forceinline__ double win_sq(typename WinVec<VEC>::T d) {
+  double s = static_cast<double>(d[0]) * static_cast<double>(d[0]);
+#pragma unroll
+  for (int v = 1; v < VEC; ++v) s = __builtin_fma(static_cast<double>(d[v]), static_cast<double>(d[v]), s);
+  return s;
+}
+
+// __launch_bounds__'s second argument is waves per SIMD: the window's KMAX x
+// VEC registers (+ a quarter more at VEC 1: one square per row per lane
+// before the folds) and ~40 others within 512 / waves
+constexpr int win_min_waves(int kmax, int vec) {
+  const int regs = kmax * vec + (vec == 1 ? kmax / 4 : 0);
+  return regs <= 88 ? 4 : (regs <= 128 ? 3 : (regs <= 216 ? 2 : 1));
+}
+
 }  // namespace fedavg_impl

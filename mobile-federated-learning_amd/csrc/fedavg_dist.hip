@@ -111,7 +111,10 @@ __device__ __forceinline__ double sq_row(const f32x4 (&x)[C], const f32x4 (&g)[C
   return a[0];
 }
 
-template <int U, int C, int MINW = 1, int ACC = 1>
+// STYLE L > 0 (probe): each batch's U x C loads and squares interleaved in
+// (row, slice) order with at most L loads of the wave in flight, as the
+// zero-copy reduce's unit loop (fedavg_segments.hip, STYLE 2)
+template <int U, int C, int MINW = 1, int ACC = 1, int STYLE = 0>
 __global__ __launch_bounds__(kBlock, MINW) void client_sqdist_buf_kernel(
     const f32x4* __restrict__ X, int K, int64_t ld4, int64_t nvec, int tail, const f32x4* __restrict__ G,
     double* __restrict__ partials, int64_t nwaves, int64_t wave_base) {
@@ -149,6 +152,38 @@ __global__ __launch_bounds__(kBlock, MINW) void client_sqdist_buf_kernel(
     }
     constexpr int UU = U > 0 ? U : 1;
     int k = 0;
+    if constexpr (STYLE > 0) {
+      constexpr int L = STYLE, N = UU * C;
+      for (; k + UU <= K; k += UU) {
+        __amdgpu_buffer_rsrc_t rr[UU];
+#pragma unroll
+        for (int u = 0; u < UU; ++u) rr[u] = uniform_rsrc(X + static_cast<int64_t>(k + u) * ld4 + blk0, bytes);
+        double a[UU][ACC];
+#pragma unroll
+        for (int u = 0; u < UU; ++u)
+#pragma unroll
+          for (int c = 0; c < ACC; ++c) a[u][c] = 0.0;
+        f32x4 x[N];
+#pragma unroll
+        for (int i = 0; i < N + L; ++i) {
+          if (i < N) x[i] = ld_rsrc_nt(rr[i / C], off[i % C]);
+          if (i >= L) {
+            const int j = i - L;
+            a[j / C][(j % C) % ACC] = sq4_add(a[j / C][(j % C) % ACC], x[j] - g[j % C]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int u = 0; u < UU; ++u) {
+#pragma unroll
+          for (int w = 1; w < ACC; w *= 2) {
+#pragma unroll
+            for (int c = 0; c + w < ACC; c += 2 * w) a[u][c] += a[u][c + w];
+          }
+          sqdist_rows_store<U, C>(a[u][0], partials, k + u, nwaves, wave_id);
+        }
+      }
+    }
     for (; k + UU <= K; k += UU) {
       f32x4 xs[UU][C];
 #pragma unroll
@@ -834,72 +869,7 @@ int launch_fused_rs(const float* clients, int64_t K, int64_t P, int64_t ld, cons
 // zeroed before the chain.
 // MODE 1: loads only (a traffic probe: wrong results).
 // ---------------------------------------------------------------------------
-template <int VEC>
-struct WinVec {
-  typedef float T __attribute__((ext_vector_type(VEC)));
-};
-
-// lanes 0-31: a's two halves added (lane l: a[l] + a[l + 32]); lanes 32-63: b's
-__device__ __forceinline__ double fold32(double a, double b) {
-  const uint64_t ua = __builtin_bit_cast(uint64_t, a), ub = __builtin_bit_cast(uint64_t, b);
-  const auto lo = __builtin_amdgcn_permlane32_swap(static_cast<uint32_t>(ua), static_cast<uint32_t>(ub), false, false);
-  const auto hi = __builtin_amdgcn_permlane32_swap(static_cast<uint32_t>(ua >> 32), static_cast<uint32_t>(ub >> 32),
-                                                   false, false);
-  const double na = __builtin_bit_cast(double, (static_cast<uint64_t>(hi[0]) << 32) | lo[0]);
-  const double nb = __builtin_bit_cast(double, (static_cast<uint64_t>(hi[1]) << 32) | lo[1]);
-  return na + nb;
-}
-
-// 16-lane rows [a.r0 + a.r1, b.r0 + b.r1, a.r2 + a.r3, b.r2 + b.r3]
-__device__ __forceinline__ double fold16(double a, double b) {
-  const uint64_t ua = __builtin_bit_cast(uint64_t, a), ub = __builtin_bit_cast(uint64_t, b);
-  const auto lo = __builtin_amdgcn_permlane16_swap(static_cast<uint32_t>(ua), static_cast<uint32_t>(ub), false, false);
-  const auto hi = __builtin_amdgcn_permlane16_swap(static_cast<uint32_t>(ua >> 32), static_cast<uint32_t>(ub >> 32),
-                                                   false, false);
-  const double na = __builtin_bit_cast(double, (static_cast<uint64_t>(hi[0]) << 32) | lo[0]);
-  const double nb = __builtin_bit_cast(double, (static_cast<uint64_t>(hi[1]) << 32) | lo[1]);
-  return na + nb;
-}
-
-// lanes with bit 3 clear keep a's value + the lane 8 above; set: b's + the lane 8 below
-__device__ __forceinline__ double fold8(double a, double b, bool upper) {
-  const double send = upper ? a : b;
-  const double keep = upper ? b : a;
-  return keep + dpp_move_f64<0x128, 0xF>(send);  // row_ror:8 = lane xor 8 within a 16-lane row
-}
-
-// batch row held by lane l after fold32 / fold16 / fold8
-__device__ __forceinline__ int win_batch_row(int lane) {
-  const int r = lane >> 4;
-  return 4 * ((lane >> 3) & 1) + (((r & 1) << 1) | (r >> 1));
-}
-
-template <int VEC>
-__device__ __forceinline__ typename WinVec<VEC>::T win_load(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t soff = 0) {
-  typedef typename WinVec<VEC>::T V;
-  if constexpr (VEC == 1)
-    return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b32(r, static_cast<int>(off), static_cast<int>(soff), 2));
-  else if constexpr (VEC == 2)
-    return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b64(r, static_cast<int>(off), static_cast<int>(soff), 2));
-  else
-    return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(off), static_cast<int>(soff), 2));
-}
-
-template <int VEC>
-__device__ __forceinline__ double win_sq(typename WinVec<VEC>::T d) {
-  double s = static_cast<double>(d[0]) * static_cast<double>(d[0]);
-#pragma unroll
-  for (int v = 1; v < VEC; ++v) s = __builtin_fma(static_cast<double>(d[v]), static_cast<double>(d[v]), s);
-  return s;
-}
-
-// __launch_bounds__'s second argument is waves per SIMD: the window's KMAX x
-// VEC registers (+ a quarter more at VEC 1: one square per row per lane
-// before the folds) and ~40 others within 512 / waves
-constexpr int win_min_waves(int kmax, int vec) {
-  const int regs = kmax * vec + (vec == 1 ? kmax / 4 : 0);
-  return regs <= 88 ? 4 : (regs <= 128 ? 3 : (regs <= 216 ? 2 : 1));
-}
+// (window helpers: WinVec, fold32/16/8, win_batch_row, win_load, win_sq in common.hpp)
 
 template <int KMAX, int VEC, int NW, int MODE = 0, int MINW = win_min_waves(KMAX, VEC)>
 __global__ __launch_bounds__(64 * NW, MINW) void reduce_sqdist_win_kernel(
@@ -914,6 +884,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void reduce_sqdist_win_kernel(
   const uint32_t voff = static_cast<uint32_t>(lane) * VEC * 4;
   const int64_t P4 = (P + 3) & ~static_cast<int64_t>(3);  // rows are read up to their last 16-B slice
   const int64_t row_bytes = ld * 4;
+  const uint32_t rb32 = static_cast<uint32_t>(row_bytes);  // MODE 128: soffset steps
   const bool upper = (lane & 8) != 0;
 
   // window w's bytes per row (0: no such window -- its loads return 0 and move nothing)
@@ -1003,7 +974,29 @@ __global__ __launch_bounds__(64 * NW, MINW) void reduce_sqdist_win_kernel(
       }
       rp += E * row_bytes;  // the VGPR rows start at row E
     }
+    // MODE 128 (probe): one descriptor per 8 rows with the row in soffset.
+    // The range check covers soffset + voffset, so a group's record count
+    // ends at its last existing row's window bytes (rows past K, and the
+    // window past the model's last slice on that row, read 0); the other
+    // rows of a ragged window read their padding (zeroed before the chain).
+    // Needs 7 row pitches + a window < 4 GiB (the launcher checks).
+    __amdgpu_buffer_rsrc_t grs;
+    const char* gp = reinterpret_cast<const char*>(X + (w + GW) * WC) + E * row_bytes;
     const auto reload = [&](int i) {  // row i of the next window into x[i]
+      if constexpr ((MODE & 128) != 0) {
+        const int j = i & 7;
+        if (j == 0) {
+          asm volatile("" : "+s"(gp));
+          const int rows = Kw - (i & ~7);  // rows of this group that exist
+          const uint32_t nr = (nbn == 0 || rows <= 0)
+                                  ? 0u
+                                  : static_cast<uint32_t>((rows < 8 ? rows : 8) - 1) * rb32 + static_cast<uint32_t>(nbn);
+          grs = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(gp), 0, static_cast<int>(nr), 0x00020000);
+          gp += 8 * row_bytes;
+        }
+        x[i] = win_load<VEC>(grs, voff, static_cast<uint32_t>(j) * rb32);
+        return;
+      }
       asm volatile("" : "+s"(rp));
       x[i] = win_load<VEC>(__builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(rp), 0, i < Kw ? nbn : 0, 0x00020000),
                            voff);
@@ -1127,6 +1120,8 @@ int launch_fused_win(const float* clients, int64_t K, int64_t P, int64_t ld, con
                      const char* what) {
   if (K > KMAX) return set_error(FEDAVG_EMODE, "%s: this window kernel covers K <= %d", what, KMAX);
   if ((MODE & 64) != 0 && K <= 24) return set_error(FEDAVG_EMODE, "%s: LDS rows need K > 24", what);
+  if ((MODE & 128) != 0 && ld * 4 * 7 + 64 * VEC * 4 >= (int64_t(1) << 32))
+    return set_error(FEDAVG_EMODE, "%s: 8-row descriptors need 7 row pitches + a window < 4 GiB", what);
   const int64_t waves = fused_win_waves<KMAX, VEC, NW, MODE, MINW>(P, blocks_per_cu);
   if (waves <= 0) return set_error(FEDAVG_EMODE, "%s: the window kernel is not resident", what);
   if (partial_elems < K * waves)
@@ -1283,7 +1278,7 @@ int64_t sqdist_waves_for(int64_t P, int cols) {
   return blocks * (kBlock / 64);
 }
 
-template <int U, int C, bool BUF = false, int MINW = 1, int ACC = 1>
+template <int U, int C, bool BUF = false, int MINW = 1, int ACC = 1, int STYLE = 0>
 void launch_sqdist(const float* clients, int K, int64_t ld, int64_t P, const float* glob, double* partials,
                    int64_t nwaves, int max_blocks, hipStream_t s) {
   const int64_t nvec = (P + 3) / 4;
@@ -1300,7 +1295,7 @@ void launch_sqdist(const float* clients, int K, int64_t ld, int64_t P, const flo
     const int64_t n = (nvec - v0) < nb * span ? (nvec - v0) : nb * span;
     const int tail = (v0 + n == nvec) ? static_cast<int>(P & 3) : 0;
     if constexpr (BUF)
-      hipLaunchKernelGGL((client_sqdist_buf_kernel<U, C, MINW, ACC>), dim3(static_cast<unsigned>(nb)), dim3(kBlock), 0, s,
+      hipLaunchKernelGGL((client_sqdist_buf_kernel<U, C, MINW, ACC, STYLE>), dim3(static_cast<unsigned>(nb)), dim3(kBlock), 0, s,
                          X + v0, K, ld / 4, n, tail, Gv + v0, partials, nwaves, b0 * (kBlock / 64));
     else
       hipLaunchKernelGGL((client_sqdist_f32x4_kernel<U, C>), dim3(static_cast<unsigned>(nb)), dim3(kBlock), 0, s,
@@ -1440,6 +1435,16 @@ int sqdist_buf_impl(const float* clients, int64_t K, int64_t P, int64_t ld, cons
     case 4000801: launch_sqdist<8, 1, true, 1, 1>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
     case 4001601: launch_sqdist<16, 1, true, 1, 1>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
     case 4000116: launch_sqdist<1, 16, true, 1, 4>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+#ifdef FEDAVG_TUNING
+    // interleaved loads and squares, L loads in flight: + 100000000 x L
+    case 204000216: launch_sqdist<2, 16, true, 1, 4, 2>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    case 404000216: launch_sqdist<2, 16, true, 1, 4, 4>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    case 804000216: launch_sqdist<2, 16, true, 1, 4, 8>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    case 204000404: launch_sqdist<4, 4, true, 1, 4, 2>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    case 404000404: launch_sqdist<4, 4, true, 1, 4, 4>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    case 204000408: launch_sqdist<4, 8, true, 1, 4, 2>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+    case 404000408: launch_sqdist<4, 8, true, 1, 4, 4>(clients, k, ld, P, glob, workspace, nwaves, max_blocks, s); break;
+#endif
     default: return set_error(FEDAVG_EMODE, "%s: unsupported unroll=%d cols=%d", what, unroll, cols);
   }
   rc = launch_status(what);
@@ -1731,6 +1736,10 @@ int fedavg_reduce_sqdist_f32_variant(const float* clients, int64_t K, int64_t P,
     FEDAVG_WIN_CASE(2, 8, 16)
     FEDAVG_WIN_CASE(2, 8, 0)
     FEDAVG_WIN_CASE(2, 4, 64)
+    FEDAVG_WIN_CASE(2, 4, 128)
+    case 60000000 + 192 * 1000000 + 42:  // LDS rows + 8-row descriptors
+      return launch_fused_win<100, 2, 4, 192>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq,
+                                              blocks_per_cu, s, what);
 #define FEDAVG_WINK_CASE(KMAX, VEC, MINW)                                                                         \
   case 70000000 + KMAX * 100 + 40 + VEC:                                                                         \
     return launch_fused_win<KMAX, VEC, 4, 0, MINW>(clients, K, P, ld, weights, out, workspace, workspace_elems,  \

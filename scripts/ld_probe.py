@@ -31,12 +31,15 @@ def main():
     ap.add_argument("--P", type=int, default=25_000_000)
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--reps", type=int, default=8)
+    ap.add_argument("--pads", nargs="*", type=int, default=[0, 64, 256, 1024, 4096, 32768])
+    ap.add_argument("--fused", action="store_true",
+                    help="also time the fused aggregate + :291 pass (reduce_with_sqdist) at every pitch")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     K, P = args.K, args.P
     base_ld = (P + 63) // 64 * 64
-    pads = [0, 64, 256, 1024, 4096, 32768]  # elements of padding per row
+    pads = args.pads  # elements of padding per row
     buf = torch.empty(K * (base_ld + max(pads)), device=dev)
     g = torch.Generator(device=dev).manual_seed(1)
     src = torch.randn((K, P), generator=g, device=dev) * 0.05
@@ -48,6 +51,7 @@ def main():
         outs[pad] = torch.empty(P, device=dev)
 
     times = {pad: [] for pad in pads}
+    ftimes = {pad: [] for pad in pads}
     ref = None
     for _ in range(args.rounds):
         for pad in pads:
@@ -64,6 +68,13 @@ def main():
                 mfl_amd.reduce_packed(x, w, P, outs[pad])
                 e.record()
                 times[pad].append((s, e, same))
+            if args.fused:
+                for _ in range(args.reps):
+                    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    s.record()
+                    o2, _ = mfl_amd.reduce_with_sqdist(x, w, P)
+                    e.record()
+                    ftimes[pad].append((s, e, torch.equal(o2.view(torch.int32), ref.view(torch.int32))))
             torch.cuda.synchronize()
     alg = 4 * K * P + 4 * P + 4 * K
     for pad in pads:
@@ -71,6 +82,11 @@ def main():
         print(json.dumps({"ld": base_ld + pad, "pad_elems": pad, "row_pitch_bytes": 4 * (base_ld + pad), "K": K,
                           "P": P, "ms_median": round(ms, 4), "GBps": round(alg / ms / 1e6, 1),
                           "bit_identical": all(t[2] for t in times[pad])}), flush=True)
+        if args.fused:
+            fms = float(np.median([s.elapsed_time(e) for s, e, _ in ftimes[pad]]))
+            print(json.dumps({"ld": base_ld + pad, "pad_elems": pad, "fused_ms_median": round(fms, 4),
+                              "fused_GBps": round(alg / fms / 1e6, 1),
+                              "fused_bit_identical": all(t[2] for t in ftimes[pad])}), flush=True)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,9 @@
+set -euo pipefail
+cd "${GRAFT_REPO_ROOT:-.}"
+export TMPDIR=/tmp
+O=gpurun_out/r03/g29
+mkdir -p $O
+timeout -k 10 400 python -u scripts/ld_probe.py --K 100 --P 25000000 --rounds 3 --reps 6 --fused --pads 0 64 128 192 256 384 512 1024 4096 > $O/pitch_k100.jsonl 2> $O/pitch_k100.err
+echo k100 ok
+timeout -k 10 400 python -u scripts/ld_probe.py --K 100 --P 12500000 --rounds 3 --reps 6 --fused --pads 0 64 128 256 512 > $O/pitch_k100_p12.jsonl 2> $O/pitch_k100_p12.err
+echo k100 p12 ok
