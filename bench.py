@@ -439,10 +439,17 @@ def fused_round(red, w_dev, reps: int = 10) -> dict:
     ms = {n: float(np.median([a.elapsed_time(b) for a, b in v])) for n, v in times.items()}
     alg = algorithmic_bytes(K, P)
     rel = float(((sums["fused"] - sums["two_pass"]).abs() / sums["two_pass"].abs().clamp_min(1e-300)).max())
+    plan = int(mfl_amd._lib.load().fedavg_fused_plan_of(K, P))
+    kind, tile, slots = plan // 1000000, (plan // 100) % 10000, plan % 100
+    kernel = {0: "two passes", 1: f"reduce_sqdist_f32_kernel<S={tile}> (LDS-DMA tiles)",
+              2: f"reduce_sqdist_rs_kernel<S={tile},SLOTS={slots}> (register-staged tiles)",
+              3: f"reduce_sqdist_win_kernel<KMAX={tile},VEC={slots}> (wave-owned windows)"}.get(kind, str(plan))
     return {"what": "aggregate + :291 sums of squares over the same resident rows (fedavg_trainer.py:217, :291)",
             "two_pass_ms": round(ms["two_pass"], 4), "fused_ms": round(ms["fused"], 4),
             "speedup": round(ms["two_pass"] / ms["fused"], 3),
+            "fused_kernel": kernel,
             "fused_GBps_of_round_bytes": round(alg / ms["fused"] / 1e6, 1),
+            "fused_frac_of_hbm_peak": round(alg / ms["fused"] / 1e6 / HBM_PEAK_GBS, 4),
             "out_bits_equal": bool(torch.equal(o1.view(torch.int32), o2.view(torch.int32))),
             "sums_max_rel_vs_two_pass": rel,
             "timing": f"median of {reps} interleaved calls, HIP events around each call"}

@@ -123,12 +123,21 @@ int fedavg_client_sqdist_f32(const float* clients, int64_t K, int64_t P, int64_t
  *           fixed order; not necessarily the same summation tree).
  * Needs 16-B aligned rows and ld % 4 == 0 (FEDAVG_EALIGN otherwise, before
  * any work: fedavg_reduce_f32 alone takes unaligned rows).  K <= 512 runs a
- * fused kernel (tiles of K rows x 32-256 columns staged in LDS per
- * workgroup, by LDS-DMA or through registers); K > 512 runs the two passes
- * back to back.  workspace : fedavg_reduce_sqdist_workspace(K, P) doubles of
+ * fused kernel: for 17-128 clients on long rows one wave per window of
+ * 64 x VEC columns x all K rows in registers; otherwise tiles of K rows x
+ * 32-256 columns staged in LDS per workgroup (by LDS-DMA or through
+ * registers); K > 512 runs the two passes back to back
+ * (fedavg_fused_plan_of says which).  workspace : fedavg_reduce_sqdist_workspace(K, P) doubles of
  * device scratch.  P == 0 writes sumsq = 0.
  */
 int64_t fedavg_reduce_sqdist_workspace(int64_t K, int64_t P);
+/* Which kernel fedavg_reduce_sqdist_f32 runs for K x P rows on the current
+ * device: kind x 1000000 + S x 100 + slots.  kind 0: the two passes; 1:
+ * LDS-DMA tiles of S columns; 2: register-staged tiles of S columns and
+ * `slots` 16-B slots per thread; 3: wave-owned windows of KMAX = S rows and
+ * VEC = slots columns per lane (17-128 clients on rows of >= 16 windows per
+ * wave). */
+int64_t fedavg_fused_plan_of(int64_t K, int64_t P);
 int fedavg_reduce_sqdist_f32(const float* clients, int64_t K, int64_t P, int64_t ld,
                              const float* weights, float* out, double* workspace,
                              int64_t workspace_elems, double* sumsq, void* stream);

@@ -174,11 +174,6 @@ int fedavg_reduce_sqdist_f32_variant(const float* clients, int64_t K, int64_t P,
                                      const float* weights, float* out, double* workspace,
                                      int64_t workspace_elems, double* sumsq, int cols,
                                      int blocks_per_cu, void* stream);
-/* fedavg_reduce_sqdist_f32's kernel choice for K x P: kind x 1000000 + S x 100
- * + slots (kind 0: two passes, 1: LDS-DMA tiles of S columns, 2:
- * register-staged tiles of S columns and `slots` slots, 3: wave-owned
- * windows of KMAX = S rows and VEC = slots columns per lane). */
-int64_t fedavg_fused_plan_of(int64_t K, int64_t P);
 int fedavg_client_sqdist_buf(const float* clients, int64_t K, int64_t P, int64_t ld, const float* glob,
                              double* workspace, int64_t workspace_elems, double* sumsq, int unroll, int cols,
                              int max_blocks, void* stream);

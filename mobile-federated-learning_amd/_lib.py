@@ -45,6 +45,7 @@ SIGNATURES = {
     "fedavg_client_sqdist_f32": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_i64, _vp, _vp]),
     "fedavg_client_sqdist_workspace_elems": (_c_i64, [_c_i64, _c_i64, _c_i64]),
     "fedavg_reduce_sqdist_workspace": (_c_i64, [_c_i64, _c_i64]),
+    "fedavg_fused_plan_of": (_c_i64, [_c_i64, _c_i64]),
     "fedavg_reduce_sqdist_f32": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _c_i64, _vp, _vp]),
     "fedavg_client_sqdist_f64": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_i64, _vp, _vp]),
     "fedavg_client_sqdist_f16": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_i64, _vp, _vp]),
@@ -87,7 +88,6 @@ TUNING_SIGNATURES = {
                                               _c_int, _vp]),
     "fedavg_client_sqdist_buf": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_i64, _vp, _c_int, _c_int,
                                           _c_int, _vp]),
-    "fedavg_fused_plan_of": (_c_i64, [_c_i64, _c_i64]),
     "fedavg_reduce_sqdist_f32_variant": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _c_i64, _vp, _c_int,
                                                   _c_int, _vp]),
     "fedavg_reduce_vec_buf": (_c_int, [_c_int, _vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_int, _c_int, _c_int, _vp]),

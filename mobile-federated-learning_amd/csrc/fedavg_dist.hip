@@ -1602,8 +1602,7 @@ int fedavg_reduce_sqdist_f32(const float* clients, int64_t K, int64_t P, int64_t
   return fedavg_client_sqdist_f32(clients, K, P, ld, out, workspace, workspace_elems, sumsq, stream);
 }
 
-#ifdef FEDAVG_TUNING  // probe library only (libfedavg_amd_probe.so)
-// the production plan of fedavg_reduce_sqdist_f32 for K x P (tests): kind x
+// the production plan of fedavg_reduce_sqdist_f32 for K x P: kind x
 // 1000000 + S x 100 + slots (kind 0 two passes, 1 LDS-DMA tiles, 2
 // register-staged tiles, 3 wave-owned windows with S = KMAX, slots = VEC)
 int64_t fedavg_fused_plan_of(int64_t K, int64_t P) {
@@ -1611,6 +1610,7 @@ int64_t fedavg_fused_plan_of(int64_t K, int64_t P) {
   return static_cast<int64_t>(pl.kind) * 1000000 + pl.S * 100 + pl.slots;
 }
 
+#ifdef FEDAVG_TUNING  // probe library only (libfedavg_amd_probe.so)
 // the fused pass with an explicit tile width (64 / 128 / 256 columns) and
 // workgroups per CU (0 = as many as LDS allows); workspace >= K x grid
 int fedavg_reduce_sqdist_f32_variant(const float* clients, int64_t K, int64_t P, int64_t ld, const float* weights,
