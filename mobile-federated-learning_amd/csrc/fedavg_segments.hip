@@ -539,6 +539,231 @@ __global__ __launch_bounds__(kBlock) void reduce_sqdist_segments_f32_kernel(cons
   fused_finish(lds, acc, K, partials);
 }
 
+// ---------------------------------------------------------------------------
+// Zero-copy wave-owned windows (round 3): fedavg_dist.hip's
+// reduce_sqdist_win_kernel on the key / pointer tables.  Each key is cut
+// into windows of WC = 64 x VEC columns (stage_tables with that span); a
+// wave holds one window of all K clients in registers, runs the reference's
+// chain per lane, squares fl32(x - g) in fp64 and folds 8 rows at a time
+// across the wave (common.hpp).
+//   fast window (fp32 key, all WC columns): one SGPR buffer descriptor per
+//     client; row i's registers are reloaded from the NEXT fast window's
+//     client i right after row i is squared (its 8-row group's client
+//     addresses come from the pointer table by scalar loads one group ahead);
+//   slow window (a key's ragged last window): loaded after the squares by
+//     element loads, columns past the key 0.
+// Models with integer / bool keys keep the LDS-DMA tiles (the host checks).
+// The next window's key comes from a scalar scan forward from the current
+// one (a wave's windows only move forward), so no vector load besides the
+// rows is in flight in the loop.  Rows K..KMAX-1 are padding: empty
+// descriptors (0, no traffic) or 0, weight -0.0, sums never written.  The
+// pointer table is padded by kSegWinTablePad entries so every group's 8
+// addresses load unconditionally (a padding row's is never dereferenced).
+// ---------------------------------------------------------------------------
+constexpr int64_t kSegWinTablePad = 128;
+constexpr int64_t kSegWinMinPerWave = 16;  // windows per wave below which the LDS-DMA tiles keep the round
+
+template <int KMAX, int VEC, int NW, int MINW = win_min_waves(KMAX, VEC)>
+__global__ __launch_bounds__(64 * NW, MINW) void reduce_sqdist_segwin_kernel(
+    const SegKey* __restrict__ keys, const int64_t* __restrict__ ptrs, int64_t n_keys, int64_t units, int K,
+    const float* __restrict__ W, float* __restrict__ out, double* __restrict__ partials) {
+  typedef typename WinVec<VEC>::T V;
+  constexpr int WC = 64 * VEC;
+  constexpr int NB = (KMAX + 7) / 8;
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t GW = static_cast<int64_t>(gridDim.x) * NW;
+  const int64_t gw = static_cast<int64_t>(blockIdx.x) * NW + wv;
+  const uint32_t voff = static_cast<uint32_t>(lane) * VEC * 4;
+  const bool upper = (lane & 8) != 0;
+  __shared__ __attribute__((aligned(16))) float wl[(KMAX + 3) & ~3];
+  __shared__ double accl[NW][NB][64];
+  for (int i = threadIdx.x; i < ((KMAX + 3) & ~3); i += 64 * NW) wl[i] = i < K ? W[i] : -0.0f;
+  double* acc = &accl[wv][0][lane];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) acc[64 * b] = 0.0;
+  __syncthreads();
+
+  V x[KMAX];
+  // A window's K client addresses arrive as one vector load per 64 clients
+  // (lane l: clients l and 64 + l), issued before the chain that precedes
+  // their use -- the chain has waited for every older load by then -- and
+  // row i reads its address with v_readlane (an SGPR pair: the descriptor
+  // stays uniform).  Scalar loads would be hoisted for all KMAX rows at once.
+  int64_t pv[2];
+  const auto load_ptrs = [&](const int64_t* P) __attribute__((always_inline)) {
+    const gptr<int64_t> q = to_global<int64_t>(P);
+    pv[0] = q[lane];
+    if constexpr (KMAX > 64) pv[1] = q[64 + lane];
+  };
+  const auto ptr_of = [&](int i) __attribute__((always_inline)) {
+    const int64_t v = pv[i >> 6];
+    int li = i & 63;
+    asm volatile("" : "+s"(li));  // read where it is used: the KMAX addresses would not fit the SGPRs
+    const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(v), li);
+    const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(static_cast<uint64_t>(v) >> 32), li);
+    return reinterpret_cast<const float*>((static_cast<uint64_t>(hi) << 32) | lo);
+  };
+  // a slow window (a key's ragged last window) into x: element loads, 0 past the key
+  const auto load_slow = [&](int64_t c0, int n, int Kw) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < KMAX; ++i) {
+      const gptr<float> base = to_global<float>(ptr_of(i));
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) {
+        const int col = lane * VEC + v;
+        x[i][v] = (i < Kw && col < n) ? base[c0 + col] : 0.f;
+      }
+    }
+  };
+  // client i of a fast window
+  const auto load_fast = [&](int i, int64_t c0, int Kw, bool on) __attribute__((always_inline)) {
+    const float* base = ptr_of(i) + c0;
+    const int bytes = (on && i < Kw) ? WC * 4 : 0;
+    x[i] = win_load<VEC>(__builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, bytes, 0x00020000), voff);
+  };
+
+  // window / key indices in 32 bits (the host checks units < 2^31): 64-bit
+  // compares run on the VALU, and a descriptor built from a VALU result
+  // would cost a waterfall loop per load
+  const int units32 = static_cast<int>(units), nkeys32 = static_cast<int>(n_keys);
+  const int GW32 = static_cast<int>(GW);
+  // valid columns of window `w` of a key with `numel` elements (uniform)
+  const auto cols_of = [&](int64_t numel, int w) __attribute__((always_inline)) {
+    const int64_t left = numel - static_cast<int64_t>(w) * WC;
+    return (left >> 31) != 0 ? WC : (static_cast<int>(left) < WC ? static_cast<int>(left) : WC);
+  };
+  int u = static_cast<int>(gw), j = 0, n = 0;
+  int64_t c0 = 0;
+  if (u < units32) {
+    j = __builtin_amdgcn_readfirstlane(static_cast<int>(find_key(keys, n_keys, u)));  // wave-wide search, then scans
+    const SegKey key = keys[j];
+    const int w = u - static_cast<int>(key.unit_start);
+    c0 = static_cast<int64_t>(w) * WC;
+    n = cols_of(key.numel, w);
+    load_ptrs(ptrs + static_cast<int64_t>(j) * K);
+    if (n == WC) {
+#pragma unroll
+      for (int i = 0; i < KMAX; ++i) load_fast(i, c0, K, true);
+    } else {
+      load_slow(c0, n, K);
+    }
+  }
+  for (; u < units32; u += GW32) {
+    int Kw = K;
+    asm volatile("" : "+s"(Kw));
+    const int64_t out_off = keys[j].out_offset;
+    // the next window: its key by a forward scan
+    const int un = u + GW32;
+    int jn = j, nn = 0;
+    int64_t c0n = 0;
+    if (un < units32) {
+      while (jn + 1 < nkeys32 && static_cast<int>(keys[jn + 1].unit_start) <= un) ++jn;
+      const SegKey kn = keys[jn];
+      const int w = un - static_cast<int>(kn.unit_start);
+      c0n = static_cast<int64_t>(w) * WC;
+      nn = cols_of(kn.numel, w);
+    }
+    const bool fastn = un < units32 && nn == WC;
+    load_ptrs(ptrs + static_cast<int64_t>(jn) * K);  // the next window's addresses, before the chain
+    // the chain (a slow window's columns past its key are 0)
+    int wo = 0;
+    asm volatile("" : "+v"(wo));
+    V a;
+#pragma unroll
+    for (int q = 0; q < (KMAX + 3) / 4; ++q) {
+      const f32x4 w4 = *reinterpret_cast<const f32x4*>(&wl[wo + 4 * q]);
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int i = 4 * q + jj;
+        if (i == 0) {
+          a = x[0] * w4[0];
+        } else if (i < KMAX) {
+          const V t = x[i] * w4[jj];
+          a = a + t;
+        }
+      }
+    }
+    float* o = out + out_off + c0 + lane * VEC;
+    if (n == WC) {
+      *reinterpret_cast<V*>(o) = a;
+    } else {
+#pragma unroll
+      for (int v = 0; v < VEC; ++v)
+        if (lane * VEC + v < n) o[v] = a[v];
+    }
+    // squares; row i reloaded from the next window right after (a slow next
+    // window: empty descriptors here, its element loads after the squares)
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      double p[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int i = 8 * b + r;
+        p[r] = 0.0;
+        if (i < KMAX) {
+          p[r] = win_sq<VEC>(x[i] - a);
+          load_fast(i, c0n, Kw, fastn);
+        }
+      }
+      const double q01 = fold32(p[0], p[1]), q23 = fold32(p[2], p[3]);
+      const double q45 = fold32(p[4], p[5]), q67 = fold32(p[6], p[7]);
+      acc[64 * b] += fold8(fold16(q01, q23), fold16(q45, q67), upper);
+    }
+    if (un < units32 && !fastn) load_slow(c0n, nn, Kw);
+    j = jn;
+    c0 = c0n;
+    n = nn;
+  }
+  const int row_in = win_batch_row(lane);
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    double sm = acc[64 * b];
+    sm += dpp_move_f64<0xB1, 0xF>(sm);
+    sm += dpp_move_f64<0x4E, 0xF>(sm);
+    sm += dpp_move_f64<0x141, 0xF>(sm);
+    const int row = 8 * b + row_in;
+    if ((lane & 7) == 0 && row < K) partials[static_cast<int64_t>(row) * GW + gw] = sm;
+  }
+}
+
+// FEDAVG_SEGWIN=0 keeps the LDS-DMA tiles for every device round (probes, A/B)
+inline bool segwin_disabled() {
+  static const bool off = [] {
+    const char* e = std::getenv("FEDAVG_SEGWIN");
+    return e && e[0] == '0';
+  }();
+  return off;
+}
+
+// waves of a zero-copy window launch over `units` windows
+template <int KMAX, int VEC, int NW>
+int64_t segwin_waves(int64_t units) {
+  const int64_t per_cu = resident_blocks(reduce_sqdist_segwin_kernel<KMAX, VEC, NW>, 64 * NW) / cu_count();
+  const int64_t grid = per_cu * cu_count();
+  const int64_t need = (units + NW - 1) / NW;
+  return (grid < need ? grid : need) * NW;
+}
+
+// the window instance for K clients (0 outside 17..128).  The rows kernel's
+// 100 x 2 band is 128 x 1 here: the table's addresses take the VGPRs a
+// 100 x 2 window would need (it spills; device round 100 x 25M 3.66 ms vs
+// 2.75 for the tiles, profiles/r03/segwin/)
+inline int segwin_kmax(int64_t K) {
+  return K <= 16 || K > 128 ? 0 : (K <= 48 ? 48 : (K <= 64 ? 64 : (K <= 80 ? 80 : 128)));
+}
+inline int segwin_vec(int kmax) { return kmax == 48 ? 4 : (kmax == 128 ? 1 : 2); }
+
+inline int64_t segwin_waves_for(int kmax, int64_t units) {
+  switch (kmax) {
+    case 48: return segwin_waves<48, 4, 4>(units);
+    case 64: return segwin_waves<64, 2, 4>(units);
+    case 80: return segwin_waves<80, 2, 4>(units);
+    case 128: return segwin_waves<128, 1, 4>(units);
+    default: return 0;
+  }
+}
+
 constexpr int kSegFusedMaxK = kBlock;
 
 // tile width: as fedavg_dist.hip's fused_cols (32 above 128 clients, 64 above
@@ -667,7 +892,8 @@ extern "C" {
 
 int64_t fedavg_segments_workspace(int64_t K, int64_t n_keys) {
   if (K <= 0 || n_keys <= 0) return 0;
-  return n_keys * static_cast<int64_t>(sizeof(SegKey)) + n_keys * K * static_cast<int64_t>(sizeof(int64_t));
+  return n_keys * static_cast<int64_t>(sizeof(SegKey)) +
+         (n_keys * K + kSegWinTablePad) * static_cast<int64_t>(sizeof(int64_t));
 }
 
 int64_t fedavg_segments_partials(const int64_t* key_numel, int64_t n_keys, int64_t K) {
@@ -772,7 +998,9 @@ int64_t fedavg_reduce_sqdist_segments_partials(int64_t K) {
   const int S = seg_fused_cols(K);
   const int per_cu = S == 32 ? seg_fused_per_cu<32>(K)
                      : (S == 64 ? seg_fused_per_cu<64>(K) : (S == 128 ? seg_fused_per_cu<128>(K) : seg_fused_per_cu<256>(K)));
-  return K * static_cast<int64_t>(per_cu > 0 ? per_cu : 1) * cu_count();
+  const int64_t tiles = K * static_cast<int64_t>(per_cu > 0 ? per_cu : 1) * cu_count();
+  const int64_t windows = K * segwin_waves_for(segwin_kmax(K), INT64_MAX / 2);  // a full window launch
+  return tiles > windows ? tiles : windows;
 }
 
 int fedavg_reduce_sqdist_segments_f32(const int64_t* client_ptrs, const int64_t* key_numel, const int64_t* key_offset,
@@ -792,6 +1020,51 @@ int fedavg_reduce_sqdist_segments_f32(const int64_t* client_ptrs, const int64_t*
           return set_error(FEDAVG_EALIGN, "%s: client %lld key %lld is not 16-B aligned (use the two passes)", what,
                            (long long)k, (long long)j);
   hipStream_t s = static_cast<hipStream_t>(stream);
+  // long models, 17-128 clients: the zero-copy wave-owned windows
+  const int kmax = segwin_kmax(K);
+  if (kmax > 0 && key_numel && n_keys > 0 && !segwin_disabled()) {
+    const int64_t wc = 64 * segwin_vec(kmax);
+    bool ok = key_kind != nullptr;
+    for (int64_t jk = 0; ok && jk < n_keys; ++jk) ok = key_numel[jk] >= 0 && key_kind[jk] == kRaw;
+    const int64_t wunits = ok ? units_of(key_numel, n_keys, wc) : 0;
+    const int64_t waves = segwin_waves_for(kmax, wunits);
+    if (ok && waves > 0 && wunits >= kSegWinMinPerWave * waves && wunits < (int64_t(1) << 31) &&
+        n_keys < (int64_t(1) << 31)) {
+      if (partial_elems < K * waves)
+        return set_error(FEDAVG_EINVAL, "%s: partials need %lld doubles", what, (long long)(K * waves));
+      const int64_t units = stage_tables(what, client_ptrs, key_numel, key_offset, key_kind, n_keys, K, host_ws,
+                                         dev_ws, ws_bytes, s, wc);
+      if (units < 0) return static_cast<int>(units);
+      const auto* keys = static_cast<const SegKey*>(dev_ws);
+      const auto* tptrs = reinterpret_cast<const int64_t*>(static_cast<const char*>(dev_ws) +
+                                                           n_keys * static_cast<int64_t>(sizeof(SegKey)));
+      const dim3 grid(static_cast<unsigned>(waves / 4)), block(256);
+      const int k32 = static_cast<int>(K);
+      switch (kmax) {
+        case 48:
+          hipLaunchKernelGGL((reduce_sqdist_segwin_kernel<48, 4, 4>), grid, block, 0, s, keys, tptrs, n_keys, units,
+                             k32, weights, out, partials);
+          break;
+        case 64:
+          hipLaunchKernelGGL((reduce_sqdist_segwin_kernel<64, 2, 4>), grid, block, 0, s, keys, tptrs, n_keys, units,
+                             k32, weights, out, partials);
+          break;
+        case 80:
+          hipLaunchKernelGGL((reduce_sqdist_segwin_kernel<80, 2, 4>), grid, block, 0, s, keys, tptrs, n_keys, units,
+                             k32, weights, out, partials);
+          break;
+        default:
+          hipLaunchKernelGGL((reduce_sqdist_segwin_kernel<128, 1, 4>), grid, block, 0, s, keys, tptrs, n_keys, units,
+                             k32, weights, out, partials);
+          break;
+      }
+      int rc = launch_status(what);
+      if (rc) return rc;
+      hipLaunchKernelGGL(segments_finalize_kernel, dim3(static_cast<unsigned>(K)), dim3(kBlock), 0, s, partials,
+                         waves, sumsq);
+      return launch_status(what);
+    }
+  }
   const int S = seg_fused_cols(K);
   const int64_t units = stage_tables(what, client_ptrs, key_numel, key_offset, key_kind, n_keys, K, host_ws, dev_ws,
                                      ws_bytes, s, S);

@@ -33,6 +33,11 @@ def clients_for(name, dev):
         K, shapes = 100, [("w", (25_000_000,))]
     elif name == "flat200":
         K, shapes = 200, [("w", (10_000_000,))]
+    elif name.startswith("flatk"):  # flatk64: 64 clients of one 25M key
+        K, shapes = int(name[5:]), [("w", (25_000_000,))]
+    elif name == "resnet18_gn_k100":  # the cfg4 layout (all fp32 keys) at 100 clients
+        from model_shapes import CONFIGS
+        K, shapes = 100, CONFIGS["resnet18_gn"][1]
     else:
         from model_shapes import CONFIGS
         K, shapes = CONFIGS[name]

@@ -151,3 +151,34 @@ def test_window_plan_short_rows_and_other_k():
     for K in (1, 16, 129, 300, 512):
         assert lib.fedavg_fused_plan_of(K, 25_000_000) // 1000000 != KIND_WIN
     assert lib.fedavg_fused_plan_of(513, 25_000_000) == 0
+
+
+WIN_DEVICE_SHAPES = [("layer.weight", (8_400_017,)), ("layer.bias", (1001,)), ("tiny", (3,)),
+                     ("proj.weight", (800, 1000)), ("proj.bias", (640,))]
+
+
+@pytest.mark.parametrize("K", [20, 64, 100, 128])
+def test_window_device_clients_bit_exact(K):
+    """Device-resident clients of an all-fp32 model long enough for the
+    zero-copy windows (reduce_sqdist_segwin_kernel): ragged key ends at every
+    window width, keys shorter than a window; the aggregate's bits against the
+    reference loop on host copies, the fused :291 distances within one fp32
+    unit of the exact restatement."""
+    from collections import OrderedDict
+
+    from test_gpu_model_shapes import _check_distances, _oracle
+
+    torch.cuda.empty_cache()
+    g = torch.Generator(device=DEV).manual_seed(K)
+    base = {k: torch.randn(s, generator=g, device=DEV) * 0.05 for k, s in WIN_DEVICE_SHAPES}
+    w_locals = []
+    for i in range(K):
+        sd = OrderedDict((k, base[k] + torch.randn(s, generator=g, device=DEV) * 1e-3) for k, s in WIN_DEVICE_SHAPES)
+        w_locals.append((int(np.random.default_rng(i).integers(1, 1000)), sd))
+    expected = _oracle(w_locals)
+    out = mfl_amd.aggregate(w_locals, device=DEV)
+    for k, e in expected.items():
+        assert torch.equal(out[k].cpu().reshape(-1).view(torch.int32), e.reshape(-1).view(torch.int32)), k
+    _check_distances(w_locals, out, max_checked=16)
+    del w_locals, out, expected, base
+    torch.cuda.empty_cache()
