@@ -1152,7 +1152,8 @@ int launch_fused_win(const float* clients, int64_t K, int64_t P, int64_t ld, con
 //     K <= 100  100 x 2 (100 x 25M 1.531-1.665 vs 1.601-1.797 by box; 90 x
 //               25M 1.578 vs 2.440; 100 x 6.25M 0.431 vs 0.451)
 //     K <= 128  128 x 1 (128 x 8M 0.693 vs 0.879; 112 x 8M 0.610 vs 0.640)
-//   shorter rows (100 x 3.1M: window 0.230 vs 0.218), other K:
+//   shorter rows (100 x 3.1M: window 0.230 vs 0.218; 65-96 rows from 400K
+//   columns up stay on the windows, see kWinHoleMinP), other K:
 //   K <= 16    register-staged, 256-column tiles (8 x 125M 0.896 vs 0.880
 //              LDS-DMA; FEMNIST 10 x 1.2M 16.6 vs 22.2 us)
 //   K <= 32    LDS-DMA, 128 columns (24 x 41.7M 0.733 vs 0.738 register-staged)
@@ -1170,6 +1171,13 @@ int launch_fused_win(const float* clients, int64_t K, int64_t P, int64_t ld, con
 constexpr int kFusedNone = 0, kFusedLds = 1, kFusedRs = 2, kFusedWin = 3;
 constexpr int64_t kFusedRowsMaxK = 512;
 constexpr int64_t kWinMinPerWave = 16;  // windows per wave below which the tile kernels keep the round
+// ... except in the LDS-DMA tiles' weak band, 65-96 rows, where the windows
+// win down to ~400K columns (profiles/r03/win/short_rows_*.jsonl, ms, tiles
+// vs windows: 70 x 600K 0.052 vs 0.043; 70 x 3M 0.217 vs 0.143; 80 x 1.5M
+// 0.129 vs 0.090; 90 x 600K 0.065 vs 0.051; 90 x 3M 0.285 vs 0.190; 92 x
+// 1.5M 0.108 vs 0.102; 98 x 1.5M 0.109 vs 0.109; 100 x 600K 0.059 vs 0.059;
+// 65 x 200K 0.022 vs 0.023)
+constexpr int64_t kWinHoleMinK = 65, kWinHoleMaxK = 96, kWinHoleMinP = 400000;
 struct FusedPlan {
   int kind, S, slots;  // kFusedWin: S = KMAX, slots = VEC
 };
@@ -1204,7 +1212,8 @@ inline int64_t win_waves(const FusedPlan& pl, int64_t P) {
 inline FusedPlan fused_plan(int64_t K, int64_t P) {
   if (K < 1 || K > kFusedRowsMaxK) return {kFusedNone, 0, 0};
   const FusedPlan win = win_plan(K);
-  if (win.kind == kFusedWin && (P + 64 * win.slots - 1) / (64 * win.slots) >= kWinMinPerWave * win_waves(win, P))
+  if (win.kind == kFusedWin && ((P + 64 * win.slots - 1) / (64 * win.slots) >= kWinMinPerWave * win_waves(win, P) ||
+                                 (K >= kWinHoleMinK && K <= kWinHoleMaxK && P >= kWinHoleMinP)))
     return win;
   if (K <= 16) return {kFusedRs, 256, 8};
   if (K <= 32) return {kFusedLds, 128, 0};

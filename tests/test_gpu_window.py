@@ -151,6 +151,13 @@ def test_window_plan_short_rows_and_other_k():
     for K in (1, 16, 129, 300, 512):
         assert lib.fedavg_fused_plan_of(K, 25_000_000) // 1000000 != KIND_WIN
     assert lib.fedavg_fused_plan_of(513, 25_000_000) == 0
+    # the LDS-DMA tiles' weak band (65-96 rows) keeps the windows down to 400K columns
+    assert lib.fedavg_fused_plan_of(70, 600_000) == KIND_WIN * 1000000 + 80 * 100 + 2
+    assert lib.fedavg_fused_plan_of(90, 400_000) == KIND_WIN * 1000000 + 100 * 100 + 2
+    assert lib.fedavg_fused_plan_of(96, 1_500_000) == KIND_WIN * 1000000 + 100 * 100 + 2
+    assert lib.fedavg_fused_plan_of(90, 399_999) // 1000000 != KIND_WIN
+    assert lib.fedavg_fused_plan_of(97, 1_500_000) // 1000000 != KIND_WIN
+    assert lib.fedavg_fused_plan_of(64, 1_500_000) // 1000000 != KIND_WIN
 
 
 WIN_DEVICE_SHAPES = [("layer.weight", (8_400_017,)), ("layer.bias", (1001,)), ("tiny", (3,)),
