@@ -1136,6 +1136,179 @@ int launch_fused_win(const float* clients, int64_t K, int64_t P, int64_t ld, con
   return launch_status(what);
 }
 
+#ifdef FEDAVG_TUNING
+// ---------------------------------------------------------------------------
+// Probe (round 3): split-row windows.  With K = 100 rows in one wave the
+// window kernel above keeps more loads than the hardware's 63-load vmcnt cap
+// can hold, so each window's reloads go out in two generations and the wave
+// sits with nothing in flight between its last row's arrival and the first
+// reload.  Here a workgroup of TWO waves owns a window: wave h holds rows
+// h*KH .. h*KH + KH - 1 (KH <= 63: every reload of a window is in flight at
+// once; KH x VEC registers, so three waves per SIMD at KH 50, VEC 2).  The
+// chain stays the reference's sequential order: wave 0 runs rows 0..KH-1,
+// hands its fp32 partial over LDS, wave 1 continues with rows KH..2KH-1 and
+// returns the final average (two barriers per window).  Each wave squares and
+// reloads its own rows; row sums as in reduce_sqdist_win_kernel, one partial
+// per (row, workgroup).
+// ---------------------------------------------------------------------------
+template <int KH, int VEC>
+__global__ __launch_bounds__(128, win_min_waves(KH, VEC)) void reduce_sqdist_win2_kernel(
+    const float* __restrict__ X, int K, int64_t ld, int64_t P, int64_t nwin, const float* __restrict__ W,
+    float* __restrict__ out, double* __restrict__ partials) {
+  typedef typename WinVec<VEC>::T V;
+  constexpr int WC = 64 * VEC;
+  constexpr int NB = (KH + 7) / 8;
+  constexpr int KP = (KH + 3) & ~3;
+  const int lane = threadIdx.x & 63;
+  const int h = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r0 = h * KH;
+  const int64_t G = gridDim.x;
+  const uint32_t voff = static_cast<uint32_t>(lane) * VEC * 4;
+  const int64_t P4 = (P + 3) & ~static_cast<int64_t>(3);
+  const int64_t row_bytes = ld * 4;
+  const bool upper = (lane & 8) != 0;
+  const auto win_bytes = [&](int64_t w) -> int {
+    if (w >= nwin) return 0;
+    const int64_t n = P4 - w * WC;
+    return static_cast<int>((n < WC ? n : WC) * 4);
+  };
+  __shared__ __attribute__((aligned(16))) float wl[2][KP];
+  __shared__ double accl[2][NB][64];
+  __shared__ __attribute__((aligned(16))) V xa[64];
+  for (int i = threadIdx.x; i < 2 * KP; i += 128) {
+    const int hh = i / KP, j = i % KP, row = hh * KH + j;
+    wl[hh][j] = (j < KH && row < K) ? W[row] : -0.0f;
+  }
+  double* acc = &accl[h][0][lane];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) acc[64 * b] = 0.0;
+  __syncthreads();
+  V x[KH];
+  {
+    int Kw = K;
+    asm volatile("" : "+s"(Kw));
+    const int nb = win_bytes(blockIdx.x);
+    const char* rp = reinterpret_cast<const char*>(X + static_cast<int64_t>(blockIdx.x) * WC) + r0 * row_bytes;
+#pragma unroll
+    for (int i = 0; i < KH; ++i) {
+      asm volatile("" : "+s"(rp));
+      x[i] = win_load<VEC>(
+          __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(rp), 0, r0 + i < Kw ? nb : 0, 0x00020000), voff);
+      rp += row_bytes;
+    }
+  }
+  // a = a + fl32(x_i w_i) over this wave's rows (first: a = fl32(x_0 w_0) first)
+  const auto chain = [&](V& a, bool first) {
+    int wo = h * KP;  // opaque: the weights are re-read per window, not held in registers
+    asm volatile("" : "+v"(wo));
+    const float* wp = &wl[0][0] + wo;
+#pragma unroll
+    for (int q = 0; q < KP / 4; ++q) {
+      const f32x4 w4 = *reinterpret_cast<const f32x4*>(wp + 4 * q);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int i = 4 * q + j;
+        if (i >= KH) continue;
+        if (first && i == 0) {
+          a = x[0] * w4[0];
+        } else {
+          const V t = x[i] * w4[j];
+          a = a + t;
+        }
+      }
+    }
+  };
+  for (int64_t w = blockIdx.x; w < nwin; w += G) {
+    int Kw = K;
+    asm volatile("" : "+s"(Kw));
+    const int64_t c0 = w * WC;
+    const int64_t cl = c0 + lane * VEC;
+    const int nbn = win_bytes(w + G);
+    const char* rp = reinterpret_cast<const char*>(X + (w + G) * WC) + r0 * row_bytes;
+    const bool ragged = c0 + WC > P;
+    if (ragged) {
+#pragma unroll
+      for (int i = 0; i < KH; ++i) {
+#pragma unroll
+        for (int v = 0; v < VEC; ++v)
+          if (cl + v >= P) x[i][v] = 0.f;
+      }
+    }
+    V a;
+    if (h == 0) {
+      chain(a, true);
+      xa[lane] = a;
+    }
+    __syncthreads();
+    if (h == 1) {
+      a = xa[lane];
+      chain(a, false);
+      xa[lane] = a;
+      if (!ragged) {
+        __builtin_nontemporal_store(a, reinterpret_cast<V*>(out + cl));
+      } else {
+#pragma unroll
+        for (int v = 0; v < VEC; ++v)
+          if (cl + v < P) out[cl + v] = a[v];
+      }
+    }
+    __syncthreads();
+    if (h == 0) a = xa[lane];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      double p[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = 8 * b + j;
+        p[j] = 0.0;
+        if (i < KH) {
+          p[j] = win_sq<VEC>(x[i] - a);
+          asm volatile("" : "+s"(rp));
+          x[i] = win_load<VEC>(
+              __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(rp), 0, r0 + i < Kw ? nbn : 0, 0x00020000), voff);
+          rp += row_bytes;
+        }
+      }
+      const double q01 = fold32(p[0], p[1]), q23 = fold32(p[2], p[3]);
+      const double q45 = fold32(p[4], p[5]), q67 = fold32(p[6], p[7]);
+      acc[64 * b] += fold8(fold16(q01, q23), fold16(q45, q67), upper);
+    }
+  }
+  const int row_in = win_batch_row(lane);
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    double s = acc[64 * b];
+    s += dpp_move_f64<0xB1, 0xF>(s);
+    s += dpp_move_f64<0x4E, 0xF>(s);
+    s += dpp_move_f64<0x141, 0xF>(s);
+    const int row = 8 * b + row_in;
+    if ((lane & 7) == 0 && row < KH && r0 + row < K) partials[static_cast<int64_t>(r0 + row) * G + blockIdx.x] = s;
+  }
+}
+
+template <int KH, int VEC>
+int launch_fused_win2(const float* clients, int64_t K, int64_t P, int64_t ld, const float* weights, float* out,
+                      double* partials, int64_t partial_elems, double* sumsq, int blocks_per_cu, hipStream_t s,
+                      const char* what) {
+  if (K > 2 * KH) return set_error(FEDAVG_EMODE, "%s: this split window kernel covers K <= %d", what, 2 * KH);
+  const auto kern = reduce_sqdist_win2_kernel<KH, VEC>;
+  const int64_t per_cu = blocks_per_cu > 0 ? blocks_per_cu : resident_blocks(kern, 128) / cu_count();
+  const int64_t nwin = (P + 64 * VEC - 1) / (64 * VEC);
+  int64_t grid = per_cu * cu_count();
+  if (grid > nwin) grid = nwin;
+  if (grid <= 0) return set_error(FEDAVG_EMODE, "%s: the split window kernel is not resident", what);
+  if (partial_elems < K * grid)
+    return set_error(FEDAVG_EINVAL, "%s: workspace needs %lld doubles", what, (long long)(K * grid));
+  hipLaunchKernelGGL((reduce_sqdist_win2_kernel<KH, VEC>), dim3(static_cast<unsigned>(grid)), dim3(128), 0, s,
+                     clients, static_cast<int>(K), ld, P, nwin, weights, out, partials);
+  int rc = launch_status(what);
+  if (rc) return rc;
+  hipLaunchKernelGGL(client_sqdist_finalize_kernel, dim3(static_cast<unsigned>(K)), dim3(kBlock), 0, s, partials,
+                     grid, sumsq);
+  return launch_status(what);
+}
+#endif  // FEDAVG_TUNING
+
 // Which one-read kernel serves K rows (production), from interleaved
 // measurements of every candidate against the others and the two passes on
 // ~4 GB of rows (scripts/fused_probe.py, profiles/r03/fused_rule/*.jsonl and
@@ -1762,6 +1935,17 @@ int fedavg_reduce_sqdist_f32_variant(const float* clients, int64_t K, int64_t P,
     FEDAVG_WINK_CASE(128, 1, 2)
 #undef FEDAVG_WINK_CASE
 #undef FEDAVG_WIN_CASE
+    // split-row windows (reduce_sqdist_win2_kernel): 80000000 + KH * 100 + VEC, K <= 2 KH
+#define FEDAVG_WIN2_CASE(KH, VEC)                                                                                 \
+  case 80000000 + KH * 100 + VEC:                                                                                \
+    return launch_fused_win2<KH, VEC>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq,        \
+                                      blocks_per_cu, s, what);
+    FEDAVG_WIN2_CASE(50, 2)
+    FEDAVG_WIN2_CASE(40, 2)
+    FEDAVG_WIN2_CASE(32, 2)
+    FEDAVG_WIN2_CASE(25, 4)
+    FEDAVG_WIN2_CASE(60, 2)
+#undef FEDAVG_WIN2_CASE
     default: return set_error(FEDAVG_EMODE, "%s: cols must be 32, 64, 128 or 256 (+1000: double-buffered)", what);
   }
 }

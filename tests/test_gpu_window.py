@@ -189,3 +189,20 @@ def test_window_device_clients_bit_exact(K):
     _check_distances(w_locals, out, max_checked=16)
     del w_locals, out, expected, base
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("kh,vec", [(50, 2), (40, 2), (32, 2), (25, 4), (60, 2)])
+def test_split_row_windows_vs_oracle(kh, vec):
+    """The split-row probe (reduce_sqdist_win2_kernel: two waves per window,
+    the chain handed from rows 0..KH-1 to KH..2KH-1 over LDS): oracle bits and
+    sums with K inside the first wave, across the split and at 2 KH."""
+    for K in sorted({1, kh - 1, kh, kh + 1, 2 * kh - 3, 2 * kh}):
+        for P in (1, 3, 64 * vec + 5, 100_003):
+            x, ld, weights = _rows(K, P, kh * 7127 + K * 31 + P)
+            w = mfl_amd.weights_tensor(weights, torch.float32, DEV)
+            out, s = _win(x, K, P, ld, w, kh, vec, code=80000000 + kh * 100 + vec)
+            exp = O.reduce_f32(x[:, :P].cpu().numpy(), np.array([np.float32(v) for v in weights], dtype=np.float32))
+            assert out.cpu().numpy().view(np.uint32).tobytes() == exp.view(np.uint32).tobytes(), (kh, vec, K, P)
+            ref = _sumsq_ref(x, out, P)
+            rel = ((s - ref).abs() / ref.clamp_min(1e-300)).max().item()
+            assert rel < 1e-12, (kh, vec, K, P, rel)
