@@ -1945,6 +1945,7 @@ int fedavg_reduce_sqdist_f32_variant(const float* clients, int64_t K, int64_t P,
     FEDAVG_WIN2_CASE(32, 2)
     FEDAVG_WIN2_CASE(25, 4)
     FEDAVG_WIN2_CASE(60, 2)
+    FEDAVG_WIN2_CASE(50, 4)
 #undef FEDAVG_WIN2_CASE
     default: return set_error(FEDAVG_EMODE, "%s: cols must be 32, 64, 128 or 256 (+1000: double-buffered)", what);
   }

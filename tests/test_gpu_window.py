@@ -191,7 +191,7 @@ def test_window_device_clients_bit_exact(K):
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("kh,vec", [(50, 2), (40, 2), (32, 2), (25, 4), (60, 2)])
+@pytest.mark.parametrize("kh,vec", [(50, 2), (40, 2), (32, 2), (25, 4), (60, 2), (50, 4)])
 def test_split_row_windows_vs_oracle(kh, vec):
     """The split-row probe (reduce_sqdist_win2_kernel: two waves per window,
     the chain handed from rows 0..KH-1 to KH..2KH-1 over LDS): oracle bits and
