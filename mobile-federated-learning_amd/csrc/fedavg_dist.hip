@@ -1918,6 +1918,8 @@ int fedavg_reduce_sqdist_f32_variant(const float* clients, int64_t K, int64_t P,
     FEDAVG_WIN_CASE(2, 8, 16)
     FEDAVG_WIN_CASE(2, 8, 0)
     FEDAVG_WIN_CASE(2, 4, 64)
+    FEDAVG_WIN_CASE(2, 1, 64)
+    FEDAVG_WIN_CASE(2, 2, 64)
     FEDAVG_WIN_CASE(2, 4, 128)
     case 60000000 + 192 * 1000000 + 42:  // LDS rows + 8-row descriptors
       return launch_fused_win<100, 2, 4, 192>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq,
