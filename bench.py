@@ -43,6 +43,7 @@ Rank 0 prints ONE JSON line.  Besides the contract keys it carries:
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
 import math
 import os
@@ -66,6 +67,7 @@ WORKLOADS = {
     "resnet18_gn": (500, 11_227_812, "cfg4 fed_cifar100 + resnet18_gn, 500 clients"),
     "synthetic_1000x100m": (1000, 100_000_000, "cfg5 synthetic 1000 clients x 100M fp32 params"),
     "synthetic_1000x100m_slice": (1000, 12_500_000, "cfg5's per-GPU slice at N = 8 (1000 x 12.5M)"),
+    "rehearsal_small": (8, 200_003, "CPU rehearsal of the multi-rank machinery (8 x 200,003; --cpu-rehearsal)"),
 }
 
 # One rank's client rows may take this much HBM (MI355X: 288 GB); a larger
@@ -77,6 +79,11 @@ ROW_BUDGET_BYTES = int(float(os.environ.get("FEDAVG_BENCH_ROW_BUDGET_GB", "230")
 # full-chip launch of the short-row schedule (see auto_chunks)
 MIN_CHUNK_COLS = 700_000
 MAX_CHUNKS = 8
+# ... and at N > 1 the warm-up times these depths (plus the rule's pick) and
+# keeps the fastest whole step; a candidate needs >= SWEEP_MIN_BLOCK columns
+# per chunk
+SWEEP_CHUNKS = (1, 2, 4, 8)
+SWEEP_MIN_BLOCK = 1024
 
 
 def env_int(name, default):
@@ -157,7 +164,8 @@ def _thread_count():
     return n_aff, (omp if 0 < omp < n_aff else None)
 
 
-def cpu_baseline(K: int, P: int, flat_seconds: float = 6.0, model_seconds: float = 4.0, rep_budget_s: float = 2.5):
+def cpu_baseline(K: int, P: int, flat_seconds: float = 6.0, model_seconds: float = 4.0, rep_budget_s: float = 2.5,
+                 model: str = "resnet56"):
     """The reference's torch CPU loop (fedavg_trainer.py:444-458, restated in
     oracle/fedavg_oracle.py) on the GPU box's host cores, per BASELINE.md's
     CPU-baseline plan:
@@ -231,7 +239,7 @@ def cpu_baseline(K: int, P: int, flat_seconds: float = 6.0, model_seconds: float
         note(f"flat at {n} threads ({label}): {layouts[-1]['value']} GB/s (K={Kt})")
     del rows
     torch.set_num_threads(n_omp or n_aff)
-    Km, shapes = CONFIGS["resnet56"]
+    Km, shapes = CONFIGS[model]
     Pm = numel(shapes)
     mbase = {k: torch.randn(s, generator=g) * 0.05 for k, s in shapes}
     dicts = []
@@ -248,24 +256,36 @@ def cpu_baseline(K: int, P: int, flat_seconds: float = 6.0, model_seconds: float
     torch.set_num_threads(n_m)
     best_m, reps_m = timed(lambda: [(mcounts[0], dict(dicts[0]))] + list(zip(mcounts[1:], dicts[1:])), model_seconds,
                            max_reps=20)
-    layouts.append({"layout": "model-shaped (resnet56)", "threads": n_m,
+    layouts.append({"layout": f"model-shaped ({model})", "threads": n_m,
                     "threads_from": "OMP_NUM_THREADS" if n_omp else "affinity",
                     "value": round(algorithmic_bytes(Km, Pm) / best_m / 1e9, 3), "unit": "GB/s",
-                    "sample": f"cfg3 resnet56 state_dicts: K={Km} x P={Pm}, {len(shapes)} keys; best of {reps_m} "
+                    "sample": f"{model} state_dicts: K={Km} x P={Pm}, {len(shapes)} keys; best of {reps_m} "
                               f"reps after 1 warm-up, {best_m * 1e3:.1f} ms/reduce, {n_m} torch threads"})
     note(f"model-shaped: {layouts[-1]['value']} GB/s")
     torch.set_num_threads(n_omp or n_aff)
     flat = layouts[0]
-    return {
+    out = {
         "value": flat["value"],
         "unit": "GB/s",
         "cores": n_aff,
         "kind": "port",
-        "sample": flat["sample"] + " (value; torch.set_num_threads(len(os.sched_getaffinity(0))), BASELINE.md); "
-                                   "reference torch CPU loop restated (oracle/fedavg_oracle.py aggregate_torch)",
+        "sample": flat["sample"] + " (value; torch.set_num_threads(len(os.sched_getaffinity(0))), BASELINE.md; "
+                                   "threads_from: affinity); reference torch CPU loop restated "
+                                   "(oracle/fedavg_oracle.py aggregate_torch)",
         "affinity_cpus": n_aff,
         "layouts": layouts,
     }
+    # the figure at the job's own CPU share (OMP_NUM_THREADS on the GPU box):
+    # on a shared box the affinity count oversubscribes the share many times
+    # over, so `value` times the scheduler as much as the loop
+    share = [lay for lay in layouts if lay["layout"] == "flat" and lay["threads_from"] == "OMP_NUM_THREADS"]
+    src = share[0] if share else flat
+    out["value_at_share"] = src["value"]
+    out["value_at_share_threads"] = src["threads"]
+    out["value_at_share_K"] = src["K"]
+    out["value_at_share_note"] = (f"flat layout at {src['threads']} torch threads "
+                                  f"({src['threads_from']}), K={src['K']} x P={P}")
+    return out
 
 
 # ---------------------------------------------------------------------------
@@ -381,18 +401,7 @@ def overlap_diagnostics(red, w_dev, steps: int, step_elapsed: float, reps: int =
     import torch.distributed as dist
 
     def timed(fn):
-        torch.cuda.synchronize()
-        dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            fn()
-        torch.cuda.synchronize()
-        dist.barrier()
-        torch.cuda.synchronize()
-        t = torch.tensor([(time.perf_counter() - t0) / reps], dtype=torch.float64, device=red.device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item()) * 1e3
+        return timed_steps(fn, reps, red.device, True) / reps * 1e3
 
     gather = red.gather
     red.gather = False
@@ -479,16 +488,68 @@ def launch_check(args):
         dist.destroy_process_group()
 
 
+def _sync(dev) -> None:
+    import torch
+
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+def _rehearsal_reduce(clients, weights, P, out):
+    """``--cpu-rehearsal`` only: a torch stand-in for the HIP kernel (client 0
+    first, mul then add) so the multi-rank bench machinery -- chunk sweep,
+    exchange, parity checks, the CPU baseline at N > 1 -- runs on CPU with
+    gloo.  Its numbers are not a measurement and the line says so."""
+    acc = clients[0, :P] * weights[0]
+    for i in range(1, clients.shape[0]):
+        acc = acc + clients[i, :P] * weights[i]
+    out[:P].copy_(acc)
+
+
+def timed_steps(step, n: int, dev, use_pg: bool) -> float:
+    """``n`` steps bracketed by barrier + synchronize on both sides; the
+    MAX over ranks of the wall time (seconds)."""
+    import torch
+    import torch.distributed as dist
+
+    _sync(dev)
+    if use_pg:
+        dist.barrier()
+    _sync(dev)
+    t0 = time.perf_counter()
+    for _ in range(n):
+        step()
+    _sync(dev)
+    if use_pg:
+        dist.barrier()
+    _sync(dev)
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    if use_pg:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def chunk_candidates(P_global: int, world: int, auto: int) -> list:
+    """Pipeline depths the N > 1 warm-up times: 1/2/4/8 chunks and the kernel-
+    band rule's pick, each while its chunks keep >= SWEEP_MIN_BLOCK columns."""
+    from mfl_amd.distributed import plan_shards
+
+    return [c for c in sorted({auto, *SWEEP_CHUNKS})
+            if c == auto or plan_shards(P_global, world, 0, c).block >= SWEEP_MIN_BLOCK]
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="target", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default=None, choices=sorted(WORKLOADS), help="default: target")
     ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
                     help="strong: the workload's P is the global model split over the ranks (BASELINE configs); "
                          "weak: every rank owns P columns")
-    ap.add_argument("--chunks", type=int, default=0, help="all-gather pipeline chunks (0 = auto)")
+    ap.add_argument("--chunks", type=int, default=0,
+                    help="all-gather pipeline chunks (0 = auto: at N > 1 the fastest step of a warm-up sweep)")
+    ap.add_argument("--no-chunk-sweep", action="store_true", help="N>1: take the kernel-band rule's chunk count")
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the all-gather (reduce only)")
     ap.add_argument("--force-gather", action="store_true",
                     help="run the RCCL all-gather even at N=1 (world-size-1 nccl group)")
@@ -502,11 +563,19 @@ def main(argv=None):
     ap.add_argument("--shard-of", type=int, default=0,
                     help="N=1 only: reduce rank 0's shard of an N-GPU strong-scaled plan (its chunks, no exchange) "
                          "-- the per-rank kernel at the N-GPU geometry, measured on one GPU")
+    ap.add_argument("--cpu-rehearsal", action="store_true",
+                    help="CPU + gloo, a torch stand-in for the kernel: exercises the multi-rank machinery "
+                         "(chunk sweep, exchange, parity, CPU baseline); prints no value")
     ap.add_argument("--launch-check", action="store_true", help="CPU-only: check the multi-rank launch path")
     ap.add_argument("--fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
     args = ap.parse_args(argv)
     if args.launch_check:
         return launch_check(args)
+    rehearsal = args.cpu_rehearsal
+    if args.workload is None:
+        args.workload = "rehearsal_small" if rehearsal else "target"
+    if rehearsal and (args.graph or args.host_out or args.unroll or args.nt >= 0):
+        raise SystemExit("--cpu-rehearsal runs the plain step only")
 
     import numpy as np
     import torch
@@ -525,11 +594,15 @@ def main(argv=None):
     # Rehearsal knobs (a 1-GPU box): FEDAVG_DIST_BACKEND=gloo and
     # FEDAVG_SAME_DEVICE=1 run N ranks on cuda:0.  The driver's runs use the
     # defaults: RCCL ("nccl") with one GPU per rank.
-    backend = os.environ.get("FEDAVG_DIST_BACKEND", "nccl")
-    dev_index = 0 if os.environ.get("FEDAVG_SAME_DEVICE") == "1" else local_rank
-    torch.cuda.set_device(dev_index)
-    dev = torch.device("cuda", dev_index)
+    backend = "gloo" if rehearsal else os.environ.get("FEDAVG_DIST_BACKEND", "nccl")
+    if rehearsal:
+        dev = torch.device("cpu")
+    else:
+        dev_index = 0 if os.environ.get("FEDAVG_SAME_DEVICE") == "1" else local_rank
+        torch.cuda.set_device(dev_index)
+        dev = torch.device("cuda", dev_index)
     use_pg = world > 1 or args.force_gather
+    cpu_group = None
     if use_pg:
         if world == 1:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -538,9 +611,19 @@ def main(argv=None):
             os.environ.setdefault("WORLD_SIZE", "1")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
+            if world > 1:
+                # the other ranks wait on a host-side (gloo) barrier while rank 0
+                # times the CPU baseline after the timed region: no collective
+                # kernel spins on the GPUs meanwhile
+                try:
+                    cpu_group = dist.new_group(backend="gloo", timeout=datetime.timedelta(minutes=30))
+                except Exception as e:  # noqa: BLE001 -- the default group's barrier still works
+                    print(f"[bench] gloo side group unavailable ({type(e).__name__}: {e}); "
+                          f"the CPU-baseline wait uses the RCCL barrier", file=sys.stderr, flush=True)
         else:
-            dist.init_process_group(backend)
-    mfl_amd._lib.load()
+            dist.init_process_group(backend, timeout=datetime.timedelta(minutes=30))
+    if not rehearsal:
+        mfl_amd._lib.load()
 
     K, P_w, desc = WORKLOADS[args.workload]
     P_global = P_w if args.scaling == "strong" else P_w * world
@@ -550,7 +633,7 @@ def main(argv=None):
             raise SystemExit("--shard-of is a single-GPU rehearsal without exchange")
         plan_world = args.shard_of
     shard_cols = -(-P_global // plan_world)
-    chunks = args.chunks or auto_chunks(K, shard_cols, plan_world, args.host_out)
+    rule_chunks = auto_chunks(K, shard_cols, plan_world, args.host_out)
 
     # single-GPU workloads larger than the row budget: P-chunked passes
     passes = 1
@@ -564,12 +647,44 @@ def main(argv=None):
 
     host_out = torch.empty(P_pass, dtype=torch.float32, pin_memory=True) if args.host_out else None
     gather = False if args.no_gather else (True if args.force_gather else None)
-    red = ShardedReducer(K, P_pass, chunks=chunks, device=dev, gather=gather, host_out=host_out,
-                         as_rank=(plan_world, 0) if plan_world != world else None)
-    synthetic.fill_rows(red.clients, red.plan.local_segments())
     counts = synthetic.sample_counts(K)
     weights = mfl_amd.sample_weights(counts)
-    w_dev = mfl_amd.weights_tensor(weights, torch.float32, dev)
+    w_dev = (torch.tensor(np.array(weights, np.float64).astype(np.float32)) if rehearsal
+             else mfl_amd.weights_tensor(weights, torch.float32, dev))
+
+    def make_reducer(chunks):
+        red = ShardedReducer(K, P_pass, chunks=chunks, device=dev, gather=gather, host_out=host_out,
+                             as_rank=(plan_world, 0) if plan_world != world else None,
+                             local_reduce=_rehearsal_reduce if rehearsal else None)
+        synthetic.fill_rows(red.clients, red.plan.local_segments())
+        return red
+
+    # N > 1 with the exchange: the pipeline depth is the one whose whole step
+    # (reduce + overlapped all-gather) is fastest, timed here in the warm-up on
+    # this node (the kernel-band rule optimises the reduce alone, and the
+    # strong-scaled N = 8 step is bound by the gather)
+    chunk_sweep = None
+    sweeping = (world > 1 and args.chunks == 0 and not args.no_chunk_sweep and not args.no_gather
+                and not args.host_out and passes == 1)
+    if sweeping:
+        cands = chunk_candidates(P_global, world, rule_chunks)
+        sweep_steps = max(5, min(args.steps, 20))
+        ms = {}
+        for c in cands:
+            red = make_reducer(c)
+            for _ in range(max(2, args.warmup)):
+                red.step(w_dev)
+            ms[c] = timed_steps(lambda: red.step(w_dev), sweep_steps, dev, use_pg) / sweep_steps * 1e3
+            del red
+            if dev.type == "cuda":
+                torch.cuda.empty_cache()
+        chunks = min(ms, key=ms.get)
+        chunk_sweep = {"step_ms": {str(c): round(v, 4) for c, v in ms.items()}, "chosen": chunks,
+                       "rule_choice": rule_chunks, "steps_per_candidate": sweep_steps,
+                       "timing": "warm-up, per candidate: barrier + sync, then the steps, max over ranks"}
+    else:
+        chunks = args.chunks or rule_chunks
+    red = make_reducer(chunks)
 
     tuned = None
     if args.unroll or args.nt >= 0:
@@ -577,7 +692,7 @@ def main(argv=None):
 
     S = red.plan.block
     ld = red.clients.stride(0)
-    sched = mfl_amd._lib.f32_schedule(K, S, ld) if tuned is None else None
+    sched = mfl_amd._lib.f32_schedule(K, S, ld) if tuned is None and not rehearsal else None
     launches_per_call = sched["launches"] if sched else 1
     ev_pairs = []
 
@@ -593,17 +708,19 @@ def main(argv=None):
     bytes_call_est = algorithmic_bytes(K, red.plan.block)
     sample_every = 1 if bytes_call_est >= 1e9 else (4 if bytes_call_est >= 2.5e8 else 8)
     n_calls = args.steps * red.plan.chunks * passes
-    pool = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-            for _ in range(-(-n_calls // sample_every))]
-    for a, b in pool:
-        a.record()
-        b.record()
-    torch.cuda.synchronize()
+    pool = []
+    if not rehearsal:
+        pool = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                for _ in range(-(-n_calls // sample_every))]
+        for a, b in pool:
+            a.record()
+            b.record()
+    _sync(dev)
     call_no = [0]
     timing_on = [False]
 
     def timing(c):
-        if not timing_on[0]:
+        if not timing_on[0] or rehearsal:
             return None
         i = call_no[0]
         call_no[0] += 1
@@ -644,10 +761,7 @@ def main(argv=None):
 
     for _ in range(args.warmup):
         red_step(w_dev)
-    torch.cuda.synchronize()
-    if use_pg:
-        dist.barrier()
-    torch.cuda.synchronize()
+    _sync(dev)
 
     step = lambda: red_step(w_dev)  # noqa: E731
     if args.graph:
@@ -683,25 +797,22 @@ def main(argv=None):
     else:
         timing_on[0] = True
         calls_per_event = 1
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if use_pg:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    elapsed_max = timed_steps(step, args.steps, dev, use_pg)
     timing_on[0] = False
 
     kernel_ms = [s.elapsed_time(e) / calls_per_event for s, e in ev_pairs]
-    t = torch.tensor([elapsed, float(np.mean(kernel_ms))], dtype=torch.float64, device=dev)
-    if use_pg:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed_max, kernel_ms_max = float(t[0]), float(t[1])
+    kernel_ms_max = float("nan")
+    if kernel_ms:
+        t = torch.tensor([float(np.mean(kernel_ms))], dtype=torch.float64, device=dev)
+        if use_pg:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        kernel_ms_max = float(t[0])
 
     diagnostics = None
     if world > 1 and red.gather:
         diagnostics = overlap_diagnostics(red, w_dev, args.steps, elapsed_max)
+        if chunk_sweep is not None:
+            diagnostics["chunk_sweep"] = chunk_sweep
 
     parity = sampled_parity(red, weights, passes=passes, pass_cols=red.plan.local_cols if passes > 1 else 0)
     if red.gather:
@@ -719,50 +830,10 @@ def main(argv=None):
             P_done = red.plan.valid_local_cols()  # the one shard this GPU reduced
         bytes_step = algorithmic_bytes(K, P_done)
         value = bytes_step * args.steps / elapsed_max / 1e9
-        # one reduce call = one chunk of one rank's shard = `launches_per_call`
-        # round-split kernel launches of equal size
-        bytes_call = algorithmic_bytes(K, S)
-        achieved = bytes_call / (kernel_ms_max * 1e-3) / 1e9
-        if sched:
-            kname = f"{sched['kernel']}<U={sched['unroll']},C={sched['cols']},nt={min(1, sched['nontemporal'])}"
-            if sched.get("block", 256) != 256:
-                kname += f",B={sched['block']}"
-            kname += f"> (exact, sequential client order; round-split x{launches_per_call})"
-        else:
-            kname = f"tuned variant {tuned}"
-        roofline = {
-            "bound": "hbm",
-            "achieved": round(achieved, 1),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": None,
-            "kernel": kname,
-            "bytes_per_launch": bytes_call // launches_per_call,
-            "avg_launch_ms": round(kernel_ms_max / launches_per_call, 4),
-            "launches": len(kernel_ms) * calls_per_event * launches_per_call,
-            "timing": ("hipGraph replay bracketed by events" if args.graph else
-                       ("hipEventRecord pairs around" if tuned is not None else
-                        "launch-attached HIP events (hipExtLaunchKernel) on the launch stream of")
-                       + (" every reduce call" if sample_every == 1 else f" every {sample_every}th reduce call")
-                       + " of the timed region"),
-        }
-        tj = args.traffic_json or str(ROOT / "profiles" / f"traffic_{args.workload}.json")
-        if Path(tj).exists():
-            try:
-                tr = json.loads(Path(tj).read_text())
-                src = os.path.relpath(tj, ROOT)
-                if tr.get("algorithmic_bytes_per_launch") == roofline["bytes_per_launch"]:
-                    roofline["traffic"] = tr.get("hbm_bytes_per_launch")
-                    roofline["traffic_source"] = src
-                elif tr.get("traffic_over_algorithmic"):
-                    # other launch geometry (e.g. N > 1: chunks per rank): the PMC
-                    # traffic/algorithmic ratio of the same kernel, applied to this launch
-                    ratio = float(tr["traffic_over_algorithmic"])
-                    roofline["traffic"] = int(round(ratio * roofline["bytes_per_launch"]))
-                    roofline["traffic_source"] = f"{src} (PMC ratio {ratio} x this launch's algorithmic bytes)"
-            except (ValueError, OSError, KeyError):
-                pass
+        roofline = None
+        if not rehearsal:
+            roofline = roofline_entry(args, K, S, kernel_ms_max, launches_per_call, sched, tuned, sample_every,
+                                      len(kernel_ms) * calls_per_event * launches_per_call, world)
         if red.gather:
             exchange = ("rccl" if backend == "nccl" else backend) + " all_gather_into_tensor, overlapped per chunk"
         elif host_out is not None:
@@ -776,6 +847,8 @@ def main(argv=None):
             "P_per_gpu": red.plan.valid_local_cols() * passes,
             "scaling_mode": args.scaling,
             "chunks": red.plan.chunks,
+            "chunks_from": ("warm-up step sweep (diagnostics.chunk_sweep)" if chunk_sweep is not None else
+                            ("--chunks" if args.chunks else "kernel-band rule (bench.auto_chunks)")),
             "chunk_cols": S,
             "exchange": exchange,
             "parallelism": f"p-shard{world}",
@@ -812,21 +885,112 @@ def main(argv=None):
             "step_frac_of_node_hbm": round(value / (world * HBM_PEAK_GBS), 4),
             "parity": parity,
         }
+        if rehearsal:
+            out["rehearsal"] = ("CPU + gloo with a torch stand-in for the HIP kernel: exercises the multi-rank "
+                                "machinery only; NOT a measurement")
+            out["rehearsal_value"] = out["value"]
+            out["value"] = None
+            out["dtype"] = "f32"
         if diagnostics is not None:
             out["diagnostics"] = diagnostics
-        if world == 1 and passes == 1 and plan_world == 1 and K <= 512 and red.plan.chunks == 1:
+        if (not rehearsal and world == 1 and passes == 1 and plan_world == 1 and K <= 512
+                and red.plan.chunks == 1):
             try:  # a side measurement: never the reason the bench line is missing
                 out["round_with_distances"] = fused_round(red, w_dev)
             except Exception as e:  # noqa: BLE001
                 out["round_with_distances"] = {"error": f"{type(e).__name__}: {e}"}
-        if world == 1 and not args.no_cpu_baseline:
-            # the workload's own K x P while its rows fit a bounded host sample
+        if not args.no_cpu_baseline:
+            # at every N, on rank 0 after the timed region and the parity
+            # checks (the other ranks wait at the barrier below): the
+            # workload's own K x P while its rows fit a bounded host sample
             # (<= 10 GB: the target); cfg5's 400 GB is timed on a P-slice
-            out["cpu_baseline"] = cpu_baseline(K, min(P_global, 10_000_000_000 // (4 * K)))
+            try:
+                if rehearsal:
+                    out["cpu_baseline"] = cpu_baseline(K, P_global, flat_seconds=0.2, model_seconds=0.2,
+                                                       model="mnist_lr")
+                else:
+                    out["cpu_baseline"] = cpu_baseline(K, min(P_global, 10_000_000_000 // (4 * K)))
+                out["cpu_baseline"]["n_gpus_in_run"] = world
+            except Exception as e:  # noqa: BLE001 -- never the reason the bench line is missing
+                out["cpu_baseline"] = {"error": f"{type(e).__name__}: {e}"}
         print(json.dumps(out), flush=True)
     if use_pg:
-        dist.barrier()
+        # the ranks leave together once rank 0 has printed (a host-side barrier
+        # when the gloo side group exists: rank 0's CPU baseline runs 10-30 s)
+        dist.barrier(group=cpu_group)
         dist.destroy_process_group()
+
+
+def roofline_entry(args, K, S, kernel_ms_max, launches_per_call, sched, tuned, sample_every, launches, world):
+    """The dominant kernel's algorithmic bytes per launch over its average
+    launch time (launch-attached HIP events), with the PMC traffic of the
+    same launch shape when profiles/ holds it."""
+    bytes_call = algorithmic_bytes(K, S)
+    achieved = bytes_call / (kernel_ms_max * 1e-3) / 1e9
+    if sched:
+        kname = f"{sched['kernel']}<U={sched['unroll']},C={sched['cols']},nt={min(1, sched['nontemporal'])}"
+        if sched.get("block", 256) != 256:
+            kname += f",B={sched['block']}"
+        kname += f"> (exact, sequential client order; round-split x{launches_per_call})"
+    else:
+        kname = f"tuned variant {tuned}"
+    roofline = {
+        "bound": "hbm",
+        "achieved": round(achieved, 1),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "traffic": None,
+        "kernel": kname,
+        "bytes_per_launch": bytes_call // launches_per_call,
+        "avg_launch_ms": round(kernel_ms_max / launches_per_call, 4),
+        "launches": launches,
+        "timing": ("hipGraph replay bracketed by events" if args.graph else
+                   ("hipEventRecord pairs around" if tuned is not None else
+                    "launch-attached HIP events (hipExtLaunchKernel) on the launch stream of")
+                   + (" every reduce call" if sample_every == 1 else f" every {sample_every}th reduce call")
+                   + " of the timed region"),
+    }
+    attach_traffic(roofline, args, world)
+    return roofline
+
+
+def attach_traffic(roofline: dict, args, world: int) -> None:
+    """PMC traffic for this launch shape: the summaries under profiles/ hold
+    per-launch HBM bytes for the launch geometries they were collected on
+    (``traffic_<workload>.json`` at N = 1, ``traffic_<workload>_shard<N>.json``
+    for one rank of an N-GPU plan, optionally a ``launches`` list).  An exact
+    geometry match gives the measured bytes; otherwise the same kernel's PMC
+    traffic/algorithmic ratio is applied to this launch and labelled so."""
+    n = args.shard_of if args.shard_of > 1 else world
+    cands = [args.traffic_json] if args.traffic_json else []
+    if n > 1:
+        cands.append(str(ROOT / "profiles" / f"traffic_{args.workload}_shard{n}.json"))
+    cands.append(str(ROOT / "profiles" / f"traffic_{args.workload}.json"))
+    entries = []
+    for tj in cands:
+        if not Path(tj).exists():
+            continue
+        try:
+            tr = json.loads(Path(tj).read_text())
+        except (ValueError, OSError):
+            continue
+        src = os.path.relpath(tj, ROOT)
+        for e in [tr, *tr.get("launches", [])]:
+            if "algorithmic_bytes_per_launch" in e:
+                entries.append((src, e))
+    for src, e in entries:
+        if e.get("algorithmic_bytes_per_launch") == roofline["bytes_per_launch"] and e.get("hbm_bytes_per_launch"):
+            roofline["traffic"] = int(e["hbm_bytes_per_launch"])
+            roofline["traffic_source"] = f"{src} (PMC, this launch shape)"
+            return
+    for src, e in entries:
+        if e.get("traffic_over_algorithmic"):
+            ratio = float(e["traffic_over_algorithmic"])
+            roofline["traffic"] = int(round(ratio * roofline["bytes_per_launch"]))
+            roofline["traffic_source"] = (f"{src} (PMC ratio {ratio} of a {e['algorithmic_bytes_per_launch']}-B launch "
+                                          f"x this launch's algorithmic bytes; not this geometry)")
+            return
 
 
 def side_bench(argv) -> bool:

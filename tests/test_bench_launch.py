@@ -181,3 +181,55 @@ def test_as_rank_plans_one_shard_of_a_larger_world():
             assert red.plan.local_segments() == plan_shards(P, N, r, chunks).local_segments()
     with pytest.raises(ValueError):
         ShardedReducer(4, 100, device="cpu", local_reduce=_torch_loop_reduce, as_rank=(2, 0), gather=True)
+
+
+@pytest.mark.parametrize("n", [2, 8])
+def test_cpu_rehearsal_line_has_chunk_sweep_and_cpu_baseline(n):
+    """``bench.py --gpus N --cpu-rehearsal``: the whole N > 1 bench path on CPU
+    with gloo (a torch stand-in for the kernel).  Rank 0's one JSON line
+    carries the warm-up chunk sweep (the chosen depth is the fastest step of
+    the candidates), the parity checks of the gathered model, and the CPU
+    baseline timed on rank 0 after the timed region while the other ranks
+    wait -- the same line the driver's N-GPU run prints."""
+    r = _run_bench("--gpus", str(n), "--cpu-rehearsal", "--steps", "2", "--warmup", "1", timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == n and out["value"] is None and "NOT a measurement" in out["rehearsal"]
+    sweep = out["diagnostics"]["chunk_sweep"]
+    ms = {int(c): v for c, v in sweep["step_ms"].items()}
+    assert sweep["chosen"] == min(ms, key=ms.get) == out["config"]["chunks"]
+    assert sweep["rule_choice"] in ms and len(ms) >= 2
+    assert out["config"]["chunks_from"].startswith("warm-up step sweep")
+    assert out["parity"]["ok"] and out["parity"]["ranks"] == n and out["parity"]["reassembly_checksums_ok"]
+    cb = out["cpu_baseline"]
+    assert cb["value"] > 0 and cb["n_gpus_in_run"] == n and cb["value_at_share"] > 0
+    assert {lay["layout"] for lay in cb["layouts"]} >= {"flat", "model-shaped (mnist_lr)"}
+
+
+def test_chunk_candidates():
+    # the target at N = 8: 1/2/4/8 chunks of rank 0's 3.125M columns, incl. the rule's 2
+    assert bench.chunk_candidates(25_000_000, 8, 2) == [1, 2, 4, 8]
+    # a tiny shard: only depths whose chunks keep >= SWEEP_MIN_BLOCK columns (and the rule's pick)
+    assert bench.chunk_candidates(10_000, 8, 1) == [1]
+
+
+def test_attach_traffic_exact_shape_then_ratio(tmp_path):
+    """The PMC traffic of the launch shape when a summary holds it (N-GPU
+    shard files may list several chunk geometries), else the kernel's PMC
+    ratio applied and labelled as another geometry."""
+    import types
+    f = tmp_path / "t.json"
+    f.write_text(json.dumps({"algorithmic_bytes_per_launch": 1000, "hbm_bytes_per_launch": 1010,
+                             "traffic_over_algorithmic": 1.01,
+                             "launches": [{"algorithmic_bytes_per_launch": 500, "hbm_bytes_per_launch": 501,
+                                           "traffic_over_algorithmic": 1.002}]}))
+    args = types.SimpleNamespace(traffic_json=str(f), shard_of=0, workload="none")
+    for b, exp in ((1000, 1010), (500, 501)):
+        rf = {"bytes_per_launch": b}
+        bench.attach_traffic(rf, args, world=8)
+        assert rf["traffic"] == exp and "this launch shape" in rf["traffic_source"]
+    rf = {"bytes_per_launch": 2000}
+    bench.attach_traffic(rf, args, world=8)
+    assert rf["traffic"] == 2020 and "not this geometry" in rf["traffic_source"]
