@@ -1005,6 +1005,12 @@ def install(trainer_cls, device: Optional[torch.device] = None, client_cls=None,
 
         client_cls = getattr(sys.modules.get(trainer_cls.__module__), "Client", None)
     streaming = bool(stream_clients) and client_cls is not None and hasattr(trainer_cls, "train")
+    # install() may run again (another device, streaming switched off): the
+    # wrappers below are installed once and read these per-class settings on
+    # every call, so a later install(stream_clients=False) stops the feed
+    # instead of leaving wrappers that upload clients nobody reduces
+    trainer_cls._mfl_stream_on = streaming
+    trainer_cls._mfl_stream_device = device
 
     def aggregate_method(self, w_locals):
         feed = self.__dict__.get("_mfl_feed") if streaming else None
@@ -1022,6 +1028,8 @@ def install(trainer_cls, device: Optional[torch.device] = None, client_cls=None,
     loop = trainer_cls.train
 
     def train_method(self, *args, **kwargs):  # fedavg_trainer.py:95, the round loop
+        if not getattr(type(self), "_mfl_stream_on", False):
+            return loop(self, *args, **kwargs)
         with autostream.trainer_scope(self):
             return loop(self, *args, **kwargs)
 
@@ -1035,8 +1043,18 @@ def install(trainer_cls, device: Optional[torch.device] = None, client_cls=None,
         def client_train_method(self, *args, **kwargs):  # client.py:38
             res = client_train(self, *args, **kwargs)
             trainer = autostream.active_trainer()
-            if trainer is not None and autostream.valid_train_result(res):  # fedavg_trainer.py:190
-                _feed_of(trainer, device).feed(self.get_sample_number(), res[0])
+            if trainer is None or not getattr(type(trainer), "_mfl_stream_on", False):
+                return res
+            if getattr(type(self), "train", None) is not client_train_method:
+                # a Client subclass overrides train() (and reached this one
+                # through super()): what it returns to the loop may differ
+                # from `res` -- nothing of this round is streamed
+                _feed_of(trainer, getattr(type(trainer), "_mfl_stream_device", None)).refuse(
+                    "Client.train is overridden by a subclass")
+                return res
+            if autostream.valid_train_result(res):  # fedavg_trainer.py:190
+                _feed_of(trainer, getattr(type(trainer), "_mfl_stream_device", None)).feed(
+                    self.get_sample_number(), res[0])
             return res
 
         client_train_method.__doc__ = client_train.__doc__

@@ -19,21 +19,39 @@ path (178.8 ms).
   (``RoundSession.add``) while the loop deep-copies it (:199) and the next
   client trains;
 * the patched ``aggregate(w_locals)`` waits for the feed to drain, checks
-  that ``w_locals`` is what was fed -- same count, the same sample numbers in
-  order, the same key set, and bit-identical values at sampled positions of
-  the largest and a middle key (compared while the reduce runs) -- and
-  then only the weights, the kernel and the result's D2H remain.
+  that ``w_locals`` is what was fed and then only the weights, the kernel
+  and the result's D2H remain.  The check (``fedavg_collect_ext.verify_rows``,
+  one native walk while the reduce runs): the same count and sample numbers
+  in order, distinct dicts, every client's keys in the table's order with
+  the table's dtypes and shapes, and element values at ~4,096 (client, key,
+  position) probes drawn afresh every round -- every key at least once, the
+  rest uniform over clients and keys -- against the pinned staging rows the
+  GPU reduces (converted as the packer converts).  A fixed pattern of
+  positions cannot miss an edit every round; an edit of one element of one
+  client can still go unseen in a given round (sampling), which is why the
+  structural guards below keep known editors out of the stream.
 
 Anything else falls back to the plain drop-in on ``w_locals`` (same bits,
 the reference's exceptions): a count or sample-number mismatch, a retried
 client the loop did not append, a key-table change, device-resident
 clients, more clients than the trainer's ``client_list``, any error inside
-the feed, or ``FEDAVG_STREAM_CLIENTS=0``.
+the feed, a Client subclass that overrides ``train`` (it may change what it
+returns after the wrapped reference method fed it), a client tensor whose
+version counter moved while the worker packed it (a ``Client.train`` that
+returns tensors the next client's training updates in place; the
+reference's returns a fresh deep copy, client.py:96 / fedavg_trainer.py:189),
+or ``FEDAVG_STREAM_CLIENTS=0``.
+
+Contract for Client.train implementations under streaming: the returned
+state_dict's tensors must not change after train() returns -- the reference
+(``net.cpu().state_dict()`` of a per-call ``copy.deepcopy`` of the global
+model) keeps it.
 """
 from __future__ import annotations
 
 import os
 import queue
+import random
 import threading
 import time
 from typing import Optional
@@ -83,18 +101,6 @@ class trainer_scope:
         return False
 
 
-def _bits(t: torch.Tensor):
-    """The elements of a host tensor as a flat integer numpy view (bit patterns)."""
-    size = t.element_size()
-    ity = {1: torch.uint8, 2: torch.int16, 4: torch.int32, 8: torch.int64}[size]
-    flat = t.reshape(-1)
-    if t.dtype == torch.bool:
-        flat = flat.view(torch.uint8)
-    elif t.dtype != ity:
-        flat = flat.view(ity)
-    return flat.numpy()
-
-
 class _Release(list):
     """Host tensors a finished round displaced, for the feed worker to drop."""
 
@@ -103,7 +109,8 @@ class ClientFeed:
     """One trainer's streaming state: at most one open ``RoundSession`` (the
     round being fed), filled by a background thread."""
 
-    SAMPLE_KEYS = 2  # keys compared per client (the largest and the middle one)
+    VERIFY_PROBES = 4096  # (client, key) pairs whose values are compared per round (two positions each)
+    VERIFY_FULL_ELEMS = 1 << 20  # rounds of at most this many elements (K x P) are compared in full
 
     def __init__(self, aggregator_fn, max_clients: int):
         self._aggregator_fn = aggregator_fn  # () -> DeviceAggregator (created lazily, on first use)
@@ -112,8 +119,7 @@ class ClientFeed:
         self.broken = False
         self._small = False  # this round fits SMALL_ROUND_BYTES: left to the plain path
         self.fed = []  # sample numbers in feed order
-        self._prints = []  # per fed client: what _compare checks (worker-made, see _fingerprint)
-        self._picks = ([], {})
+        self._vplan = None  # verify_rows' table arrays for the open session (worker-made)
         self._graveyard = []  # _Release lists waiting for the next round (worker thread only)
         self._q: Optional[queue.Queue] = None
         self._worker: Optional[threading.Thread] = None
@@ -145,7 +151,15 @@ class ClientFeed:
             self._worker = threading.Thread(target=self._run, name="mfl-client-feed", daemon=True)
             self._worker.start()
         self._t_fed = time.perf_counter()
-        self._q.put((sample_num, state_dict))
+        # version counters now, before the loop trains the next client: the
+        # worker re-reads them after packing (an in-place update meanwhile
+        # means the packed row may mix two states)
+        self._q.put((sample_num, state_dict, [v._version for v in state_dict.values()]))
+
+    def refuse(self, why: str) -> None:
+        """This round is not streamed (the plain drop-in runs at :217)."""
+        if not self._small:
+            self._break(why)
 
     @staticmethod
     def _row_bytes(sd) -> int:
@@ -178,18 +192,19 @@ class ClientFeed:
             t0 = time.perf_counter()
             try:
                 if not self.broken and self._err is None:
-                    n, sd = item
+                    n, sd, vers = item
                     if self.session is None:
                         self.session = self._aggregator_fn().begin_round(sd, self.max_clients)
                         self.session.keep_dicts = False
                         self.session.defer_release = self._defer_release
-                        self._picks = self._sample_plan(sd)
+                        self._vplan = self._verify_plan(self.session)
                     self.session.add(n, sd)
-                    self._prints.append(self._fingerprint(sd))
+                    if [v._version for v in sd.values()] != vers:
+                        raise RuntimeError("a client's tensors changed while they were packed")
             except BaseException as e:  # noqa: BLE001 -- any failure means: fall back at aggregate
                 self._err = e
             finally:
-                item = n = sd = None  # drop the client's tensors now (the loop holds its own copy)
+                item = n = sd = vers = None  # drop the client's tensors now (the loop holds its own copy)
                 t1 = time.perf_counter()
                 self._add_ms.append((t1 - t0) * 1e3)
                 self._t_done = t1
@@ -235,7 +250,8 @@ class ClientFeed:
             self.stats["last_round"]["finish_ms"] = (time.perf_counter() - t_f) * 1e3
             self.stats["last_round"]["finish_profile"] = dict(getattr(sess, "finish_profile", {}))
             if out is None:
-                self.stats["last_fallback"] = "sampled values differ from the fed clients"
+                self.stats["last_fallback"] = ("w_locals differs from the fed clients (verify_rows status "
+                                               f"{self.stats.get('last_verify', {}).get('status')})")
                 self.stats["rounds_fallback"] += 1
             else:
                 self.stats["rounds_streamed"] += 1
@@ -248,62 +264,47 @@ class ClientFeed:
             return self.stats["last_fallback"] or "feed broken"
         if self._err is not None:
             return f"feed error: {self._err!r}"
-        if sess is None:
+        if sess is None or self._vplan is None:
             return "nothing fed"
         if type(w_locals) is not list or len(w_locals) != len(self.fed) or len(sess.counts) != len(self.fed):
             return "client count differs from the fed clients"
         for (n, _), n2 in zip(w_locals, self.fed):
             if n != n2:
                 return "sample numbers differ from the fed clients"
-        if len(self._prints) != len(self.fed):
-            return "a fed client was not recorded"
         return ""
 
-    def _same_values(self, w_locals) -> bool:
-        """Key sets equal and sampled element bits equal, client by client.
-        Never raises (it runs while the round's GPU work is in flight)."""
-        try:
-            return self._compare(w_locals)
-        except Exception:  # noqa: BLE001 -- anything unexpected: not the fed round
-            return False
+    @staticmethod
+    def _verify_plan(sess):
+        """verify_rows' arrays for a session: the key table (names, meta
+        templates, dtype group, offset and packer kind per key) and each
+        group's pinned staging rows (what the H2D copies upload)."""
+        from .layout import _PACK_KIND, _collect_ext
 
-    def _sample_plan(self, sd):
-        """(keys, {key: positions}) compared per client: the largest and the
-        middle key with at least one element, five positions each."""
-        names = [k for k in sd.keys() if sd[k].numel() > 0]
-        if not names:
-            return list(sd), {}
-        big = max(names, key=lambda k: sd[k].numel())
-        picks = list(dict.fromkeys([big, names[len(names) // 2]]))[:self.SAMPLE_KEYS]
-        pos = {}
-        for k in picks:
-            n = sd[k].numel()
-            pos[k] = sorted({0, n - 1, n // 2, (n * 7) // 13, (n * 5) // 11})
-        return list(sd), pos
-
-    def _fingerprint(self, sd):
-        """What ``_compare`` checks of one fed client, taken when it was fed:
-        its key tuple and, per sampled key, (dtype, shape, element bits)."""
-        keys, pos = self._picks
-        if list(sd) != keys:
+        ext = _collect_ext()
+        if ext is None or not hasattr(ext, "verify_rows"):
             return None
-        return {k: (sd[k].dtype, tuple(sd[k].shape), _bits(sd[k])[p].copy()) for k, p in pos.items()}
+        table = sess.table
+        gidx = {dt: k for k, dt in enumerate(table.groups)}
+        stag = [sess._staging[dt].host for dt in table.groups]
+        return (ext, [e.name for e in table.entries],
+                table.meta_template(),
+                [gidx[e.dtype] for e in table.entries], [int(e.offset) for e in table.entries],
+                [0 if e.src_dtype == e.dtype else _PACK_KIND[e.src_dtype] for e in table.entries],
+                [t.data_ptr() for t in stag], [int(t.stride(0)) for t in stag], [t.element_size() for t in stag])
 
-    def _compare(self, w_locals) -> bool:
-        keys, pos = self._picks
-        if not pos:
+    def _same_values(self, w_locals) -> bool:
+        """``verify_rows`` (module docstring).  Never raises: it runs while the
+        round's GPU work is in flight, and anything unexpected means the
+        round is not the fed one."""
+        try:
+            ext, names, templ, group, offset, kind, sptr, sld, ses = self._vplan
+            st = ext.verify_rows(w_locals, list(self.fed), names, templ, group, offset, kind, sptr, sld, ses,
+                                 self.VERIFY_PROBES, random.getrandbits(64), self.VERIFY_FULL_ELEMS)
+            self.stats["last_verify"] = {"status": int(st[0]), "client": int(st[1]), "key": int(st[2]),
+                                         "probes": int(st[3])}
+            return st[0] == 0
+        except Exception:  # noqa: BLE001
             return False
-        for (_, sd), fp in zip(w_locals, self._prints):
-            if fp is None or list(sd) != keys:
-                return False
-            for k, p in pos.items():
-                a = sd[k]
-                dt, shape, bits = fp[k]
-                if not isinstance(a, torch.Tensor) or a.dtype != dt or tuple(a.shape) != shape or a.is_cuda:
-                    return False
-                if not (_bits(a)[p] == bits).all():
-                    return False
-        return True
 
     def _reset(self):
         sess = self.session
@@ -311,7 +312,7 @@ class ClientFeed:
             sess.abandon()
         self.session = None
         self.fed = []
-        self._prints = []
+        self._vplan = None
         self.broken = self._small = False
         self._err = None
         self._add_ms = []

@@ -92,7 +92,7 @@ def build_collect_ext(force: bool = False, verbose: bool = False) -> Path:
 
     LIB_DIR.mkdir(parents=True, exist_ok=True)
     load(name=COLLECT_NAME, sources=[str(CSRC_COLLECT)], build_directory=str(LIB_DIR),
-         extra_cflags=["-O2"], verbose=verbose)
+         extra_cflags=["-O2", "-fopenmp"], extra_ldflags=["-fopenmp"], verbose=verbose)
     return out
 
 

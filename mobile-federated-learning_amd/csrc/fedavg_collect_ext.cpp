@@ -16,6 +16,8 @@
 #include <torch/csrc/autograd/python_variable.h>
 #include <torch/extension.h>
 
+#include <algorithm>
+#include <cstring>
 #include <vector>
 
 #include <pybind11/stl.h>
@@ -35,28 +37,82 @@ static py::tuple collect(py::list dicts, py::list names, py::list templ, int64_t
     sizes[j] = ten.sizes().vec();
     dtypes[j] = ten.scalar_type();
   }
-  auto ptrs = torch::empty({static_cast<int64_t>(K), static_cast<int64_t>(N)}, torch::kInt64);
-  int64_t* out = ptrs.data_ptr<int64_t>();
+  // pass 1 (GIL): the value objects, [K][N].  A dict whose entries are the
+  // names in order (the deep copies of :199 share client 0's key strings) is
+  // read by PyDict_Next with identity compares; anything else by lookups,
+  // whose new references are held until the end
+  std::vector<PyObject*> vals(static_cast<size_t>(K) * N);
+  std::vector<PyObject*> owned;
+  auto release = [&owned] {
+    for (PyObject* o : owned) Py_DECREF(o);
+    owned.clear();
+  };
   for (Py_ssize_t i = 0; i < K; ++i) {
     PyObject* d = PyList_GET_ITEM(dicts.ptr(), i);
-    for (Py_ssize_t j = 0; j < N; ++j) {
-      PyObject* t = PyObject_GetItem(d, PyList_GET_ITEM(names.ptr(), j));  // new reference
-      if (!t) {
-        PyErr_Clear();
-        return py::make_tuple(py::none(), i, j);
+    PyObject** row = &vals[static_cast<size_t>(i) * N];
+    bool fast = PyDict_Check(d) && PyDict_Size(d) == N;
+    if (fast) {
+      Py_ssize_t pos = 0, j = 0;
+      PyObject *key, *val;
+      while (PyDict_Next(d, &pos, &key, &val)) {
+        if (j >= N || key != PyList_GET_ITEM(names.ptr(), j)) {
+          fast = false;
+          break;
+        }
+        row[j++] = val;
+        __builtin_prefetch(val);
       }
-      bool ok = THPVariable_Check(t);
-      if (ok) {
-        const at::Tensor& ten = THPVariable_Unpack(t);
-        const bool where = device_index < 0 ? ten.is_cpu() : (ten.is_cuda() && ten.get_device() == device_index);
-        ok = ten.scalar_type() == dtypes[j] && ten.sizes() == c10::IntArrayRef(sizes[j]) && where &&
-             ten.is_contiguous();
-        if (ok) out[i * N + j] = reinterpret_cast<int64_t>(ten.data_ptr());
+      fast = fast && j == N;
+    }
+    if (!fast) {
+      for (Py_ssize_t j = 0; j < N; ++j) {
+        PyObject* t = PyObject_GetItem(d, PyList_GET_ITEM(names.ptr(), j));  // new reference
+        if (!t) {
+          PyErr_Clear();
+          release();
+          return py::make_tuple(py::none(), i, j);
+        }
+        owned.push_back(t);
+        row[j] = t;
       }
-      Py_DECREF(t);  // the dict keeps the tensor alive
-      if (!ok) return py::make_tuple(py::none(), i, j);
     }
   }
+  // pass 2 (torch's intra-op threads, the GIL held by this thread: no Python
+  // code runs meanwhile and no Python API is called): metadata checks and
+  // data pointers, bound by cache misses on scattered tensor objects
+  auto ptrs = torch::empty({static_cast<int64_t>(K), static_cast<int64_t>(N)}, torch::kInt64);
+  int64_t* out = ptrs.data_ptr<int64_t>();
+  std::vector<int64_t> bad(static_cast<size_t>(K), -1);  // per client: first failing key
+  at::parallel_for(0, K, 1, [&](int64_t i0, int64_t i1) {
+    for (int64_t i = i0; i < i1; ++i) {
+      PyObject* const* row = &vals[static_cast<size_t>(i) * N];
+      constexpr Py_ssize_t kAhead = 8;
+      for (Py_ssize_t j = 0; j < N && j < kAhead; ++j)
+        if (THPVariable_CheckExact(row[j])) __builtin_prefetch(THPVariable_Unpack(row[j]).unsafeGetTensorImpl());
+      for (Py_ssize_t j = 0; j < N; ++j) {
+        if (j + kAhead < N && THPVariable_CheckExact(row[j + kAhead]))
+          __builtin_prefetch(THPVariable_Unpack(row[j + kAhead]).unsafeGetTensorImpl());
+        PyObject* t = row[j];
+        // exact Tensor / Parameter only (no isinstance walk off the GIL
+        // thread): a Tensor subclass goes to the general Python path
+        bool ok = THPVariable_CheckExact(t);
+        if (ok) {
+          const at::Tensor& ten = THPVariable_Unpack(t);
+          const bool where = device_index < 0 ? ten.is_cpu() : (ten.is_cuda() && ten.get_device() == device_index);
+          ok = ten.scalar_type() == dtypes[j] && ten.sizes() == c10::IntArrayRef(sizes[j]) && where &&
+               ten.is_contiguous();
+          if (ok) out[i * N + j] = reinterpret_cast<int64_t>(ten.data_ptr());
+        }
+        if (!ok) {
+          bad[i] = j;
+          break;
+        }
+      }
+    }
+  });
+  release();  // the dicts keep their tensors alive
+  for (Py_ssize_t i = 0; i < K; ++i)
+    if (bad[i] >= 0) return py::make_tuple(py::none(), i, bad[i]);
   return py::make_tuple(ptrs, -1, -1);
 }
 
@@ -68,6 +124,7 @@ static py::list unpack(const at::Tensor& flat, py::list offsets, py::list shapes
   const Py_ssize_t N = PyList_GET_SIZE(offsets.ptr());
   if (PyList_GET_SIZE(shapes.ptr()) != N) throw std::invalid_argument("offsets/shapes length mismatch");
   if (flat.dim() != 1 || !flat.is_contiguous()) throw std::invalid_argument("flat must be a contiguous 1-D tensor");
+  if (flat.requires_grad()) throw std::invalid_argument("unpack: flat must not require grad");
   py::list out(N);
   std::vector<int64_t> size, stride;
   for (Py_ssize_t j = 0; j < N; ++j) {
@@ -83,7 +140,13 @@ static py::list unpack(const at::Tensor& flat, py::list offsets, py::list shapes
       numel *= size[d];
     }
     if (off < 0 || off + numel > flat.numel()) throw std::out_of_range("unpack: key range outside the buffer");
-    out[j] = flat.as_strided(size, stride, flat.storage_offset() + off);
+    // a tensor on flat's storage with this key's sizes and offset, made
+    // directly (as_strided's dispatch costs ~1.4 us a key: 0.5 ms for
+    // resnet56's 350 keys, every round)
+    auto impl = c10::make_intrusive<c10::TensorImpl>(c10::TensorImpl::VIEW, c10::Storage(flat.storage()),
+                                                     flat.key_set(), flat.dtype());
+    impl->set_sizes_and_strides(size, stride, std::make_optional<int64_t>(flat.storage_offset() + off));
+    out[j] = py::reinterpret_steal<py::object>(THPVariable_Wrap(at::Tensor(std::move(impl))));
   }
   return out;
 }
@@ -218,10 +281,223 @@ static py::tuple small_round(py::list w_locals, py::list names, py::list templ, 
   return py::make_tuple(0, out_dev, out_host);
 }
 
+// verify_rows(w_locals, counts, names, templ, group, offset, kind, stage_ptr, stage_ld, stage_esize,
+//             probes, seed) -> (status, client, key, probes_checked)
+//
+// Does w_locals (the reference's :199 deep copies) hold what a streamed
+// round's staging rows were packed from?  autostream.py fed each client's
+// Client.train result to the packer while the loop went on; at :217 this walk
+// checks, with the GIL held,
+//   * len(w_locals) == len(counts) and every w_locals[i] is a (n, dict) pair
+//     whose n == counts[i] (Python ==) and whose dict is not another
+//     client's dict object;
+//   * every client's dict holds exactly the table's keys in order
+//     (PyDict_Next, key identity or ==: the deep copies share the key
+//     strings), and every value is a contiguous host tensor with the
+//     template's dtype and sizes;
+// and then, with the GIL released, compares element values at `probes`
+// (client, key, position) triples drawn afresh from `seed` every round --
+// every key at least once (at a random client), the rest spread uniformly
+// over all (client, key) pairs, positions uniform inside the key -- against
+// the pinned staging rows the H2D copies uploaded, converted as the packer
+// converts (fp32/fp64/fp16/bf16 keys raw, integer/bool keys static_cast to
+// fp32: fedavg_host.cpp).  Equal converted values reduce to the same bits,
+// so a match is exactly the reduction's criterion at that element.
+// Returns probes_checked = elements compared.
+// status 0: all checks passed; 1 count; 2 sample number; 3 not a (n, dict)
+// pair; 4 repeated dict; 5 keys; 6 tensor metadata; 7 value (client, key).
+namespace {
+inline uint64_t mix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+struct Probe {
+  const char* src;
+  const char* dst;
+  int kind;
+  int esize;
+  int i, j;
+};
+
+bool probe_equal(const Probe& p) {
+  if (p.kind == 0) return std::memcmp(p.src, p.dst, static_cast<size_t>(p.esize)) == 0;
+  float v;
+  switch (p.kind) {  // fedavg_pack_item kinds (include/fedavg_amd.h), as fedavg_host.cpp converts
+    case 1: { int64_t s; std::memcpy(&s, p.src, 8); v = static_cast<float>(s); break; }
+    case 2: { int32_t s; std::memcpy(&s, p.src, 4); v = static_cast<float>(s); break; }
+    case 3: { int16_t s; std::memcpy(&s, p.src, 2); v = static_cast<float>(s); break; }
+    case 4: v = static_cast<float>(*reinterpret_cast<const int8_t*>(p.src)); break;
+    case 5: v = static_cast<float>(*reinterpret_cast<const uint8_t*>(p.src)); break;
+    case 6: v = *reinterpret_cast<const uint8_t*>(p.src) ? 1.0f : 0.0f; break;
+    default: return false;
+  }
+  return std::memcmp(&v, p.dst, 4) == 0;
+}
+}  // namespace
+
+static py::tuple verify_rows(py::list w_locals, py::list counts, py::list names, py::list templ,
+                             const std::vector<int64_t>& group, const std::vector<int64_t>& offset,
+                             const std::vector<int64_t>& kind, const std::vector<int64_t>& stage_ptr,
+                             const std::vector<int64_t>& stage_ld, const std::vector<int64_t>& stage_esize,
+                             int64_t probes, uint64_t seed, int64_t full_elems) {
+  const Py_ssize_t K = PyList_GET_SIZE(w_locals.ptr());
+  const Py_ssize_t N = PyList_GET_SIZE(names.ptr());
+  auto res = [](int status, Py_ssize_t i, Py_ssize_t j, int64_t n) { return py::make_tuple(status, i, j, n); };
+  if (K != PyList_GET_SIZE(counts.ptr()) || K == 0) return res(1, -1, -1, 0);
+  if (PyList_GET_SIZE(templ.ptr()) != N || static_cast<Py_ssize_t>(group.size()) != N ||
+      static_cast<Py_ssize_t>(offset.size()) != N || static_cast<Py_ssize_t>(kind.size()) != N)
+    throw std::invalid_argument("verify_rows: table arrays differ in length");
+  std::vector<const at::Tensor*> tp(N);
+  std::vector<int64_t> numel(N);
+  for (Py_ssize_t j = 0; j < N; ++j) {
+    PyObject* t = PyList_GET_ITEM(templ.ptr(), j);
+    if (!THPVariable_Check(t)) throw std::invalid_argument("template entries must be tensors");
+    tp[j] = &THPVariable_Unpack(t);
+    numel[j] = tp[j]->numel();
+    const int64_t g = group[j];
+    if (g < 0 || g >= static_cast<int64_t>(stage_ptr.size())) throw std::invalid_argument("verify_rows: bad group");
+  }
+  // a round of at most full_elems elements (K x the table's elements) is
+  // compared in full, every element of every client; larger ones by probes
+  int64_t row_elems = 0;
+  for (Py_ssize_t j = 0; j < N; ++j) row_elems += numel[j];
+  const bool full = static_cast<int64_t>(K) * row_elems <= full_elems;
+  // probe density: ~`probes` pairs over K x N, plus one anchor client per key
+  const double frac = static_cast<double>(probes) / (static_cast<double>(K) * static_cast<double>(N));
+  const uint64_t thresh = frac >= 1.0 ? ~0ull : static_cast<uint64_t>(frac * 18446744073709551615.0);
+  std::vector<PyObject*> dicts(K);
+  for (Py_ssize_t i = 0; i < K; ++i) {
+    PyObject* pair = PyList_GET_ITEM(w_locals.ptr(), i);
+    if (!PyTuple_Check(pair) || PyTuple_GET_SIZE(pair) != 2) return res(3, i, -1, 0);
+    const int eq = PyObject_RichCompareBool(PyTuple_GET_ITEM(pair, 0), PyList_GET_ITEM(counts.ptr(), i), Py_EQ);
+    if (eq != 1) {
+      if (eq < 0) PyErr_Clear();
+      return res(2, i, -1, 0);
+    }
+    PyObject* d = PyTuple_GET_ITEM(pair, 1);
+    if (!PyDict_Check(d) || PyDict_Size(d) != N) return res(PyDict_Check(d) ? 5 : 3, i, -1, 0);
+    dicts[i] = d;
+  }
+  {
+    std::vector<PyObject*> sorted(dicts);
+    std::sort(sorted.begin(), sorted.end());
+    for (size_t a = 1; a < sorted.size(); ++a)
+      if (sorted[a] == sorted[a - 1]) return res(4, -1, -1, 0);  // the plain path handles aliased clients
+  }
+  // pass 1 (GIL): each dict's entry table in order -- the keys by identity
+  // (the deep copies share the key strings; == otherwise), the values'
+  // object pointers, nothing dereferenced
+  std::vector<PyObject*> vals(static_cast<size_t>(K) * N);
+  for (Py_ssize_t i = 0; i < K; ++i) {
+    Py_ssize_t pos = 0, j = 0;
+    PyObject *key, *val;
+    while (PyDict_Next(dicts[i], &pos, &key, &val)) {
+      if (j >= N) return res(5, i, j, 0);
+      PyObject* name = PyList_GET_ITEM(names.ptr(), j);
+      if (key != name) {
+        const int eq = PyObject_RichCompareBool(key, name, Py_EQ);
+        if (eq != 1) {
+          if (eq < 0) PyErr_Clear();
+          return res(5, i, j, 0);
+        }
+      }
+      vals[static_cast<size_t>(i) * N + j] = val;
+      __builtin_prefetch(val);  // the THPVariable: pass 2 reads its tensor pointer
+      ++j;
+    }
+    if (j != N) return res(5, i, j, 0);
+  }
+  // pass 2 (torch's intra-op threads; the GIL stays with this thread, so no
+  // Python code runs and no object changes meanwhile; no Python API is
+  // called): every value's tensor metadata, then the probed element values.
+  // The walk is bound by cache misses on 35,000 scattered objects
+  // (resnet56 x 100): one thread pays ~150 ns per tensor, so the clients are
+  // split over the threads (5.2 -> 0.4 ms on 8 cores) and each thread
+  // prefetches the TensorImpls a few keys ahead
+  std::vector<int64_t> status(static_cast<size_t>(K), 0);  // per client: 0, or (code << 32 | key)
+  std::vector<int64_t> nprobe(static_cast<size_t>(K), 0);
+  at::parallel_for(0, K, 1, [&](int64_t i0, int64_t i1) {
+    std::vector<Probe> todo;
+    for (int64_t i = i0; i < i1; ++i) {
+      todo.clear();
+      int64_t st = 0;
+      PyObject* const* row_vals = &vals[static_cast<size_t>(i) * N];
+      constexpr Py_ssize_t kAhead = 8;  // TensorImpls prefetched this many keys ahead (scattered heap objects)
+      for (Py_ssize_t j = 0; j < N && j < kAhead; ++j)
+        if (THPVariable_CheckExact(row_vals[j])) __builtin_prefetch(THPVariable_Unpack(row_vals[j]).unsafeGetTensorImpl());
+      for (Py_ssize_t j = 0; j < N && !st; ++j) {
+        if (j + kAhead < N && THPVariable_CheckExact(row_vals[j + kAhead]))
+          __builtin_prefetch(THPVariable_Unpack(row_vals[j + kAhead]).unsafeGetTensorImpl());
+        PyObject* val = row_vals[j];
+        if (!THPVariable_CheckExact(val)) {  // a Tensor subclass: the plain path decides
+          st = (int64_t(6) << 32) | j;
+          break;
+        }
+        const at::Tensor& ten = THPVariable_Unpack(val);
+        if (ten.scalar_type() != tp[j]->scalar_type() || ten.sizes() != tp[j]->sizes() || !ten.is_cpu() ||
+            !ten.is_contiguous()) {
+          st = (int64_t(6) << 32) | j;
+          break;
+        }
+        const int64_t n = numel[j];
+        if (n <= 0) continue;
+        if (full) {
+          const int64_t g = group[j];
+          const int es = static_cast<int>(stage_esize[g]);
+          const int src_es = static_cast<int>(ten.element_size());
+          const char* src = static_cast<const char*>(ten.data_ptr());
+          const char* row = reinterpret_cast<const char*>(stage_ptr[g]) + (i * stage_ld[g] + offset[j]) * es;
+          bool same = true;
+          if (kind[j] == 0) {
+            same = std::memcmp(src, row, static_cast<size_t>(n) * es) == 0;
+          } else {
+            for (int64_t p = 0; p < n && same; ++p)
+              same = probe_equal(Probe{src + p * src_es, row + p * es, static_cast<int>(kind[j]), es, 0, 0});
+          }
+          if (!same) st = (int64_t(7) << 32) | j;
+          nprobe[i] += n;
+          continue;
+        }
+        const uint64_t h = mix64(seed ^ mix64(static_cast<uint64_t>(i) * 0x100000001B3ull + static_cast<uint64_t>(j)));
+        const bool anchor = static_cast<int64_t>(mix64(seed + static_cast<uint64_t>(j)) % static_cast<uint64_t>(K)) == i;
+        if (!anchor && h > thresh) continue;
+        const int64_t g = group[j];
+        const int es = static_cast<int>(stage_esize[g]);
+        const int src_es = static_cast<int>(ten.element_size());
+        const char* src = static_cast<const char*>(ten.data_ptr());
+        const char* row = reinterpret_cast<const char*>(stage_ptr[g]) + (i * stage_ld[g] + offset[j]) * es;
+        for (int q = 0; q < 2; ++q) {  // two positions per probed pair
+          const int64_t p = static_cast<int64_t>(mix64(h + 1 + q) % static_cast<uint64_t>(n));
+          todo.push_back(Probe{src + p * src_es, row + p * es, static_cast<int>(kind[j]), es, static_cast<int>(i),
+                               static_cast<int>(j)});
+        }
+      }
+      if (!st)
+        for (const Probe& p : todo)
+          if (!probe_equal(p)) {
+            st = (int64_t(7) << 32) | p.j;
+            break;
+          }
+      status[i] = st;
+      nprobe[i] += static_cast<int64_t>(todo.size());
+    }
+  });
+  int64_t total = 0;
+  for (Py_ssize_t i = 0; i < K; ++i) {
+    total += nprobe[i];
+    if (status[i]) return res(static_cast<int>(status[i] >> 32), i, static_cast<Py_ssize_t>(status[i] & 0xffffffff), total);
+  }
+  return res(0, -1, -1, total);
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "native state_dict walk for mfl_amd (host metadata only)";
   m.def("collect", &collect, "validate clients against client 0 and gather data pointers", py::arg("dicts"),
         py::arg("names"), py::arg("templ"), py::arg("device_index") = -1);
   m.def("unpack", &unpack, "views of a flat buffer shaped like the key table's keys");
   m.def("small_round", &small_round, "the host side of a small fp32 round in one call");
+  m.def("verify_rows", &verify_rows, "w_locals against a streamed round's staging rows (randomly sampled values)");
 }

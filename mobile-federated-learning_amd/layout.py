@@ -108,6 +108,8 @@ def _collect_ext():
     return _COLLECT[0]
 
 
+_META_TEMPLATES: Dict[tuple, List[torch.Tensor]] = {}  # KeyTable.meta_template, by signature
+
 # fedavg_pack_item.kind codes (include/fedavg_amd.h)
 _PACK_KIND = {torch.int64: 1, torch.int32: 2, torch.int16: 3, torch.int8: 4, torch.uint8: 5, torch.bool: 6}
 
@@ -199,8 +201,21 @@ class KeyTable:
         table retained across rounds does not keep a round's host tensors
         alive.  Idempotent; returns self."""
         if self._template and self._template[0].device.type != "meta":
-            self._template = [torch.empty(e.shape, dtype=e.src_dtype, device="meta") for e in self.entries]
+            self._template = self.meta_template()
         return self
+
+    def meta_template(self) -> List[torch.Tensor]:
+        """Meta tensors with the keys' shapes and source dtypes, shared by every
+        table of the same signature (350 meta tensors cost ~1 ms to make; a
+        streamed round's finish needs them on its critical path)."""
+        sig = self.signature()
+        got = _META_TEMPLATES.get(sig)
+        if got is None:
+            got = [torch.empty(e.shape, dtype=e.src_dtype, device="meta") for e in self.entries]
+            if len(_META_TEMPLATES) >= 16:
+                _META_TEMPLATES.clear()
+            _META_TEMPLATES[sig] = got
+        return list(got)
 
     def try_collect(self, state_dicts: Sequence[Mapping[str, torch.Tensor]]):
         """:meth:`collect` for a table reused from an earlier round: the
@@ -244,7 +259,10 @@ class KeyTable:
         return sum(g.P for g in self.groups.values())
 
     def signature(self):
-        return tuple((e.name, e.shape, e.src_dtype) for e in self.entries)
+        sig = self.__dict__.get("_sig")
+        if sig is None:
+            sig = self._sig = tuple((e.name, e.shape, e.src_dtype) for e in self.entries)
+        return sig
 
     def validate(self, state_dicts: Sequence[Mapping[str, torch.Tensor]], first_index: int = 0) -> None:
         """Every client must hold every key of client 0 with the same shape/dtype.

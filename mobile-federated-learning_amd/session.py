@@ -72,6 +72,7 @@ class RoundSession:
         self._ready = {}
         self._client_dev = None
         self._out_host = {}
+        self._views = {}  # dtype -> the result's key views of _out_host[dtype], made before finish()
         self.finish_profile = {}
         self.add_ms = 0.0
         self.add_profile = {}  # host ms per phase of add(), summed over the round's clients
@@ -103,6 +104,11 @@ class RoundSession:
                 self._out_host = {g.dtype: torch.empty(g.P, dtype=g.dtype, pin_memory=True)
                                   for g in self.table.groups.values()}
                 self._warm_finish_path()
+                # the averaged model's key views of those buffers: a view needs
+                # no data, so they are made here, while clients train, instead
+                # of in finish() (350 views: ~0.5 ms, resnet56)
+                self._views = {g.dtype: self.table.unpack(g, self._out_host[g.dtype])
+                               for g in self.table.groups.values()}
         ptrs, keep = self.table.collect([state_dict], self._client_dev)
         if self._client_dev.type == "cuda":
             # device-resident client: one packing kernel on the copy stream,
@@ -256,7 +262,8 @@ class RoundSession:
             self._forget_table()
             return None
         for g, out_host in outs:
-            self._set_results(acc_dict, self.table.unpack(g, out_host))
+            views = self._views.get(g.dtype)
+            self._set_results(acc_dict, views if views is not None else self.table.unpack(g, out_host))
         # host-side phases of the finish (ms): issuing weights/reduce/D2H, waiting for them, unpacking
         self.finish_profile = {"issue_ms": (t1 - t0) * 1e3, "verify_ms": (t_v - t1) * 1e3, "wait_ms": (t2 - t_v) * 1e3,
                                "unpack_ms": (time.perf_counter() - t2) * 1e3}

@@ -14,17 +14,37 @@ from loop_replay import fresh_classes
 AGG_MOD = sys.modules["mfl_amd.aggregate"]
 
 
+class _FakeStaging:
+    def __init__(self, K, ld, dtype):
+        self.host = torch.zeros((K, ld), dtype=dtype)  # the pinned rows' stand-in
+
+
 class _FakeSession:
+    """A RoundSession stand-in: the real key table and host packer
+    (fedavg_pack_rows runs on the CPU), no GPU -- so the feed's native
+    verification (verify_rows) compares w_locals against real packed rows."""
+
     def __init__(self, template, max_clients):
+        from mfl_amd.layout import KeyTable
+
         self.keys = list(template.keys())
         self.max_clients = max_clients
         self.counts, self.dicts = [], []
         self._finished = False
         self.verified = None
         self.keep_dicts = True
+        self.table = KeyTable(template)
+        self._staging = {g.dtype: _FakeStaging(max_clients, g.ld, g.dtype) for g in self.table.groups.values()}
 
     def add(self, n, sd):
         assert list(sd.keys()) == self.keys
+        ptrs, _ = self.table.collect([sd])
+        lib = mfl_amd._lib.load()
+        for g in self.table.groups.values():
+            st = self._staging[g.dtype]
+            items = self.table.pack_items(g, ptrs, len(self.counts), g.ld)
+            mfl_amd._lib.check(lib.fedavg_pack_rows(items.ctypes.data, items.shape[0], st.host.data_ptr(),
+                                                    st.host.element_size(), 1), "fedavg_pack_rows")
         self.counts.append(n)
         self.dicts.append(sd)
 
@@ -121,10 +141,17 @@ def test_small_round_left_to_plain_path(plain_calls):
     assert len(agg.sessions) == 1 and "__streamed__" in tr.results[0]
 
 
-def test_sampled_value_change_falls_back(plain_calls):
+@pytest.mark.parametrize("key,pos", [("w", 0), ("w", 7), ("b", 2), ("nbt", None)])
+def test_sampled_value_change_falls_back(plain_calls, key, pos):
+    # a small round (<= VERIFY_FULL_ELEMS) is compared element by element:
+    # any edit of any key, int64 buffers included, is seen
     def mutate(r, w_locals):
-        if r == 1:  # the largest key's first element, a sampled position
-            w_locals[2][1]["w"][0] += 1.0
+        if r == 1:
+            t = w_locals[2][1][key]
+            if pos is None:
+                t += 1
+            else:
+                t[pos] += 1.0
 
     tr, agg = _run(_rounds(2), after_append=mutate)
     assert "__streamed__" in tr.results[0] and "__plain__" in tr.results[1]
@@ -178,3 +205,78 @@ def test_valid_train_result_mirrors_reference_check():
         r[i] = None
         assert not valid_train_result(tuple(r))
     assert not valid_train_result(None)
+
+
+def test_client_subclass_overriding_train_is_not_streamed(plain_calls):
+    """A Client subclass whose train() edits what the wrapped reference
+    method returned (clipping, noise, ...): the feed saw the pre-edit dict,
+    so the round must not be streamed."""
+    T, C = fresh_classes()
+
+    class Clipping(C):
+        def train(self, *a, **k):
+            res = super().train(*a, **k)
+            if res[1] is not None:
+                for v in res[0].values():
+                    if v.is_floating_point():
+                        v.clamp_(-0.5, 0.5)
+            return res
+
+    T.client_cls = Clipping
+    mfl_amd.install(T, client_cls=C)
+    tr = T({"w": torch.zeros(10)}, _rounds(2))
+    agg = _FakeAgg()
+    from mfl_amd.autostream import ClientFeed
+
+    feed = ClientFeed(lambda: agg, len(tr.client_list))
+    feed.SMALL_ROUND_BYTES = 0
+    tr.__dict__["_mfl_feed"] = feed
+    tr.train()
+    assert agg.sessions == [] and len(plain_calls) == 2
+    assert feed.stats["rounds_fallback"] == 2 and "overridden" in feed.stats["last_fallback"]
+
+
+def test_reinstall_with_streaming_off_stops_the_feed(plain_calls):
+    T, C = fresh_classes()
+    mfl_amd.install(T, stream_clients=True)
+    mfl_amd.install(T, stream_clients=False)  # the wrappers stay, but read the class's setting
+    tr = T({"w": torch.zeros(10)}, _rounds(2))
+    tr.train()
+    assert "_mfl_feed" not in tr.__dict__ and len(plain_calls) == 2
+    mfl_amd.install(T, stream_clients=True)  # and on again
+    agg = _FakeAgg()
+    from mfl_amd.autostream import ClientFeed
+
+    feed = ClientFeed(lambda: agg, len(tr.client_list))
+    feed.SMALL_ROUND_BYTES = 0
+    tr.__dict__["_mfl_feed"] = feed
+    tr.results.clear()
+    tr.train()
+    assert feed.stats["rounds_streamed"] == 2
+
+
+def test_tensor_changed_while_packed_breaks_the_round(plain_calls):
+    """The feed records each fed tensor's version counter on the loop's
+    thread; an in-place update before the worker packed it (a Client.train
+    whose tensors the next client's training updates) fails the round."""
+    import threading
+
+    from mfl_amd.autostream import ClientFeed
+
+    gate = threading.Event()
+    agg = _FakeAgg()
+
+    def slow_agg():
+        gate.wait(10)
+        return agg
+
+    feed = ClientFeed(slow_agg, 4)
+    feed.SMALL_ROUND_BYTES = 0
+    sd = OrderedDict(w=torch.arange(10.0), b=torch.zeros(3))
+    feed.feed(5, sd)
+    sd["w"].add_(1.0)  # in place, after train() returned, before the worker packed it
+    gate.set()
+    w_locals = [(5, OrderedDict((k, v.clone()) for k, v in sd.items()))]
+    assert feed.take(w_locals) is None
+    assert "changed while they were packed" in feed.stats["last_fallback"]
+    feed.close()
