@@ -12,6 +12,7 @@ Layers:
   aggregate                the drop-in (DeviceAggregator, install, mixin)
   session                  streaming rounds: pack + upload each client as it arrives
   distributed              P-sharded multi-GPU reduce + RCCL all-gather
+  multi                    one process, N GPUs: host rounds by columns over N PCIe links
   fpf                      FPF2 bookkeeping (local_w_diffs / A_mat / G_mat) in HBM
 """
 from ._lib import FedAvgLibraryError, library_path
@@ -29,6 +30,7 @@ from .aggregate import (
 from .layout import KeyTable, ShapeMismatchError, result_dtype
 from .reduce import ALIGN_ELEMS, client_sqdist, reduce_packed, reduce_tensors, reduce_with_sqdist, weights_tensor
 from .session import RoundSession
+from .multi import ShardedAggregator, sharded_aggregator
 from .fpf import FPFTracker
 
 __all__ = [
@@ -53,5 +55,7 @@ __all__ = [
     "reduce_tensors",
     "weights_tensor",
     "RoundSession",
+    "ShardedAggregator",
+    "sharded_aggregator",
     "FPFTracker",
 ]

@@ -938,11 +938,30 @@ def default_aggregator(device: Optional[torch.device] = None) -> DeviceAggregato
     return agg
 
 
-def aggregate(w_locals, model_global=None, device: Optional[torch.device] = None):
-    """Functional form of ``FedAvgTrainer.aggregate``."""
+def _devices_arg(device, devices):
+    """The device list a functional call routes to: ``devices`` when given,
+    else FEDAVG_DEVICES when no single ``device`` was named; None = one GPU."""
+    if devices is None and device is None:
+        from .multi import devices_from_env
+
+        devices = devices_from_env()
+    if devices is not None and len(devices) > 1:
+        return list(devices)
+    return None
+
+
+def aggregate(w_locals, model_global=None, device: Optional[torch.device] = None, devices=None):
+    """Functional form of ``FedAvgTrainer.aggregate``.  ``devices`` (or
+    FEDAVG_DEVICES=0,1,...): host rounds split by columns over those GPUs,
+    each over its own PCIe link (multi.ShardedAggregator, same bits)."""
     done, answer = _trivial(w_locals, model_global)
     if done:
         return answer  # answered on the host: no GPU needed
+    devs = _devices_arg(device, devices)
+    if devs is not None:
+        from .multi import sharded_aggregator
+
+        return sharded_aggregator(devs).aggregate(w_locals, model_global=model_global)
     if device is None:  # device-resident clients are reduced on their own device
         first = next(iter(w_locals[0][1].values()))
         if isinstance(first, torch.Tensor) and first.is_cuda:
@@ -950,17 +969,22 @@ def aggregate(w_locals, model_global=None, device: Optional[torch.device] = None
     return default_aggregator(device).aggregate(w_locals, model_global=model_global)
 
 
-def client_distances(w_locals, w_glob, device: Optional[torch.device] = None):
+def client_distances(w_locals, w_glob, device: Optional[torch.device] = None, devices=None):
     """Functional form of fedavg_trainer.py:291 (see DeviceAggregator.client_distances)."""
+    devs = _devices_arg(device, devices)
+    if devs is not None:
+        from .multi import sharded_aggregator
+
+        return sharded_aggregator(devs).client_distances(w_locals, w_glob)
     return default_aggregator(device).client_distances(w_locals, w_glob)
 
 
-def estimate_delta(w_locals, w_glob, lr, device: Optional[torch.device] = None):
+def estimate_delta(w_locals, w_glob, lr, device: Optional[torch.device] = None, devices=None):
     """fedavg_trainer.py:289-293: ``sum(n_i * ||w_i - w_glob||) / sum(n_i) / lr``."""
     import numpy as np
 
     sample_nums = np.array([n for n, _ in w_locals])
-    norms = client_distances(w_locals, w_glob, device)
+    norms = client_distances(w_locals, w_glob, device, devices)
     return np.sum(sample_nums * norms) / np.sum(sample_nums) / lr
 
 
@@ -986,7 +1010,8 @@ def _feed_of(trainer, device):
     return feed
 
 
-def install(trainer_cls, device: Optional[torch.device] = None, client_cls=None, stream_clients: Optional[bool] = None):
+def install(trainer_cls, device: Optional[torch.device] = None, client_cls=None, stream_clients: Optional[bool] = None,
+            devices=None):
     """Patch ``trainer_cls.aggregate`` (e.g. the reference ``FedAvgTrainer``) in place.
 
     With ``stream_clients`` (default: on unless ``FEDAVG_STREAM_CLIENTS=0``)
@@ -995,7 +1020,11 @@ def install(trainer_cls, device: Optional[torch.device] = None, client_cls=None,
     ``trainer_cls``'s module imported) so each valid client result is packed
     and uploaded while the loop goes on, and ``aggregate`` at :217 only
     reduces (autostream.py; falls back to the plain path whenever
-    ``w_locals`` is not what was streamed)."""
+    ``w_locals`` is not what was streamed).
+
+    ``devices`` (or FEDAVG_DEVICES=0,1,... when ``device`` is None): the
+    plain path's host rounds run over those GPUs by columns, one PCIe link
+    each (multi.ShardedAggregator); streaming stays on the first device."""
     from . import autostream
 
     if stream_clients is None:
@@ -1018,7 +1047,7 @@ def install(trainer_cls, device: Optional[torch.device] = None, client_cls=None,
             out = feed.take(w_locals)
             if out is not None:
                 return out
-        return aggregate(w_locals, getattr(self, "model_global", None), device)
+        return aggregate(w_locals, getattr(self, "model_global", None), device, devices)
 
     aggregate_method.__doc__ = FedAvgAggregateMixin.aggregate.__doc__
     aggregate_method.__wrapped_reference__ = getattr(trainer_cls, "aggregate", None)

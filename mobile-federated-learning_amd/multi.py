@@ -1,0 +1,300 @@
+"""One process, several GPUs: the drop-in's host path over N PCIe links.
+
+The reference drives ``aggregate`` from one process (main_fedavg.py:337-338,
+fedavg_trainer.py:217) with host state_dicts in and a host state_dict out
+(client.py:96, :219).  On one GPU that round is bound by one PCIe link:
+100 clients x 25M fp32 = 10 GB of rows at ~56 GB/s.
+SURVEY.md section 8e's host-consumer form needs no collective: every output
+column depends only on the same column of the K clients
+(fedavg_trainer.py:451-457), so
+
+* the K client rows are packed once into pinned host staging (the native
+  packer, row chunks of ``CHUNK_BYTES``);
+* GPU d takes the contiguous column shard ``[c_d, c_{d+1})`` of every row
+  with ONE strided DMA per row chunk over ITS OWN PCIe link
+  (``fedavg_upload_shard`` = hipMemcpy2DAsync: height = rows, width = the
+  shard, source pitch = the staging row), overlapped with the packing of the
+  next row chunk;
+* each GPU reduces its shard with the exact sequential kernel (same bits as
+  one GPU: a column's chain is the same wherever it runs) -- fused with the
+  :291 sums of squares where the single-GPU path fuses them -- and copies its
+  finished columns straight to their global positions in the one pinned
+  output buffer, whose key views become ``w_locals[0][1]``'s values.
+
+Rounds the extra links cannot help are handed to the first device's
+``DeviceAggregator`` unchanged: small rounds (one native call,
+``SMALL_ROUND_BYTES``), device-resident clients (reduced where they lie) and
+streaming sessions (``begin_round``).  ``client_distances`` (:291) after a
+sharded round adds the per-device fp64 sums of squares in device order.
+
+Use: ``mfl_amd.install(FedAvgTrainer, devices=[0, 1, ..., 7])``,
+``FEDAVG_DEVICES=0,1,...,7 python -m mfl_amd.launch main_fedavg.py ...`` or
+``mfl_amd.sharded_aggregator([0, 1, ...]).aggregate(w_locals)``.  The same
+device may appear more than once (tests rehearse N shards on one GPU).
+"""
+from __future__ import annotations
+
+import os
+import threading
+import time
+import weakref
+from collections import OrderedDict
+from typing import List, Optional, Sequence
+
+import torch
+
+from . import _lib
+from .distributed import upload_segments
+from .layout import KeyTable
+from .reduce import ALIGN_ELEMS, client_sqdist
+
+__all__ = ["ShardedAggregator", "sharded_aggregator", "shard_bounds", "devices_from_env"]
+
+
+def shard_bounds(P: int, n: int, align: int = ALIGN_ELEMS) -> List[int]:
+    """Column boundaries ``[c_0 = 0, c_1, ..., c_n = P]`` of n contiguous
+    shards; every interior boundary a multiple of ``align`` (a shard's rows
+    then start 256-B aligned in HBM and its host source 256-B aligned in the
+    staging row).  Shards may be empty when P is small."""
+    if n < 1:
+        raise ValueError("need at least one shard")
+    bounds = [0]
+    for d in range(1, n):
+        b = -(-P * d // n)
+        bounds.append(min(P, -(-b // align) * align))
+    bounds.append(P)
+    return bounds
+
+
+def devices_from_env() -> Optional[List[torch.device]]:
+    """``FEDAVG_DEVICES=0,1,2,3`` -> those HIP devices (None when unset)."""
+    v = os.environ.get("FEDAVG_DEVICES", "").strip()
+    if not v:
+        return None
+    return [torch.device("cuda", int(t)) for t in v.split(",") if t.strip()]
+
+
+class _Shard:
+    """One device's part: its column range, rows buffer, weights and streams."""
+
+    def __init__(self, device: torch.device):
+        from .aggregate import _Weights
+
+        self.device = device
+        self.copy = torch.cuda.Stream(device)
+        self.d2h = torch.cuda.Stream(device)
+        self.rows = {}  # dtype -> [K, ld_d] device buffer
+        self.weights = {}  # weight dtype -> _Weights
+        self._Weights = _Weights
+
+    def rows_for(self, dtype, K, cols):
+        ld = max(-(-cols // ALIGN_ELEMS) * ALIGN_ELEMS, ALIGN_ELEMS)
+        buf = self.rows.get(dtype)
+        if buf is None or buf.shape[0] < K or buf.shape[1] != ld:
+            buf = torch.empty((K, ld), dtype=dtype, device=self.device)
+            self.rows[dtype] = buf
+        return buf[:K]
+
+    def weights_for(self, dtype, K):
+        wdt = torch.float64 if dtype == torch.float64 else torch.float32
+        w = self.weights.get(wdt)
+        if w is None or w.K < K:
+            w = self._Weights(K, wdt, self.device)
+            self.weights[wdt] = w
+        return w
+
+
+class ShardedAggregator:
+    """``FedAvgTrainer.aggregate`` over several GPUs (module docstring)."""
+
+    CHUNK_BYTES = int(os.environ.get("FEDAVG_CHUNK_BYTES", str(32 << 20)))
+    SMALL_ROUND_BYTES = None  # rounds up to this many row bytes stay on one device (None: DeviceAggregator's)
+
+    def __init__(self, devices: Sequence):
+        devs = [torch.device(d) if not isinstance(d, int) else torch.device("cuda", d) for d in devices]
+        if not devs:
+            raise ValueError("ShardedAggregator needs at least one device")
+        for d in devs:
+            if d.type != "cuda":
+                raise ValueError(f"{d}: HIP devices only (no CPU fallback)")
+        self.devices = [torch.device("cuda", d.index if d.index is not None else 0) for d in devs]
+        self._shards = [_Shard(d) for d in self.devices]
+        self._host = {}  # dtype -> pinned [K, ld] staging
+        self._lock = threading.Lock()
+        self._table_hint = None
+        self._last = {}
+        self.last_profile = {}
+        self.rounds_sharded = 0
+        self.rounds_delegated = 0
+
+    @property
+    def primary(self):
+        from .aggregate import default_aggregator
+
+        return default_aggregator(self.devices[0])
+
+    def begin_round(self, template, max_clients: int):
+        """Streaming sessions run on the first device (RoundSession)."""
+        return self.primary.begin_round(template, max_clients)
+
+    # ------------------------------------------------------------------
+    def aggregate(self, w_locals, model_global=None):
+        from .aggregate import _Prepared, _trivial, prepare
+
+        done, answer = _trivial(w_locals, model_global)
+        if done:
+            return answer  # empty list / no keys: answered on the host
+        sd0 = w_locals[0][1]
+        first = next(iter(sd0.values()))
+        if isinstance(first, torch.Tensor) and first.is_cuda:
+            # device-resident clients are reduced where they lie (zero-copy)
+            from .aggregate import default_aggregator
+
+            self.rounds_delegated += 1
+            return default_aggregator(first.device).aggregate(w_locals, model_global)
+        row_bytes = sum(v.numel() * max(4, v.element_size()) for v in sd0.values() if isinstance(v, torch.Tensor))
+        small = self.primary.SMALL_ROUND_BYTES if self.SMALL_ROUND_BYTES is None else self.SMALL_ROUND_BYTES
+        if len(self.devices) == 1 or len(w_locals) * row_bytes <= small:
+            # a small round is one native call on one device (fedavg_round_f32)
+            self.rounds_delegated += 1
+            return self.primary.aggregate(w_locals, model_global)
+        prep = prepare(w_locals, model_global, self._table_hint)
+        if not isinstance(prep, _Prepared):
+            return prep
+        acc_dict, table, dicts, weights, ptrs, keepalive = prep
+        self._table_hint = table
+        if table.client_device(dicts).type == "cuda":  # mixed placement: the primary raises the reference's error
+            del keepalive
+            return self.primary.aggregate(w_locals, model_global)
+        with self._lock:
+            results = self._reduce_sharded(table, ptrs, weights)
+        del keepalive
+        table.forget_tensors()
+        try:
+            self._last["refs"] = [weakref.ref(sd) for sd in dicts]
+            self._last["acc"] = weakref.ref(acc_dict)
+        except TypeError:
+            self._last = {}
+        for e in table.entries:
+            acc_dict[e.name] = results[e.name]
+        self.rounds_sharded += 1
+        return acc_dict
+
+    def _reduce_sharded(self, table: KeyTable, ptrs, weights):
+        from .aggregate import _fetch, reduce_rows
+
+        lib = _lib.load()
+        K = ptrs.shape[0]
+        n = len(self._shards)
+        threads = max(1, torch.get_num_threads())
+        t0 = time.perf_counter()
+        for sh in self._shards:  # earlier users of the shard's rows are done
+            sh.copy.wait_stream(torch.cuda.current_stream(sh.device))
+        plan = []
+        for g in table.groups.values():
+            es = _elem(g.dtype)
+            host = self._host.get(g.dtype)
+            if host is None or host.shape[0] < K or host.shape[1] != g.ld:
+                host = torch.empty((K, g.ld), dtype=g.dtype, pin_memory=True)
+                self._host[g.dtype] = host
+            host = host[:K]
+            bounds = shard_bounds(g.P, n)
+            rows = [sh.rows_for(g.dtype, K, bounds[d + 1] - bounds[d]) for d, sh in enumerate(self._shards)]
+            step = max(1, min(K, self.CHUNK_BYTES // max(1, g.ld * es)))
+            for i0 in range(0, K, step):
+                i1 = min(K, i0 + step)
+                items = table.pack_items(g, ptrs[i0:i1], i0, g.ld)
+                _lib.check(lib.fedavg_pack_rows(items.ctypes.data, items.shape[0], host.data_ptr(), es, threads),
+                           "fedavg_pack_rows")
+                for d, sh in enumerate(self._shards):  # each device's columns over its own link
+                    c0, c1 = bounds[d], bounds[d + 1]
+                    if c1 > c0:
+                        with torch.cuda.device(sh.device):
+                            upload_segments(rows[d][i0:i1], host[i0:i1], [(0, c0, c1 - c0)], sh.copy)
+            plan.append((g, bounds, rows))
+        t1 = time.perf_counter()
+        outs = []
+        per_dev = [dict() for _ in self._shards]
+        for g, bounds, rows in plan:
+            out_host = torch.empty(g.P, dtype=g.dtype, pin_memory=True)
+            for d, sh in enumerate(self._shards):
+                c0, c1 = bounds[d], bounds[d + 1]
+                if c1 <= c0:
+                    continue
+                with torch.cuda.device(sh.device):
+                    compute = torch.cuda.current_stream(sh.device)
+                    compute.wait_stream(sh.copy)
+                    w_dev = sh.weights_for(g.dtype, K).upload(weights, compute)
+                    out_dev = torch.empty(c1 - c0, dtype=g.dtype, device=sh.device)
+                    sums = []
+                    reduce_rows(rows[d], w_dev, c1 - c0, out_dev, sums)
+                    sh.d2h.wait_stream(compute)
+                    _fetch(out_dev, out_host[c0:c1], sh.d2h)
+                    per_dev[d][g.dtype] = (rows[d], out_dev, sums[0] if sums else None, c0, c1)
+            outs.append((g, out_host))
+        for sh in self._shards:
+            sh.d2h.synchronize()
+        t2 = time.perf_counter()
+        results = OrderedDict()
+        for g, out_host in outs:
+            results.update(table.unpack(g, out_host))
+        self._last = {"table": table, "K": K, "per_dev": per_dev}
+        self.last_profile = {"pack_and_h2d_issue_ms": (t1 - t0) * 1e3, "reduce_d2h_wait_ms": (t2 - t1) * 1e3,
+                             "shards": n}
+        return results
+
+    # ------------------------------------------------------------------
+    def client_distances(self, w_locals, w_glob):
+        """fedavg_trainer.py:291 after a sharded round: every device's fp64
+        sums of squares of its columns (fused into the aggregate's pass, or
+        one client_sqdist pass over its rows), added in device order; other
+        calls go to the first device's DeviceAggregator."""
+        import numpy as np
+
+        from .aggregate import _round_to_dtype
+
+        last = self._last
+        refs = last.get("refs")
+        cached = (refs is not None and last["acc"]() is w_glob and len(refs) == len(w_locals)
+                  and all(r() is sd for r, (_, sd) in zip(refs, w_locals)))
+        if not cached or not w_locals:
+            return self.primary.client_distances(w_locals, w_glob)
+        table = last["table"]
+        if any(e.src_dtype == torch.bool for e in table.entries) and any(sd is not w_glob for _, sd in w_locals):
+            raise RuntimeError("Subtraction, the `-` operator, with a bool tensor is not supported "
+                               "(fedavg_trainer.py:291 on a state_dict with bool buffers)")
+        total = np.zeros(len(w_locals), dtype=np.float64)
+        glob_finite = True
+        for d, parts in enumerate(last["per_dev"]):
+            for dt, (rows, out_dev, sums, c0, c1) in parts.items():
+                with torch.cuda.device(out_dev.device):
+                    s = sums if sums is not None else client_sqdist(rows, out_dev, c1 - c0)
+                    total += s.cpu().numpy()
+                    glob_finite = glob_finite and bool(torch.isfinite(out_dev).all())
+        cat_dtype = None
+        for dt in table.groups:
+            cat_dtype = dt if cat_dtype is None else torch.promote_types(cat_dtype, dt)
+        norms = _round_to_dtype(np.sqrt(total), cat_dtype)
+        for i, (_, sd) in enumerate(w_locals):
+            if sd is w_glob:
+                norms[i] = 0.0 if glob_finite else float("nan")
+        return norms
+
+
+def _elem(dtype: torch.dtype) -> int:
+    return torch.empty(0, dtype=dtype).element_size()
+
+
+_sharded = {}
+_sharded_lock = threading.Lock()
+
+
+def sharded_aggregator(devices: Sequence) -> ShardedAggregator:
+    """The process-wide ShardedAggregator for this device list."""
+    key = tuple(int(torch.device(d).index if not isinstance(d, int) else d) for d in devices)
+    with _sharded_lock:
+        agg = _sharded.get(key)
+        if agg is None:
+            agg = ShardedAggregator(list(key))
+            _sharded[key] = agg
+    return agg

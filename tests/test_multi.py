@@ -1,0 +1,34 @@
+"""multi.ShardedAggregator's host logic on CPU: the column split and the
+device-list routing (the GPU runs are tests/test_gpu_multi.py)."""
+import pytest
+import torch
+
+import mfl_amd
+from mfl_amd.multi import devices_from_env, shard_bounds
+
+
+@pytest.mark.parametrize("P,n", [(25_000_000, 8), (600_372, 8), (7_850, 2), (1, 8), (64, 3), (1_000_003, 7)])
+def test_shard_bounds_partition_aligned(P, n):
+    b = shard_bounds(P, n)
+    assert len(b) == n + 1 and b[0] == 0 and b[-1] == P
+    assert all(b[i] <= b[i + 1] for i in range(n))  # contiguous, ordered, covering
+    assert all(x % 64 == 0 for x in b[1:-1] if x < P)  # interior starts 256-B aligned
+    widths = [b[i + 1] - b[i] for i in range(n)]
+    if P >= 64 * n:
+        assert max(widths) - min(widths) <= 128  # balanced to two alignment units
+
+
+def test_shard_bounds_target():
+    assert shard_bounds(25_000_000, 8)[1] == 3_125_056
+
+
+def test_devices_from_env(monkeypatch):
+    monkeypatch.delenv("FEDAVG_DEVICES", raising=False)
+    assert devices_from_env() is None
+    monkeypatch.setenv("FEDAVG_DEVICES", "0, 1,2,3")
+    assert devices_from_env() == [torch.device("cuda", i) for i in range(4)]
+
+
+def test_sharded_aggregator_refuses_cpu_devices():
+    with pytest.raises(ValueError):
+        mfl_amd.ShardedAggregator([torch.device("cpu")])
