@@ -675,6 +675,9 @@ __device__ __forceinline__ void fused_finish(float* lds, const double (&acc)[RM]
 template <int VEC>
 struct WinVec {
   typedef float T __attribute__((ext_vector_type(VEC)));
+  // the same vector at dword alignment: window stores into outputs that are
+  // only 4-B aligned (a key's offset inside the packed model is any element)
+  typedef float TA __attribute__((ext_vector_type(VEC), aligned(4)));
 };
 
 // lanes 0-31: a's two halves added (lane l: a[l] + a[l + 32]); lanes 32-63: b's

@@ -1055,7 +1055,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void reduce_sqdist_win_kernel(
     }
     }
     if (!ragged) {
-      __builtin_nontemporal_store(a, reinterpret_cast<V*>(out + cl));
+      __builtin_nontemporal_store(static_cast<typename WinVec<VEC>::TA>(a), reinterpret_cast<typename WinVec<VEC>::TA*>(out + cl));
     } else {
 #pragma unroll
       for (int v = 0; v < VEC; ++v)
@@ -1245,7 +1245,7 @@ __global__ __launch_bounds__(128, win_min_waves(KH, VEC)) void reduce_sqdist_win
       chain(a, false);
       xa[lane] = a;
       if (!ragged) {
-        __builtin_nontemporal_store(a, reinterpret_cast<V*>(out + cl));
+        __builtin_nontemporal_store(static_cast<typename WinVec<VEC>::TA>(a), reinterpret_cast<typename WinVec<VEC>::TA*>(out + cl));
       } else {
 #pragma unroll
         for (int v = 0; v < VEC; ++v)

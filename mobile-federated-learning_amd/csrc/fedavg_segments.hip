@@ -686,7 +686,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void reduce_sqdist_segwin_kernel(
     }
     float* o = out + out_off + c0 + lane * VEC;
     if (n == WC) {
-      *reinterpret_cast<V*>(o) = a;
+      *reinterpret_cast<typename WinVec<VEC>::TA*>(o) = a;  // o: only dword-aligned (key offsets)
     } else {
 #pragma unroll
       for (int v = 0; v < VEC; ++v)

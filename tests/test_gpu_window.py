@@ -120,10 +120,34 @@ def test_window_negative_zero_and_nonfinite(kmax, vec):
     assert torch.equal(torch.isnan(s), torch.isnan(ref))
 
 
+def _oracle_windows(x, out, weights, P, n=6, width=2053, seed=0):
+    """Sampled column windows of the fused output, bit for bit against the
+    oracle (fedavg_trainer.py:450-457 restated) on host copies of the same
+    columns: the first, the last and random ones."""
+    rng = np.random.default_rng(seed)
+    w32 = np.array([np.float32(v) for v in weights], dtype=np.float32)
+    for s in sorted({0, P - width, *[int(v) for v in rng.integers(0, P - width, size=n)]}):
+        exp = O.reduce_f32(x[:, s:s + width].cpu().numpy(), w32)
+        got = out[s:s + width].cpu().numpy()
+        assert got.tobytes() == exp.tobytes(), f"window at column {s}"
+
+
+def _sumsq_torch64(x, out, P, step=1 << 20):
+    """:291's sums of squares by plain torch: the fp32 difference as the
+    reference forms it, squared and summed in fp64 (column chunks)."""
+    tot = torch.zeros(x.shape[0], dtype=torch.float64, device=DEV)
+    for c0 in range(0, P, step):
+        c1 = min(P, c0 + step)
+        tot += ((x[:, c0:c1] - out[None, c0:c1]).double() ** 2).sum(1)
+    return tot
+
+
 @pytest.mark.parametrize("K", [17, 48, 49, 64, 65, 80, 81, 100, 101, 128])
 def test_window_plan_bands_bit_exact(K):
     """Long rows: the production plan takes the window instance of K's band;
-    the reduce's bits, sums within 1e-12 of the two production passes."""
+    sampled windows of its average bit-exact against the oracle, its :291 sums
+    within 1e-12 of a plain-torch fp64 reference, and the whole average equal
+    to the production row reduce's bits."""
     lib = mfl_amd._lib.load_probe()
     P = 8_400_000 + 3
     plan = lib.fedavg_fused_plan_of(K, P)
@@ -133,12 +157,39 @@ def test_window_plan_bands_bit_exact(K):
     x, ld, weights = _rows(K, P, K * 31)
     w = mfl_amd.weights_tensor(weights, torch.float32, DEV)
     out, sumsq = mfl_amd.reduce_with_sqdist(x, w, P)
-    ref_out = mfl_amd.reduce_packed(x, w, P)
-    assert torch.equal(out.view(torch.int32), ref_out.view(torch.int32)), K
-    ref = mfl_amd.client_sqdist(x, ref_out, P)
+    _oracle_windows(x, out, weights, P, seed=K)
+    ref = _sumsq_torch64(x, out, P)
     rel = ((sumsq - ref).abs() / ref).max().item()
     assert rel < 1e-12, (K, rel)
+    ref_out = mfl_amd.reduce_packed(x, w, P)
+    assert torch.equal(out.view(torch.int32), ref_out.view(torch.int32)), K
     del x
+
+
+def test_window_target_sampled_oracle():
+    """The north-star round, 100 clients x 25M (the drop-in's fused window
+    pass, reduce_sqdist_win_kernel<100, 2>): clients generated on the device by
+    mfl_amd.synthetic, every sampled window of the average bit-exact against the
+    oracle applied to the same columns regenerated on the host by numpy, the
+    :291 sums within 1e-12 of plain torch in fp64."""
+    from mfl_amd import synthetic
+
+    K, P = 100, 25_000_000
+    ld = (P + 63) // 64 * 64
+    rows = torch.empty((K, ld), device=DEV)
+    synthetic.fill_rows(rows, [(0, 0, P)])
+    weights = mfl_amd.sample_weights(synthetic.sample_counts(K))
+    w = mfl_amd.weights_tensor(weights, torch.float32, DEV)
+    out, sumsq = mfl_amd.reduce_with_sqdist(rows, w, P)
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(11)
+    for s in [0, P - 4099, *[int(v) for v in rng.integers(0, P - 4099, size=10)]]:
+        exp = O.reduce_f32(synthetic.client_columns_numpy(K, s, 4099), weights)
+        assert out[s:s + 4099].cpu().numpy().tobytes() == exp.tobytes(), f"window at column {s}"
+    ref = _sumsq_torch64(rows, out, P)
+    assert ((sumsq - ref).abs() / ref).max().item() < 1e-12
+    del rows
+    torch.cuda.empty_cache()
 
 
 def test_window_plan_short_rows_and_other_k():
