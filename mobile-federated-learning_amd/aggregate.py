@@ -470,6 +470,9 @@ class DeviceAggregator:
         if bool(np.any(cptrs[:, raw] & 15)):
             return None
         lib = _lib.load()
+        ints = (kind != 0) & (numel > 0)
+        if bool(np.any(ints)):
+            cptrs, kind = self._int_keys_as_f32(cptrs, numel, kind, ints, stream)
         w = self._seg_weights
         if w is None or w.K < K:
             w = self._seg_weights = _Weights(K, torch.float32, self.device)
@@ -487,6 +490,50 @@ class DeviceAggregator:
                    "fedavg_reduce_sqdist_segments_f32")
         self._table_ws_done.record(stream)
         return out_dev, sumsq
+
+    def _int_keys_as_f32(self, cptrs, numel, kind, ints, stream):
+        """A device round's integer / bool keys (BatchNorm's num_batches_tracked)
+        converted to fp32 columns on the device -- the packers' static_cast, one
+        fedavg_pack_rows_device launch into a [K, S] scratch, each key 16-B
+        aligned -- and the pointer table pointed at them as fp32 keys, so the
+        fused pass runs the fp32-only window kernels on every model (round 3
+        left such models on the LDS-DMA tiles).  Returns (cptrs, kind)."""
+        import numpy as np
+
+        lib = _lib.load()
+        K = cptrs.shape[0]
+        idx = np.nonzero(ints)[0]
+        n_i = numel[idx]
+        pad = (n_i + 3) // 4 * 4
+        offs = np.concatenate([[0], np.cumsum(pad)[:-1]]).astype(np.int64)
+        S = int(pad.sum())
+        scratch = torch.empty((K, S), dtype=torch.float32, device=self.device)
+        rows = np.arange(K, dtype=np.int64)[:, None] * S
+        items = np.empty((K, len(idx), 4), dtype=np.int64)
+        items[:, :, 0] = cptrs[:, idx]
+        items[:, :, 1] = n_i[None, :]
+        items[:, :, 2] = rows + offs[None, :]
+        items[:, :, 3] = kind[idx][None, :]
+        items = items.reshape(-1, 4)
+        need = lib.fedavg_pack_rows_device_workspace(items.shape[0])
+        ws = self.__dict__.get("_int_ws")
+        if ws is None or ws[0].numel() < need:
+            cap = max(need, 1 << 14)
+            ws = self._int_ws = (torch.empty(cap, dtype=torch.uint8, pin_memory=True),
+                                 torch.empty(cap, dtype=torch.uint8, device=self.device), torch.cuda.Event())
+        ws[2].synchronize()  # the previous round's table upload has read the pinned half
+        _lib.check(lib.fedavg_pack_rows_device(items.ctypes.data, items.shape[0], scratch.data_ptr(), 4,
+                                               ws[0].data_ptr(), ws[1].data_ptr(), ws[0].numel(),
+                                               stream.cuda_stream), "fedavg_pack_rows_device")
+        ws[2].record(stream)
+        cptrs = cptrs.copy()
+        cptrs[:, idx] = scratch.data_ptr() + (rows + offs[None, :]) * 4
+        kind = kind.copy()
+        kind[idx] = 0
+        # the scratch is freed when this returns; the caching allocator hands its
+        # block out again only in `stream` order, after the kernels that read it
+        scratch.record_stream(stream)
+        return cptrs, kind
 
     def _sqdist_segments(self, table: KeyTable, dicts, glob: torch.Tensor) -> torch.Tensor:
         """:291 sums of squares straight from device-resident clients' tensors."""

@@ -551,8 +551,11 @@ __global__ __launch_bounds__(kBlock) void reduce_sqdist_segments_f32_kernel(cons
 //     client i right after row i is squared (its 8-row group's client
 //     addresses come from the pointer table by scalar loads one group ahead);
 //   slow window (a key's ragged last window): loaded after the squares by
-//     element loads, columns past the key 0.
-// Models with integer / bool keys keep the LDS-DMA tiles (the host checks).
+//     one dword buffer load per element through a descriptor ranged to the
+//     key, columns past it 0.
+// fp32 keys only (the host checks): a model's integer / bool keys
+// (BatchNorm's num_batches_tracked) are converted to fp32 columns on the
+// device first and passed as fp32 keys (aggregate.py, round 4).
 // The next window's key comes from a scalar scan forward from the current
 // one (a wave's windows only move forward), so no vector load besides the
 // rows is in flight in the loop.  Rows K..KMAX-1 are padding: empty
@@ -604,16 +607,20 @@ __global__ __launch_bounds__(64 * NW, MINW) void reduce_sqdist_segwin_kernel(
     const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(static_cast<uint64_t>(v) >> 32), li);
     return reinterpret_cast<const float*>((static_cast<uint64_t>(hi) << 32) | lo);
   };
-  // a slow window (a key's ragged last window) into x: element loads, 0 past the key
+  // a slow window (a key's ragged last window) into x: one dword buffer load
+  // per element through a descriptor whose range is that client's part of
+  // the window (columns past the key read 0, nothing past it is touched).
+  // No per-lane 64-bit address: the global-pointer form of this path held one
+  // per row and made the 100-row instance spill.
   const auto load_slow = [&](int64_t c0, int n, int Kw) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < KMAX; ++i) {
-      const gptr<float> base = to_global<float>(ptr_of(i));
+      const float* base = ptr_of(i) + c0;
+      const __amdgpu_buffer_rsrc_t r =
+          __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, i < Kw ? n * 4 : 0, 0x00020000);
 #pragma unroll
-      for (int v = 0; v < VEC; ++v) {
-        const int col = lane * VEC + v;
-        x[i][v] = (i < Kw && col < n) ? base[c0 + col] : 0.f;
-      }
+      for (int v = 0; v < VEC; ++v)
+        x[i][v] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (lane * VEC + v) * 4, 0, 2));
     }
   };
   // client i of a fast window
@@ -727,6 +734,16 @@ __global__ __launch_bounds__(64 * NW, MINW) void reduce_sqdist_segwin_kernel(
   }
 }
 
+// windows per wave below which the LDS-DMA tiles keep the round
+// (kSegWinMinPerWave; FEDAVG_SEGWIN_MIN_PER_WAVE overrides it for probes)
+inline int64_t segwin_min_per_wave() {
+  static const int64_t v = [] {
+    const char* e = std::getenv("FEDAVG_SEGWIN_MIN_PER_WAVE");
+    return e && e[0] ? static_cast<int64_t>(std::atoll(e)) : kSegWinMinPerWave;
+  }();
+  return v;
+}
+
 // FEDAVG_SEGWIN=0 keeps the LDS-DMA tiles for every device round (probes, A/B)
 inline bool segwin_disabled() {
   static const bool off = [] {
@@ -745,12 +762,13 @@ int64_t segwin_waves(int64_t units) {
   return (grid < need ? grid : need) * NW;
 }
 
-// the window instance for K clients (0 outside 17..128).  The rows kernel's
-// 100 x 2 band is 128 x 1 here: the table's addresses take the VGPRs a
-// 100 x 2 window would need (it spills; device round 100 x 25M 3.66 ms vs
-// 2.75 for the tiles, profiles/r03/segwin/)
+// the window instance for K clients (0 outside 17..128).  Round 3 ran 81-100
+// clients on the 128 x 1 instance because its 100 x 2 form spilled (device
+// round 100 x 25M 3.66 ms, profiles/r03/segwin/); the spill was the slow
+// path's per-lane 64-bit element addresses, gone with the buffer-load form
+// (232 VGPRs, no scratch), so 81-100 clients take 100 x 2 as on rows
 inline int segwin_kmax(int64_t K) {
-  return K <= 16 || K > 128 ? 0 : (K <= 48 ? 48 : (K <= 64 ? 64 : (K <= 80 ? 80 : 128)));
+  return K <= 16 || K > 128 ? 0 : (K <= 48 ? 48 : (K <= 64 ? 64 : (K <= 80 ? 80 : (K <= 100 ? 100 : 128))));
 }
 inline int segwin_vec(int kmax) { return kmax == 48 ? 4 : (kmax == 128 ? 1 : 2); }
 
@@ -759,6 +777,7 @@ inline int64_t segwin_waves_for(int kmax, int64_t units) {
     case 48: return segwin_waves<48, 4, 4>(units);
     case 64: return segwin_waves<64, 2, 4>(units);
     case 80: return segwin_waves<80, 2, 4>(units);
+    case 100: return segwin_waves<100, 2, 4>(units);
     case 128: return segwin_waves<128, 1, 4>(units);
     default: return 0;
   }
@@ -1028,7 +1047,7 @@ int fedavg_reduce_sqdist_segments_f32(const int64_t* client_ptrs, const int64_t*
     for (int64_t jk = 0; ok && jk < n_keys; ++jk) ok = key_numel[jk] >= 0 && key_kind[jk] == kRaw;
     const int64_t wunits = ok ? units_of(key_numel, n_keys, wc) : 0;
     const int64_t waves = segwin_waves_for(kmax, wunits);
-    if (ok && waves > 0 && wunits >= kSegWinMinPerWave * waves && wunits < (int64_t(1) << 31) &&
+    if (ok && waves > 0 && wunits >= segwin_min_per_wave() * waves && wunits < (int64_t(1) << 31) &&
         n_keys < (int64_t(1) << 31)) {
       if (partial_elems < K * waves)
         return set_error(FEDAVG_EINVAL, "%s: partials need %lld doubles", what, (long long)(K * waves));
@@ -1051,6 +1070,10 @@ int fedavg_reduce_sqdist_segments_f32(const int64_t* client_ptrs, const int64_t*
           break;
         case 80:
           hipLaunchKernelGGL((reduce_sqdist_segwin_kernel<80, 2, 4>), grid, block, 0, s, keys, tptrs, n_keys, units,
+                             k32, weights, out, partials);
+          break;
+        case 100:
+          hipLaunchKernelGGL((reduce_sqdist_segwin_kernel<100, 2, 4>), grid, block, 0, s, keys, tptrs, n_keys, units,
                              k32, weights, out, partials);
           break;
         default:

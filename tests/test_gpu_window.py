@@ -215,13 +215,17 @@ WIN_DEVICE_SHAPES = [("layer.weight", (8_400_017,)), ("layer.bias", (1001,)), ("
                      ("proj.weight", (800, 1000)), ("proj.bias", (640,))]
 
 
-@pytest.mark.parametrize("K", [20, 64, 100, 128])
-def test_window_device_clients_bit_exact(K):
-    """Device-resident clients of an all-fp32 model long enough for the
-    zero-copy windows (reduce_sqdist_segwin_kernel): ragged key ends at every
-    window width, keys shorter than a window; the aggregate's bits against the
-    reference loop on host copies, the fused :291 distances within one fp32
-    unit of the exact restatement."""
+@pytest.mark.parametrize("K,int_keys", [(20, False), (64, False), (81, True), (100, False), (100, True),
+                                         (128, False), (128, True)])
+def test_window_device_clients_bit_exact(K, int_keys):
+    """Device-resident clients of a model long enough for the zero-copy
+    windows (reduce_sqdist_segwin_kernel; 81-100 clients on its 100 x 2
+    instance since round 4): ragged key ends at every window width, keys
+    shorter than a window, and (int_keys) BatchNorm-style int64
+    num_batches_tracked buffers (above 2^24) plus an int32 key, converted to
+    fp32 on the device so the fp32 window kernel takes the round; the
+    aggregate's bits against the reference loop on host copies, the fused :291
+    distances within one fp32 unit of the exact restatement."""
     from collections import OrderedDict
 
     from test_gpu_model_shapes import _check_distances, _oracle
@@ -231,12 +235,21 @@ def test_window_device_clients_bit_exact(K):
     base = {k: torch.randn(s, generator=g, device=DEV) * 0.05 for k, s in WIN_DEVICE_SHAPES}
     w_locals = []
     for i in range(K):
-        sd = OrderedDict((k, base[k] + torch.randn(s, generator=g, device=DEV) * 1e-3) for k, s in WIN_DEVICE_SHAPES)
+        sd = OrderedDict()
+        for j, (k, s) in enumerate(WIN_DEVICE_SHAPES):
+            sd[k] = base[k] + torch.randn(s, generator=g, device=DEV) * 1e-3
+            if int_keys and j in (0, 2):
+                sd[f"bn{j}.num_batches_tracked"] = torch.tensor((1 << 25) + 7 * i + j, dtype=torch.int64, device=DEV)
+        if int_keys:
+            sd["counts32"] = torch.arange(i, i + 37, dtype=torch.int32, device=DEV)
         w_locals.append((int(np.random.default_rng(i).integers(1, 1000)), sd))
     expected = _oracle(w_locals)
     out = mfl_amd.aggregate(w_locals, device=DEV)
     for k, e in expected.items():
         assert torch.equal(out[k].cpu().reshape(-1).view(torch.int32), e.reshape(-1).view(torch.int32)), k
+    if int_keys:
+        agg = mfl_amd.default_aggregator(DEV)
+        assert agg._last.get("sumsq"), "the fused pass took the round"
     _check_distances(w_locals, out, max_checked=16)
     del w_locals, out, expected, base
     torch.cuda.empty_cache()
