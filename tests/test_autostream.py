@@ -90,7 +90,7 @@ def _rounds(n_rounds=2, K=4, P=10, fail_first=()):
 def plain_calls(monkeypatch):
     calls = []
 
-    def fake_plain(w_locals, model_global=None, device=None):
+    def fake_plain(w_locals, model_global=None, device=None, devices=None):
         calls.append([n for n, _ in w_locals])
         out = w_locals[0][1]
         out["__plain__"] = torch.tensor(1)
