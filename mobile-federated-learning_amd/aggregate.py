@@ -471,8 +471,9 @@ class DeviceAggregator:
             return None
         lib = _lib.load()
         ints = (kind != 0) & (numel > 0)
+        scratch = None  # held until the fused launch below is issued: it reads it
         if bool(np.any(ints)):
-            cptrs, kind = self._int_keys_as_f32(cptrs, numel, kind, ints, stream)
+            cptrs, kind, scratch = self._int_keys_as_f32(cptrs, numel, kind, ints, stream)
         w = self._seg_weights
         if w is None or w.K < K:
             w = self._seg_weights = _Weights(K, torch.float32, self.device)
@@ -489,6 +490,7 @@ class DeviceAggregator:
                                                          host_ws.numel(), stream.cuda_stream),
                    "fedavg_reduce_sqdist_segments_f32")
         self._table_ws_done.record(stream)
+        del scratch  # freed in `stream` order: later users of its block run after this launch
         return out_dev, sumsq
 
     def _int_keys_as_f32(self, cptrs, numel, kind, ints, stream):
@@ -497,7 +499,10 @@ class DeviceAggregator:
         fedavg_pack_rows_device launch into a [K, S] scratch, each key 16-B
         aligned -- and the pointer table pointed at them as fp32 keys, so the
         fused pass runs the fp32-only window kernels on every model (round 3
-        left such models on the LDS-DMA tiles).  Returns (cptrs, kind)."""
+        left such models on the LDS-DMA tiles).  Returns (cptrs, kind,
+        scratch); the caller holds ``scratch`` until the kernel that reads it
+        is issued (freed earlier, the caching allocator would hand its block
+        to the round's own output on the same stream)."""
         import numpy as np
 
         lib = _lib.load()
@@ -530,10 +535,7 @@ class DeviceAggregator:
         cptrs[:, idx] = scratch.data_ptr() + (rows + offs[None, :]) * 4
         kind = kind.copy()
         kind[idx] = 0
-        # the scratch is freed when this returns; the caching allocator hands its
-        # block out again only in `stream` order, after the kernels that read it
-        scratch.record_stream(stream)
-        return cptrs, kind
+        return cptrs, kind, scratch
 
     def _sqdist_segments(self, table: KeyTable, dicts, glob: torch.Tensor) -> torch.Tensor:
         """:291 sums of squares straight from device-resident clients' tensors."""
