@@ -313,6 +313,36 @@ class DeviceAggregator:
         self._fast_small = None
         self.fast_rounds = 0  # rounds finished by the one-call native path
         self.arena_rounds = 0  # device rounds whose fp32 rows were the clients' own (client_arena layout)
+        self._warm = False
+
+    # A process's first round paid its HIP first-use costs on the round's
+    # critical path.  The HIP API trace of round 0 at 100 x 25M (rocprofv3
+    # --hip-trace, profiles/r04/stream/round0_first_use.json) put 64.6 ms in ONE
+    # hipLaunchKernel: the first launch of torch's fp64 elementwise add (the
+    # column chunks' :291 sums added), i.e. the lazy load of that torch code
+    # object; the streams' hipStreamCreateWithPriority cost 6.2-6.6 ms each.
+    # warm_up() pays them once, off the round: install() calls it before the
+    # loop runs, and a RoundSession's first add() (while clients train).
+    WARMUP = os.environ.get("FEDAVG_WARMUP", "1") != "0"
+
+    def warm_up(self) -> None:
+        """Create the aggregator's streams and launch, once, every kernel a
+        round runs besides the reduction's own code object (torch's fp64 add,
+        isfinite / all; one tiny fused reduce loads libfedavg_amd's), on a
+        scratch problem.  Idempotent."""
+        if self._warm or not self.WARMUP:
+            return
+        self._warm = True
+        with torch.cuda.device(self.device):
+            copy_s, d2h = self._copy_stream_for(), self._d2h_stream_for()
+            with torch.cuda.stream(d2h):
+                rows = torch.zeros((17, 64), dtype=torch.float32, device=self.device)
+                w = torch.full((17,), 1.0 / 17, dtype=torch.float32, device=self.device)
+                out, sums = reduce_with_sqdist(rows, w, 64)
+                z = sums + sums
+                bool(torch.isfinite(out).all())  # also waits for the work above
+                del z
+            copy_s.synchronize()
 
     # ------------------------------------------------------------------
     def begin_round(self, template, max_clients: int):
@@ -1089,6 +1119,9 @@ def install(trainer_cls, device: Optional[torch.device] = None, client_cls=None,
     # instead of leaving wrappers that upload clients nobody reduces
     trainer_cls._mfl_stream_on = streaming
     trainer_cls._mfl_stream_device = device
+    if torch.cuda.is_available():  # the HIP first-use costs, before the loop's round 0
+        for d in (devices or _devices_arg(device, None) or [device]):
+            default_aggregator(d).warm_up()
 
     def aggregate_method(self, w_locals):
         feed = self.__dict__.get("_mfl_feed") if streaming else None

@@ -37,79 +37,94 @@ static py::tuple collect(py::list dicts, py::list names, py::list templ, int64_t
     sizes[j] = ten.sizes().vec();
     dtypes[j] = ten.scalar_type();
   }
-  // pass 1 (GIL): the value objects, [K][N].  A dict whose entries are the
-  // names in order (the deep copies of :199 share client 0's key strings) is
-  // read by PyDict_Next with identity compares; anything else by lookups,
-  // whose new references are held until the end
+  // the value objects, [K][N]: a dict whose entries are the names in order
+  // by identity (the deep copies of :199 share client 0's key strings) is
+  // read by PyDict_Next on torch's intra-op threads together with the
+  // metadata checks below; any other mapping afterwards on this thread by
+  // lookups (their new references held until the end).  The calling thread
+  // keeps the GIL: no Python code runs meanwhile, and the threads call no
+  // Python API besides PyDict_Next (no reference counts touched)
   std::vector<PyObject*> vals(static_cast<size_t>(K) * N);
   std::vector<PyObject*> owned;
   auto release = [&owned] {
     for (PyObject* o : owned) Py_DECREF(o);
     owned.clear();
   };
-  for (Py_ssize_t i = 0; i < K; ++i) {
-    PyObject* d = PyList_GET_ITEM(dicts.ptr(), i);
-    PyObject** row = &vals[static_cast<size_t>(i) * N];
-    bool fast = PyDict_Check(d) && PyDict_Size(d) == N;
-    if (fast) {
-      Py_ssize_t pos = 0, j = 0;
-      PyObject *key, *val;
-      while (PyDict_Next(d, &pos, &key, &val)) {
-        if (j >= N || key != PyList_GET_ITEM(names.ptr(), j)) {
-          fast = false;
-          break;
-        }
-        row[j++] = val;
-        __builtin_prefetch(val);
-      }
-      fast = fast && j == N;
-    }
-    if (!fast) {
-      for (Py_ssize_t j = 0; j < N; ++j) {
-        PyObject* t = PyObject_GetItem(d, PyList_GET_ITEM(names.ptr(), j));  // new reference
-        if (!t) {
-          PyErr_Clear();
-          release();
-          return py::make_tuple(py::none(), i, j);
-        }
-        owned.push_back(t);
-        row[j] = t;
-      }
-    }
-  }
-  // pass 2 (torch's intra-op threads, the GIL held by this thread: no Python
-  // code runs meanwhile and no Python API is called): metadata checks and
-  // data pointers, bound by cache misses on scattered tensor objects
+  std::vector<PyObject*> name_ptr(N);
+  for (Py_ssize_t j = 0; j < N; ++j) name_ptr[j] = PyList_GET_ITEM(names.ptr(), j);
+  std::vector<PyObject*> dobj(K);
+  for (Py_ssize_t i = 0; i < K; ++i) dobj[i] = PyList_GET_ITEM(dicts.ptr(), i);
   auto ptrs = torch::empty({static_cast<int64_t>(K), static_cast<int64_t>(N)}, torch::kInt64);
   int64_t* out = ptrs.data_ptr<int64_t>();
-  std::vector<int64_t> bad(static_cast<size_t>(K), -1);  // per client: first failing key
-  at::parallel_for(0, K, 1, [&](int64_t i0, int64_t i1) {
-    for (int64_t i = i0; i < i1; ++i) {
-      PyObject* const* row = &vals[static_cast<size_t>(i) * N];
-      constexpr Py_ssize_t kAhead = 8;
-      for (Py_ssize_t j = 0; j < N && j < kAhead; ++j)
-        if (THPVariable_CheckExact(row[j])) __builtin_prefetch(THPVariable_Unpack(row[j]).unsafeGetTensorImpl());
-      for (Py_ssize_t j = 0; j < N; ++j) {
-        if (j + kAhead < N && THPVariable_CheckExact(row[j + kAhead]))
-          __builtin_prefetch(THPVariable_Unpack(row[j + kAhead]).unsafeGetTensorImpl());
-        PyObject* t = row[j];
-        // exact Tensor / Parameter only (no isinstance walk off the GIL
-        // thread): a Tensor subclass goes to the general Python path
-        bool ok = THPVariable_CheckExact(t);
-        if (ok) {
-          const at::Tensor& ten = THPVariable_Unpack(t);
-          const bool where = device_index < 0 ? ten.is_cpu() : (ten.is_cuda() && ten.get_device() == device_index);
-          ok = ten.scalar_type() == dtypes[j] && ten.sizes() == c10::IntArrayRef(sizes[j]) && where &&
-               ten.is_contiguous();
-          if (ok) out[i * N + j] = reinterpret_cast<int64_t>(ten.data_ptr());
-        }
-        if (!ok) {
-          bad[i] = j;
-          break;
-        }
+  std::vector<int64_t> bad(static_cast<size_t>(K), -1);  // per client: first failing key; kRedo: lookups
+  constexpr int64_t kRedo = -2;
+  // metadata checks and data pointers of client i (its vals filled)
+  const auto check_client = [&](int64_t i) {
+    PyObject* const* row = &vals[static_cast<size_t>(i) * N];
+    constexpr Py_ssize_t kAhead = 8;
+    for (Py_ssize_t j = 0; j < N && j < kAhead; ++j)
+      if (THPVariable_CheckExact(row[j])) __builtin_prefetch(THPVariable_Unpack(row[j]).unsafeGetTensorImpl());
+    for (Py_ssize_t j = 0; j < N; ++j) {
+      if (j + kAhead < N && THPVariable_CheckExact(row[j + kAhead]))
+        __builtin_prefetch(THPVariable_Unpack(row[j + kAhead]).unsafeGetTensorImpl());
+      PyObject* t = row[j];
+      // exact Tensor / Parameter only (no isinstance walk off the GIL
+      // thread): a Tensor subclass goes to the general Python path
+      bool ok = THPVariable_CheckExact(t);
+      if (ok) {
+        const at::Tensor& ten = THPVariable_Unpack(t);
+        const bool where = device_index < 0 ? ten.is_cpu() : (ten.is_cuda() && ten.get_device() == device_index);
+        ok = ten.scalar_type() == dtypes[j] && ten.sizes() == c10::IntArrayRef(sizes[j]) && where &&
+             ten.is_contiguous();
+        if (ok) out[i * N + j] = reinterpret_cast<int64_t>(ten.data_ptr());
+      }
+      if (!ok) {
+        bad[i] = j;
+        return;
       }
     }
+  };
+  at::parallel_for(0, K, 1, [&](int64_t i0, int64_t i1) {
+    for (int64_t i = i0; i < i1; ++i) {
+      PyObject* d = dobj[i];
+      bool fast = PyDict_Check(d) && PyDict_Size(d) == N;
+      if (fast) {
+        Py_ssize_t pos = 0, j = 0;
+        PyObject *key, *val;
+        PyObject** row = &vals[static_cast<size_t>(i) * N];
+        while (PyDict_Next(d, &pos, &key, &val)) {
+          if (j >= N || key != name_ptr[j]) {
+            fast = false;
+            break;
+          }
+          row[j++] = val;
+          __builtin_prefetch(val);
+        }
+        fast = fast && j == N;
+      }
+      if (!fast) {
+        bad[i] = kRedo;
+        continue;
+      }
+      check_client(i);
+    }
   });
+  for (Py_ssize_t i = 0; i < K; ++i) {  // other mappings / key objects: lookups on this thread
+    if (bad[i] != kRedo) continue;
+    bad[i] = -1;
+    PyObject** row = &vals[static_cast<size_t>(i) * N];
+    for (Py_ssize_t j = 0; j < N; ++j) {
+      PyObject* t = PyObject_GetItem(dobj[i], name_ptr[j]);  // new reference
+      if (!t) {
+        PyErr_Clear();
+        release();
+        return py::make_tuple(py::none(), i, j);
+      }
+      owned.push_back(t);
+      row[j] = t;
+    }
+    check_client(i);
+  }
   release();  // the dicts keep their tensors alive
   for (Py_ssize_t i = 0; i < K; ++i)
     if (bad[i] >= 0) return py::make_tuple(py::none(), i, bad[i]);
@@ -387,104 +402,125 @@ static py::tuple verify_rows(py::list w_locals, py::list counts, py::list names,
     for (size_t a = 1; a < sorted.size(); ++a)
       if (sorted[a] == sorted[a - 1]) return res(4, -1, -1, 0);  // the plain path handles aliased clients
   }
-  // pass 1 (GIL): each dict's entry table in order -- the keys by identity
-  // (the deep copies share the key strings; == otherwise), the values'
-  // object pointers, nothing dereferenced
+  // One walk per client, clients split over torch's intra-op threads.  The
+  // calling thread keeps the GIL throughout, so no Python code runs and no
+  // object changes meanwhile; the threads read dict entry tables
+  // (PyDict_Next: no reference counts touched) and tensor metadata, and call
+  // nothing else of the Python API.  The walk is bound by cache misses on
+  // scattered objects (resnet56 x 100: 35,000 tensors, ~150 ns each on one
+  // thread), hence the threads and the prefetches a few keys ahead.
+  // A dict whose keys are not the table's names by identity (the deep
+  // copies of :199 share client 0's key strings) is redone afterwards on
+  // this thread with == compares.
+  std::vector<PyObject*> name_ptr(N);
+  for (Py_ssize_t j = 0; j < N; ++j) name_ptr[j] = PyList_GET_ITEM(names.ptr(), j);
   std::vector<PyObject*> vals(static_cast<size_t>(K) * N);
-  for (Py_ssize_t i = 0; i < K; ++i) {
-    Py_ssize_t pos = 0, j = 0;
-    PyObject *key, *val;
-    while (PyDict_Next(dicts[i], &pos, &key, &val)) {
-      if (j >= N) return res(5, i, j, 0);
-      PyObject* name = PyList_GET_ITEM(names.ptr(), j);
-      if (key != name) {
-        const int eq = PyObject_RichCompareBool(key, name, Py_EQ);
-        if (eq != 1) {
-          if (eq < 0) PyErr_Clear();
-          return res(5, i, j, 0);
-        }
-      }
-      vals[static_cast<size_t>(i) * N + j] = val;
-      __builtin_prefetch(val);  // the THPVariable: pass 2 reads its tensor pointer
-      ++j;
-    }
-    if (j != N) return res(5, i, j, 0);
-  }
-  // pass 2 (torch's intra-op threads; the GIL stays with this thread, so no
-  // Python code runs and no object changes meanwhile; no Python API is
-  // called): every value's tensor metadata, then the probed element values.
-  // The walk is bound by cache misses on 35,000 scattered objects
-  // (resnet56 x 100): one thread pays ~150 ns per tensor, so the clients are
-  // split over the threads (5.2 -> 0.4 ms on 8 cores) and each thread
-  // prefetches the TensorImpls a few keys ahead
   std::vector<int64_t> status(static_cast<size_t>(K), 0);  // per client: 0, or (code << 32 | key)
   std::vector<int64_t> nprobe(static_cast<size_t>(K), 0);
+  constexpr int64_t kRedo = -1;  // keys not identical: == compares on the GIL thread
+  const auto fill_fast = [&](int64_t i) -> bool {
+    Py_ssize_t pos = 0, j = 0;
+    PyObject *key, *val;
+    PyObject** row = &vals[static_cast<size_t>(i) * N];
+    while (PyDict_Next(dicts[i], &pos, &key, &val)) {
+      if (j >= N || key != name_ptr[j]) return false;
+      row[j++] = val;
+      __builtin_prefetch(val);
+    }
+    return j == N;
+  };
+  // metadata checks and value probes of client i (its vals filled)
+  const auto check_client = [&](int64_t i, std::vector<Probe>& todo) {
+    todo.clear();
+    int64_t st = 0;
+    PyObject* const* row_vals = &vals[static_cast<size_t>(i) * N];
+    constexpr Py_ssize_t kAhead = 8;  // TensorImpls prefetched this many keys ahead (scattered heap objects)
+    for (Py_ssize_t j = 0; j < N && j < kAhead; ++j)
+      if (THPVariable_CheckExact(row_vals[j])) __builtin_prefetch(THPVariable_Unpack(row_vals[j]).unsafeGetTensorImpl());
+    for (Py_ssize_t j = 0; j < N && !st; ++j) {
+      if (j + kAhead < N && THPVariable_CheckExact(row_vals[j + kAhead]))
+        __builtin_prefetch(THPVariable_Unpack(row_vals[j + kAhead]).unsafeGetTensorImpl());
+      PyObject* val = row_vals[j];
+      if (!THPVariable_CheckExact(val)) {  // a Tensor subclass: the plain path decides
+        st = (int64_t(6) << 32) | j;
+        break;
+      }
+      const at::Tensor& ten = THPVariable_Unpack(val);
+      if (ten.scalar_type() != tp[j]->scalar_type() || ten.sizes() != tp[j]->sizes() || !ten.is_cpu() ||
+          !ten.is_contiguous()) {
+        st = (int64_t(6) << 32) | j;
+        break;
+      }
+      const int64_t n = numel[j];
+      if (n <= 0) continue;
+      const int64_t g = group[j];
+      const int es = static_cast<int>(stage_esize[g]);
+      const int src_es = static_cast<int>(ten.element_size());
+      const char* src = static_cast<const char*>(ten.data_ptr());
+      const char* srow = reinterpret_cast<const char*>(stage_ptr[g]) + (i * stage_ld[g] + offset[j]) * es;
+      if (full) {
+        bool same = true;
+        if (kind[j] == 0) {
+          same = std::memcmp(src, srow, static_cast<size_t>(n) * es) == 0;
+        } else {
+          for (int64_t p = 0; p < n && same; ++p)
+            same = probe_equal(Probe{src + p * src_es, srow + p * es, static_cast<int>(kind[j]), es, 0, 0});
+        }
+        if (!same) st = (int64_t(7) << 32) | j;
+        nprobe[i] += n;
+        continue;
+      }
+      const uint64_t h = mix64(seed ^ mix64(static_cast<uint64_t>(i) * 0x100000001B3ull + static_cast<uint64_t>(j)));
+      const bool anchor = static_cast<int64_t>(mix64(seed + static_cast<uint64_t>(j)) % static_cast<uint64_t>(K)) == i;
+      if (!anchor && h > thresh) continue;
+      for (int q = 0; q < 2; ++q) {  // two positions per probed pair
+        const int64_t p = static_cast<int64_t>(mix64(h + 1 + q) % static_cast<uint64_t>(n));
+        todo.push_back(Probe{src + p * src_es, srow + p * es, static_cast<int>(kind[j]), es, static_cast<int>(i),
+                             static_cast<int>(j)});
+      }
+    }
+    if (!st)
+      for (const Probe& p : todo)
+        if (!probe_equal(p)) {
+          st = (int64_t(7) << 32) | p.j;
+          break;
+        }
+    status[i] = st;
+    nprobe[i] += static_cast<int64_t>(todo.size());
+  };
   at::parallel_for(0, K, 1, [&](int64_t i0, int64_t i1) {
     std::vector<Probe> todo;
     for (int64_t i = i0; i < i1; ++i) {
-      todo.clear();
-      int64_t st = 0;
-      PyObject* const* row_vals = &vals[static_cast<size_t>(i) * N];
-      constexpr Py_ssize_t kAhead = 8;  // TensorImpls prefetched this many keys ahead (scattered heap objects)
-      for (Py_ssize_t j = 0; j < N && j < kAhead; ++j)
-        if (THPVariable_CheckExact(row_vals[j])) __builtin_prefetch(THPVariable_Unpack(row_vals[j]).unsafeGetTensorImpl());
-      for (Py_ssize_t j = 0; j < N && !st; ++j) {
-        if (j + kAhead < N && THPVariable_CheckExact(row_vals[j + kAhead]))
-          __builtin_prefetch(THPVariable_Unpack(row_vals[j + kAhead]).unsafeGetTensorImpl());
-        PyObject* val = row_vals[j];
-        if (!THPVariable_CheckExact(val)) {  // a Tensor subclass: the plain path decides
-          st = (int64_t(6) << 32) | j;
-          break;
-        }
-        const at::Tensor& ten = THPVariable_Unpack(val);
-        if (ten.scalar_type() != tp[j]->scalar_type() || ten.sizes() != tp[j]->sizes() || !ten.is_cpu() ||
-            !ten.is_contiguous()) {
-          st = (int64_t(6) << 32) | j;
-          break;
-        }
-        const int64_t n = numel[j];
-        if (n <= 0) continue;
-        if (full) {
-          const int64_t g = group[j];
-          const int es = static_cast<int>(stage_esize[g]);
-          const int src_es = static_cast<int>(ten.element_size());
-          const char* src = static_cast<const char*>(ten.data_ptr());
-          const char* row = reinterpret_cast<const char*>(stage_ptr[g]) + (i * stage_ld[g] + offset[j]) * es;
-          bool same = true;
-          if (kind[j] == 0) {
-            same = std::memcmp(src, row, static_cast<size_t>(n) * es) == 0;
-          } else {
-            for (int64_t p = 0; p < n && same; ++p)
-              same = probe_equal(Probe{src + p * src_es, row + p * es, static_cast<int>(kind[j]), es, 0, 0});
-          }
-          if (!same) st = (int64_t(7) << 32) | j;
-          nprobe[i] += n;
-          continue;
-        }
-        const uint64_t h = mix64(seed ^ mix64(static_cast<uint64_t>(i) * 0x100000001B3ull + static_cast<uint64_t>(j)));
-        const bool anchor = static_cast<int64_t>(mix64(seed + static_cast<uint64_t>(j)) % static_cast<uint64_t>(K)) == i;
-        if (!anchor && h > thresh) continue;
-        const int64_t g = group[j];
-        const int es = static_cast<int>(stage_esize[g]);
-        const int src_es = static_cast<int>(ten.element_size());
-        const char* src = static_cast<const char*>(ten.data_ptr());
-        const char* row = reinterpret_cast<const char*>(stage_ptr[g]) + (i * stage_ld[g] + offset[j]) * es;
-        for (int q = 0; q < 2; ++q) {  // two positions per probed pair
-          const int64_t p = static_cast<int64_t>(mix64(h + 1 + q) % static_cast<uint64_t>(n));
-          todo.push_back(Probe{src + p * src_es, row + p * es, static_cast<int>(kind[j]), es, static_cast<int>(i),
-                               static_cast<int>(j)});
-        }
+      if (!fill_fast(i)) {
+        status[i] = kRedo;
+        continue;
       }
-      if (!st)
-        for (const Probe& p : todo)
-          if (!probe_equal(p)) {
-            st = (int64_t(7) << 32) | p.j;
-            break;
-          }
-      status[i] = st;
-      nprobe[i] += static_cast<int64_t>(todo.size());
+      check_client(i, todo);
     }
   });
+  {  // dicts whose keys are equal but not identical to the names: == on this thread
+    std::vector<Probe> todo;
+    for (Py_ssize_t i = 0; i < K; ++i) {
+      if (status[i] != kRedo) continue;
+      Py_ssize_t pos = 0, j = 0;
+      PyObject *key, *val;
+      status[i] = 0;
+      while (PyDict_Next(dicts[i], &pos, &key, &val)) {
+        if (j >= N) break;
+        const int eq = key == name_ptr[j] ? 1 : PyObject_RichCompareBool(key, name_ptr[j], Py_EQ);
+        if (eq != 1) {
+          if (eq < 0) PyErr_Clear();
+          break;
+        }
+        vals[static_cast<size_t>(i) * N + j++] = val;
+      }
+      if (j != N) {
+        status[i] = (int64_t(5) << 32) | j;
+        continue;
+      }
+      check_client(i, todo);
+    }
+  }
   int64_t total = 0;
   for (Py_ssize_t i = 0; i < K; ++i) {
     total += nprobe[i];

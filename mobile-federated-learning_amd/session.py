@@ -145,6 +145,7 @@ class RoundSession:
         if getattr(agg, "_finish_warm", False) or not self.FINISH_WARMUP:
             return
         agg._finish_warm = True
+        agg.warm_up()  # streams, torch's kernels of the finish and :291 (DeviceAggregator.warm_up)
         from .aggregate import _fetch, reduce_rows
 
         with torch.cuda.device(self.dev):

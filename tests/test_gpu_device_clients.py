@@ -156,6 +156,52 @@ def test_pack_kernel_matches_host_packer():
     assert dev.cpu().view(torch.int32).numpy().tobytes() == host.view(torch.int32).numpy().tobytes()
 
 
+@pytest.mark.parametrize("es", [4, 8, 2])
+def test_pack_kernel_many_tiny_items(es):
+    """Thousands of 1-40 element items (BatchNorm's scalar num_batches_tracked
+    over every client): fedavg_pack_rows_device takes its thread-per-item
+    kernel (average <= 64 elements); byte for byte against the host packer,
+    every kind for fp32 rows, raw items for 8- and 2-byte rows."""
+    lib = mfl_amd._lib.load()
+    rng = np.random.default_rng(es)
+    g = torch.Generator().manual_seed(es)
+    kinds = {0: {4: torch.float32, 8: torch.float64, 2: torch.float16}[es], 1: torch.int64, 2: torch.int32,
+             3: torch.int16, 4: torch.int8, 5: torch.uint8, 6: torch.bool}
+    srcs_h, items, off = [], [], 3
+    for j in range(3000):
+        kind = int(rng.integers(0, 7)) if es == 4 else 0
+        n = int(rng.integers(0, 41)) if j % 5 else 1
+        dt = kinds[kind]
+        if dt == torch.bool:
+            t = torch.rand(n, generator=g) > 0.5
+        elif dt.is_floating_point:
+            t = torch.randn(n, generator=g).to(dt)
+        elif dt == torch.uint8:
+            t = torch.randint(0, 256, (n,), generator=g).to(dt)
+        else:
+            t = torch.randint(-(2**31), 2**31 - 1, (n,), generator=g).to(dt)
+            if dt == torch.int64:
+                t = t * 4099 + 3
+        srcs_h.append(t)
+        items.append((kind, off, n))
+        off += n + int(rng.integers(0, 3))
+    srcs_d = [t.to(DEV) for t in srcs_h]
+    it_h = np.array([[t.data_ptr(), n, o, k] for t, (k, o, n) in zip(srcs_h, items)], dtype=np.int64)
+    it_d = np.array([[t.data_ptr(), n, o, k] for t, (k, o, n) in zip(srcs_d, items)], dtype=np.int64)
+    dt_row = kinds[0]
+    host = torch.full((off + 5,), -7.0, dtype=dt_row)
+    mfl_amd._lib.check(lib.fedavg_pack_rows(it_h.ctypes.data, len(items), host.data_ptr(), es, 4), "pack")
+    dev = torch.full((off + 5,), -7.0, dtype=dt_row, device=DEV)
+    need = lib.fedavg_pack_rows_device_workspace(len(items))
+    ws_h = torch.empty(need, dtype=torch.uint8, pin_memory=True)
+    ws_d = torch.empty(need, dtype=torch.uint8, device=DEV)
+    s = torch.cuda.current_stream(DEV)
+    mfl_amd._lib.check(lib.fedavg_pack_rows_device(it_d.ctypes.data, len(items), dev.data_ptr(), es, ws_h.data_ptr(),
+                                                   ws_d.data_ptr(), need, s.cuda_stream), "pack_device")
+    s.synchronize()
+    assert dev.cpu().view(torch.uint8).numpy().tobytes() == host.view(torch.uint8).numpy().tobytes()
+
+
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float16, torch.bfloat16])
 def test_pack_kernel_raw_other_widths(dtype):
     lib = mfl_amd._lib.load()
