@@ -324,6 +324,7 @@ class DeviceAggregator:
     # warm_up() pays them once, off the round: install() calls it before the
     # loop runs, and a RoundSession's first add() (while clients train).
     WARMUP = os.environ.get("FEDAVG_WARMUP", "1") != "0"
+    WARMUP_COPIES = int(os.environ.get("FEDAVG_WARMUP_COPIES", "16"))
 
     def warm_up(self) -> None:
         """Create the aggregator's streams and launch, once, every kernel a
@@ -342,6 +343,18 @@ class DeviceAggregator:
                 z = sums + sums
                 bool(torch.isfinite(out).all())  # also waits for the work above
                 del z
+            # the runtime's first DMA copies each way: rounds 0-1 of a process
+            # issued their D2H chunks 10x slower than later rounds (DESIGN.md
+            # section 6); a few round-trips of a 4 MB scratch here
+            host = torch.empty(1 << 20, dtype=torch.float32, pin_memory=True)
+            dev = torch.empty(1 << 20, dtype=torch.float32, device=self.device)
+            for _ in range(self.WARMUP_COPIES):
+                with torch.cuda.stream(copy_s):
+                    dev.copy_(host, non_blocking=True)
+                d2h.wait_stream(copy_s)
+                _fetch(dev, host, d2h)
+                copy_s.wait_stream(d2h)
+            d2h.synchronize()
             copy_s.synchronize()
 
     # ------------------------------------------------------------------

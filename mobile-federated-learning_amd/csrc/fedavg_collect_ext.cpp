@@ -24,6 +24,27 @@
 
 namespace py = pybind11;
 
+// Key equality without the Python API, for the walker threads: the key
+// objects of different clients' state_dicts are equal strings but rarely the
+// same objects (each net.cpu().state_dict() call builds its own names,
+// client.py:96), so an identity test alone sends every client to the slow
+// path.  Exact str objects compare by length, kind and bytes (immutable once
+// ready; the cached hashes when both exist); anything else reports "unknown"
+// and the caller falls back to PyObject_RichCompareBool under the GIL.
+enum class KeyEq { kSame, kDiffer, kUnknown };
+static inline KeyEq key_eq(PyObject* a, PyObject* b) {
+  if (a == b) return KeyEq::kSame;
+  if (!PyUnicode_CheckExact(a) || !PyUnicode_CheckExact(b) || !PyUnicode_IS_READY(a) || !PyUnicode_IS_READY(b))
+    return KeyEq::kUnknown;
+  const Py_ssize_t n = PyUnicode_GET_LENGTH(a);
+  if (n != PyUnicode_GET_LENGTH(b) || PyUnicode_KIND(a) != PyUnicode_KIND(b)) return KeyEq::kDiffer;
+  const Py_hash_t ha = reinterpret_cast<PyASCIIObject*>(a)->hash, hb = reinterpret_cast<PyASCIIObject*>(b)->hash;
+  if (ha != -1 && hb != -1 && ha != hb) return KeyEq::kDiffer;
+  return std::memcmp(PyUnicode_DATA(a), PyUnicode_DATA(b), static_cast<size_t>(n) * PyUnicode_KIND(a)) == 0
+             ? KeyEq::kSame
+             : KeyEq::kDiffer;
+}
+
 static py::tuple collect(py::list dicts, py::list names, py::list templ, int64_t device_index) {
   const Py_ssize_t K = PyList_GET_SIZE(dicts.ptr());
   const Py_ssize_t N = PyList_GET_SIZE(names.ptr());
@@ -38,8 +59,7 @@ static py::tuple collect(py::list dicts, py::list names, py::list templ, int64_t
     dtypes[j] = ten.scalar_type();
   }
   // the value objects, [K][N]: a dict whose entries are the names in order
-  // by identity (the deep copies of :199 share client 0's key strings) is
-  // read by PyDict_Next on torch's intra-op threads together with the
+  // (exact strings, key_eq) is read by PyDict_Next on torch's intra-op threads together with the
   // metadata checks below; any other mapping afterwards on this thread by
   // lookups (their new references held until the end).  The calling thread
   // keeps the GIL: no Python code runs meanwhile, and the threads call no
@@ -93,7 +113,7 @@ static py::tuple collect(py::list dicts, py::list names, py::list templ, int64_t
         PyObject *key, *val;
         PyObject** row = &vals[static_cast<size_t>(i) * N];
         while (PyDict_Next(d, &pos, &key, &val)) {
-          if (j >= N || key != name_ptr[j]) {
+          if (j >= N || key_eq(key, name_ptr[j]) != KeyEq::kSame) {
             fast = false;
             break;
           }
@@ -297,28 +317,29 @@ static py::tuple small_round(py::list w_locals, py::list names, py::list templ, 
 }
 
 // verify_rows(w_locals, counts, names, templ, group, offset, kind, stage_ptr, stage_ld, stage_esize,
-//             probes, seed) -> (status, client, key, probes_checked)
+//             probes, seed, full_elems) -> (status, client, key, elements_checked)
 //
 // Does w_locals (the reference's :199 deep copies) hold what a streamed
 // round's staging rows were packed from?  autostream.py fed each client's
-// Client.train result to the packer while the loop went on; at :217 this walk
-// checks, with the GIL held,
+// Client.train result to the packer while the loop went on; at :217 this
+// walk checks
 //   * len(w_locals) == len(counts) and every w_locals[i] is a (n, dict) pair
 //     whose n == counts[i] (Python ==) and whose dict is not another
 //     client's dict object;
 //   * every client's dict holds exactly the table's keys in order
-//     (PyDict_Next, key identity or ==: the deep copies share the key
-//     strings), and every value is a contiguous host tensor with the
-//     template's dtype and sizes;
-// and then, with the GIL released, compares element values at `probes`
-// (client, key, position) triples drawn afresh from `seed` every round --
-// every key at least once (at a random client), the rest spread uniformly
-// over all (client, key) pairs, positions uniform inside the key -- against
-// the pinned staging rows the H2D copies uploaded, converted as the packer
-// converts (fp32/fp64/fp16/bf16 keys raw, integer/bool keys static_cast to
-// fp32: fedavg_host.cpp).  Equal converted values reduce to the same bits,
-// so a match is exactly the reduction's criterion at that element.
-// Returns probes_checked = elements compared.
+//     (PyDict_Next; key_eq, or == for keys that are not exact strings), and
+//     every value is a contiguous host tensor with the template's dtype and
+//     sizes;
+//   * element values at `probes` (client, key, position) triples drawn
+//     afresh from `seed` every round -- every key at least once (at a random
+//     client), the rest spread uniformly over all (client, key) pairs,
+//     positions uniform inside the key -- against the pinned staging rows
+//     the H2D copies uploaded (every element when the round has at most
+//     `full_elems` of them), converted as the packer converts
+//     (fp32/fp64/fp16/bf16 keys raw, integer/bool keys static_cast to fp32:
+//     fedavg_host.cpp).  Equal converted values reduce to the same bits, so
+//     a match is exactly the reduction's criterion at that element.
+// The per-client walks run on torch's intra-op threads (see below).
 // status 0: all checks passed; 1 count; 2 sample number; 3 not a (n, dict)
 // pair; 4 repeated dict; 5 keys; 6 tensor metadata; 7 value (client, key).
 namespace {
@@ -409,9 +430,8 @@ static py::tuple verify_rows(py::list w_locals, py::list counts, py::list names,
   // nothing else of the Python API.  The walk is bound by cache misses on
   // scattered objects (resnet56 x 100: 35,000 tensors, ~150 ns each on one
   // thread), hence the threads and the prefetches a few keys ahead.
-  // A dict whose keys are not the table's names by identity (the deep
-  // copies of :199 share client 0's key strings) is redone afterwards on
-  // this thread with == compares.
+  // A dict whose keys are not the table's names as exact strings (key_eq)
+  // is redone afterwards on this thread with == compares.
   std::vector<PyObject*> name_ptr(N);
   for (Py_ssize_t j = 0; j < N; ++j) name_ptr[j] = PyList_GET_ITEM(names.ptr(), j);
   std::vector<PyObject*> vals(static_cast<size_t>(K) * N);
@@ -423,7 +443,7 @@ static py::tuple verify_rows(py::list w_locals, py::list counts, py::list names,
     PyObject *key, *val;
     PyObject** row = &vals[static_cast<size_t>(i) * N];
     while (PyDict_Next(dicts[i], &pos, &key, &val)) {
-      if (j >= N || key != name_ptr[j]) return false;
+      if (j >= N || key_eq(key, name_ptr[j]) != KeyEq::kSame) return false;
       row[j++] = val;
       __builtin_prefetch(val);
     }
