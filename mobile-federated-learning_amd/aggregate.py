@@ -81,6 +81,11 @@ class _Prepared(tuple):
     """(acc_dict, KeyTable, state_dicts, weights, src_ptrs, keepalive) for a non-trivial call."""
 
 
+class _Flats(list):
+    """[(Group, flat result)] of a round: written into client 0's dict by
+    KeyTable.unpack_into (one native call per dtype group)."""
+
+
 def prepare(w_locals, model_global=None, table_hint: Optional[KeyTable] = None):
     """Host-side part of ``aggregate``: the reference's early returns and errors.
 
@@ -427,10 +432,15 @@ class DeviceAggregator:
         if self._last.get("segments"):
             # client 0's own tensors: its dict is about to hold the average
             # (:449), and the rows of a zero-copy round are packed on demand
-            self._last["seg_keep0"] = OrderedDict((e.name, acc_dict[e.name]) for e in table.entries)
+            # (its keys are exactly the table's: prepare checked them)
+            self._last["seg_keep0"] = OrderedDict(acc_dict)
         # replace values in place, keeping client 0's key order (fedavg_trainer.py:450-457)
-        for e in table.entries:
-            acc_dict[e.name] = results[e.name]
+        if isinstance(results, _Flats):
+            for g, flat in results:
+                table.unpack_into(acc_dict, g, flat)
+        else:
+            for e in table.entries:
+                acc_dict[e.name] = results[e.name]
         return acc_dict
 
     def _client_device(self, table: KeyTable, dicts) -> torch.device:
@@ -676,7 +686,7 @@ class DeviceAggregator:
         reference's torch ops on device tensors)."""
         K, dev = ptrs.shape[0], self.device
         t0 = time.perf_counter()
-        results: "OrderedDict[str, torch.Tensor]" = OrderedDict()
+        results = _Flats()
         with torch.cuda.device(dev):
             compute = torch.cuda.current_stream(dev)
             if self._copy_stream is not None:
@@ -717,7 +727,7 @@ class DeviceAggregator:
                     self._last["dev"][g.dtype] = (st.dev[:K], out_dev)
                     if sums:
                         self._last.setdefault("sumsq", {})[g.dtype] = sums[0]
-                results.update(table.unpack(g, out_dev))
+                results.append((g, out_dev))
         self.last_profile = {"pack_issue_ms": (time.perf_counter() - t0) * 1e3, "h2d_kernel_d2h_ms": 0.0}
         return results
 
@@ -847,8 +857,7 @@ class DeviceAggregator:
             # reduce, so its completion covers the kernels too
             d2h.synchronize()
             t2 = time.perf_counter()
-        for g, out_host in outs:
-            results.update(table.unpack(g, out_host))
+        results = _Flats(outs)
         self.last_profile = {"pack_issue_ms": (t1 - t0) * 1e3, "h2d_kernel_d2h_ms": (t2 - t1) * 1e3}
         return results
 

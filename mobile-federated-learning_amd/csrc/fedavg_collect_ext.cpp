@@ -155,12 +155,14 @@ static py::tuple collect(py::list dicts, py::list names, py::list templ, int64_t
 // offsets[j] + numel(shapes[j])] shaped shapes[j] -- the averaged model's keys
 // as views of the one host buffer the reduction wrote (the Python loop costs
 // ~3.6 us per key: 1.3 ms for resnet56's 350 keys every round).
-static py::list unpack(const at::Tensor& flat, py::list offsets, py::list shapes) {
+// the key views of flat (unpack's) for every (offset, shape); view j is
+// handed to put(j, object) -- a list slot or a dict item
+template <typename Put>
+static void make_views(const at::Tensor& flat, py::list offsets, py::list shapes, Put put) {
   const Py_ssize_t N = PyList_GET_SIZE(offsets.ptr());
   if (PyList_GET_SIZE(shapes.ptr()) != N) throw std::invalid_argument("offsets/shapes length mismatch");
   if (flat.dim() != 1 || !flat.is_contiguous()) throw std::invalid_argument("flat must be a contiguous 1-D tensor");
   if (flat.requires_grad()) throw std::invalid_argument("unpack: flat must not require grad");
-  py::list out(N);
   std::vector<int64_t> size, stride;
   for (Py_ssize_t j = 0; j < N; ++j) {
     const int64_t off = PyLong_AsLongLong(PyList_GET_ITEM(offsets.ptr(), j));
@@ -181,9 +183,25 @@ static py::list unpack(const at::Tensor& flat, py::list offsets, py::list shapes
     auto impl = c10::make_intrusive<c10::TensorImpl>(c10::TensorImpl::VIEW, c10::Storage(flat.storage()),
                                                      flat.key_set(), flat.dtype());
     impl->set_sizes_and_strides(size, stride, std::make_optional<int64_t>(flat.storage_offset() + off));
-    out[j] = py::reinterpret_steal<py::object>(THPVariable_Wrap(at::Tensor(std::move(impl))));
+    put(j, py::reinterpret_steal<py::object>(THPVariable_Wrap(at::Tensor(std::move(impl)))));
   }
+}
+
+static py::list unpack(const at::Tensor& flat, py::list offsets, py::list shapes) {
+  py::list out(PyList_GET_SIZE(offsets.ptr()));
+  make_views(flat, offsets, shapes, [&](Py_ssize_t j, py::object v) { out[j] = std::move(v); });
   return out;
+}
+
+// unpack_into(target, flat, names, offsets, shapes): target[names[j]] = view j
+// (fedavg_trainer.py:455 assigns the averages into client 0's dict; existing
+// keys keep their place) without an intermediate dict
+static void unpack_into(py::object target, const at::Tensor& flat, py::list names, py::list offsets, py::list shapes) {
+  if (PyList_GET_SIZE(names.ptr()) != PyList_GET_SIZE(offsets.ptr()))
+    throw std::invalid_argument("names/offsets length mismatch");
+  make_views(flat, offsets, shapes, [&](Py_ssize_t j, py::object v) {
+    if (PyObject_SetItem(target.ptr(), PyList_GET_ITEM(names.ptr(), j), v.ptr()) != 0) throw py::error_already_set();
+  });
 }
 
 // small_round(w_locals, names, templ, numel, offset, kind, shapes, P, ld, rows_host, rows_dev, w_host, w_dev,
@@ -554,6 +572,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("collect", &collect, "validate clients against client 0 and gather data pointers", py::arg("dicts"),
         py::arg("names"), py::arg("templ"), py::arg("device_index") = -1);
   m.def("unpack", &unpack, "views of a flat buffer shaped like the key table's keys");
+  m.def("unpack_into", &unpack_into, "those views assigned into a dict by key name");
   m.def("small_round", &small_round, "the host side of a small fp32 round in one call");
   m.def("verify_rows", &verify_rows, "w_locals against a streamed round's staging rows (randomly sampled values)");
 }

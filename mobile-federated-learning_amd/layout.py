@@ -294,6 +294,27 @@ class KeyTable:
                     # TensorIterator applies when it promotes `int * float`
                     dst.copy_(src.reshape(-1).to(dst.dtype))
 
+    def unpack_into(self, target, group: Group, flat: torch.Tensor) -> None:
+        """``target[name] = `` the view of ``flat`` for every key of ``group``
+        (existing keys keep their place: fedavg_trainer.py:455 assigns into
+        client 0's dict) -- one native call, no intermediate dict."""
+        ext = _collect_ext()
+        if ext is not None and hasattr(ext, "unpack_into") and flat.dim() == 1 and flat.is_contiguous():
+            names, offsets, shapes = self._unpack_meta_of(group)
+            ext.unpack_into(target, flat, names, offsets, shapes)
+            return
+        for name, t in self.unpack(group, flat).items():
+            target[name] = t
+
+    @staticmethod
+    def _unpack_meta_of(group: Group):
+        meta = group.__dict__.get("_unpack_meta")
+        if meta is None:
+            meta = ([e.name for e in group.keys], [int(e.offset) for e in group.keys],
+                    [tuple(int(d) for d in e.shape) for e in group.keys])
+            group._unpack_meta = meta
+        return meta
+
     def unpack(self, group: Group, flat: torch.Tensor) -> "OrderedDict[str, torch.Tensor]":
         """Views of ``flat`` [>=P] shaped as the group's keys (result dtype)."""
         ext = _collect_ext()

@@ -41,6 +41,7 @@ def device_clients(name, dev, seed=0):
     for i in range(K):
         sd = OrderedDict()
         for k, s in shapes:
+            k = "".join(list(k))  # each client's own key strings, as every state_dict() call builds them
             if k.endswith("num_batches_tracked"):
                 sd[k] = torch.tensor(1000 + i, dtype=torch.int64, device=dev)
             else:
