@@ -344,10 +344,10 @@ static py::tuple small_round(py::list w_locals, py::list names, py::list templ, 
 //   * len(w_locals) == len(counts) and every w_locals[i] is a (n, dict) pair
 //     whose n == counts[i] (Python ==) and whose dict is not another
 //     client's dict object;
-//   * every client's dict holds exactly the table's keys in order
-//     (PyDict_Next; key_eq, or == for keys that are not exact strings), and
-//     every value is a contiguous host tensor with the template's dtype and
-//     sizes;
+//   * every client's dict holds exactly the table's keys in order (matched
+//     by the hashes in the dict's entry table, == where those differ);
+//   * at the probed pairs below, the value is a contiguous host tensor with
+//     the template's dtype and sizes;
 //   * element values at `probes` (client, key, position) triples drawn
 //     afresh from `seed` every round -- every key at least once (at a random
 //     client), the rest spread uniformly over all (client, key) pairs,
@@ -451,19 +451,31 @@ static py::tuple verify_rows(py::list w_locals, py::list counts, py::list names,
   // A dict whose keys are not the table's names as exact strings (key_eq)
   // is redone afterwards on this thread with == compares.
   std::vector<PyObject*> name_ptr(N);
-  for (Py_ssize_t j = 0; j < N; ++j) name_ptr[j] = PyList_GET_ITEM(names.ptr(), j);
+  std::vector<Py_hash_t> name_hash(N);
+  for (Py_ssize_t j = 0; j < N; ++j) {
+    name_ptr[j] = PyList_GET_ITEM(names.ptr(), j);
+    name_hash[j] = PyObject_Hash(name_ptr[j]);
+    if (name_hash[j] == -1) {
+      PyErr_Clear();
+      return res(5, -1, j, 0);
+    }
+  }
   std::vector<PyObject*> vals(static_cast<size_t>(K) * N);
   std::vector<int64_t> status(static_cast<size_t>(K), 0);  // per client: 0, or (code << 32 | key)
   std::vector<int64_t> nprobe(static_cast<size_t>(K), 0);
   constexpr int64_t kRedo = -1;  // keys not identical: == compares on the GIL thread
+  // The keys are matched by the hashes stored in the dict's own entry table
+  // (_PyDict_Next): the key objects themselves -- one cache miss each, every
+  // client's own strings -- are never read.  A dict whose entries do not
+  // match the names' hashes in order is redone on this thread with ==.
   const auto fill_fast = [&](int64_t i) -> bool {
     Py_ssize_t pos = 0, j = 0;
     PyObject *key, *val;
+    Py_hash_t h;
     PyObject** row = &vals[static_cast<size_t>(i) * N];
-    while (PyDict_Next(dicts[i], &pos, &key, &val)) {
-      if (j >= N || key_eq(key, name_ptr[j]) != KeyEq::kSame) return false;
+    while (_PyDict_Next(dicts[i], &pos, &key, &val, &h)) {
+      if (j >= N || (key != name_ptr[j] && h != name_hash[j])) return false;
       row[j++] = val;
-      __builtin_prefetch(val);
     }
     return j == N;
   };
@@ -472,12 +484,20 @@ static py::tuple verify_rows(py::list w_locals, py::list counts, py::list names,
     todo.clear();
     int64_t st = 0;
     PyObject* const* row_vals = &vals[static_cast<size_t>(i) * N];
-    constexpr Py_ssize_t kAhead = 8;  // TensorImpls prefetched this many keys ahead (scattered heap objects)
-    for (Py_ssize_t j = 0; j < N && j < kAhead; ++j)
-      if (THPVariable_CheckExact(row_vals[j])) __builtin_prefetch(THPVariable_Unpack(row_vals[j]).unsafeGetTensorImpl());
+    // the (client, key) pairs probed this round: each value's tensor checked
+    // (dtype, sizes, host, contiguous) and its elements compared; the other
+    // pairs are matched by key only -- every key is probed at one client or
+    // more each round (its anchor), so an edit of a key across clients is
+    // always seen, and the tensor objects of the rest are never touched
+    const auto probed = [&](Py_ssize_t j, uint64_t* hp) {
+      const uint64_t h = mix64(seed ^ mix64(static_cast<uint64_t>(i) * 0x100000001B3ull + static_cast<uint64_t>(j)));
+      *hp = h;
+      return full || h <= thresh ||
+             static_cast<int64_t>(mix64(seed + static_cast<uint64_t>(j)) % static_cast<uint64_t>(K)) == i;
+    };
     for (Py_ssize_t j = 0; j < N && !st; ++j) {
-      if (j + kAhead < N && THPVariable_CheckExact(row_vals[j + kAhead]))
-        __builtin_prefetch(THPVariable_Unpack(row_vals[j + kAhead]).unsafeGetTensorImpl());
+      uint64_t h;
+      if (!probed(j, &h)) continue;
       PyObject* val = row_vals[j];
       if (!THPVariable_CheckExact(val)) {  // a Tensor subclass: the plain path decides
         st = (int64_t(6) << 32) | j;
@@ -508,9 +528,6 @@ static py::tuple verify_rows(py::list w_locals, py::list counts, py::list names,
         nprobe[i] += n;
         continue;
       }
-      const uint64_t h = mix64(seed ^ mix64(static_cast<uint64_t>(i) * 0x100000001B3ull + static_cast<uint64_t>(j)));
-      const bool anchor = static_cast<int64_t>(mix64(seed + static_cast<uint64_t>(j)) % static_cast<uint64_t>(K)) == i;
-      if (!anchor && h > thresh) continue;
       for (int q = 0; q < 2; ++q) {  // two positions per probed pair
         const int64_t p = static_cast<int64_t>(mix64(h + 1 + q) % static_cast<uint64_t>(n));
         todo.push_back(Probe{src + p * src_es, srow + p * es, static_cast<int>(kind[j]), es, static_cast<int>(i),

@@ -334,10 +334,15 @@ class RoundSession:
 
     def _set_results(self, acc_dict, results) -> None:
         """acc_dict[name] = result (fedavg_trainer.py:455 replaces client 0's values)."""
-        old = []
-        for name, t in results.items():
-            old.append(acc_dict.get(name))
-            acc_dict[name] = t
+        if len(results) == len(acc_dict) and acc_dict.keys() == results.keys():
+            # every value replaced (one dtype group): two C-level calls
+            old = list(acc_dict.values())
+            acc_dict.update(results)
+        else:
+            old = []
+            for name, t in results.items():
+                old.append(acc_dict.get(name))
+                acc_dict[name] = t
         self._release(old)
 
     def _close(self, K, dev_state, acc_dict, sums=None):
