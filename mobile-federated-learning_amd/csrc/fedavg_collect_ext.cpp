@@ -71,7 +71,15 @@ static py::tuple collect(py::list dicts, py::list names, py::list templ, int64_t
     owned.clear();
   };
   std::vector<PyObject*> name_ptr(N);
-  for (Py_ssize_t j = 0; j < N; ++j) name_ptr[j] = PyList_GET_ITEM(names.ptr(), j);
+  std::vector<Py_hash_t> name_hash(N);
+  for (Py_ssize_t j = 0; j < N; ++j) {
+    name_ptr[j] = PyList_GET_ITEM(names.ptr(), j);
+    name_hash[j] = PyObject_Hash(name_ptr[j]);
+    if (name_hash[j] == -1) {
+      PyErr_Clear();
+      return py::make_tuple(py::none(), 0, j);
+    }
+  }
   std::vector<PyObject*> dobj(K);
   for (Py_ssize_t i = 0; i < K; ++i) dobj[i] = PyList_GET_ITEM(dicts.ptr(), i);
   auto ptrs = torch::empty({static_cast<int64_t>(K), static_cast<int64_t>(N)}, torch::kInt64);
@@ -111,16 +119,27 @@ static py::tuple collect(py::list dicts, py::list names, py::list templ, int64_t
       if (fast) {
         Py_ssize_t pos = 0, j = 0;
         PyObject *key, *val;
+        Py_hash_t h;
         PyObject** row = &vals[static_cast<size_t>(i) * N];
-        while (PyDict_Next(d, &pos, &key, &val)) {
-          if (j >= N || key_eq(key, name_ptr[j]) != KeyEq::kSame) {
+        thread_local std::vector<PyObject*> keys;
+        keys.resize(N);
+        // the dict's entry table in order: hashes against the names' (a miss
+        // ends the fast walk), key and value objects prefetched together ...
+        while (_PyDict_Next(d, &pos, &key, &val, &h)) {
+          if (j >= N || (key != name_ptr[j] && h != name_hash[j])) {
             fast = false;
             break;
           }
+          keys[j] = key;
           row[j++] = val;
+          __builtin_prefetch(key);
           __builtin_prefetch(val);
         }
         fast = fast && j == N;
+        // ... then the exact compare of every key (client i's own strings,
+        // already on their way into the cache)
+        for (Py_ssize_t jj = 0; fast && jj < N; ++jj)
+          fast = key_eq(keys[jj], name_ptr[jj]) == KeyEq::kSame;
       }
       if (!fast) {
         bad[i] = kRedo;
