@@ -397,6 +397,40 @@ int fedavg_reduce_sqdist_segments_f32(const int64_t* client_ptrs, const int64_t*
                                       int64_t partial_elems, double* sumsq, void* host_ws, void* dev_ws,
                                       int64_t ws_bytes, void* stream);
 
+/*
+ * A device-resident round's fp32 group in ONE call (the host side of
+ * fedavg_trainer.py:441-458 after the walk over the clients' state_dicts,
+ * with :291's sums when asked): replaces the per-round sequence "gather the
+ * group's pointer columns, convert the integer keys, upload the weights,
+ * stage the tables" with one pass over the walk's address table and one H2D.
+ *   client_ptrs [K][ptr_ld]: client k's device address of every key of the
+ *     model (the walk's table); key_index [n_keys]: the group key j's column
+ *     in it (NULL: column j); key_numel / key_offset / key_kind as
+ *     fedavg_reduce_segments_f32;
+ *   weights [K]: the reference's n_i / N as host doubles, rounded here to
+ *     fp32 (nearest even, as ATen rounds the scalar at :455);
+ *   sumsq (NULL: the reduce alone) with partials :
+ *     fedavg_reduce_sqdist_segments_partials(K) doubles;
+ *   int_scratch: device fp32, fedavg_device_round_scratch(...) floats, 16-B
+ *     aligned (NULL when that is 0): a fused round's integer / bool keys
+ *     (BatchNorm's num_batches_tracked) are converted into it first;
+ *   host_ws (pinned) / dev_ws (device): fedavg_device_round_workspace(K,
+ *     n_keys) bytes, 16-B aligned; host_ws must not be rewritten until
+ *     `stream` has passed the call.
+ * Returns 0 when `out` and the sums were written (the fused pass), 1 when
+ * only `out` was (sumsq NULL, K > 256 or an fp32 source not 16-B aligned:
+ * the caller forms :291 with fedavg_client_sqdist_segments_f32), or a
+ * negative code.  `out` has the bits of fedavg_reduce_segments_f32 either
+ * way.  Stream-ordered and asynchronous.
+ */
+int64_t fedavg_device_round_workspace(int64_t K, int64_t n_keys);
+int64_t fedavg_device_round_scratch(const int64_t* key_numel, const int64_t* key_kind, int64_t n_keys, int64_t K);
+int fedavg_device_round_f32(const int64_t* client_ptrs, int64_t ptr_ld, const int64_t* key_index,
+                            const int64_t* key_numel, const int64_t* key_offset, const int64_t* key_kind,
+                            int64_t n_keys, int64_t K, const double* weights, float* out, double* partials,
+                            int64_t partial_elems, double* sumsq, float* int_scratch, int64_t scratch_elems,
+                            void* host_ws, void* dev_ws, int64_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -39,6 +39,10 @@ SIGNATURES = {
     "fedavg_reduce_sqdist_segments_f32": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_i64, _vp, _vp, _vp, _c_i64, _vp,
                                                    _vp, _vp, _c_i64, _vp]),
     "fedavg_pack_rows_device": (_c_int, [_vp, _c_i64, _vp, _c_i64, _vp, _vp, _c_i64, _vp]),
+    "fedavg_device_round_workspace": (_c_i64, [_c_i64, _c_i64]),
+    "fedavg_device_round_scratch": (_c_i64, [_vp, _vp, _c_i64, _c_i64]),
+    "fedavg_device_round_f32": (_c_int, [_vp, _c_i64, _vp, _vp, _vp, _vp, _c_i64, _c_i64, _vp, _vp, _vp, _c_i64, _vp,
+                                         _vp, _c_i64, _vp, _vp, _c_i64, _vp]),
     "fedavg_round_f32": (_c_int, [_vp, _c_i64, _vp, _vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _c_int,
                                   _vp]),
     "fedavg_client_sqdist_workspace": (_c_i64, [_c_i64, _c_i64]),

@@ -490,105 +490,70 @@ class DeviceAggregator:
         return (np.ascontiguousarray(ptrs[:, g.key_index]), np.ascontiguousarray(g.numel),
                 np.ascontiguousarray(g.offset), np.ascontiguousarray(g.kind))
 
-    def _reduce_segments(self, g, ptrs, weights, stream) -> torch.Tensor:
-        """The fp32 group reduced from the clients' own tensors (zero-copy)."""
-        lib = _lib.load()
-        K = ptrs.shape[0]
-        cptrs, numel, offset, kind = self._segment_tables(g, ptrs)
-        w = self._seg_weights
-        if w is None or w.K < K:
-            w = self._seg_weights = _Weights(K, torch.float32, self.device)
-        w_dev = w.upload(weights, stream)
-        out_dev = torch.empty(g.P, dtype=torch.float32, device=self.device)
-        host_ws, dev_ws = self._stage_ws(lib.fedavg_segments_workspace(K, len(numel)))
-        _lib.check(lib.fedavg_reduce_segments_f32(cptrs.ctypes.data, numel.ctypes.data, offset.ctypes.data,
-                                                  kind.ctypes.data, len(numel), K, w_dev.data_ptr(),
-                                                  out_dev.data_ptr(), host_ws.data_ptr(), dev_ws.data_ptr(),
-                                                  host_ws.numel(), stream.cuda_stream), "fedavg_reduce_segments_f32")
-        self._table_ws_done.record(stream)
-        return out_dev
-
-    def _reduce_sqdist_segments(self, g, ptrs, weights, stream):
-        """The zero-copy reduce and the round's :291 sums in one pass
-        (fedavg_reduce_sqdist_segments_f32) when the round qualifies (K <= 256,
-        fused distances on, every fp32 source 16-B aligned): ``(out, sumsq)``,
-        else None."""
+    @staticmethod
+    def _round_meta(g, n_cols: int):
+        """The group's key columns for fedavg_device_round_f32, built once per
+        table: (key_index or None when the group is every key in order, numel,
+        offset, kind) as contiguous int64 arrays, and a per-K cache of the
+        integer keys' scratch size."""
         import numpy as np
 
-        K = ptrs.shape[0]
-        if not FUSE_DISTANCES or K > FUSED_SEGMENTS_MAX_K:
-            return None
-        cptrs, numel, offset, kind = self._segment_tables(g, ptrs)
-        raw = (kind == 0) & (numel > 0)
-        if bool(np.any(cptrs[:, raw] & 15)):
-            return None
-        lib = _lib.load()
-        ints = (kind != 0) & (numel > 0)
-        scratch = None  # held until the fused launch below is issued: it reads it
-        if bool(np.any(ints)):
-            cptrs, kind, scratch = self._int_keys_as_f32(cptrs, numel, kind, ints, stream)
-        w = self._seg_weights
-        if w is None or w.K < K:
-            w = self._seg_weights = _Weights(K, torch.float32, self.device)
-        w_dev = w.upload(weights, stream)
-        out_dev = torch.empty(g.P, dtype=torch.float32, device=self.device)
-        partials = torch.empty(max(1, lib.fedavg_reduce_sqdist_segments_partials(K)), dtype=torch.float64,
-                               device=self.device)
-        sumsq = torch.empty(K, dtype=torch.float64, device=self.device)
-        host_ws, dev_ws = self._stage_ws(lib.fedavg_segments_workspace(K, len(numel)))
-        _lib.check(lib.fedavg_reduce_sqdist_segments_f32(cptrs.ctypes.data, numel.ctypes.data, offset.ctypes.data,
-                                                         kind.ctypes.data, len(numel), K, w_dev.data_ptr(),
-                                                         out_dev.data_ptr(), partials.data_ptr(), partials.numel(),
-                                                         sumsq.data_ptr(), host_ws.data_ptr(), dev_ws.data_ptr(),
-                                                         host_ws.numel(), stream.cuda_stream),
-                   "fedavg_reduce_sqdist_segments_f32")
-        self._table_ws_done.record(stream)
-        del scratch  # freed in `stream` order: later users of its block run after this launch
-        return out_dev, sumsq
+        meta = g.__dict__.get("_round_meta")
+        if meta is None or meta[0] != n_cols:
+            ki = np.ascontiguousarray(g.key_index, dtype=np.int64)
+            whole = len(ki) == n_cols and bool(np.array_equal(ki, np.arange(n_cols)))
+            meta = g._round_meta = (n_cols, None if whole else ki, np.ascontiguousarray(g.numel, dtype=np.int64),
+                                    np.ascontiguousarray(g.offset, dtype=np.int64),
+                                    np.ascontiguousarray(g.kind, dtype=np.int64), {})
+        return meta
 
-    def _int_keys_as_f32(self, cptrs, numel, kind, ints, stream):
-        """A device round's integer / bool keys (BatchNorm's num_batches_tracked)
-        converted to fp32 columns on the device -- the packers' static_cast, one
-        fedavg_pack_rows_device launch into a [K, S] scratch, each key 16-B
-        aligned -- and the pointer table pointed at them as fp32 keys, so the
-        fused pass runs the fp32-only window kernels on every model (round 3
-        left such models on the LDS-DMA tiles).  Returns (cptrs, kind,
-        scratch); the caller holds ``scratch`` until the kernel that reads it
-        is issued (freed earlier, the caching allocator would hand its block
-        to the round's own output on the same stream)."""
+    def _device_round(self, g, ptrs, weights, stream):
+        """The fp32 group of a device-resident round from the clients' own
+        tensors in ONE native call (fedavg_device_round_f32): the walk's
+        address table, the reference's weights and the key table go in; the
+        averaged group and -- fused by default (K <= 256, 16-B aligned fp32
+        sources) -- the round's :291 sums come out.  Integer keys of a fused
+        round are converted into a device scratch first (held here until the
+        launches that read it are issued: freed earlier, the caching allocator
+        would hand its block to the round's own output on the same stream).
+        Returns ``(out, sumsq or None)``."""
         import numpy as np
 
         lib = _lib.load()
-        K = cptrs.shape[0]
-        idx = np.nonzero(ints)[0]
-        n_i = numel[idx]
-        pad = (n_i + 3) // 4 * 4
-        offs = np.concatenate([[0], np.cumsum(pad)[:-1]]).astype(np.int64)
-        S = int(pad.sum())
-        scratch = torch.empty((K, S), dtype=torch.float32, device=self.device)
-        rows = np.arange(K, dtype=np.int64)[:, None] * S
-        items = np.empty((K, len(idx), 4), dtype=np.int64)
-        items[:, :, 0] = cptrs[:, idx]
-        items[:, :, 1] = n_i[None, :]
-        items[:, :, 2] = rows + offs[None, :]
-        items[:, :, 3] = kind[idx][None, :]
-        items = items.reshape(-1, 4)
-        need = lib.fedavg_pack_rows_device_workspace(items.shape[0])
-        ws = self.__dict__.get("_int_ws")
-        if ws is None or ws[0].numel() < need:
-            cap = max(need, 1 << 14)
-            ws = self._int_ws = (torch.empty(cap, dtype=torch.uint8, pin_memory=True),
-                                 torch.empty(cap, dtype=torch.uint8, device=self.device), torch.cuda.Event())
-        ws[2].synchronize()  # the previous round's table upload has read the pinned half
-        _lib.check(lib.fedavg_pack_rows_device(items.ctypes.data, items.shape[0], scratch.data_ptr(), 4,
-                                               ws[0].data_ptr(), ws[1].data_ptr(), ws[0].numel(),
-                                               stream.cuda_stream), "fedavg_pack_rows_device")
-        ws[2].record(stream)
-        cptrs = cptrs.copy()
-        cptrs[:, idx] = scratch.data_ptr() + (rows + offs[None, :]) * 4
-        kind = kind.copy()
-        kind[idx] = 0
-        return cptrs, kind, scratch
+        K, n_cols = ptrs.shape
+        _, key_index, numel, offset, kind, scratch_of = self._round_meta(g, n_cols)
+        n = len(numel)
+        fuse = FUSE_DISTANCES and K <= FUSED_SEGMENTS_MAX_K
+        scratch = None
+        if fuse:
+            n_s = scratch_of.get(K)
+            if n_s is None:
+                n_s = scratch_of[K] = lib.fedavg_device_round_scratch(numel.ctypes.data, kind.ctypes.data, n, K)
+            if n_s:
+                scratch = torch.empty(n_s, dtype=torch.float32, device=self.device)
+            partials = torch.empty(max(1, lib.fedavg_reduce_sqdist_segments_partials(K)), dtype=torch.float64,
+                                   device=self.device)
+            sumsq = torch.empty(K, dtype=torch.float64, device=self.device)
+        else:
+            partials = sumsq = None
+        ptrs = np.ascontiguousarray(ptrs, dtype=np.int64)
+        w64 = np.array(weights, dtype=np.float64)
+        out_dev = torch.empty(g.P, dtype=torch.float32, device=self.device)
+        host_ws, dev_ws = self._stage_ws(lib.fedavg_device_round_workspace(K, n))
+        rc = lib.fedavg_device_round_f32(ptrs.ctypes.data, n_cols, None if key_index is None else key_index.ctypes.data,
+                                         numel.ctypes.data, offset.ctypes.data, kind.ctypes.data, n, K,
+                                         w64.ctypes.data, out_dev.data_ptr(),
+                                         None if partials is None else partials.data_ptr(),
+                                         0 if partials is None else partials.numel(),
+                                         None if sumsq is None else sumsq.data_ptr(),
+                                         None if scratch is None else scratch.data_ptr(),
+                                         0 if scratch is None else scratch.numel(), host_ws.data_ptr(),
+                                         dev_ws.data_ptr(), host_ws.numel(), stream.cuda_stream)
+        self._table_ws_done.record(stream)
+        if rc not in (0, 1):
+            _lib.check(rc, "fedavg_device_round_f32")
+        del scratch, partials  # freed in `stream` order, after the launches that read them
+        return out_dev, (sumsq if rc == 0 else None)
 
     def _sqdist_segments(self, table: KeyTable, dicts, glob: torch.Tensor) -> torch.Tensor:
         """:291 sums of squares straight from device-resident clients' tensors."""
@@ -709,12 +674,9 @@ class DeviceAggregator:
                         self._last.setdefault("sumsq", {})[g.dtype] = sums[0]
                     self.arena_rounds += 1
                 elif g.dtype == torch.float32 and self.DEVICE_SEGMENTS:
-                    fused = self._reduce_sqdist_segments(g, ptrs, weights, compute)
-                    if fused is not None:
-                        out_dev, sums = fused
+                    out_dev, sums = self._device_round(g, ptrs, weights, compute)
+                    if sums is not None:
                         self._last.setdefault("sumsq", {})[g.dtype] = sums
-                    else:
-                        out_dev = self._reduce_segments(g, ptrs, weights, compute)
                     self._last["dev"][g.dtype] = (None, out_dev)  # no rows: see materialize_rows
                     self._last["segments"] = True
                 else:

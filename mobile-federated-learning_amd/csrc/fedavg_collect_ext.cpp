@@ -89,12 +89,25 @@ static py::tuple collect(py::list dicts, py::list names, py::list templ, int64_t
   // metadata checks and data pointers of client i (its vals filled)
   const auto check_client = [&](int64_t i) {
     PyObject* const* row = &vals[static_cast<size_t>(i) * N];
-    constexpr Py_ssize_t kAhead = 8;
-    for (Py_ssize_t j = 0; j < N && j < kAhead; ++j)
-      if (THPVariable_CheckExact(row[j])) __builtin_prefetch(THPVariable_Unpack(row[j]).unsafeGetTensorImpl());
+    // two prefetch stages: the TensorImpl kImpl keys ahead, then -- once it
+    // has arrived -- the StorageImpl behind data_ptr() kStore keys ahead (the
+    // third dependent miss of every tensor; 35,000 of them in a resnet56 x 100
+    // round)
+    constexpr Py_ssize_t kImpl = 16, kStore = 8;
+    const auto impl_of = [&](Py_ssize_t j) -> c10::TensorImpl* {
+      return THPVariable_CheckExact(row[j]) ? THPVariable_Unpack(row[j]).unsafeGetTensorImpl() : nullptr;
+    };
+    const auto prefetch_storage = [&](Py_ssize_t j) {
+      if (c10::TensorImpl* ti = impl_of(j))
+        if (ti->has_storage()) __builtin_prefetch(ti->unsafe_storage().unsafeGetStorageImpl());
+    };
+    for (Py_ssize_t j = 0; j < N && j < kImpl; ++j)
+      if (c10::TensorImpl* ti = impl_of(j)) __builtin_prefetch(ti);
+    for (Py_ssize_t j = 0; j < N && j < kStore; ++j) prefetch_storage(j);
     for (Py_ssize_t j = 0; j < N; ++j) {
-      if (j + kAhead < N && THPVariable_CheckExact(row[j + kAhead]))
-        __builtin_prefetch(THPVariable_Unpack(row[j + kAhead]).unsafeGetTensorImpl());
+      if (j + kImpl < N)
+        if (c10::TensorImpl* ti = impl_of(j + kImpl)) __builtin_prefetch(ti);
+      if (j + kStore < N) prefetch_storage(j + kStore);
       PyObject* t = row[j];
       // exact Tensor / Parameter only (no isinstance walk off the GIL
       // thread): a Tensor subclass goes to the general Python path

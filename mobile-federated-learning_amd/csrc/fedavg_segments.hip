@@ -20,6 +20,8 @@
 // one compact window of every client's tensors, like the row-major reduce.
 #include "common.hpp"
 
+#include <vector>
+
 namespace {
 using namespace fedavg_impl;
 
@@ -905,6 +907,139 @@ void launch_reduce_segments(const SegKey* keys, const int64_t* ptrs, int64_t n_k
   }
 }
 
+// The fused pass a round takes: the wave-owned windows for 17-128 clients
+// when every key is fp32 and each wave gets at least segwin_min_per_wave()
+// windows, else the LDS-DMA tiles.  `span` is the unit width the key table is
+// staged with.
+struct SegFusedPlan {
+  bool win;
+  int kmax;
+  int64_t span, waves;
+};
+
+SegFusedPlan seg_fused_plan(const int64_t* numel, int64_t n_keys, int64_t K, bool all_raw) {
+  SegFusedPlan p{false, segwin_kmax(K), seg_fused_cols(K), 0};
+  if (p.kmax > 0 && all_raw && numel && n_keys > 0 && n_keys < (int64_t(1) << 31) && !segwin_disabled()) {
+    const int64_t wc = 64 * segwin_vec(p.kmax);
+    const int64_t wunits = units_of(numel, n_keys, wc);
+    const int64_t waves = segwin_waves_for(p.kmax, wunits);
+    if (waves > 0 && wunits >= segwin_min_per_wave() * waves && wunits < (int64_t(1) << 31)) {
+      p.win = true;
+      p.span = wc;
+      p.waves = waves;
+    }
+  }
+  return p;
+}
+
+// The fused launch (+ the sums' finalize) on tables staged with plan.span
+int launch_seg_fused(const SegFusedPlan& p, const SegKey* keys, const int64_t* tptrs, int64_t n_keys, int64_t units,
+                     int64_t K, const float* weights, float* out, double* partials, int64_t partial_elems,
+                     double* sumsq, hipStream_t s, const char* what) {
+  if (units == 0) {
+    const hipError_t e = hipMemsetAsync(sumsq, 0, static_cast<size_t>(K) * sizeof(double), s);
+    return e == hipSuccess ? FEDAVG_OK : set_error(-static_cast<int>(e), "%s: hipMemsetAsync failed", what);
+  }
+  const int k32 = static_cast<int>(K);
+  int64_t nparts = 0;
+  if (p.win) {
+    if (partial_elems < K * p.waves)
+      return set_error(FEDAVG_EINVAL, "%s: partials need %lld doubles", what, (long long)(K * p.waves));
+    const dim3 grid(static_cast<unsigned>(p.waves / 4)), block(256);
+    switch (p.kmax) {
+      case 48:
+        hipLaunchKernelGGL((reduce_sqdist_segwin_kernel<48, 4, 4>), grid, block, 0, s, keys, tptrs, n_keys, units, k32,
+                           weights, out, partials);
+        break;
+      case 64:
+        hipLaunchKernelGGL((reduce_sqdist_segwin_kernel<64, 2, 4>), grid, block, 0, s, keys, tptrs, n_keys, units, k32,
+                           weights, out, partials);
+        break;
+      case 80:
+        hipLaunchKernelGGL((reduce_sqdist_segwin_kernel<80, 2, 4>), grid, block, 0, s, keys, tptrs, n_keys, units, k32,
+                           weights, out, partials);
+        break;
+      case 100:
+        hipLaunchKernelGGL((reduce_sqdist_segwin_kernel<100, 2, 4>), grid, block, 0, s, keys, tptrs, n_keys, units, k32,
+                           weights, out, partials);
+        break;
+      default:
+        hipLaunchKernelGGL((reduce_sqdist_segwin_kernel<128, 1, 4>), grid, block, 0, s, keys, tptrs, n_keys, units, k32,
+                           weights, out, partials);
+        break;
+    }
+    nparts = p.waves;
+  } else {
+    const int S = static_cast<int>(p.span);
+#define FEDAVG_SEG_FUSED(C)                                                                                        \
+  if (S == C) {                                                                                                    \
+    if (seg_fused_per_cu<C>(K) <= 0) return set_error(FEDAVG_EMODE, "%s: tile does not fit LDS", what);            \
+    nparts = seg_fused_grid<C>(K, units);                                                                          \
+    if (partial_elems < K * nparts)                                                                                \
+      return set_error(FEDAVG_EINVAL, "%s: partials need %lld doubles", what, (long long)(K * nparts));             \
+    hipLaunchKernelGGL((reduce_sqdist_segments_f32_kernel<C>), dim3(static_cast<unsigned>(nparts)), dim3(kBlock),    \
+                       static_cast<unsigned>(seg_fused_lds_bytes(K, C)), s, keys, tptrs, n_keys, units, k32, weights, \
+                       out, partials);                                                                             \
+  }
+    FEDAVG_SEG_FUSED(32)
+    FEDAVG_SEG_FUSED(64)
+    FEDAVG_SEG_FUSED(128)
+    FEDAVG_SEG_FUSED(256)
+#undef FEDAVG_SEG_FUSED
+  }
+  int rc = launch_status(what);
+  if (rc) return rc;
+  hipLaunchKernelGGL(segments_finalize_kernel, dim3(static_cast<unsigned>(K)), dim3(kBlock), 0, s, partials, nparts,
+                     sumsq);
+  return launch_status(what);
+}
+
+// ---------------------------------------------------------------------------
+// A device-resident round in one call (round 5: fedavg_device_round_f32).
+// The Python layer used to gather the group's pointer columns, convert the
+// integer keys through a pack launch of its own, upload the weights and stage
+// the tables in four steps (0.3 ms of host time for resnet56 x 100's 35,000
+// tensors against a 0.08 ms kernel); here one pass over the walk's address
+// table writes the key table, the key-major pointer table, the fp32 weights
+// and the integer keys' conversion table into the pinned workspace, one H2D
+// ships them, and the launches follow.
+// Workspace layout (host and device alike, 16-B aligned parts):
+//   SegKey[n_keys] | int64 ptrs[n_keys * K + kSegWinTablePad] | float w[K] |
+//   IntKey[n_keys] | int64 int_src[n_keys * K]
+// ---------------------------------------------------------------------------
+struct IntKey {
+  int64_t numel, kind, col;  // col: the key's first column in a client's scratch row
+};
+
+inline int64_t round16(int64_t b) { return (b + 15) & ~int64_t(15); }
+
+struct RoundWs {
+  int64_t ptrs, w, ik, isrc, end;
+};
+
+inline RoundWs round_ws(int64_t K, int64_t n_keys) {
+  RoundWs r;
+  r.ptrs = n_keys * static_cast<int64_t>(sizeof(SegKey));
+  r.w = round16(r.ptrs + (n_keys * K + kSegWinTablePad) * static_cast<int64_t>(sizeof(int64_t)));
+  r.ik = r.w + round16(K * static_cast<int64_t>(sizeof(float)));
+  r.isrc = r.ik + round16(n_keys * static_cast<int64_t>(sizeof(IntKey)));
+  r.end = r.isrc + n_keys * K * static_cast<int64_t>(sizeof(int64_t));
+  return r;
+}
+
+// a fused round's integer / bool keys as fp32 columns of the [K, S] scratch:
+// one wave per (key, client) item, the packers' static_cast (fedavg_pack.hip)
+__global__ __launch_bounds__(64) void int_keys_to_f32_kernel(const IntKey* __restrict__ ik,
+                                                             const int64_t* __restrict__ src, int K, int64_t S,
+                                                             float* __restrict__ scratch) {
+  const int64_t item = blockIdx.x;  // key q, client k: item = q * K + k
+  const int64_t q = item / K, k = item - q * K;
+  const IntKey key = ik[q];
+  const void* p = reinterpret_cast<const void*>(src[item]);
+  float* d = scratch + k * S + key.col;
+  for (int64_t e = threadIdx.x; e < key.numel; e += 64) d[e] = load_cvt(p, key.kind, e);
+}
+
 }  // namespace
 
 extern "C" {
@@ -1039,87 +1174,190 @@ int fedavg_reduce_sqdist_segments_f32(const int64_t* client_ptrs, const int64_t*
           return set_error(FEDAVG_EALIGN, "%s: client %lld key %lld is not 16-B aligned (use the two passes)", what,
                            (long long)k, (long long)j);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  // long models, 17-128 clients: the zero-copy wave-owned windows
-  const int kmax = segwin_kmax(K);
-  if (kmax > 0 && key_numel && n_keys > 0 && !segwin_disabled()) {
-    const int64_t wc = 64 * segwin_vec(kmax);
-    bool ok = key_kind != nullptr;
-    for (int64_t jk = 0; ok && jk < n_keys; ++jk) ok = key_numel[jk] >= 0 && key_kind[jk] == kRaw;
-    const int64_t wunits = ok ? units_of(key_numel, n_keys, wc) : 0;
-    const int64_t waves = segwin_waves_for(kmax, wunits);
-    if (ok && waves > 0 && wunits >= segwin_min_per_wave() * waves && wunits < (int64_t(1) << 31) &&
-        n_keys < (int64_t(1) << 31)) {
-      if (partial_elems < K * waves)
-        return set_error(FEDAVG_EINVAL, "%s: partials need %lld doubles", what, (long long)(K * waves));
-      const int64_t units = stage_tables(what, client_ptrs, key_numel, key_offset, key_kind, n_keys, K, host_ws,
-                                         dev_ws, ws_bytes, s, wc);
-      if (units < 0) return static_cast<int>(units);
-      const auto* keys = static_cast<const SegKey*>(dev_ws);
-      const auto* tptrs = reinterpret_cast<const int64_t*>(static_cast<const char*>(dev_ws) +
-                                                           n_keys * static_cast<int64_t>(sizeof(SegKey)));
-      const dim3 grid(static_cast<unsigned>(waves / 4)), block(256);
-      const int k32 = static_cast<int>(K);
-      switch (kmax) {
-        case 48:
-          hipLaunchKernelGGL((reduce_sqdist_segwin_kernel<48, 4, 4>), grid, block, 0, s, keys, tptrs, n_keys, units,
-                             k32, weights, out, partials);
-          break;
-        case 64:
-          hipLaunchKernelGGL((reduce_sqdist_segwin_kernel<64, 2, 4>), grid, block, 0, s, keys, tptrs, n_keys, units,
-                             k32, weights, out, partials);
-          break;
-        case 80:
-          hipLaunchKernelGGL((reduce_sqdist_segwin_kernel<80, 2, 4>), grid, block, 0, s, keys, tptrs, n_keys, units,
-                             k32, weights, out, partials);
-          break;
-        case 100:
-          hipLaunchKernelGGL((reduce_sqdist_segwin_kernel<100, 2, 4>), grid, block, 0, s, keys, tptrs, n_keys, units,
-                             k32, weights, out, partials);
-          break;
-        default:
-          hipLaunchKernelGGL((reduce_sqdist_segwin_kernel<128, 1, 4>), grid, block, 0, s, keys, tptrs, n_keys, units,
-                             k32, weights, out, partials);
-          break;
-      }
-      int rc = launch_status(what);
-      if (rc) return rc;
-      hipLaunchKernelGGL(segments_finalize_kernel, dim3(static_cast<unsigned>(K)), dim3(kBlock), 0, s, partials,
-                         waves, sumsq);
-      return launch_status(what);
-    }
-  }
-  const int S = seg_fused_cols(K);
+  // long models, 17-128 clients, fp32 keys only: the zero-copy wave-owned windows
+  bool all_raw = key_kind != nullptr && key_numel != nullptr;
+  for (int64_t jk = 0; all_raw && jk < n_keys; ++jk) all_raw = key_numel[jk] >= 0 && key_kind[jk] == kRaw;
+  const SegFusedPlan plan = seg_fused_plan(key_numel, n_keys, K, all_raw);
+  if (plan.win && partial_elems < K * plan.waves)
+    return set_error(FEDAVG_EINVAL, "%s: partials need %lld doubles", what, (long long)(K * plan.waves));
   const int64_t units = stage_tables(what, client_ptrs, key_numel, key_offset, key_kind, n_keys, K, host_ws, dev_ws,
-                                     ws_bytes, s, S);
+                                     ws_bytes, s, plan.span);
   if (units < 0) return static_cast<int>(units);
-  if (units == 0) {
-    const hipError_t e = hipMemsetAsync(sumsq, 0, static_cast<size_t>(K) * sizeof(double), s);
-    return e == hipSuccess ? FEDAVG_OK : set_error(-static_cast<int>(e), "%s: hipMemsetAsync failed", what);
-  }
   const auto* keys = static_cast<const SegKey*>(dev_ws);
   const auto* tptrs = reinterpret_cast<const int64_t*>(static_cast<const char*>(dev_ws) +
                                                        n_keys * static_cast<int64_t>(sizeof(SegKey)));
-  int64_t grid = 0;
-#define FEDAVG_SEG_FUSED(C)                                                                                        \
-  if (S == C) {                                                                                                    \
-    if (seg_fused_per_cu<C>(K) <= 0) return set_error(FEDAVG_EMODE, "%s: tile does not fit LDS", what);            \
-    grid = seg_fused_grid<C>(K, units);                                                                            \
-    if (partial_elems < K * grid)                                                                                  \
-      return set_error(FEDAVG_EINVAL, "%s: partials need %lld doubles", what, (long long)(K * grid));              \
-    hipLaunchKernelGGL((reduce_sqdist_segments_f32_kernel<C>), dim3(static_cast<unsigned>(grid)), dim3(kBlock),      \
-                       static_cast<unsigned>(seg_fused_lds_bytes(K, C)), s, keys, tptrs, n_keys, units,             \
-                       static_cast<int>(K), weights, out, partials);                                               \
+  return launch_seg_fused(plan, keys, tptrs, n_keys, units, K, weights, out, partials, partial_elems, sumsq, s, what);
+}
+
+int64_t fedavg_device_round_workspace(int64_t K, int64_t n_keys) {
+  if (K <= 0 || n_keys <= 0) return 0;
+  return round_ws(K, n_keys).end;
+}
+
+int64_t fedavg_device_round_scratch(const int64_t* key_numel, const int64_t* key_kind, int64_t n_keys, int64_t K) {
+  if (!key_numel || !key_kind || n_keys <= 0 || K <= 0) return 0;
+  int64_t S = 0;
+  for (int64_t j = 0; j < n_keys; ++j)
+    if (key_kind[j] != kRaw && key_numel[j] > 0) S += (key_numel[j] + 3) & ~int64_t(3);
+  return K * S;
+}
+
+int fedavg_device_round_f32(const int64_t* client_ptrs, int64_t ptr_ld, const int64_t* key_index,
+                            const int64_t* key_numel, const int64_t* key_offset, const int64_t* key_kind,
+                            int64_t n_keys, int64_t K, const double* weights, float* out, double* partials,
+                            int64_t partial_elems, double* sumsq, float* int_scratch, int64_t scratch_elems,
+                            void* host_ws, void* dev_ws, int64_t ws_bytes, void* stream) {
+  const char* what = "fedavg_device_round_f32";
+  if (!client_ptrs || !key_numel || !key_offset || !key_kind || !weights || !out || n_keys <= 0 || K <= 0 ||
+      K > INT32_MAX || n_keys >= (int64_t(1) << 31) || (!key_index && ptr_ld < n_keys) || !host_ws || !dev_ws)
+    return set_error(FEDAVG_EINVAL, "%s: bad arguments", what);
+  if (sumsq && !partials) return set_error(FEDAVG_EINVAL, "%s: sums need partials", what);
+  const RoundWs L = round_ws(K, n_keys);
+  if (ws_bytes < L.end) return set_error(FEDAVG_EINVAL, "%s: workspace needs %lld bytes", what, (long long)L.end);
+  if (!aligned16(host_ws) || !aligned16(dev_ws)) return set_error(FEDAVG_EALIGN, "%s: workspaces must be 16-B aligned", what);
+  if (!is_pinned_host_memory(host_ws)) return set_error(FEDAVG_EINVAL, "%s: host_ws is not pinned host memory", what);
+  if (!is_device_memory(dev_ws) || !is_device_memory(out))
+    return set_error(FEDAVG_EINVAL, "%s: dev_ws and out must be device memory", what);
+  if (sumsq && (!is_device_memory(sumsq) || !is_device_memory(partials)))
+    return set_error(FEDAVG_EINVAL, "%s: partials and sumsq must be device memory", what);
+  char* hb = static_cast<char*>(host_ws);
+  auto* hk = reinterpret_cast<SegKey*>(hb);
+  auto* hp = reinterpret_cast<int64_t*>(hb + L.ptrs);
+  auto* hw = reinterpret_cast<float*>(hb + L.w);
+  auto* hik = reinterpret_cast<IntKey*>(hb + L.ik);
+  auto* hsrc = reinterpret_cast<int64_t*>(hb + L.isrc);
+  // keys: validation, the integer keys' scratch columns
+  int64_t S = 0, n_int = 0;
+  for (int64_t j = 0; j < n_keys; ++j) {
+    const int64_t col = key_index ? key_index[j] : j;
+    if (key_numel[j] < 0 || key_offset[j] < 0 || key_kind[j] < kRaw || key_kind[j] > kBool || col < 0 ||
+        (key_index && col >= ptr_ld))
+      return set_error(FEDAVG_EINVAL, "%s: bad key %lld", what, (long long)j);
+    if (key_kind[j] != kRaw && key_numel[j] > 0) {
+      S += (key_numel[j] + 3) & ~int64_t(3);
+      ++n_int;
+    }
   }
-  FEDAVG_SEG_FUSED(32)
-  FEDAVG_SEG_FUSED(64)
-  FEDAVG_SEG_FUSED(128)
-  FEDAVG_SEG_FUSED(256)
-#undef FEDAVG_SEG_FUSED
-  int rc = launch_status(what);
+  const int64_t ld = ptr_ld;
+  if (S >= (int64_t(1) << 31)) return set_error(FEDAVG_EINVAL, "%s: integer keys too large", what);
+  bool fuse = sumsq != nullptr && K <= kSegFusedMaxK;
+  // a fused round takes its integer keys as fp32 scratch columns (the
+  // window kernels read fp32 only); the two-pass reduce converts in-kernel
+  if (fuse && n_int > 0 &&
+      (!int_scratch || scratch_elems < K * S || !aligned16(int_scratch) || !is_device_memory(int_scratch)))
+    return set_error(FEDAVG_EINVAL, "%s: integer keys need an aligned device scratch of %lld floats", what,
+                     (long long)(K * S));
+  // the pointer table, key-major; fused rounds need 16-B aligned fp32 sources
+  // (a misaligned one sends the round to the reduce alone, rewritten below).
+  // Client-major walk: the walk's table was just written by other threads
+  // (fedavg_collect_ext), and read row by row -- the order the hardware
+  // prefetcher follows -- the whole call costs 73-78 us right after a
+  // resnet56 x 100 walk, against 182-200 us filling key-major and 79-86 us
+  // in blocks of 8 clients
+  // (scripts/device_round_call_probe.py, profiles/r05/device_round/).
+  const void* first_src = nullptr;
+  const void* last_src = nullptr;
+  thread_local std::vector<int64_t> kcol, kconv;  // per key: table column; (int_src row << 32 | scratch column + 1), 0: as is
+  kcol.resize(static_cast<size_t>(n_keys));
+  kconv.resize(static_cast<size_t>(n_keys));
+  const auto fill = [&](bool convert) -> int {
+    int64_t q = 0, soff = 0;
+    for (int64_t j = 0; j < n_keys; ++j) {
+      kcol[j] = key_index ? key_index[j] : j;
+      const bool conv = convert && key_kind[j] != kRaw && key_numel[j] > 0;
+      kconv[j] = conv ? ((q << 32) | (soff + 1)) : 0;  // int_src row, scratch column + 1
+      if (conv) {
+        hik[q++] = IntKey{key_numel[j], key_kind[j], soff};
+        soff += (key_numel[j] + 3) & ~int64_t(3);
+      }
+    }
+    // one (client, key) entry
+    const auto put = [&](int64_t k, int64_t j, int64_t p) -> bool {
+      if (key_numel[j] > 0) {
+        if (p == 0 || (key_kind[j] == kRaw && (p & 3) != 0)) return false;
+        if (!first_src) first_src = reinterpret_cast<const void*>(p);
+        last_src = reinterpret_cast<const void*>(p);
+        if (key_kind[j] == kRaw && (p & 15) != 0) fuse = false;
+      }
+      if (kconv[j]) {
+        hsrc[(kconv[j] >> 32) * K + k] = p;
+        hp[j * K + k] = (int_scratch ? reinterpret_cast<int64_t>(int_scratch + k * S) : 0) +
+                        ((kconv[j] & 0xffffffffLL) - 1) * static_cast<int64_t>(sizeof(float));
+      } else {
+        hp[j * K + k] = p;
+      }
+      return true;
+    };
+    for (int64_t k = 0; k < K; ++k)
+      for (int64_t j = 0; j < n_keys; ++j)
+        if (!put(k, j, client_ptrs[k * ld + kcol[j]]))
+          return set_error(FEDAVG_EINVAL, "%s: client %lld key %lld: null or misaligned source", what, (long long)k,
+                           (long long)j);
+    return FEDAVG_OK;
+  };
+  const bool convert = fuse && n_int > 0;
+  int rc = fill(convert);
   if (rc) return rc;
-  hipLaunchKernelGGL(segments_finalize_kernel, dim3(static_cast<unsigned>(K)), dim3(kBlock), 0, s, partials, grid,
-                     sumsq);
-  return launch_status(what);
+  if (convert && !fuse) {  // a misaligned fp32 source: the integer keys stay as they are
+    rc = fill(false);
+    if (rc) return rc;
+  }
+  const bool converted = convert && fuse;
+  if (!first_src) {  // every key empty
+    if (sumsq) {
+      const hipError_t e = hipMemsetAsync(sumsq, 0, static_cast<size_t>(K) * sizeof(double), static_cast<hipStream_t>(stream));
+      if (e != hipSuccess) return set_error(-static_cast<int>(e), "%s: hipMemsetAsync failed", what);
+    }
+    return sumsq ? FEDAVG_OK : 1;
+  }
+  // a host address would fault the kernels: spot check of the first and last
+  // source (the Python layer checks every tensor's device)
+  if (!is_device_memory(first_src) || !is_device_memory(last_src))
+    return set_error(FEDAVG_EINVAL, "%s: client sources must be device memory", what);
+  // the unit width, then the key table
+  const bool all_raw = converted || n_int == 0;
+  const SegFusedPlan plan = fuse ? seg_fused_plan(key_numel, n_keys, K, all_raw) : SegFusedPlan{false, 0, 0, 0};
+  const bool small = !fuse && segments_small(key_numel, n_keys);
+  const int64_t span = fuse ? plan.span : (small ? kSegSmallSpan : kSegSpan);
+  int64_t units = 0;
+  for (int64_t j = 0; j < n_keys; ++j) {
+    hk[j] = SegKey{key_numel[j], key_offset[j], converted ? kRaw : key_kind[j], units};
+    units += (key_numel[j] + span - 1) / span;
+  }
+  // the reference's weights n_i / N (fedavg_trainer.py:453) rounded once to
+  // fp32 (nearest even, the cast ATen applies to the scalar at :455)
+  for (int64_t k = 0; k < K; ++k) hw[k] = static_cast<float>(weights[k]);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t bytes = converted ? L.isrc + n_int * K * static_cast<int64_t>(sizeof(int64_t)) : L.ik;
+  const hipError_t e = hipMemcpyAsync(dev_ws, host_ws, static_cast<size_t>(bytes), hipMemcpyHostToDevice, s);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return set_error(-static_cast<int>(e), "%s: hipMemcpyAsync failed: %s", what, hipGetErrorString(e));
+  }
+  const char* db = static_cast<const char*>(dev_ws);
+  const auto* keys = reinterpret_cast<const SegKey*>(db);
+  const auto* tptrs = reinterpret_cast<const int64_t*>(db + L.ptrs);
+  const auto* dw = reinterpret_cast<const float*>(db + L.w);
+  if (converted) {
+    if (n_int * K > INT32_MAX) return set_error(FEDAVG_EINVAL, "%s: too many integer keys", what);
+    hipLaunchKernelGGL(int_keys_to_f32_kernel, dim3(static_cast<unsigned>(n_int * K)), dim3(64), 0, s,
+                       reinterpret_cast<const IntKey*>(db + L.ik), reinterpret_cast<const int64_t*>(db + L.isrc),
+                       static_cast<int>(K), S, int_scratch);
+    rc = launch_status(what);
+    if (rc) return rc;
+  }
+  if (fuse) {
+    rc = launch_seg_fused(plan, keys, tptrs, n_keys, units, K, dw, out, partials, partial_elems, sumsq, s, what);
+    return rc ? rc : FEDAVG_OK;
+  }
+  if (small)
+    launch_reduce_segments<kSegU, kSegSmallC, kSegStyle>(keys, tptrs, n_keys, units, K, dw, out,
+                                                         static_cast<int64_t>(kSegSmallBlocksPerCU) * cu_count(), s);
+  else
+    launch_reduce_segments<kSegU, kSegC, kSegStyle>(keys, tptrs, n_keys, units, K, dw, out,
+                                                    static_cast<int64_t>(kSegBlocksPerCU) * cu_count(), s);
+  rc = launch_status(what);
+  return rc ? rc : 1;
 }
 
 // tuning hook (fedavg_amd_tuning.h): the zero-copy reduce with an explicit
