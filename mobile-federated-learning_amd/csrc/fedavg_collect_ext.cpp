@@ -6,13 +6,17 @@
 // 0.75 us per tensor (26 ms for resnet56 x 100 clients, 35,000 tensors); here
 // the dict lookups and tensor metadata are read through the torch C++ API.
 //
-// collect(dicts, names, template, device_index=-1) -> (ptrs[K, N] int64, bad_client, bad_key)
+// collect(dicts, names, template, device_index=-1, strict0=False) -> (ptrs[K, N] int64, bad_client, bad_key)
 //   template[j] is client 0's tensor for names[j].  A client tensor passes
 //   when it has the template's sizes and dtype and is contiguous, on the host
 //   (device_index -1) or on HIP device `device_index` (device-resident clients).
 //   On the first one that does not (or a missing key), the scan stops and
 //   returns its (client, key) index so the Python layer can raise the
 //   reference's exception or take its general path; otherwise (-1, -1).
+//   strict0: client 0 must be a dict whose entries are exactly `names` in
+//   order (else (None, 0, -1) at once) -- KeyTable.try_collect's check that a
+//   table from an earlier round still fits, without a Python pass over the
+//   key strings.
 #include <torch/csrc/autograd/python_variable.h>
 #include <torch/extension.h>
 
@@ -45,7 +49,7 @@ static inline KeyEq key_eq(PyObject* a, PyObject* b) {
              : KeyEq::kDiffer;
 }
 
-static py::tuple collect(py::list dicts, py::list names, py::list templ, int64_t device_index) {
+static py::tuple collect(py::list dicts, py::list names, py::list templ, int64_t device_index, bool strict0) {
   const Py_ssize_t K = PyList_GET_SIZE(dicts.ptr());
   const Py_ssize_t N = PyList_GET_SIZE(names.ptr());
   if (PyList_GET_SIZE(templ.ptr()) != N) throw std::invalid_argument("template/names length mismatch");
@@ -161,6 +165,9 @@ static py::tuple collect(py::list dicts, py::list names, py::list templ, int64_t
       check_client(i);
     }
   });
+  // strict0: client 0 must be a dict holding exactly `names`, in order (a
+  // table reused from an earlier round; anything else takes a fresh table)
+  if (strict0 && K > 0 && bad[0] == kRedo) return py::make_tuple(py::none(), 0, -1);
   for (Py_ssize_t i = 0; i < K; ++i) {  // other mappings / key objects: lookups on this thread
     if (bad[i] != kRedo) continue;
     bad[i] = -1;
@@ -619,7 +626,7 @@ static py::tuple verify_rows(py::list w_locals, py::list counts, py::list names,
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "native state_dict walk for mfl_amd (host metadata only)";
   m.def("collect", &collect, "validate clients against client 0 and gather data pointers", py::arg("dicts"),
-        py::arg("names"), py::arg("templ"), py::arg("device_index") = -1);
+        py::arg("names"), py::arg("templ"), py::arg("device_index") = -1, py::arg("strict0") = false);
   m.def("unpack", &unpack, "views of a flat buffer shaped like the key table's keys");
   m.def("unpack_into", &unpack_into, "those views assigned into a dict by key name");
   m.def("small_round", &small_round, "the host side of a small fp32 round in one call");

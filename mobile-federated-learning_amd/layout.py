@@ -225,11 +225,15 @@ class KeyTable:
         ``None`` -- never raises for a mismatch; the caller then builds a fresh
         table from client 0."""
         ext = _collect_ext()
-        if ext is None or not state_dicts or list(state_dicts[0].keys()) != self._names:
+        if ext is None or not state_dicts:
             return None
-        device = self.client_device(state_dicts)
+        try:
+            device = self.client_device(state_dicts)
+        except (KeyError, TypeError):  # client 0 without this table's first key: a fresh table decides
+            return None
+        # strict0: client 0's dict entries must be exactly this table's keys in order
         got, _, _ = ext.collect(list(state_dicts), self._names, self._template,
-                                -1 if device.type == "cpu" else device.index)
+                                -1 if device.type == "cpu" else device.index, True)
         return None if got is None else (got.numpy(), [])
 
     def pack_items(self, group: "Group", ptrs: np.ndarray, row0: int, ld: int) -> np.ndarray:

@@ -7,7 +7,8 @@ table from KeyTable.collect; then the native call alone, timed per call
 (each followed by a stream synchronize outside the timed region), in its
 forms: fused with the integer keys' scratch (production), the reduce alone
 (no conversion), fused right after a fresh walk (the address table just
-written by the walker threads, as in a round), and, for scale, hipPointerGetAttributes and an empty
+written by the walker threads, as in a round), the walk itself
+(KeyTable.collect) at 1, 2, 4, 8 and all intra-op threads, and, for scale, hipPointerGetAttributes and an empty
 hipMemcpyAsync-sized H2D of the table bytes through torch.  One JSON line
 per form with the median and min call time in microseconds.
 """
@@ -91,6 +92,11 @@ def main():
     recs["fused_us"] = timed(lambda: call(True), args.calls)
     recs["reduce_only_us"] = timed(lambda: call(False), args.calls)
     recs["fused_after_walk_us"] = timed(lambda: call(True), args.calls, setup=walk)
+    nt = torch.get_num_threads()
+    for t in sorted({1, 2, 4, 8, nt}):
+        torch.set_num_threads(t)
+        recs[f"walk_us_threads_{t}"] = timed(walk, args.calls, sync=False)
+    torch.set_num_threads(nt)
     hip = ctypes.CDLL("libamdhip64.so")
     attr = ctypes.create_string_buffer(256)
     p = ctypes.c_void_p(out.data_ptr())

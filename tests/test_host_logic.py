@@ -308,6 +308,31 @@ def test_client_device_and_mixed_device_rejection():
     assert table.try_collect(mixed) is None
 
 
+def test_try_collect_needs_client0_exactly_the_table():
+    """A table kept from an earlier round is reused only when client 0 is a
+    dict holding exactly its keys in order (the native walk's strict0 check);
+    other clients may hold their keys in any order or extra keys, as the
+    reference only reads client 0's keys from them (fedavg_trainer.py:450-457)."""
+    _, w_locals, _ = load_case("resnet_like_bn_k5")
+    dicts = [OrderedDict(sd) for _, sd in w_locals]
+    table = KeyTable(dicts[0])
+    got = table.try_collect(dicts)
+    assert got is not None and np.array_equal(got[0], table.collect(dicts)[0])
+    names = list(dicts[0])
+    reordered = OrderedDict((k, dicts[0][k]) for k in reversed(names))
+    assert table.try_collect([reordered] + dicts[1:]) is None
+    extra = OrderedDict(dicts[0])
+    extra["extra.key"] = torch.zeros(3)
+    assert table.try_collect([extra] + dicts[1:]) is None
+    missing = OrderedDict((k, v) for k, v in dicts[0].items() if k != names[-1])
+    assert table.try_collect([missing] + dicts[1:]) is None
+    assert table.try_collect([dict(dicts[0])] + dicts[1:]) is not None  # a plain dict in the same order
+    later = [dicts[0]] + [OrderedDict((k, sd[k]) for k in reversed(names)) for sd in dicts[1:]]
+    got = table.try_collect(later)
+    assert got is not None and np.array_equal(got[0], table.collect(dicts)[0])
+    assert table.try_collect([{names[1]: dicts[0][names[1]]}]) is None  # first key missing: no KeyError
+
+
 def test_synthetic_inputs_torch_and_numpy_bit_identical():
     """bench.py's device-generated clients (mfl_amd.synthetic) are reproduced
     bit for bit by the numpy form the parity checks regenerate them with."""
