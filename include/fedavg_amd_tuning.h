@@ -130,6 +130,15 @@ int fedavg_reduce_f32_xcd(const float* clients, int64_t K, int64_t P, int64_t ld
  * columns; round-split launches of <= blocks_per_cu x CUs workgroups
  * (0 = one launch).  Same bits as the production call.
  */
+/*
+ * Host-side phase times of this thread's last fedavg_device_round_f32 call
+ * (probe library build only): cumulative microseconds at up to `cap` marks
+ * -- 0 start, 1 argument / pointer-attribute checks, 2 key validation, 3 the
+ * pointer-table fill, 4 the sources' spot check, 5 plan + key table +
+ * weights, 6 the tables' H2D issued, 7 the integer keys' launch, 8 the
+ * reduce launches.  Returns the number of marks written.
+ */
+int fedavg_device_round_phases(double* us, int cap);
 int fedavg_reduce_segments_f32_variant(const int64_t* client_ptrs, const int64_t* key_numel, const int64_t* key_offset,
                                        const int64_t* key_kind, int64_t n_keys, int64_t K, const float* weights,
                                        float* out, void* host_ws, void* dev_ws, int64_t ws_bytes, int unroll, int cols,

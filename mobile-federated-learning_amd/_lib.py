@@ -78,6 +78,7 @@ TUNING_SIGNATURES = {
                                                     _c_int, _c_int, _c_int, _vp]),
     "fedavg_client_sqdist_segments_f32_variant": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_i64, _vp, _vp, _c_i64, _vp,
                                                            _vp, _vp, _c_i64, _c_int, _c_int, _vp]),
+    "fedavg_device_round_phases": (_c_int, [_vp, _c_int]),
     "fedavg_fpf_index_workspace": (_c_i64, [_c_i64, _c_i64]),
     "fedavg_fpf_index_variant": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _c_i64, _c_int, _c_int,
                                           _c_int, _vp]),

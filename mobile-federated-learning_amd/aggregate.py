@@ -433,7 +433,8 @@ class DeviceAggregator:
             # client 0's own tensors: its dict is about to hold the average
             # (:449), and the rows of a zero-copy round are packed on demand
             # (its keys are exactly the table's: prepare checked them)
-            self._last["seg_keep0"] = OrderedDict(acc_dict)
+            # (names, tensors) -- a dict is made only if a later call needs one
+            self._last["seg_keep0"] = (list(acc_dict), list(acc_dict.values()))
         # replace values in place, keeping client 0's key order (fedavg_trainer.py:450-457)
         if isinstance(results, _Flats):
             for g, flat in results:
@@ -493,18 +494,21 @@ class DeviceAggregator:
     @staticmethod
     def _round_meta(g, n_cols: int):
         """The group's key columns for fedavg_device_round_f32, built once per
-        table: (key_index or None when the group is every key in order, numel,
-        offset, kind) as contiguous int64 arrays, and a per-K cache of the
-        integer keys' scratch size."""
+        table: (n_cols, arrays, their addresses, per-K sizes).  The arrays --
+        key_index (None when the group is every key in order), numel, offset,
+        kind, contiguous int64 -- are kept alive here; the addresses are what
+        the call takes (``ndarray.ctypes`` costs ~1 us per access); per K: the
+        integer keys' scratch floats, the partials and the workspace bytes."""
         import numpy as np
 
         meta = g.__dict__.get("_round_meta")
         if meta is None or meta[0] != n_cols:
             ki = np.ascontiguousarray(g.key_index, dtype=np.int64)
             whole = len(ki) == n_cols and bool(np.array_equal(ki, np.arange(n_cols)))
-            meta = g._round_meta = (n_cols, None if whole else ki, np.ascontiguousarray(g.numel, dtype=np.int64),
-                                    np.ascontiguousarray(g.offset, dtype=np.int64),
-                                    np.ascontiguousarray(g.kind, dtype=np.int64), {})
+            arrs = (None if whole else ki, np.ascontiguousarray(g.numel, dtype=np.int64),
+                    np.ascontiguousarray(g.offset, dtype=np.int64), np.ascontiguousarray(g.kind, dtype=np.int64))
+            addrs = tuple(None if a is None else a.ctypes.data for a in arrs)
+            meta = g._round_meta = (n_cols, arrs, addrs, {})
         return meta
 
     def _device_round(self, g, ptrs, weights, stream):
@@ -521,33 +525,33 @@ class DeviceAggregator:
 
         lib = _lib.load()
         K, n_cols = ptrs.shape
-        _, key_index, numel, offset, kind, scratch_of = self._round_meta(g, n_cols)
-        n = len(numel)
-        fuse = FUSE_DISTANCES and K <= FUSED_SEGMENTS_MAX_K
-        scratch = None
-        if fuse:
-            n_s = scratch_of.get(K)
-            if n_s is None:
-                n_s = scratch_of[K] = lib.fedavg_device_round_scratch(numel.ctypes.data, kind.ctypes.data, n, K)
+        _, arrs, (ki_p, numel_p, offset_p, kind_p), sizes = self._round_meta(g, n_cols)
+        n = len(arrs[1])
+        per_k = sizes.get(K)
+        if per_k is None:
+            per_k = sizes[K] = (lib.fedavg_device_round_scratch(numel_p, kind_p, n, K),
+                                max(1, lib.fedavg_reduce_sqdist_segments_partials(K)),
+                                lib.fedavg_device_round_workspace(K, n))
+        n_s, n_part, ws_need = per_k
+        dev = self.device
+        scratch = partials = sumsq = None
+        if FUSE_DISTANCES and K <= FUSED_SEGMENTS_MAX_K:
             if n_s:
-                scratch = torch.empty(n_s, dtype=torch.float32, device=self.device)
-            partials = torch.empty(max(1, lib.fedavg_reduce_sqdist_segments_partials(K)), dtype=torch.float64,
-                                   device=self.device)
-            sumsq = torch.empty(K, dtype=torch.float64, device=self.device)
-        else:
-            partials = sumsq = None
-        ptrs = np.ascontiguousarray(ptrs, dtype=np.int64)
+                scratch = torch.empty(n_s, dtype=torch.float32, device=dev)
+            partials = torch.empty(n_part, dtype=torch.float64, device=dev)
+            sumsq = torch.empty(K, dtype=torch.float64, device=dev)
+        if not ptrs.flags.c_contiguous:
+            ptrs = np.ascontiguousarray(ptrs, dtype=np.int64)
         w64 = np.array(weights, dtype=np.float64)
-        out_dev = torch.empty(g.P, dtype=torch.float32, device=self.device)
-        host_ws, dev_ws = self._stage_ws(lib.fedavg_device_round_workspace(K, n))
-        rc = lib.fedavg_device_round_f32(ptrs.ctypes.data, n_cols, None if key_index is None else key_index.ctypes.data,
-                                         numel.ctypes.data, offset.ctypes.data, kind.ctypes.data, n, K,
+        out_dev = torch.empty(g.P, dtype=torch.float32, device=dev)
+        host_ws, dev_ws = self._stage_ws(ws_need)
+        rc = lib.fedavg_device_round_f32(ptrs.ctypes.data, n_cols, ki_p, numel_p, offset_p, kind_p, n, K,
                                          w64.ctypes.data, out_dev.data_ptr(),
                                          None if partials is None else partials.data_ptr(),
-                                         0 if partials is None else partials.numel(),
+                                         0 if partials is None else n_part,
                                          None if sumsq is None else sumsq.data_ptr(),
                                          None if scratch is None else scratch.data_ptr(),
-                                         0 if scratch is None else scratch.numel(), host_ws.data_ptr(),
+                                         0 if scratch is None else n_s, host_ws.data_ptr(),
                                          dev_ws.data_ptr(), host_ws.numel(), stream.cuda_stream)
         self._table_ws_done.record(stream)
         if rc not in (0, 1):
@@ -576,6 +580,16 @@ class DeviceAggregator:
         del keep
         return sumsq
 
+    @staticmethod
+    def _client0_tensors(last) -> "OrderedDict[str, torch.Tensor]":
+        """Client 0's own tensors of a zero-copy round as a dict (its dict
+        holds the average since :449), made from the (names, tensors) the
+        round kept."""
+        keep = last["seg_keep0"]
+        if isinstance(keep, tuple):
+            keep = last["seg_keep0"] = OrderedDict(zip(*keep))
+        return keep
+
     def materialize_rows(self):
         """The last round's client rows in HBM (``[K, ld]``), packing them on
         demand after a zero-copy round: client 0 from its original tensors
@@ -586,7 +600,7 @@ class DeviceAggregator:
             dev = last.get("dev", {}).get(torch.float32)
             return None if dev is None else dev[0]
         refs = last.get("refs")
-        dicts = [last["seg_keep0"]] + [r() for r in refs[1:]] if refs is not None else [None]
+        dicts = [self._client0_tensors(last)] + [r() for r in refs[1:]] if refs is not None else [None]
         if any(d is None for d in dicts):
             return None
         table, K = last["table"], last["K"]
@@ -619,12 +633,14 @@ class DeviceAggregator:
         ok, whole, off4 = meta
         if dicts is None or not ok:
             return None
-        cols = ptrs if whole and ptrs.shape[1] == len(off4) else ptrs[:, g.key_index]
-        base = int(cols[0, 0]) - int(off4[0])
-        K = cols.shape[0]
-        pitch = int(cols[1, 0] - cols[0, 0]) if K > 1 else (g.P + 3) // 4 * 16
+        K, j0, j1 = ptrs.shape[0], int(g.key_index[0]), int(g.key_index[-1])
+        base = int(ptrs[0, j0]) - int(off4[0])
+        pitch = int(ptrs[1, j0] - ptrs[0, j0]) if K > 1 else (g.P + 3) // 4 * 16
         if base % 16 or pitch % 16 or pitch < g.P * 4:
             return None
+        if int(ptrs[K - 1, j1]) != base + (K - 1) * pitch + int(off4[-1]):  # the far corner first: O(1) reject
+            return None
+        cols = ptrs if whole and ptrs.shape[1] == len(off4) else ptrs[:, g.key_index]
         expect = off4 + base if K == 1 else (np.arange(base, base + K * pitch, pitch)[:, None] + off4)
         if not np.array_equal(cols, expect.reshape(cols.shape)):
             return None
@@ -858,7 +874,10 @@ class DeviceAggregator:
         # the reference's `w[para] - w_glob[para]` raises on bool buffers; the
         # round's key table already holds every client's (validated) dtypes
         if cached:
-            has_bool = any(e.src_dtype == torch.bool for e in last["table"].entries)
+            t = last["table"]
+            has_bool = t.__dict__.get("_has_bool")
+            if has_bool is None:
+                has_bool = t._has_bool = any(e.src_dtype == torch.bool for e in t.entries)
         else:
             has_bool = any(t.dtype == torch.bool for _, sd in w_locals if sd is not w_glob for t in sd.values())
         if has_bool and any(sd is not w_glob for _, sd in w_locals):
@@ -876,7 +895,8 @@ class DeviceAggregator:
                     elif devbuf is None:  # zero-copy round: read the clients' tensors where they lie
                         # the dict aliased to w_glob (client 0, :449) holds the average
                         # now; its own tensors stand in (its norm is overridden below)
-                        dicts = [last["seg_keep0"] if sd is w_glob else sd for _, sd in w_locals]
+                        keep0 = self._client0_tensors(last)
+                        dicts = [keep0 if sd is w_glob else sd for _, sd in w_locals]
                         parts.append((dt, self._sqdist_segments(table, dicts, out_dev), out_dev[:P]))
                     else:
                         parts.append((dt, client_sqdist(devbuf, out_dev, P), out_dev[:P]))

@@ -20,6 +20,7 @@
 // one compact window of every client's tensors, like the row-major reduce.
 #include "common.hpp"
 
+#include <chrono>
 #include <vector>
 
 namespace {
@@ -1202,12 +1203,39 @@ int64_t fedavg_device_round_scratch(const int64_t* key_numel, const int64_t* key
   return K * S;
 }
 
+#ifdef FEDAVG_TUNING  // probe library only: host-side phase times of the last device round call
+}  // extern "C"
+namespace {
+thread_local double g_round_phase_us[10];
+thread_local int g_round_nphase = 0;
+thread_local std::chrono::steady_clock::time_point g_round_t0;
+}  // namespace
+#define FEDAVG_ROUND_MARK(i)                                                                              \
+  do {                                                                                                    \
+    const auto t_ = std::chrono::steady_clock::now();                                                     \
+    if ((i) == 0) g_round_t0 = t_;                                                                        \
+    g_round_phase_us[i] = std::chrono::duration<double, std::micro>(t_ - g_round_t0).count();             \
+    g_round_nphase = (i) + 1;                                                                             \
+  } while (0)
+extern "C" {
+int fedavg_device_round_phases(double* us, int cap) {
+  const int n = g_round_nphase < cap ? g_round_nphase : cap;
+  for (int i = 0; i < n; ++i) us[i] = g_round_phase_us[i];
+  return n;
+}
+#else
+#define FEDAVG_ROUND_MARK(i) \
+  do {                       \
+  } while (0)
+#endif
+
 int fedavg_device_round_f32(const int64_t* client_ptrs, int64_t ptr_ld, const int64_t* key_index,
                             const int64_t* key_numel, const int64_t* key_offset, const int64_t* key_kind,
                             int64_t n_keys, int64_t K, const double* weights, float* out, double* partials,
                             int64_t partial_elems, double* sumsq, float* int_scratch, int64_t scratch_elems,
                             void* host_ws, void* dev_ws, int64_t ws_bytes, void* stream) {
   const char* what = "fedavg_device_round_f32";
+  FEDAVG_ROUND_MARK(0);
   if (!client_ptrs || !key_numel || !key_offset || !key_kind || !weights || !out || n_keys <= 0 || K <= 0 ||
       K > INT32_MAX || n_keys >= (int64_t(1) << 31) || (!key_index && ptr_ld < n_keys) || !host_ws || !dev_ws)
     return set_error(FEDAVG_EINVAL, "%s: bad arguments", what);
@@ -1220,6 +1248,7 @@ int fedavg_device_round_f32(const int64_t* client_ptrs, int64_t ptr_ld, const in
     return set_error(FEDAVG_EINVAL, "%s: dev_ws and out must be device memory", what);
   if (sumsq && (!is_device_memory(sumsq) || !is_device_memory(partials)))
     return set_error(FEDAVG_EINVAL, "%s: partials and sumsq must be device memory", what);
+  FEDAVG_ROUND_MARK(1);  // argument and pointer-attribute checks
   char* hb = static_cast<char*>(host_ws);
   auto* hk = reinterpret_cast<SegKey*>(hb);
   auto* hp = reinterpret_cast<int64_t*>(hb + L.ptrs);
@@ -1247,62 +1276,86 @@ int fedavg_device_round_f32(const int64_t* client_ptrs, int64_t ptr_ld, const in
       (!int_scratch || scratch_elems < K * S || !aligned16(int_scratch) || !is_device_memory(int_scratch)))
     return set_error(FEDAVG_EINVAL, "%s: integer keys need an aligned device scratch of %lld floats", what,
                      (long long)(K * S));
+  FEDAVG_ROUND_MARK(2);  // key validation
   // the pointer table, key-major; fused rounds need 16-B aligned fp32 sources
   // (a misaligned one sends the round to the reduce alone, rewritten below).
   // Client-major walk: the walk's table was just written by other threads
   // (fedavg_collect_ext), and read row by row -- the order the hardware
-  // prefetcher follows -- the whole call costs 73-78 us right after a
-  // resnet56 x 100 walk, against 182-200 us filling key-major and 79-86 us
-  // in blocks of 8 clients
-  // (scripts/device_round_call_probe.py, profiles/r05/device_round/).
+  // prefetcher follows -- the call took 73-78 us right after a resnet56 x 100
+  // walk, against 182-200 us filling key-major and 79-86 us in blocks of 8
+  // clients; with the checks branch-free per row, 63-65 us, 44 of them the
+  // fill (scripts/device_round_call_probe.py, profiles/r05/device_round/).
   const void* first_src = nullptr;
   const void* last_src = nullptr;
-  thread_local std::vector<int64_t> kcol, kconv;  // per key: table column; (int_src row << 32 | scratch column + 1), 0: as is
-  kcol.resize(static_cast<size_t>(n_keys));
-  kconv.resize(static_cast<size_t>(n_keys));
+  // per key: table column, the masks its sources are checked with (a
+  // non-empty key needs a non-null source; fp32 sources 4-B aligned, 16-B
+  // for the fused pass), and for a converted integer key its int_src row and
+  // scratch column
+  struct KeyFill {
+    int64_t col, need, align, fuse_mask;
+  };
+  thread_local std::vector<KeyFill> kf;
+  thread_local std::vector<int64_t> conv_j, conv_col;
+  kf.resize(static_cast<size_t>(n_keys));
+  for (int64_t j = 0; j < n_keys; ++j) {
+    const bool live = key_numel[j] > 0, raw = key_kind[j] == kRaw;
+    kf[j] = KeyFill{key_index ? key_index[j] : j, live ? 1 : 0, live && raw ? 3 : 0, live && raw ? 15 : 0};
+  }
   const auto fill = [&](bool convert) -> int {
-    int64_t q = 0, soff = 0;
-    for (int64_t j = 0; j < n_keys; ++j) {
-      kcol[j] = key_index ? key_index[j] : j;
-      const bool conv = convert && key_kind[j] != kRaw && key_numel[j] > 0;
-      kconv[j] = conv ? ((q << 32) | (soff + 1)) : 0;  // int_src row, scratch column + 1
-      if (conv) {
-        hik[q++] = IntKey{key_numel[j], key_kind[j], soff};
-        soff += (key_numel[j] + 3) & ~int64_t(3);
+    // every entry as is, branch-free checks accumulated per client row ...
+    int64_t fuse_bits = 0;
+    for (int64_t k = 0; k < K; ++k) {
+      const int64_t* row = client_ptrs + k * ld;
+      int64_t bad = 0;
+      for (int64_t j = 0; j < n_keys; ++j) {
+        const KeyFill f = kf[j];
+        const int64_t p = row[f.col];
+        hp[j * K + k] = p;
+        bad |= (f.need & static_cast<int64_t>(p == 0)) | (p & f.align);
+        fuse_bits |= p & f.fuse_mask;
+      }
+      if (bad) {
+        for (int64_t j = 0; j < n_keys; ++j) {
+          const int64_t p = row[kf[j].col];
+          if ((kf[j].need && p == 0) || (p & kf[j].align))
+            return set_error(FEDAVG_EINVAL, "%s: client %lld key %lld: null or misaligned source", what,
+                             (long long)k, (long long)j);
+        }
       }
     }
-    // one (client, key) entry
-    const auto put = [&](int64_t k, int64_t j, int64_t p) -> bool {
-      if (key_numel[j] > 0) {
-        if (p == 0 || (key_kind[j] == kRaw && (p & 3) != 0)) return false;
-        if (!first_src) first_src = reinterpret_cast<const void*>(p);
-        last_src = reinterpret_cast<const void*>(p);
-        if (key_kind[j] == kRaw && (p & 15) != 0) fuse = false;
-      }
-      if (kconv[j]) {
-        hsrc[(kconv[j] >> 32) * K + k] = p;
-        hp[j * K + k] = (int_scratch ? reinterpret_cast<int64_t>(int_scratch + k * S) : 0) +
-                        ((kconv[j] & 0xffffffffLL) - 1) * static_cast<int64_t>(sizeof(float));
-      } else {
-        hp[j * K + k] = p;
-      }
-      return true;
-    };
-    for (int64_t k = 0; k < K; ++k)
+    if (fuse_bits) fuse = false;
+    // ... then the converted integer keys pointed at their scratch columns
+    conv_j.clear();
+    conv_col.clear();
+    if (convert && fuse) {
+      int64_t soff = 0;
       for (int64_t j = 0; j < n_keys; ++j)
-        if (!put(k, j, client_ptrs[k * ld + kcol[j]]))
-          return set_error(FEDAVG_EINVAL, "%s: client %lld key %lld: null or misaligned source", what, (long long)k,
-                           (long long)j);
+        if (key_kind[j] != kRaw && key_numel[j] > 0) {
+          hik[conv_j.size()] = IntKey{key_numel[j], key_kind[j], soff};
+          conv_j.push_back(j);
+          conv_col.push_back(soff);
+          soff += (key_numel[j] + 3) & ~int64_t(3);
+        }
+      for (size_t q = 0; q < conv_j.size(); ++q) {
+        const int64_t j = conv_j[q];
+        for (int64_t k = 0; k < K; ++k) {
+          hsrc[static_cast<int64_t>(q) * K + k] = hp[j * K + k];
+          hp[j * K + k] = reinterpret_cast<int64_t>(int_scratch + k * S + conv_col[q]);
+        }
+      }
+    }
+    // the spot-checked sources: client 0's first and client K-1's last non-empty key
+    for (int64_t j = 0; j < n_keys && !first_src; ++j)
+      if (kf[j].need) first_src = reinterpret_cast<const void*>(client_ptrs[kf[j].col]);
+    for (int64_t j = n_keys - 1; j >= 0 && !last_src; --j)
+      if (kf[j].need) last_src = reinterpret_cast<const void*>(client_ptrs[(K - 1) * ld + kf[j].col]);
     return FEDAVG_OK;
   };
   const bool convert = fuse && n_int > 0;
-  int rc = fill(convert);
+  int rc = fill(convert);  // a misaligned fp32 source clears `fuse`: the integer keys then stay as they are
   if (rc) return rc;
-  if (convert && !fuse) {  // a misaligned fp32 source: the integer keys stay as they are
-    rc = fill(false);
-    if (rc) return rc;
-  }
   const bool converted = convert && fuse;
+  FEDAVG_ROUND_MARK(3);  // the pointer-table fill
   if (!first_src) {  // every key empty
     if (sumsq) {
       const hipError_t e = hipMemsetAsync(sumsq, 0, static_cast<size_t>(K) * sizeof(double), static_cast<hipStream_t>(stream));
@@ -1314,6 +1367,7 @@ int fedavg_device_round_f32(const int64_t* client_ptrs, int64_t ptr_ld, const in
   // source (the Python layer checks every tensor's device)
   if (!is_device_memory(first_src) || !is_device_memory(last_src))
     return set_error(FEDAVG_EINVAL, "%s: client sources must be device memory", what);
+  FEDAVG_ROUND_MARK(4);  // the sources' spot check
   // the unit width, then the key table
   const bool all_raw = converted || n_int == 0;
   const SegFusedPlan plan = fuse ? seg_fused_plan(key_numel, n_keys, K, all_raw) : SegFusedPlan{false, 0, 0, 0};
@@ -1327,6 +1381,7 @@ int fedavg_device_round_f32(const int64_t* client_ptrs, int64_t ptr_ld, const in
   // the reference's weights n_i / N (fedavg_trainer.py:453) rounded once to
   // fp32 (nearest even, the cast ATen applies to the scalar at :455)
   for (int64_t k = 0; k < K; ++k) hw[k] = static_cast<float>(weights[k]);
+  FEDAVG_ROUND_MARK(5);  // plan, key table, weights
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int64_t bytes = converted ? L.isrc + n_int * K * static_cast<int64_t>(sizeof(int64_t)) : L.ik;
   const hipError_t e = hipMemcpyAsync(dev_ws, host_ws, static_cast<size_t>(bytes), hipMemcpyHostToDevice, s);
@@ -1334,6 +1389,7 @@ int fedavg_device_round_f32(const int64_t* client_ptrs, int64_t ptr_ld, const in
     (void)hipGetLastError();
     return set_error(-static_cast<int>(e), "%s: hipMemcpyAsync failed: %s", what, hipGetErrorString(e));
   }
+  FEDAVG_ROUND_MARK(6);  // the tables' H2D issued
   const char* db = static_cast<const char*>(dev_ws);
   const auto* keys = reinterpret_cast<const SegKey*>(db);
   const auto* tptrs = reinterpret_cast<const int64_t*>(db + L.ptrs);
@@ -1346,8 +1402,10 @@ int fedavg_device_round_f32(const int64_t* client_ptrs, int64_t ptr_ld, const in
     rc = launch_status(what);
     if (rc) return rc;
   }
+  FEDAVG_ROUND_MARK(7);  // the integer keys' launch
   if (fuse) {
     rc = launch_seg_fused(plan, keys, tptrs, n_keys, units, K, dw, out, partials, partial_elems, sumsq, s, what);
+    FEDAVG_ROUND_MARK(8);  // the fused launch and the sums' finalize
     return rc ? rc : FEDAVG_OK;
   }
   if (small)
@@ -1357,6 +1415,7 @@ int fedavg_device_round_f32(const int64_t* client_ptrs, int64_t ptr_ld, const in
     launch_reduce_segments<kSegU, kSegC, kSegStyle>(keys, tptrs, n_keys, units, K, dw, out,
                                                     static_cast<int64_t>(kSegBlocksPerCU) * cu_count(), s);
   rc = launch_status(what);
+  FEDAVG_ROUND_MARK(8);  // the reduce's launches
   return rc ? rc : 1;
 }
 

@@ -8,7 +8,8 @@ table from KeyTable.collect; then the native call alone, timed per call
 forms: fused with the integer keys' scratch (production), the reduce alone
 (no conversion), fused right after a fresh walk (the address table just
 written by the walker threads, as in a round), the walk itself
-(KeyTable.collect) at 1, 2, 4, 8 and all intra-op threads, and, for scale, hipPointerGetAttributes and an empty
+(KeyTable.collect) at 1, 2, 4, 8 and all intra-op threads, the call's host
+phases after a walk (probe library build, fedavg_device_round_phases), and, for scale, hipPointerGetAttributes and an empty
 hipMemcpyAsync-sized H2D of the table bytes through torch.  One JSON line
 per form with the median and min call time in microseconds.
 """
@@ -92,6 +93,29 @@ def main():
     recs["fused_us"] = timed(lambda: call(True), args.calls)
     recs["reduce_only_us"] = timed(lambda: call(False), args.calls)
     recs["fused_after_walk_us"] = timed(lambda: call(True), args.calls, setup=walk)
+    # the same call from the probe library, which records its host phases
+    try:
+        probe = mfl_amd._lib.load_probe()
+    except Exception:  # noqa: BLE001 -- probe library not built
+        probe = None
+    if probe is not None:
+        names = ["checks", "key_validation", "fill", "spot_check", "plan_keys_weights", "h2d_issue",
+                 "int_launch", "reduce_launches"]
+        buf = (ctypes.c_double * 10)()
+        ph = {nm: [] for nm in names}
+        for _ in range(args.calls):
+            walk()
+            rc = probe.fedavg_device_round_f32(cur["ptrs"].ctypes.data, n_cols, ki.ctypes.data, numel.ctypes.data,
+                                               offset.ctypes.data, kind.ctypes.data, n, K, w64.ctypes.data,
+                                               out.data_ptr(), partials.data_ptr(), partials.numel(),
+                                               sumsq.data_ptr(), scr.data_ptr(), scr.numel(), ws_h.data_ptr(),
+                                               ws_d.data_ptr(), need, s)
+            assert rc == 0, rc
+            m = probe.fedavg_device_round_phases(buf, 10)
+            for i, nm in enumerate(names[: m - 1]):
+                ph[nm].append(buf[i + 1] - buf[i])
+            torch.cuda.synchronize()
+        recs["phases_after_walk_us"] = {nm: round(float(np.median(v)), 2) for nm, v in ph.items() if v}
     nt = torch.get_num_threads()
     for t in sorted({1, 2, 4, 8, nt}):
         torch.set_num_threads(t)
