@@ -10,7 +10,11 @@ with the clients' tensors placed three ways:
   arena    : one allocation for the whole round, client after client, each
              key 256-B aligned (not the packed [K, ld] layout the row
              kernel's arena check accepts);
-  shuffled : the same arena, the (client, key) tensors at shuffled slots.
+  shuffled : the same arena, the (client, key) tensors at shuffled slots;
+  packed   : the [K, ld] rows layout (client i's key j at i * ld + offset_j),
+             so the same bytes also run the row kernel (fedavg_reduce_sqdist_f32,
+             `rows_gpu_us_*`) -- the host rows' fused pass the device round is
+             held against.
 Run under rocprofv3 --kernel-trace --stats: the kernels' average durations
 per layout answer whether address translation (many 2 MB segments per
 window) or the kernel's own structure costs the time against the packed
@@ -38,7 +42,25 @@ from host_cost_probe import device_clients
 
 def relayout(dicts, layout, dev):
     if layout == "separate":
-        return dicts
+        return dicts, None
+    if layout == "packed":
+        table = mfl_amd.KeyTable(dicts[0])
+        g = table.groups[torch.float32]
+        K, ld = len(dicts), g.ld
+        rows = torch.empty((K, ld), device=dev)
+        out = []
+        for i, sd in enumerate(dicts):
+            nd = type(sd)()
+            for e in table.entries:
+                t = sd[e.name]
+                if t.dtype == torch.float32:
+                    v = rows[i, e.offset:e.offset + e.numel].view(t.shape)
+                    v.copy_(t)
+                    nd[e.name] = v
+                else:
+                    nd[e.name] = t
+            out.append(nd)
+        return out, rows
     slots = [(i, k) for i, sd in enumerate(dicts) for k in sd]
     sizes = {(i, k): (dicts[i][k].numel() * dicts[i][k].element_size() + 255) // 256 * 256 for i, k in slots}
     order = list(slots)
@@ -60,12 +82,12 @@ def relayout(dicts, layout, dev):
             v.copy_(t)
             nd[k] = v
         out.append(nd)
-    return out
+    return out, None
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--layout", default="separate", choices=["separate", "arena", "shuffled"])
+    ap.add_argument("--layout", default="separate", choices=["separate", "arena", "shuffled", "packed"])
     ap.add_argument("--config", default="resnet56")
     ap.add_argument("--calls", type=int, default=30)
     args = ap.parse_args()
@@ -73,7 +95,7 @@ def main():
     torch.cuda.set_device(dev)
     lib = mfl_amd._lib.load()
     counts, dicts = device_clients(args.config, dev)
-    dicts = relayout(dicts, args.layout, dev)
+    dicts, rows = relayout(dicts, args.layout, dev)
     torch.cuda.synchronize()
     table = mfl_amd.KeyTable(dicts[0])
     g = table.groups[torch.float32]
@@ -104,13 +126,26 @@ def main():
                                          partials.data_ptr(), partials.numel(), sumsq.data_ptr(), scr.data_ptr(),
                                          scr.numel(), ws_h.data_ptr(), ws_d.data_ptr(), need, stream.cuda_stream)
         e1.record(stream)
-        assert rc == 0, rc
+        assert rc in (0, 1), rc  # 1: a source not 16-B aligned (packed keys), the reduce alone ran
         torch.cuda.synchronize()
         ts.append(e0.elapsed_time(e1) * 1e3)
-    print(json.dumps({"layout": args.layout, "config": args.config, "K": K, "keys": n,
-                      "round_gpu_us_median": round(float(np.median(ts)), 2),
-                      "round_gpu_us_min": round(float(np.min(ts)), 2),
-                      "out_checksum": float(out.double().sum()), "sums_checksum": float(sumsq.sum())}), flush=True)
+    rec = {"layout": args.layout, "config": args.config, "K": K, "keys": n, "fused": rc == 0,
+           "round_gpu_us_median": round(float(np.median(ts)), 2), "round_gpu_us_min": round(float(np.min(ts)), 2),
+           "out_checksum": float(out.double().sum()), "sums_checksum": float(sumsq.sum())}
+    if rows is not None:  # the row kernel on the same bytes (int keys are not in these rows: fp32 keys only)
+        w_dev = torch.tensor(w64, dtype=torch.float32, device=dev)
+        out_r = torch.empty(g.P, device=dev)
+        tr = []
+        for _ in range(args.calls):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            mfl_amd.reduce_with_sqdist(rows, w_dev, g.P, out_r)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            tr.append(e0.elapsed_time(e1) * 1e3)
+        rec["rows_gpu_us_median"] = round(float(np.median(tr)), 2)
+        rec["rows_gpu_us_min"] = round(float(np.min(tr)), 2)
+    print(json.dumps(rec), flush=True)
 
 
 if __name__ == "__main__":
