@@ -475,13 +475,22 @@ __global__ __launch_bounds__(kBlock) void segments_finalize_kernel(const double*
 // in registers (reloaded at a key change only).  K <= 256.
 constexpr int kSegFusedRowsPerThread = 8;  // ceil(K * S / 4 / 256) slots per thread at K <= 128, S <= 64 ... 256
 
-template <int S>
+// MAP (round 5): `umap` maps every unit to its key (staged with the tables),
+// and the NEXT unit's key and client addresses are fetched while this unit's
+// loads are in flight -- the key by scalar loads, the addresses behind the
+// tile's LDS-DMA, so both have arrived at the tile's barrier.  Without it a
+// unit waits for a wave-wide search over the key table (two rounds of vector
+// loads at 350 keys) and, at a key change, for its client addresses before
+// its data loads can start: four dependent latencies per tile, and a small
+// model's tiles change key almost every time.
+template <int S, bool MAP = false>
 __global__ __launch_bounds__(kBlock) void reduce_sqdist_segments_f32_kernel(const SegKey* __restrict__ keys,
                                                                             const int64_t* __restrict__ ptrs,
                                                                             int64_t n_keys, int64_t units, int K,
                                                                             const float* __restrict__ W,
                                                                             float* __restrict__ out,
-                                                                            double* __restrict__ partials) {
+                                                                            double* __restrict__ partials,
+                                                                            const int* __restrict__ umap) {
   constexpr int V = S / 4;
   extern __shared__ __attribute__((aligned(16))) float lds[];  // [K][S] swizzled tile, then the average [S]
   float* tile = lds;
@@ -491,19 +500,39 @@ __global__ __launch_bounds__(kBlock) void reduce_sqdist_segments_f32_kernel(cons
   double acc[1][4] = {{0.0, 0.0, 0.0, 0.0}};
   int64_t cur_key = -1;
   int64_t src[kSegFusedRowsPerThread];  // client address of the row of this thread's m-th load slot
-  for (int64_t u = blockIdx.x; u < units; u += gridDim.x) {
-    const int64_t j = find_key(keys, n_keys, u);
-    const SegKey key = keys[j];
+  const auto load_src = [&](const int64_t* P, int64_t (&d)[kSegFusedRowsPerThread]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int m = 0; m < kSegFusedRowsPerThread; ++m) {
+      const int i = wave * 64 + m * kBlock + lane;
+      d[m] = i < nload ? P[i / V] : 0;
+    }
+  };
+  int64_t u = blockIdx.x;
+  int64_t j = 0;
+  SegKey key{};
+  if constexpr (MAP) {
+    if (u < units) {
+      j = umap[u];
+      key = keys[j];
+      if (key.kind == kRaw) {
+        load_src(ptrs + j * K, src);
+        cur_key = j;
+      }
+    }
+  }
+  for (; u < units; u += gridDim.x) {
+    if constexpr (!MAP) {
+      j = find_key(keys, n_keys, u);
+      key = keys[j];
+    }
     const int64_t c0 = (u - key.unit_start) * S;
     const int n = key.numel - c0 < S ? static_cast<int>(key.numel - c0) : S;
     const int64_t* P = ptrs + j * K;
     if (key.kind == kRaw) {
-      if (j != cur_key) {
-        cur_key = j;
-#pragma unroll
-        for (int m = 0; m < kSegFusedRowsPerThread; ++m) {
-          const int i = wave * 64 + m * kBlock + lane;
-          src[m] = i < nload ? P[i / V] : 0;
+      if constexpr (!MAP) {
+        if (j != cur_key) {
+          cur_key = j;
+          load_src(P, src);
         }
       }
       const int nfull = n >> 2;  // whole 16-B slices of this unit
@@ -533,11 +562,37 @@ __global__ __launch_bounds__(kBlock) void reduce_sqdist_segments_f32_kernel(cons
         tile[fused_at<S>(row, col)] = col < n ? load_cvt(reinterpret_cast<const void*>(P[row]), key.kind, c0 + col) : 0.f;
       }
     }
+    // MAP: the next unit's key (scalar loads) and, at a key change, its
+    // client addresses (behind this tile's loads): in hand at the barrier
+    int64_t jn = j;
+    SegKey keyn = key;
+    bool fresh = false;
+    int64_t srcn[kSegFusedRowsPerThread];
+    if constexpr (MAP) {
+      const int64_t un = u + gridDim.x;
+      if (un < units) {
+        jn = umap[un];
+        keyn = keys[jn];
+        if (keyn.kind == kRaw && jn != cur_key) {
+          load_src(ptrs + jn * K, srcn);
+          fresh = true;
+        }
+      }
+    }
     barrier_loads();
     fused_average<S>(tile, gs, K, W, n, out + key.out_offset + c0);
     barrier_lds();
     fused_squares<S, 1, false>(tile, gs, K, n, acc);
     barrier_lds();  // the tile is read out before the next one lands
+    if constexpr (MAP) {
+      j = jn;
+      key = keyn;
+      if (fresh) {
+#pragma unroll
+        for (int m = 0; m < kSegFusedRowsPerThread; ++m) src[m] = srcn[m];
+        cur_key = jn;
+      }
+    }
   }
   fused_finish(lds, acc, K, partials);
 }
@@ -797,7 +852,7 @@ inline int64_t seg_fused_lds_bytes(int64_t K, int S) {
   return b > kBlock * 8 ? b : kBlock * 8;
 }
 
-template <int S>
+template <int S, bool MAP = false>
 int seg_fused_per_cu(int64_t K) {
   static std::mutex mu;
   static std::map<std::pair<int, int64_t>, int> cache;
@@ -806,7 +861,7 @@ int seg_fused_per_cu(int64_t K) {
   std::lock_guard<std::mutex> lk(mu);
   auto it = cache.find({dev, K});
   if (it != cache.end()) return it->second;
-  const auto kern = reduce_sqdist_segments_f32_kernel<S>;
+  const auto kern = reduce_sqdist_segments_f32_kernel<S, MAP>;
   const int64_t lds = seg_fused_lds_bytes(K, S);
   int per_cu = 0;
   if (lds > 65536 && hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -822,10 +877,17 @@ int seg_fused_per_cu(int64_t K) {
   return per_cu;
 }
 
-template <int S>
+template <int S, bool MAP = false>
 int64_t seg_fused_grid(int64_t K, int64_t units) {
-  const int64_t g = static_cast<int64_t>(seg_fused_per_cu<S>(K)) * cu_count();
+  const int64_t g = static_cast<int64_t>(seg_fused_per_cu<S, MAP>(K)) * cu_count();
   return units < g ? units : g;
+}
+
+// resident workgroups per CU of either tile kernel (the partials' bound)
+template <int S>
+int seg_fused_per_cu_max(int64_t K) {
+  const int a = seg_fused_per_cu<S, false>(K), b = seg_fused_per_cu<S, true>(K);
+  return a > b ? a : b;
 }
 
 int64_t units_of(const int64_t* numel, int64_t n_keys, int64_t span = kSegSpan) {
@@ -936,7 +998,7 @@ SegFusedPlan seg_fused_plan(const int64_t* numel, int64_t n_keys, int64_t K, boo
 // The fused launch (+ the sums' finalize) on tables staged with plan.span
 int launch_seg_fused(const SegFusedPlan& p, const SegKey* keys, const int64_t* tptrs, int64_t n_keys, int64_t units,
                      int64_t K, const float* weights, float* out, double* partials, int64_t partial_elems,
-                     double* sumsq, hipStream_t s, const char* what) {
+                     double* sumsq, hipStream_t s, const char* what, const int* umap = nullptr) {
   if (units == 0) {
     const hipError_t e = hipMemsetAsync(sumsq, 0, static_cast<size_t>(K) * sizeof(double), s);
     return e == hipSuccess ? FEDAVG_OK : set_error(-static_cast<int>(e), "%s: hipMemsetAsync failed", what);
@@ -974,13 +1036,19 @@ int launch_seg_fused(const SegFusedPlan& p, const SegKey* keys, const int64_t* t
     const int S = static_cast<int>(p.span);
 #define FEDAVG_SEG_FUSED(C)                                                                                        \
   if (S == C) {                                                                                                    \
-    if (seg_fused_per_cu<C>(K) <= 0) return set_error(FEDAVG_EMODE, "%s: tile does not fit LDS", what);            \
-    nparts = seg_fused_grid<C>(K, units);                                                                          \
+    if ((umap ? seg_fused_per_cu<C, true>(K) : seg_fused_per_cu<C>(K)) <= 0)                                      \
+      return set_error(FEDAVG_EMODE, "%s: tile does not fit LDS", what);                                           \
+    nparts = umap ? seg_fused_grid<C, true>(K, units) : seg_fused_grid<C>(K, units);                               \
     if (partial_elems < K * nparts)                                                                                \
       return set_error(FEDAVG_EINVAL, "%s: partials need %lld doubles", what, (long long)(K * nparts));             \
-    hipLaunchKernelGGL((reduce_sqdist_segments_f32_kernel<C>), dim3(static_cast<unsigned>(nparts)), dim3(kBlock),    \
-                       static_cast<unsigned>(seg_fused_lds_bytes(K, C)), s, keys, tptrs, n_keys, units, k32, weights, \
-                       out, partials);                                                                             \
+    if (umap)                                                                                                      \
+      hipLaunchKernelGGL((reduce_sqdist_segments_f32_kernel<C, true>), dim3(static_cast<unsigned>(nparts)),         \
+                         dim3(kBlock), static_cast<unsigned>(seg_fused_lds_bytes(K, C)), s, keys, tptrs, n_keys,    \
+                         units, k32, weights, out, partials, umap);                                                 \
+    else                                                                                                           \
+      hipLaunchKernelGGL((reduce_sqdist_segments_f32_kernel<C>), dim3(static_cast<unsigned>(nparts)), dim3(kBlock),  \
+                         static_cast<unsigned>(seg_fused_lds_bytes(K, C)), s, keys, tptrs, n_keys, units, k32,      \
+                         weights, out, partials, nullptr);                                                          \
   }
     FEDAVG_SEG_FUSED(32)
     FEDAVG_SEG_FUSED(64)
@@ -1018,13 +1086,19 @@ struct RoundWs {
   int64_t ptrs, w, ik, isrc, end;
 };
 
+// the tile kernel's unit -> key map is staged for rounds of at most this many
+// units (256 KiB; a model of more units at 17-128 clients takes the windows)
+constexpr int64_t kSegUnitMapMax = 65536;
+
 inline RoundWs round_ws(int64_t K, int64_t n_keys) {
   RoundWs r;
   r.ptrs = n_keys * static_cast<int64_t>(sizeof(SegKey));
   r.w = round16(r.ptrs + (n_keys * K + kSegWinTablePad) * static_cast<int64_t>(sizeof(int64_t)));
   r.ik = r.w + round16(K * static_cast<int64_t>(sizeof(float)));
   r.isrc = r.ik + round16(n_keys * static_cast<int64_t>(sizeof(IntKey)));
-  r.end = r.isrc + n_keys * K * static_cast<int64_t>(sizeof(int64_t));
+  // + room for the unit map, placed right after whatever part is used
+  r.end = round16(r.isrc + n_keys * K * static_cast<int64_t>(sizeof(int64_t))) +
+          kSegUnitMapMax * static_cast<int64_t>(sizeof(int));
   return r;
 }
 
@@ -1151,8 +1225,9 @@ int fedavg_client_sqdist_segments_f32(const int64_t* client_ptrs, const int64_t*
 int64_t fedavg_reduce_sqdist_segments_partials(int64_t K) {
   if (K <= 0 || K > kSegFusedMaxK) return 0;
   const int S = seg_fused_cols(K);
-  const int per_cu = S == 32 ? seg_fused_per_cu<32>(K)
-                     : (S == 64 ? seg_fused_per_cu<64>(K) : (S == 128 ? seg_fused_per_cu<128>(K) : seg_fused_per_cu<256>(K)));
+  const int per_cu = S == 32 ? seg_fused_per_cu_max<32>(K)
+                     : (S == 64 ? seg_fused_per_cu_max<64>(K)
+                                : (S == 128 ? seg_fused_per_cu_max<128>(K) : seg_fused_per_cu_max<256>(K)));
   const int64_t tiles = K * static_cast<int64_t>(per_cu > 0 ? per_cu : 1) * cu_count();
   const int64_t windows = K * segwin_waves_for(segwin_kmax(K), INT64_MAX / 2);  // a full window launch
   return tiles > windows ? tiles : windows;
@@ -1270,8 +1345,11 @@ int fedavg_device_round_f32(const int64_t* client_ptrs, int64_t ptr_ld, const in
   const int64_t ld = ptr_ld;
   if (S >= (int64_t(1) << 31)) return set_error(FEDAVG_EINVAL, "%s: integer keys too large", what);
   bool fuse = sumsq != nullptr && K <= kSegFusedMaxK;
-  // a fused round takes its integer keys as fp32 scratch columns (the
-  // window kernels read fp32 only); the two-pass reduce converts in-kernel
+  // a fused round takes its integer keys as fp32 scratch columns: the window
+  // kernels read fp32 only, and the tiles' in-kernel conversion (element by
+  // element, one tile per key and client block) made resnet56 x 100's fused
+  // tile kernel 104 us against 77 + 4.7 us with the conversion launch
+  // (profiles/r05/segwin_layout/); the two-pass reduce converts in-kernel
   if (fuse && n_int > 0 &&
       (!int_scratch || scratch_elems < K * S || !aligned16(int_scratch) || !is_device_memory(int_scratch)))
     return set_error(FEDAVG_EINVAL, "%s: integer keys need an aligned device scratch of %lld floats", what,
@@ -1378,12 +1456,23 @@ int fedavg_device_round_f32(const int64_t* client_ptrs, int64_t ptr_ld, const in
     hk[j] = SegKey{key_numel[j], key_offset[j], converted ? kRaw : key_kind[j], units};
     units += (key_numel[j] + span - 1) / span;
   }
+  // the tiles' unit -> key map (reduce_sqdist_segments_f32_kernel MAP)
+  const int64_t used = converted ? L.isrc + n_int * K * static_cast<int64_t>(sizeof(int64_t)) : L.ik;
+  const int64_t moff = round16(used);
+  const bool with_map = fuse && !plan.win && units > 0 && units <= kSegUnitMapMax;
+  if (with_map) {
+    int* hm = reinterpret_cast<int*>(hb + moff);
+    for (int64_t j = 0; j < n_keys; ++j) {
+      const int64_t u1 = j + 1 < n_keys ? hk[j + 1].unit_start : units;
+      for (int64_t u = hk[j].unit_start; u < u1; ++u) hm[u] = static_cast<int>(j);
+    }
+  }
   // the reference's weights n_i / N (fedavg_trainer.py:453) rounded once to
   // fp32 (nearest even, the cast ATen applies to the scalar at :455)
   for (int64_t k = 0; k < K; ++k) hw[k] = static_cast<float>(weights[k]);
   FEDAVG_ROUND_MARK(5);  // plan, key table, weights
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const int64_t bytes = converted ? L.isrc + n_int * K * static_cast<int64_t>(sizeof(int64_t)) : L.ik;
+  const int64_t bytes = with_map ? moff + units * static_cast<int64_t>(sizeof(int)) : used;
   const hipError_t e = hipMemcpyAsync(dev_ws, host_ws, static_cast<size_t>(bytes), hipMemcpyHostToDevice, s);
   if (e != hipSuccess) {
     (void)hipGetLastError();
@@ -1404,7 +1493,8 @@ int fedavg_device_round_f32(const int64_t* client_ptrs, int64_t ptr_ld, const in
   }
   FEDAVG_ROUND_MARK(7);  // the integer keys' launch
   if (fuse) {
-    rc = launch_seg_fused(plan, keys, tptrs, n_keys, units, K, dw, out, partials, partial_elems, sumsq, s, what);
+    rc = launch_seg_fused(plan, keys, tptrs, n_keys, units, K, dw, out, partials, partial_elems, sumsq, s, what,
+                          with_map ? reinterpret_cast<const int*>(db + moff) : nullptr);
     FEDAVG_ROUND_MARK(8);  // the fused launch and the sums' finalize
     return rc ? rc : FEDAVG_OK;
   }

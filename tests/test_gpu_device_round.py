@@ -227,3 +227,31 @@ def test_drop_in_device_round_takes_the_one_call(monkeypatch):
     exact = O.client_distances_exact(ref_locals, ref_glob)
     assert d[0] == 0.0
     assert np.all(np.abs(d - exact) <= np.spacing(exact.astype(np.float32)).astype(np.float64))
+
+
+@pytest.mark.parametrize("K", [5, 40, 100])
+def test_legacy_fused_segments_entry_matches(K):
+    """fedavg_reduce_sqdist_segments_f32 (the separate-table entry, integer
+    keys converted inside the tiles, no unit map) gives the bits and sums of
+    the one-call round on the same clients."""
+    counts, dicts = _clients(K, _SPECS, seed=50 + K)
+    r = _Round(counts, dicts)
+    rc, out, sumsq = r.run()
+    assert rc == 0
+    lib = r.lib
+    cptrs = np.ascontiguousarray(r.ptrs[:, r.key_index])
+    w_dev = torch.tensor(r.w64, dtype=torch.float32, device=DEV)
+    out2 = torch.full((r.g.P,), float("nan"), device=DEV)
+    partials = torch.empty(max(1, lib.fedavg_reduce_sqdist_segments_partials(K)), dtype=torch.float64, device=DEV)
+    sums2 = torch.empty(K, dtype=torch.float64, device=DEV)
+    need = lib.fedavg_segments_workspace(K, r.n)
+    ws_h = torch.empty(need, dtype=torch.uint8, pin_memory=True)
+    ws_d = torch.empty(need, dtype=torch.uint8, device=DEV)
+    rc2 = lib.fedavg_reduce_sqdist_segments_f32(cptrs.ctypes.data, r.numel.ctypes.data, r.offset.ctypes.data,
+                                                r.kind.ctypes.data, r.n, K, w_dev.data_ptr(), out2.data_ptr(),
+                                                partials.data_ptr(), partials.numel(), sums2.data_ptr(),
+                                                ws_h.data_ptr(), ws_d.data_ptr(), need, None)
+    torch.cuda.synchronize()
+    assert rc2 == 0
+    assert_bits(out2.cpu(), out.cpu(), f"legacy fused entry K={K}")
+    assert np.allclose(sums2.cpu().numpy(), sumsq.cpu().numpy(), rtol=1e-12, atol=0.0)
