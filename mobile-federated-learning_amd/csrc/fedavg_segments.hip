@@ -775,7 +775,14 @@ __global__ __launch_bounds__(64 * NW, MINW) void reduce_sqdist_segwin_kernel(
       const double q45 = fold32(p[4], p[5]), q67 = fold32(p[6], p[7]);
       acc[64 * b] += fold8(fold16(q01, q23), fold16(q45, q67), upper);
     }
-    if (un < units32 && !fastn) load_slow(c0n, nn, Kw);
+    if (un < units32 && !fastn) {
+      // a fresh opaque K: with the squares' Kw the compiler kept their KMAX
+      // row masks (i < Kw) alive for these loads -- 139 SGPRs spilled to
+      // VGPR lanes, two v_writelane per row in the squares loop
+      int Ks = K;
+      asm volatile("" : "+s"(Ks));
+      load_slow(c0n, nn, Ks);
+    }
     j = jn;
     c0 = c0n;
     n = nn;

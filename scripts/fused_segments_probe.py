@@ -79,7 +79,8 @@ def main():
                 if "sumsq" in last and torch.float32 in last["sumsq"]:
                     s = last["sumsq"][torch.float32]
                 else:
-                    dicts = [last["seg_keep0"] if sd is w_glob else sd for _, sd in w_locals]
+                    keep0 = agg._client0_tensors(last)
+                    dicts = [keep0 if sd is w_glob else sd for _, sd in w_locals]
                     s = agg._sqdist_segments(last["table"], dicts, last["dev"][torch.float32][1])
                 b.record()
                 if r >= 2:
