@@ -475,7 +475,7 @@ __global__ __launch_bounds__(kBlock) void segments_finalize_kernel(const double*
 // in registers (reloaded at a key change only).  K <= 256.
 constexpr int kSegFusedRowsPerThread = 8;  // ceil(K * S / 4 / 256) slots per thread at K <= 128, S <= 64 ... 256
 
-// MAP (round 5): `umap` maps every unit to its key (staged with the tables),
+// MAP (round 4): `umap` maps every unit to its key (staged with the tables),
 // and the NEXT unit's key and client addresses are fetched while this unit's
 // loads are in flight -- the key by scalar loads, the addresses behind the
 // tile's LDS-DMA, so both have arrived at the tile's barrier.  Without it a
@@ -1071,7 +1071,7 @@ int launch_seg_fused(const SegFusedPlan& p, const SegKey* keys, const int64_t* t
 }
 
 // ---------------------------------------------------------------------------
-// A device-resident round in one call (round 5: fedavg_device_round_f32).
+// A device-resident round in one call (round 4: fedavg_device_round_f32).
 // The Python layer used to gather the group's pointer columns, convert the
 // integer keys through a pack launch of its own, upload the weights and stage
 // the tables in four steps (0.3 ms of host time for resnet56 x 100's 35,000
@@ -1356,7 +1356,7 @@ int fedavg_device_round_f32(const int64_t* client_ptrs, int64_t ptr_ld, const in
   // kernels read fp32 only, and the tiles' in-kernel conversion (element by
   // element, one tile per key and client block) made resnet56 x 100's fused
   // tile kernel 104 us against 77 + 4.7 us with the conversion launch
-  // (profiles/r05/segwin_layout/); the two-pass reduce converts in-kernel
+  // (profiles/r04/segwin_layout/); the two-pass reduce converts in-kernel
   if (fuse && n_int > 0 &&
       (!int_scratch || scratch_elems < K * S || !aligned16(int_scratch) || !is_device_memory(int_scratch)))
     return set_error(FEDAVG_EINVAL, "%s: integer keys need an aligned device scratch of %lld floats", what,
@@ -1369,7 +1369,7 @@ int fedavg_device_round_f32(const int64_t* client_ptrs, int64_t ptr_ld, const in
   // prefetcher follows -- the call took 73-78 us right after a resnet56 x 100
   // walk, against 182-200 us filling key-major and 79-86 us in blocks of 8
   // clients; with the checks branch-free per row, 63-65 us, 44 of them the
-  // fill (scripts/device_round_call_probe.py, profiles/r05/device_round/).
+  // fill (scripts/device_round_call_probe.py, profiles/r04/device_round/).
   const void* first_src = nullptr;
   const void* last_src = nullptr;
   // per key: table column, the masks its sources are checked with (a
