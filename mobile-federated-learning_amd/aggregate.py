@@ -525,6 +525,9 @@ class DeviceAggregator:
 
         lib = _lib.load()
         K, n_cols = ptrs.shape
+        if g.P == 0:  # every key of the group is empty: nothing to read (the reference's loop adds empty tensors)
+            sums = torch.zeros(K, dtype=torch.float64, device=self.device) if FUSE_DISTANCES else None
+            return torch.empty(0, dtype=torch.float32, device=self.device), sums
         _, arrs, (ki_p, numel_p, offset_p, kind_p), sizes = self._round_meta(g, n_cols)
         n = len(arrs[1])
         per_k = sizes.get(K)

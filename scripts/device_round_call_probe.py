@@ -121,6 +121,9 @@ def main():
         torch.set_num_threads(t)
         recs[f"walk_us_threads_{t}"] = timed(walk, args.calls, sync=False)
     torch.set_num_threads(nt)
+    # the walk's fixed part: one client, and the [K, N] address table's allocation
+    recs["walk_us_one_client"] = timed(lambda: table.collect(dicts[:1], dev), args.calls, sync=False)
+    recs["alloc_table_us"] = timed(lambda: torch.empty((K, n_cols), dtype=torch.int64), args.calls, sync=False)
     hip = ctypes.CDLL("libamdhip64.so")
     attr = ctypes.create_string_buffer(256)
     p = ctypes.c_void_p(out.data_ptr())

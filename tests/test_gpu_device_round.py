@@ -255,3 +255,18 @@ def test_legacy_fused_segments_entry_matches(K):
     assert rc2 == 0
     assert_bits(out2.cpu(), out.cpu(), f"legacy fused entry K={K}")
     assert np.allclose(sums2.cpu().numpy(), sumsq.cpu().numpy(), rtol=1e-12, atol=0.0)
+
+
+def test_drop_in_device_round_all_empty_keys():
+    """A model whose fp32 keys are all empty (numel 0): no native call, the
+    reference's loop result (empty tensors) and zero :291 distances."""
+    K = 4
+    dicts = [OrderedDict(a=torch.zeros(0, device=DEV), b=torch.zeros((3, 0), device=DEV)) for _ in range(K)]
+    counts = [3, 1, 4, 1]
+    agg = mfl_amd.DeviceAggregator(DEV)
+    wl = [(n, OrderedDict(sd)) for n, sd in zip(counts, dicts)]
+    glob = agg.aggregate(wl)
+    assert glob["a"].shape == (0,) and glob["b"].shape == (3, 0)
+    assert glob["a"].device.type == "cuda"
+    d = agg.client_distances(wl, glob)
+    assert np.array_equal(d, np.zeros(K))
