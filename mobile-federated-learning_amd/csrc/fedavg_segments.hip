@@ -582,7 +582,7 @@ __global__ __launch_bounds__(kBlock) void reduce_sqdist_segments_f32_kernel(cons
     barrier_loads();
     fused_average<S>(tile, gs, K, W, n, out + key.out_offset + c0);
     barrier_lds();
-    fused_squares<S, 1, false>(tile, gs, K, n, acc);
+    fused_squares<S, 1, true>(tile, gs, K, n, acc);  // full tiles unmasked (same VGPRs, round 4)
     barrier_lds();  // the tile is read out before the next one lands
     if constexpr (MAP) {
       j = jn;
