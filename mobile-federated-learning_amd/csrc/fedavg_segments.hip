@@ -681,11 +681,16 @@ __global__ __launch_bounds__(64 * NW, MINW) void reduce_sqdist_segwin_kernel(
         x[i][v] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (lane * VEC + v) * 4, 0, 2));
     }
   };
-  // client i of a fast window
-  const auto load_fast = [&](int i, int64_t c0, int Kw, bool on) __attribute__((always_inline)) {
-    const float* base = ptr_of(i) + c0;
-    const int bytes = (on && i < Kw) ? WC * 4 : 0;
-    x[i] = win_load<VEC>(__builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, bytes, 0x00020000), voff);
+  // client i of a fast window: the client's own address is the descriptor's
+  // base and the window's start goes in soffset (one SGPR per window instead
+  // of a 64-bit add per row); the range check covers soffset + voffset, so
+  // the record count is the window's end byte -- 0 for padding rows (i >= Kw)
+  // (the host keeps every key of a window plan under 2^30 elements)
+  const auto load_fast = [&](int i, uint32_t soff, uint32_t nrec, int Kw) __attribute__((always_inline)) {
+    x[i] = win_load<VEC>(
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(ptr_of(i)), 0, i < Kw ? static_cast<int>(nrec) : 0,
+                                          0x00020000),
+        voff, soff);
   };
 
   // window / key indices in 32 bits (the host checks units < 2^31): 64-bit
@@ -709,7 +714,8 @@ __global__ __launch_bounds__(64 * NW, MINW) void reduce_sqdist_segwin_kernel(
     load_ptrs(ptrs + static_cast<int64_t>(j) * K);
     if (n == WC) {
 #pragma unroll
-      for (int i = 0; i < KMAX; ++i) load_fast(i, c0, K, true);
+      for (int i = 0; i < KMAX; ++i)
+        load_fast(i, static_cast<uint32_t>(c0 * 4), static_cast<uint32_t>((c0 + WC) * 4), K);
     } else {
       load_slow(c0, n, K);
     }
@@ -730,6 +736,10 @@ __global__ __launch_bounds__(64 * NW, MINW) void reduce_sqdist_segwin_kernel(
       nn = cols_of(kn.numel, w);
     }
     const bool fastn = un < units32 && nn == WC;
+    // the next fast window's soffset and record count; no loads unless it is fast
+    const uint32_t soffn = static_cast<uint32_t>(c0n * 4), nrecn = static_cast<uint32_t>((c0n + WC) * 4);
+    int Kwn = fastn ? K : 0;
+    asm volatile("" : "+s"(Kwn));
     load_ptrs(ptrs + static_cast<int64_t>(jn) * K);  // the next window's addresses, before the chain
     // the chain (a slow window's columns past its key are 0)
     int wo = 0;
@@ -768,7 +778,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void reduce_sqdist_segwin_kernel(
         p[r] = 0.0;
         if (i < KMAX) {
           p[r] = win_sq<VEC>(x[i] - a);
-          load_fast(i, c0n, Kw, fastn);
+          load_fast(i, soffn, nrecn, Kwn);
         }
       }
       const double q01 = fold32(p[0], p[1]), q23 = fold32(p[2], p[3]);
@@ -989,7 +999,10 @@ struct SegFusedPlan {
 
 SegFusedPlan seg_fused_plan(const int64_t* numel, int64_t n_keys, int64_t K, bool all_raw) {
   SegFusedPlan p{false, segwin_kmax(K), seg_fused_cols(K), 0};
-  if (p.kmax > 0 && all_raw && numel && n_keys > 0 && n_keys < (int64_t(1) << 31) && !segwin_disabled()) {
+  // the windows address a key's bytes with 32-bit buffer offsets
+  bool small_keys = numel != nullptr;
+  for (int64_t j = 0; small_keys && j < n_keys; ++j) small_keys = numel[j] < (int64_t(1) << 30);
+  if (p.kmax > 0 && all_raw && small_keys && n_keys > 0 && n_keys < (int64_t(1) << 31) && !segwin_disabled()) {
     const int64_t wc = 64 * segwin_vec(p.kmax);
     const int64_t wunits = units_of(numel, n_keys, wc);
     const int64_t waves = segwin_waves_for(p.kmax, wunits);
