@@ -130,6 +130,23 @@ def test_weights_helper_matches_python(lib):
         assert w.tobytes() == expect.tobytes()
 
 
+def test_device_round_sizes_without_gpu(lib):
+    """fedavg_device_round_workspace / _scratch (host arithmetic, no GPU):
+    the workspace holds the key table, the padded key-major pointer table,
+    the fp32 weights, the integer keys' tables and the unit map's room; the
+    scratch is K rows of the integer / bool keys' columns, each 4-aligned."""
+    numel = np.array([432, 16, 1, 0, 7, 36864], dtype=np.int64)
+    kind = np.array([0, 0, 1, 2, 6, 0], dtype=np.int64)  # fp32, fp32, int64, int32 (empty), bool, fp32
+    for K in (1, 5, 100, 256):
+        n = len(numel)
+        ws = lib.fedavg_device_round_workspace(K, n)
+        tables = n * 32 + (n * K + 128) * 8 + K * 4 + n * 24 + n * K * 8
+        assert tables + 65536 * 4 <= ws <= tables + 65536 * 4 + 64 and ws % 16 == 0
+        assert lib.fedavg_device_round_scratch(numel.ctypes.data, kind.ctypes.data, n, K) == K * (4 + 8)
+    assert lib.fedavg_device_round_workspace(0, 3) == 0
+    assert lib.fedavg_device_round_scratch(None, None, 3, 4) == 0
+
+
 def test_weights_helper_zero_total(lib):
     n = np.zeros(3, np.int64)
     w = np.zeros(3, np.float32)
