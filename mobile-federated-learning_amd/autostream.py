@@ -22,14 +22,20 @@ path (178.8 ms).
   that ``w_locals`` is what was fed and then only the weights, the kernel
   and the result's D2H remain.  The check (``fedavg_collect_ext.verify_rows``,
   one native walk while the reduce runs): the same count and sample numbers
-  in order, distinct dicts, every client's keys in the table's order with
-  the table's dtypes and shapes, and element values at ~4,096 (client, key,
-  position) probes drawn afresh every round -- every key at least once, the
-  rest uniform over clients and keys -- against the pinned staging rows the
-  GPU reduces (converted as the packer converts).  A fixed pattern of
-  positions cannot miss an edit every round; an edit of one element of one
-  client can still go unseen in a given round (sampling), which is why the
-  structural guards below keep known editors out of the stream.
+  in order, distinct dicts, every client's keys exactly the table's in order,
+  EVERY (client, key) tensor an exact host Tensor, contiguous, with the
+  table's dtype and shape and the version counter a fresh ``copy.deepcopy``
+  gives (measured once on the running torch, ``DEEPCOPY_VERSION``), and
+  element values at ~4,096 (client, key, position) probes drawn afresh every
+  round -- every key at least once, the rest uniform over clients and keys --
+  against the pinned staging rows the GPU reduces (converted as the packer
+  converts).  The version counter makes in-place edits of w_locals between
+  :199 and :217 (clipping, noise, ``copy_``, slice assignment: any in-place
+  op) a deterministic fallback whatever elements they touch; a replaced
+  tensor object fails the same check (a fresh tensor's counter is not a deep
+  copy's).  What the counter cannot see -- writes through ``.data``/numpy
+  views or raw pointers, which bypass autograd's bookkeeping -- is left to
+  the value probes.
 
 Anything else falls back to the plain drop-in on ``w_locals`` (same bits,
 the reference's exceptions): a count or sample-number mismatch, a retried
@@ -101,6 +107,16 @@ class trainer_scope:
         return False
 
 
+def deepcopy_version() -> int:
+    """``copy.deepcopy(t)._version`` for a host tensor on this torch (cached)."""
+    v = ClientFeed.DEEPCOPY_VERSION
+    if v is None:
+        import copy
+
+        v = ClientFeed.DEEPCOPY_VERSION = int(copy.deepcopy(torch.zeros(1))._version)
+    return v
+
+
 class _Release(list):
     """Host tensors a finished round displaced, for the feed worker to drop."""
 
@@ -110,6 +126,9 @@ class ClientFeed:
     round being fed), filled by a background thread."""
 
     VERIFY_PROBES = 4096  # (client, key) pairs whose values are compared per round (two positions each)
+    # the version counter of a tensor fresh from copy.deepcopy (fedavg_trainer.py:199):
+    # 1 on torch 2.x (Tensor.__deepcopy__ ends in set_()); measured, not assumed
+    DEEPCOPY_VERSION = None
     VERIFY_FULL_ELEMS = 1 << 20  # rounds of at most this many elements (K x P) are compared in full
 
     def __init__(self, aggregator_fn, max_clients: int):
@@ -299,7 +318,8 @@ class ClientFeed:
         try:
             ext, names, templ, group, offset, kind, sptr, sld, ses = self._vplan
             st = ext.verify_rows(w_locals, list(self.fed), names, templ, group, offset, kind, sptr, sld, ses,
-                                 self.VERIFY_PROBES, random.getrandbits(64), self.VERIFY_FULL_ELEMS)
+                                 self.VERIFY_PROBES, random.getrandbits(64), self.VERIFY_FULL_ELEMS,
+                                 deepcopy_version())
             self.stats["last_verify"] = {"status": int(st[0]), "client": int(st[1]), "key": int(st[2]),
                                          "probes": int(st[3])}
             return st[0] == 0

@@ -383,10 +383,17 @@ static py::tuple small_round(py::list w_locals, py::list names, py::list templ, 
 //   * len(w_locals) == len(counts) and every w_locals[i] is a (n, dict) pair
 //     whose n == counts[i] (Python ==) and whose dict is not another
 //     client's dict object;
-//   * every client's dict holds exactly the table's keys in order (matched
-//     by the hashes in the dict's entry table, == where those differ);
-//   * at the probed pairs below, the value is a contiguous host tensor with
-//     the template's dtype and sizes;
+//   * every client's dict holds exactly the table's keys in order (exact
+//     string compares, key_eq; == on this thread for other key objects);
+//   * at EVERY (client, key) pair, the value is an exact Tensor, contiguous,
+//     on the host, with the template's dtype and sizes, and -- with
+//     expect_version >= 0 -- its version counter is expect_version: the value
+//     a fresh copy.deepcopy(tensor) carries (autostream measures it on the
+//     running torch).  The reference's :199 deep copies are made after the
+//     client's train() returned, so any in-place op on a w_locals tensor
+//     between :199 and :217 (add_, clamp_, mul_, copy_, an optimizer step,
+//     a slice assignment) moves that counter: such edits are caught every
+//     round, deterministically, whatever positions they touch;
 //   * element values at `probes` (client, key, position) triples drawn
 //     afresh from `seed` every round -- every key at least once (at a random
 //     client), the rest spread uniformly over all (client, key) pairs,
@@ -398,7 +405,8 @@ static py::tuple small_round(py::list w_locals, py::list names, py::list templ, 
 //     a match is exactly the reduction's criterion at that element.
 // The per-client walks run on torch's intra-op threads (see below).
 // status 0: all checks passed; 1 count; 2 sample number; 3 not a (n, dict)
-// pair; 4 repeated dict; 5 keys; 6 tensor metadata; 7 value (client, key).
+// pair; 4 repeated dict; 5 keys; 6 tensor metadata; 7 value (client, key);
+// 8 version counter (client, key).
 namespace {
 inline uint64_t mix64(uint64_t x) {
   x += 0x9E3779B97F4A7C15ull;
@@ -435,7 +443,7 @@ static py::tuple verify_rows(py::list w_locals, py::list counts, py::list names,
                              const std::vector<int64_t>& group, const std::vector<int64_t>& offset,
                              const std::vector<int64_t>& kind, const std::vector<int64_t>& stage_ptr,
                              const std::vector<int64_t>& stage_ld, const std::vector<int64_t>& stage_esize,
-                             int64_t probes, uint64_t seed, int64_t full_elems) {
+                             int64_t probes, uint64_t seed, int64_t full_elems, int64_t expect_version) {
   const Py_ssize_t K = PyList_GET_SIZE(w_locals.ptr());
   const Py_ssize_t N = PyList_GET_SIZE(names.ptr());
   auto res = [](int status, Py_ssize_t i, Py_ssize_t j, int64_t n) { return py::make_tuple(status, i, j, n); };
@@ -503,40 +511,70 @@ static py::tuple verify_rows(py::list w_locals, py::list counts, py::list names,
   std::vector<int64_t> status(static_cast<size_t>(K), 0);  // per client: 0, or (code << 32 | key)
   std::vector<int64_t> nprobe(static_cast<size_t>(K), 0);
   constexpr int64_t kRedo = -1;  // keys not identical: == compares on the GIL thread
-  // The keys are matched by the hashes stored in the dict's own entry table
-  // (_PyDict_Next): the key objects themselves -- one cache miss each, every
-  // client's own strings -- are never read.  A dict whose entries do not
-  // match the names' hashes in order is redone on this thread with ==.
+  // The dict's entry table in order (_PyDict_Next): hashes against the
+  // names' (a miss ends the fast walk), then every key compared exactly
+  // (key_eq: each net.cpu().state_dict() builds its own name strings, so
+  // the key objects are read -- prefetched with the values).  A dict whose
+  // keys are not exact str objects equal to the names in order is redone on
+  // this thread with ==.
   const auto fill_fast = [&](int64_t i) -> bool {
     Py_ssize_t pos = 0, j = 0;
     PyObject *key, *val;
     Py_hash_t h;
     PyObject** row = &vals[static_cast<size_t>(i) * N];
+    thread_local std::vector<PyObject*> keys;
+    keys.resize(N);
     while (_PyDict_Next(dicts[i], &pos, &key, &val, &h)) {
       if (j >= N || (key != name_ptr[j] && h != name_hash[j])) return false;
+      keys[j] = key;
       row[j++] = val;
+      __builtin_prefetch(key);
+      __builtin_prefetch(val);
     }
-    return j == N;
+    if (j != N) return false;
+    for (Py_ssize_t jj = 0; jj < N; ++jj)
+      if (key_eq(keys[jj], name_ptr[jj]) != KeyEq::kSame) return false;
+    return true;
+  };
+  // the VersionCounter object behind a tensor's _version (one more dependent
+  // miss per tensor): VariableVersion is exactly one intrusive_ptr
+  static_assert(sizeof(c10::VariableVersion) == sizeof(void*), "VariableVersion layout");
+  const auto version_obj = [](c10::TensorImpl* ti) -> const void* {
+    return *reinterpret_cast<void* const*>(&ti->version_counter());
   };
   // metadata checks and value probes of client i (its vals filled)
   const auto check_client = [&](int64_t i, std::vector<Probe>& todo) {
     todo.clear();
     int64_t st = 0;
     PyObject* const* row_vals = &vals[static_cast<size_t>(i) * N];
-    // the (client, key) pairs probed this round: each value's tensor checked
-    // (dtype, sizes, host, contiguous) and its elements compared; the other
-    // pairs are matched by key only -- every key is probed at one client or
-    // more each round (its anchor), so an edit of a key across clients is
-    // always seen, and the tensor objects of the rest are never touched
+    // every (client, key) pair: the value's tensor checked (exact Tensor,
+    // dtype, sizes, host, contiguous, version counter); the pairs probed this
+    // round also have elements compared -- every key is probed at one client
+    // or more each round (its anchor), so an edit of a key across clients is
+    // always seen by value too.  Prefetches a few keys ahead: the TensorImpl,
+    // then (once it has arrived) its VersionCounter.
     const auto probed = [&](Py_ssize_t j, uint64_t* hp) {
       const uint64_t h = mix64(seed ^ mix64(static_cast<uint64_t>(i) * 0x100000001B3ull + static_cast<uint64_t>(j)));
       *hp = h;
       return full || h <= thresh ||
              static_cast<int64_t>(mix64(seed + static_cast<uint64_t>(j)) % static_cast<uint64_t>(K)) == i;
     };
+    constexpr Py_ssize_t kImpl = 16, kVer = 8;
+    const auto impl_of = [&](Py_ssize_t j) -> c10::TensorImpl* {
+      return THPVariable_CheckExact(row_vals[j]) ? THPVariable_Unpack(row_vals[j]).unsafeGetTensorImpl() : nullptr;
+    };
+    const auto prefetch_version = [&](Py_ssize_t j) {
+      if (expect_version < 0) return;
+      if (c10::TensorImpl* ti = impl_of(j))
+        if (const void* v = version_obj(ti)) __builtin_prefetch(v);
+    };
+    for (Py_ssize_t j = 0; j < N && j < kImpl; ++j)
+      if (c10::TensorImpl* ti = impl_of(j)) __builtin_prefetch(ti);
+    for (Py_ssize_t j = 0; j < N && j < kVer; ++j) prefetch_version(j);
     for (Py_ssize_t j = 0; j < N && !st; ++j) {
-      uint64_t h;
-      if (!probed(j, &h)) continue;
+      if (j + kImpl < N)
+        if (c10::TensorImpl* ti = impl_of(j + kImpl)) __builtin_prefetch(ti);
+      if (j + kVer < N) prefetch_version(j + kVer);
       PyObject* val = row_vals[j];
       if (!THPVariable_CheckExact(val)) {  // a Tensor subclass: the plain path decides
         st = (int64_t(6) << 32) | j;
@@ -548,6 +586,15 @@ static py::tuple verify_rows(py::list w_locals, py::list counts, py::list names,
         st = (int64_t(6) << 32) | j;
         break;
       }
+      if (expect_version >= 0) {
+        const c10::VariableVersion& vc = ten.unsafeGetTensorImpl()->version_counter();
+        if (!vc.enabled() || static_cast<int64_t>(vc.current_version()) != expect_version) {
+          st = (int64_t(8) << 32) | j;
+          break;
+        }
+      }
+      uint64_t h;
+      if (!probed(j, &h)) continue;
       const int64_t n = numel[j];
       if (n <= 0) continue;
       const int64_t g = group[j];
@@ -630,5 +677,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("unpack", &unpack, "views of a flat buffer shaped like the key table's keys");
   m.def("unpack_into", &unpack_into, "those views assigned into a dict by key name");
   m.def("small_round", &small_round, "the host side of a small fp32 round in one call");
-  m.def("verify_rows", &verify_rows, "w_locals against a streamed round's staging rows (randomly sampled values)");
+  m.def("verify_rows", &verify_rows,
+        "w_locals against a streamed round's staging rows (every tensor's metadata and version counter, "
+        "randomly sampled values)",
+        py::arg("w_locals"), py::arg("counts"), py::arg("names"), py::arg("templ"), py::arg("group"),
+        py::arg("offset"), py::arg("kind"), py::arg("stage_ptr"), py::arg("stage_ld"), py::arg("stage_esize"),
+        py::arg("probes"), py::arg("seed"), py::arg("full_elems"), py::arg("expect_version") = -1);
 }

@@ -31,6 +31,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--threads", default="1,2,4,8,16")
     ap.add_argument("--reps", type=int, default=30)
+    ap.add_argument("--expect-version", type=int, default=1, help="-1: skip the version-counter check")
     args = ap.parse_args()
     ext = _collect_ext()
     K, shapes = CONFIGS["resnet56"]
@@ -63,7 +64,8 @@ def main():
         tv, tc = [], []
         for r in range(args.reps + 2):
             t0 = time.perf_counter()
-            res = ext.verify_rows(w_locals, counts, names, templ, group, offset, kind, sp, sld, ses, 4096, r, 1 << 20)
+            res = ext.verify_rows(w_locals, counts, names, templ, group, offset, kind, sp, sld, ses, 4096, r, 1 << 20,
+                                   args.expect_version)
             t1 = time.perf_counter()
             ext.collect(wdicts, names, templ, -1)
             t2 = time.perf_counter()

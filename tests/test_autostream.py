@@ -280,3 +280,39 @@ def test_tensor_changed_while_packed_breaks_the_round(plain_calls):
     assert feed.take(w_locals) is None
     assert "changed while they were packed" in feed.stats["last_fallback"]
     feed.close()
+
+
+@pytest.mark.parametrize("seed", range(20))
+def test_single_in_place_edit_falls_back_every_time(plain_calls, seed):
+    """A round large enough for sampled value checks (64 clients x 130 keys >
+    4,096 probes): one element of one client edited in place between :199
+    and :217, at a seed-chosen position, falls back deterministically -- the
+    edited tensor's version counter is no longer a fresh deep copy's."""
+    g = torch.Generator().manual_seed(seed)
+    K, n_keys = 64, 130
+    specs = []
+    for i in range(K):
+        sd = OrderedDict((f"k{j}", torch.randn(300, generator=g)) for j in range(n_keys))
+        specs.append((i + 1, [sd]))
+    rounds = [specs, specs]
+    where = torch.randint(0, K, (1,), generator=g).item(), torch.randint(0, n_keys, (1,), generator=g).item()
+    pos = torch.randint(0, 300, (1,), generator=g).item()
+
+    def edit(r, w_locals):
+        if r == 1:
+            w_locals[where[0]][1][f"k{where[1]}"][pos] += 1e-6
+
+    T, C = fresh_classes()
+    mfl_amd.install(T, stream_clients=True)
+    tr = T({"k0": torch.zeros(300)}, rounds, after_append=edit)
+    agg = _FakeAgg()
+    from mfl_amd.autostream import ClientFeed
+
+    feed = ClientFeed(lambda: agg, K)
+    feed.SMALL_ROUND_BYTES = 0
+    feed.VERIFY_FULL_ELEMS = 0  # sampled values: the version counter alone must catch it
+    tr.__dict__["_mfl_feed"] = feed
+    tr.train()
+    assert "__streamed__" in tr.results[0] and "__plain__" in tr.results[1]
+    assert feed.stats["last_verify"]["status"] == 8
+    assert (feed.stats["last_verify"]["client"], feed.stats["last_verify"]["key"]) == where

@@ -53,8 +53,8 @@ class Round:
                      [x.data_ptr() for x in st], [int(x.stride(0)) for x in st], [x.element_size() for x in st])
         self.counts = list(counts)
 
-    def verify(self, w_locals, seed=1, probes=4096, full_elems=0):
-        return ext.verify_rows(w_locals, self.counts, *self.args, probes, seed, full_elems)
+    def verify(self, w_locals, seed=1, probes=4096, full_elems=0, expect_version=-1):
+        return ext.verify_rows(w_locals, self.counts, *self.args, probes, seed, full_elems, expect_version)
 
 
 def _round(K=8, n_keys=40, numel=40_000, **kw):
@@ -192,3 +192,100 @@ def test_verify_cost_scales_with_the_walk_not_the_model():
         assert st[0] == 0
     assert st[3] >= 2 * 4096 * 0.9
     assert float(np.median(ts)) < 0.05  # generous on a shared CPU; ~1 ms on 8 cores
+
+
+def _dc_version():
+    return int(copy.deepcopy(torch.zeros(1))._version)
+
+
+@pytest.mark.parametrize("op", ["add_", "clamp_", "mul_", "copy_", "setitem", "replace", "zero_size_key"])
+def test_in_place_edit_is_caught_every_round_by_the_version_counter(op):
+    """One element of one client edited in place at a position the probes do
+    not sample (sampled mode: 64 x 121 pairs > 4,096 probes), or the tensor
+    object replaced: the version counter differs from a fresh deep copy's
+    (:199), so the check fails for every seed -- deterministic, unlike the
+    value probes (test_single_element_edit_is_found_at_the_sampling_rate)."""
+    r, wl = _round(K=64, n_keys=120, numel=20_000)
+    v = _dc_version()
+    assert all(r.verify(wl, seed=s, expect_version=v)[0] == 0 for s in range(5))
+    sd = wl[37][1]
+    key = "layer50.weight"
+    t = sd[key]
+    if op == "add_":
+        t[12_345:12_346].add_(1e-7)
+    elif op == "clamp_":
+        t.clamp_(-1e9, 1e9)  # changes no value at all: still an in-place op on the deep copy
+    elif op == "mul_":
+        t.mul_(1.0)
+    elif op == "copy_":
+        t.copy_(t.clone())
+    elif op == "setitem":
+        t[9_999] = t[9_999] + 1
+    elif op == "replace":
+        sd[key] = t.clone()  # a fresh tensor object: version 0, not a deep copy's
+    elif op == "zero_size_key":
+        sd["h"].add_(0.0)
+        key = "h"
+    j = list(sd).index(key)
+    for seed in range(20):
+        st = r.verify(wl, seed=seed, expect_version=v)
+        assert st[0] == 8 and st[1] == 37 and st[2] == j, (seed, st)
+    # without the version expectation only the sampled values could see it
+    assert r.verify(wl, seed=0)[0] in (0, 7)
+
+
+def test_metadata_checked_at_every_pair_not_only_probed_ones():
+    """A dtype or shape change at ONE (client, key) pair is found every round
+    (advisor finding: metadata used to be read at the probed pairs only)."""
+    r, wl = _round(K=64, n_keys=120, numel=2_000)
+    wl[11][1]["layer80.weight"] = wl[11][1]["layer80.weight"].double()
+    assert all(r.verify(wl, seed=s)[0] == 6 for s in range(20))
+    r, wl = _round(K=64, n_keys=120, numel=2_000)
+    wl[50][1]["layer81.weight"] = wl[50][1]["layer81.weight"][:-1].clone()
+    assert all(r.verify(wl, seed=s)[0] == 6 for s in range(20))
+
+
+class _HashTwin(str):
+    """A str subclass whose hash collides with a table name's but whose text differs."""
+
+    def __hash__(self):
+        return hash(self.target)
+
+
+def test_key_with_a_colliding_hash_is_not_taken_for_the_name():
+    """The fast walk matches keys by the hash in the dict's entry table and then
+    compares the strings (advisor finding: a same-hash key used to pass)."""
+    r, wl = _round(K=4, n_keys=6, numel=100)
+    sd = wl[2][1]
+    items = list(sd.items())
+    twin = _HashTwin("layer9.weight")
+    twin.target = items[3][0]
+    items[3] = (twin, items[3][1])
+    wl[2] = (wl[2][0], OrderedDict(items))
+    assert r.verify(wl)[0] == 5
+
+
+def test_version_walk_cost_resnet56():
+    """Every tensor's version counter read (35,000 of them) stays within the
+    walk's budget: the :217 check overlaps the GPU work of the finish."""
+    import sys
+    import time
+    from pathlib import Path
+
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "scripts"))
+    from model_shapes import CONFIGS
+
+    K, shapes = CONFIGS["resnet56"]
+    g = torch.Generator().manual_seed(0)
+    dicts = [OrderedDict((k, torch.tensor(i, dtype=torch.int64) if k.endswith("num_batches_tracked")
+                          else torch.randn(s, generator=g)) for k, s in shapes) for i in range(K)]
+    r = Round(dicts, list(range(1, K + 1)))
+    wl = [(n, copy.deepcopy(d)) for n, d in zip(r.counts, dicts)]
+    v = _dc_version()
+    ts = []
+    for s in range(5):
+        t0 = time.perf_counter()
+        st = r.verify(wl, seed=s, expect_version=v)
+        ts.append(time.perf_counter() - t0)
+        assert st[0] == 0, st
+    assert float(np.median(ts)) < 0.05
