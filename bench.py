@@ -419,6 +419,52 @@ def overlap_diagnostics(red, w_dev, steps: int, step_elapsed: float, reps: int =
             "note": "after the timed region; not part of value"}
 
 
+def shader_clock_mhz(fn, lead: int = 3, calls: int = 30, window_ms: float = 0.0) -> dict:
+    """The shader clock the chip holds while ``fn`` (one launch sequence on the
+    current stream) runs back to back: ``lead`` calls, then the clock probe
+    (libfedavg_amd_probe's fedavg_probe_clock: 8 one-wave workgroups stamping
+    s_memtime / s_memrealtime) on a side stream, then ``calls`` more calls
+    covering the probe's window.  MHz = d(memtime) / d(realtime) x 100 per
+    workgroup (MI355X_MICROARCH.md 'DVFS give-back' item 6); the median over
+    workgroups is reported.  Diagnostic only: after the timed region."""
+    import numpy as np
+    import torch
+
+    import mfl_amd
+
+    lib = mfl_amd._lib.load_probe()
+    cur = torch.cuda.current_stream()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    fn()
+    b.record()
+    torch.cuda.synchronize()
+    call_ms = max(a.elapsed_time(b), 1e-3)
+    if not window_ms:
+        window_ms = 0.6 * calls * call_ms  # inside the calls that follow the probe's launch
+    samples = 16
+    interval_us = max(1, int(window_ms * 1e3 / samples))
+    blocks = 8
+    out = torch.zeros(blocks * (samples + 1) * 2, dtype=torch.int64, device=cur.device)
+    side = torch.cuda.Stream()
+    side.wait_stream(cur)
+    for _ in range(lead):
+        fn()
+    mfl_amd._lib.check(lib.fedavg_probe_clock(out.data_ptr(), blocks, samples, interval_us, side.cuda_stream),
+                       "fedavg_probe_clock", lib)
+    for _ in range(calls):
+        fn()
+    torch.cuda.synchronize()
+    st = out.view(blocks, samples + 1, 2).cpu().numpy().astype(np.float64)
+    dc, dr = st[:, -1, 0] - st[:, 0, 0], st[:, -1, 1] - st[:, 0, 1]
+    mhz = dc / np.maximum(dr, 1) * 100.0
+    return {"clock_mhz": round(float(np.median(mhz)), 1), "min": round(float(mhz.min()), 1),
+            "max": round(float(mhz.max()), 1), "window_ms": round(float(np.median(dr)) / 1e5, 3),
+            "call_ms": round(call_ms, 4), "calls_after_probe": calls,
+            "method": "d(s_memtime)/d(s_memrealtime) x 100 MHz, 8 one-wave probe workgroups on a side stream "
+                      "beside back-to-back calls; median over workgroups"}
+
+
 def fused_round(red, w_dev, reps: int = 10) -> dict:
     """N = 1 side measurement of the round's second read: the aggregate plus
     the :291 sums of squares (fedavg_trainer.py:217 then :291) as two passes
@@ -461,7 +507,16 @@ def fused_round(red, w_dev, reps: int = 10) -> dict:
             "fused_frac_of_hbm_peak": round(alg / ms["fused"] / 1e6 / HBM_PEAK_GBS, 4),
             "out_bits_equal": bool(torch.equal(o1.view(torch.int32), o2.view(torch.int32))),
             "sums_max_rel_vs_two_pass": rel,
-            "timing": f"median of {reps} interleaved calls, HIP events around each call"}
+            "timing": f"median of {reps} interleaved calls, HIP events around each call",
+            **_clock_entry(runs["fused"])}
+
+
+def _clock_entry(fn) -> dict:
+    try:  # a diagnostic: never the reason a measurement is missing
+        c = shader_clock_mhz(fn)
+        return {"clock_mhz": c["clock_mhz"], "clock": c}
+    except Exception as e:  # noqa: BLE001
+        return {"clock_mhz": None, "clock": {"error": f"{type(e).__name__}: {e}"}}
 
 
 def launch_check(args):
@@ -893,6 +948,13 @@ def main(argv=None):
             out["dtype"] = "f32"
         if diagnostics is not None:
             out["diagnostics"] = diagnostics
+        if not rehearsal and world == 1 and passes == 1:
+            # the shader clock the chip held under the timed kernel's load (same launches, after
+            # the timed region): box-to-box spread in GB/s vs DVFS, by measurement
+            clk = _clock_entry(lambda: red_step(w_dev))
+            out["clock_mhz"] = clk["clock_mhz"]
+            if roofline is not None:
+                roofline["clock"] = clk["clock"]
         if (not rehearsal and world == 1 and passes == 1 and plan_world == 1 and K <= 512
                 and red.plan.chunks == 1):
             try:  # a side measurement: never the reason the bench line is missing

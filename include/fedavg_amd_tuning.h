@@ -210,6 +210,15 @@ int fedavg_probe_read_f32x4(const float* buf, int64_t nvec, int mode, int blocks
  */
 int fedavg_probe_busy_copy(const void* src, void* dst, int64_t bytes, int blocks, int hold_us, void* stream);
 int fedavg_stream_create_masked(int reserve_cus, int priority, void** stream);
+
+/*
+ * Shader-clock probe (measurement only): `blocks` one-wave workgroups each
+ * stamp (s_memtime, s_memrealtime) `samples + 1` times, `interval_us` apart,
+ * into out[blocks][samples + 1][2] (uint64).  Launched on a side stream
+ * beside a kernel, d(memtime) / d(realtime) * 100 is the shader clock in MHz
+ * the chip holds while that kernel runs.
+ */
+int fedavg_probe_clock(unsigned long long* out, int blocks, int samples, int interval_us, void* stream);
 int fedavg_stream_destroy(void* stream);
 
 #ifdef __cplusplus

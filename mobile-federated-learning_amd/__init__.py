@@ -30,7 +30,7 @@ from .aggregate import (
 from .layout import KeyTable, ShapeMismatchError, result_dtype
 from .reduce import ALIGN_ELEMS, client_sqdist, reduce_packed, reduce_tensors, reduce_with_sqdist, weights_tensor
 from .session import RoundSession
-from .multi import ShardedAggregator, sharded_aggregator
+from .multi import ShardedAggregator, ShardedRoundSession, sharded_aggregator
 from .fpf import FPFTracker
 
 __all__ = [
@@ -56,6 +56,7 @@ __all__ = [
     "weights_tensor",
     "RoundSession",
     "ShardedAggregator",
+    "ShardedRoundSession",
     "sharded_aggregator",
     "FPFTracker",
 ]

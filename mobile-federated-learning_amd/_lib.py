@@ -97,6 +97,7 @@ TUNING_SIGNATURES = {
                                                   _c_int, _vp]),
     "fedavg_reduce_vec_buf": (_c_int, [_c_int, _vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_int, _c_int, _c_int, _vp]),
     "fedavg_probe_busy_copy": (_c_int, [_vp, _vp, _c_i64, _c_int, _c_int, _vp]),
+    "fedavg_probe_clock": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp]),
     "fedavg_stream_create_masked": (_c_int, [_c_int, _c_int, _vp]),
     "fedavg_stream_destroy": (_c_int, [_vp]),
     "fedavg_reduce_f32_xcd": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _c_int, _vp]),

@@ -1083,15 +1083,26 @@ class FedAvgAggregateMixin:
         return aggregate(w_locals, getattr(self, "model_global", None), self.fedavg_device)
 
 
-def _feed_of(trainer, device):
-    """The trainer's ClientFeed (autostream), created on first use."""
+def _feed_of(trainer):
+    """The trainer's ClientFeed (autostream), created on first use.  Its
+    rounds stream into the installed device's DeviceAggregator, or -- with
+    ``install(devices=[...])`` / FEDAVG_DEVICES -- into the devices'
+    ShardedAggregator (every client's column shards over every device's link)."""
     from .autostream import ClientFeed
 
     feed = trainer.__dict__.get("_mfl_feed")
     if feed is None:
+        cls = type(trainer)
+        device = getattr(cls, "_mfl_stream_device", None)
+        devs = getattr(cls, "_mfl_stream_devices", None)
         clients = getattr(trainer, "client_list", None)  # fedavg_trainer.py:88: the Client objects of a round
         max_clients = len(clients) if clients else 128
-        feed = ClientFeed(lambda: default_aggregator(device), max_clients)
+        if devs is not None:
+            from .multi import sharded_aggregator
+
+            feed = ClientFeed(lambda: sharded_aggregator(devs), max_clients)
+        else:
+            feed = ClientFeed(lambda: default_aggregator(device), max_clients)
         trainer.__dict__["_mfl_feed"] = feed
     return feed
 
@@ -1108,9 +1119,16 @@ def install(trainer_cls, device: Optional[torch.device] = None, client_cls=None,
     reduces (autostream.py; falls back to the plain path whenever
     ``w_locals`` is not what was streamed).
 
-    ``devices`` (or FEDAVG_DEVICES=0,1,... when ``device`` is None): the
-    plain path's host rounds run over those GPUs by columns, one PCIe link
-    each (multi.ShardedAggregator); streaming stays on the first device."""
+    ``devices`` (or FEDAVG_DEVICES=0,1,... when ``device`` is None): host
+    rounds run over those GPUs by columns, one PCIe link each -- streamed
+    rounds (multi.ShardedRoundSession: each client's column shards uploaded
+    to every device as it arrives) and plain ones (multi.ShardedAggregator)
+    alike, with the single-GPU bits.
+
+    GPU initialisation is eager: install() creates every listed device's
+    streams and runs each first-use kernel and copy once (warm_up), before
+    the loop's round 0, so fork the process, if at all, before install().
+    ``FEDAVG_WARMUP=0`` leaves that to the first round."""
     from . import autostream
 
     if stream_clients is None:
@@ -1124,11 +1142,17 @@ def install(trainer_cls, device: Optional[torch.device] = None, client_cls=None,
     # wrappers below are installed once and read these per-class settings on
     # every call, so a later install(stream_clients=False) stops the feed
     # instead of leaving wrappers that upload clients nobody reduces
+    devs = _devices_arg(device, devices)
     trainer_cls._mfl_stream_on = streaming
     trainer_cls._mfl_stream_device = device
-    if torch.cuda.is_available():  # the HIP first-use costs, before the loop's round 0
-        for d in (devices or _devices_arg(device, None) or [device]):
+    trainer_cls._mfl_stream_devices = devs
+    if torch.cuda.is_available() and DeviceAggregator.WARMUP:  # the HIP first-use costs, before round 0
+        for d in (devs or [device]):
             default_aggregator(d).warm_up()
+        if devs is not None:
+            from .multi import sharded_aggregator
+
+            sharded_aggregator(devs)  # the shards' streams
 
     def aggregate_method(self, w_locals):
         feed = self.__dict__.get("_mfl_feed") if streaming else None
@@ -1136,7 +1160,7 @@ def install(trainer_cls, device: Optional[torch.device] = None, client_cls=None,
             out = feed.take(w_locals)
             if out is not None:
                 return out
-        return aggregate(w_locals, getattr(self, "model_global", None), device, devices)
+        return aggregate(w_locals, getattr(self, "model_global", None), device, devs)
 
     aggregate_method.__doc__ = FedAvgAggregateMixin.aggregate.__doc__
     aggregate_method.__wrapped_reference__ = getattr(trainer_cls, "aggregate", None)
@@ -1167,11 +1191,11 @@ def install(trainer_cls, device: Optional[torch.device] = None, client_cls=None,
                 # a Client subclass overrides train() (and reached this one
                 # through super()): what it returns to the loop may differ
                 # from `res` -- nothing of this round is streamed
-                _feed_of(trainer, getattr(type(trainer), "_mfl_stream_device", None)).refuse(
+                _feed_of(trainer).refuse(
                     "Client.train is overridden by a subclass")
                 return res
             if autostream.valid_train_result(res):  # fedavg_trainer.py:190
-                _feed_of(trainer, getattr(type(trainer), "_mfl_stream_device", None)).feed(
+                _feed_of(trainer).feed(
                     self.get_sample_number(), res[0])
             return res
 

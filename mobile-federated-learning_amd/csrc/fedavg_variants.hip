@@ -428,6 +428,31 @@ __global__ __launch_bounds__(kBlock) void reduce_f32x4_xcd_kernel(const f32x4* _
   }
 }
 
+// Shader-clock probe (measurement only): one wave per workgroup stamps the
+// shader cycle counter (s_memtime) and the 100 MHz constant clock
+// (s_memrealtime) `samples + 1` times, `interval_ticks` of the constant clock
+// apart, sleeping in between.  Run beside a kernel on another stream, the
+// stamps give the clock the chip holds while that kernel runs:
+// MHz = d(s_memtime) / d(s_memrealtime) * 100 (MI355X_MICROARCH.md 'DVFS
+// give-back' item 6).  Lane 0 writes (memtime, realtime) pairs to
+// out[block][sample] with ordinary vector stores.
+__global__ __launch_bounds__(64) void probe_clock_kernel(unsigned long long* __restrict__ out, int samples,
+                                                         uint64_t interval_ticks) {
+  unsigned long long* o = out + static_cast<int64_t>(blockIdx.x) * 2 * (samples + 1);
+  uint64_t t_next = __builtin_amdgcn_s_memrealtime();
+  for (int k = 0; k <= samples; ++k) {
+    while (__builtin_amdgcn_s_memrealtime() < t_next) __builtin_amdgcn_s_sleep(8);
+    unsigned long long c, r;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(c)::"memory");
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r)::"memory");
+    if (threadIdx.x == 0) {
+      o[2 * k] = c;
+      o[2 * k + 1] = r;
+    }
+    t_next = r + interval_ticks;
+  }
+}
+
 // launch_split's equal round-split launches, with the XCD-aware order
 template <int U, int C, bool NT>
 void launch_split_xcd(const float* clients, int K, int64_t ld, int64_t P, const float* W, float* out, int max_blocks,
@@ -522,6 +547,15 @@ int fedavg_probe_busy_copy(const void* src, void* dst, int64_t bytes, int blocks
   hipLaunchKernelGGL(probe_busy_copy_kernel, dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0,
                      static_cast<hipStream_t>(stream), static_cast<const f32x4*>(src), static_cast<f32x4*>(dst),
                      bytes / 16, static_cast<uint64_t>(hold_us) * 100u);
+  return launch_status(what);
+}
+
+int fedavg_probe_clock(unsigned long long* out, int blocks, int samples, int interval_us, void* stream) {
+  const char* what = "fedavg_probe_clock";
+  if (!out || blocks <= 0 || blocks > 1024 || samples <= 0 || samples > 100000 || interval_us <= 0)
+    return set_error(FEDAVG_EINVAL, "%s: bad arguments", what);
+  hipLaunchKernelGGL(probe_clock_kernel, dim3(static_cast<unsigned>(blocks)), dim3(64), 0,
+                     static_cast<hipStream_t>(stream), out, samples, static_cast<uint64_t>(interval_us) * 100u);
   return launch_status(what);
 }
 

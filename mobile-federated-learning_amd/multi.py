@@ -21,11 +21,24 @@ column depends only on the same column of the K clients
   finished columns straight to their global positions in the one pinned
   output buffer, whose key views become ``w_locals[0][1]``'s values.
 
+The streamed form (``begin_round`` -> :class:`ShardedRoundSession`, what
+``install(devices=[...])``'s zero-edit feed uses) does the same per client as
+it arrives: the client is packed once into its pinned row, and every device's
+column shard of that row goes over that device's own link while the loop
+trains the next client; at :217 each device reduces its shard and copies it
+to its global positions (N kernels on N/8 of the bytes, N D2Hs of P/N).
+
 Rounds the extra links cannot help are handed to the first device's
 ``DeviceAggregator`` unchanged: small rounds (one native call,
-``SMALL_ROUND_BYTES``), device-resident clients (reduced where they lie) and
-streaming sessions (``begin_round``).  ``client_distances`` (:291) after a
-sharded round adds the per-device fp64 sums of squares in device order.
+``SMALL_ROUND_BYTES``) and device-resident clients (reduced where they lie),
+streamed or not.  ``client_distances`` (:291) after a sharded round, streamed
+or plain, adds the per-device fp64 sums of squares in device order.
+
+Only same-device rehearsals (N shards on one GPU) have run on hardware: the
+pinned staging read by N devices' DMA engines, cross-device stream ordering
+and the per-link rates are parity-unpinned on distinct GPUs until a
+multi-GPU node runs tests/test_gpu_multi.py (its distinct-device test skips
+on fewer than 2 visible GPUs).
 
 Use: ``mfl_amd.install(FedAvgTrainer, devices=[0, 1, ..., 7])``,
 ``FEDAVG_DEVICES=0,1,...,7 python -m mfl_amd.launch main_fedavg.py ...`` or
@@ -47,8 +60,10 @@ from . import _lib
 from .distributed import upload_segments
 from .layout import KeyTable
 from .reduce import ALIGN_ELEMS, client_sqdist
+from .session import RoundSession
 
-__all__ = ["ShardedAggregator", "sharded_aggregator", "shard_bounds", "devices_from_env"]
+__all__ = ["ShardedAggregator", "ShardedRoundSession", "sharded_aggregator", "shard_bounds", "devices_from_env",
+           "normalize_device"]
 
 
 def shard_bounds(P: int, n: int, align: int = ALIGN_ELEMS) -> List[int]:
@@ -111,13 +126,9 @@ class ShardedAggregator:
     SMALL_ROUND_BYTES = None  # rounds up to this many row bytes stay on one device (None: DeviceAggregator's)
 
     def __init__(self, devices: Sequence):
-        devs = [torch.device(d) if not isinstance(d, int) else torch.device("cuda", d) for d in devices]
-        if not devs:
+        if not devices:
             raise ValueError("ShardedAggregator needs at least one device")
-        for d in devs:
-            if d.type != "cuda":
-                raise ValueError(f"{d}: HIP devices only (no CPU fallback)")
-        self.devices = [torch.device("cuda", d.index if d.index is not None else 0) for d in devs]
+        self.devices = [normalize_device(d) for d in devices]
         self._shards = [_Shard(d) for d in self.devices]
         self._host = {}  # dtype -> pinned [K, ld] staging
         self._lock = threading.Lock()
@@ -126,6 +137,8 @@ class ShardedAggregator:
         self.last_profile = {}
         self.rounds_sharded = 0
         self.rounds_delegated = 0
+        self.rounds_streamed = 0  # ShardedRoundSession rounds finished
+        self._session = None  # weakref to the open ShardedRoundSession, if any
 
     @property
     def primary(self):
@@ -134,8 +147,30 @@ class ShardedAggregator:
         return default_aggregator(self.devices[0])
 
     def begin_round(self, template, max_clients: int):
-        """Streaming sessions run on the first device (RoundSession)."""
-        return self.primary.begin_round(template, max_clients)
+        """Start a streaming round over the devices (:class:`ShardedRoundSession`:
+        each added client is packed once and its column shards go over every
+        device's own link as it arrives).  Rounds the extra links cannot help
+        get the first device's ``RoundSession``: one device, small rounds
+        (``SMALL_ROUND_BYTES``: one native call) and device-resident clients."""
+        from .layout import KeyTable
+
+        self._check_no_open_session("begin_round")
+        first = next(iter(template.values()), None) if len(template) else None
+        on_device = isinstance(first, torch.Tensor) and first.is_cuda
+        small = self.primary.SMALL_ROUND_BYTES if self.SMALL_ROUND_BYTES is None else self.SMALL_ROUND_BYTES
+        row_bytes = sum(v.numel() * max(4, v.element_size()) for v in template.values()
+                        if isinstance(v, torch.Tensor))
+        if len(self.devices) == 1 or on_device or max_clients * row_bytes <= small:
+            self.rounds_delegated += 1
+            return self.primary.begin_round(template, max_clients)
+        sess = ShardedRoundSession(self, KeyTable(template), max_clients)
+        self._session = weakref.ref(sess)
+        return sess
+
+    def _check_no_open_session(self, what: str):
+        sess = self._session() if self._session is not None else None
+        if sess is not None and not sess._finished:
+            raise RuntimeError(f"{what}: a ShardedRoundSession on these devices is still open (call finish first)")
 
     # ------------------------------------------------------------------
     def aggregate(self, w_locals, model_global=None):
@@ -161,6 +196,7 @@ class ShardedAggregator:
         prep = prepare(w_locals, model_global, self._table_hint)
         if not isinstance(prep, _Prepared):
             return prep
+        self._check_no_open_session("aggregate")  # a session owns the staging until it finishes
         acc_dict, table, dicts, weights, ptrs, keepalive = prep
         self._table_hint = table
         if table.client_device(dicts).type == "cuda":  # mixed placement: the primary raises the reference's error
@@ -180,6 +216,16 @@ class ShardedAggregator:
         self.rounds_sharded += 1
         return acc_dict
 
+    def _host_for(self, dtype, K: int, ld: int) -> torch.Tensor:
+        """The pinned ``[>=K, ld]`` host staging of a dtype group (kept across rounds)."""
+        host = self._host.get(dtype)
+        if host is None or host.shape[0] < K or host.shape[1] != ld:
+            host = None
+            self._host.pop(dtype, None)  # free the old block before pinning the new one
+            host = torch.empty((K, ld), dtype=dtype, pin_memory=True)
+            self._host[dtype] = host
+        return host
+
     def _reduce_sharded(self, table: KeyTable, ptrs, weights):
         from .aggregate import _fetch, reduce_rows
 
@@ -193,11 +239,7 @@ class ShardedAggregator:
         plan = []
         for g in table.groups.values():
             es = _elem(g.dtype)
-            host = self._host.get(g.dtype)
-            if host is None or host.shape[0] < K or host.shape[1] != g.ld:
-                host = torch.empty((K, g.ld), dtype=g.dtype, pin_memory=True)
-                self._host[g.dtype] = host
-            host = host[:K]
+            host = self._host_for(g.dtype, K, g.ld)[:K]
             bounds = shard_bounds(g.P, n)
             rows = [sh.rows_for(g.dtype, K, bounds[d + 1] - bounds[d]) for d, sh in enumerate(self._shards)]
             step = max(1, min(K, self.CHUNK_BYTES // max(1, g.ld * es)))
@@ -281,6 +323,201 @@ class ShardedAggregator:
         return norms
 
 
+class _HostRows:
+    """A group's pinned staging rows, as RoundSession's ``_staging[dtype].host``
+    (what autostream's verify_rows compares w_locals against)."""
+
+    def __init__(self, host: torch.Tensor):
+        self.host = host
+
+
+class ShardedRoundSession(RoundSession):
+    """A streaming round (session.RoundSession's contract) over N devices.
+
+    ``add`` packs the client ONCE into the pinned host row (the native
+    packer) and then issues, for every device d, the H2D of the row's column
+    shard ``[c_d, c_{d+1})`` on d's copy stream -- over d's own PCIe link --
+    in the column chunks d's finish reduces in, recording an event per chunk.
+    ``finish`` forms the weights, and for every device runs the reduce of its
+    shard (fused with the :291 sums of squares where the single-GPU finish
+    fuses them), each chunk waiting only for its own uploads, and copies the
+    finished columns straight to their global positions in the one pinned
+    output whose key views become ``w_locals[0][1]``'s values.  Every column
+    is reduced by the same sequential kernel over the same K rows as on one
+    GPU, so the bits are the single-GPU (and the reference's) bits.
+
+    Host clients only (device-resident and small rounds are the first
+    device's RoundSession, ``ShardedAggregator.begin_round``)."""
+
+    def __init__(self, sagg: "ShardedAggregator", table: KeyTable, max_clients: int):
+        if max_clients < 1:
+            raise ValueError("max_clients must be >= 1")
+        from .aggregate import column_chunks
+
+        self.agg = sagg
+        self.table = table
+        self.max_clients = max_clients
+        self.counts = []
+        self.dicts = []
+        self._keepalive = []
+        self._finished = False
+        self._verify = None
+        self._lib = _lib.load()
+        self._threads = max(1, torch.get_num_threads())
+        self.finish_profile = {}
+        self.add_ms = 0.0
+        self.add_profile = {}
+        self.keep_dicts = True
+        self.defer_release = None
+        self._small = False
+        self._client_dev = torch.device("cpu")
+        shards = sagg._shards
+        self.dev = shards[0].device
+        for sh in shards:  # earlier users of the shards' rows (a plain round's reduce) are done
+            sh.copy.wait_stream(torch.cuda.current_stream(sh.device))
+        self._staging = {}
+        self._plan = {}  # dtype -> [(shard, c0, c1, rows [max_clients, ld_d], chunks)] for non-empty shards
+        self._ready = {}  # dtype -> per plan entry, the latest add's chunk events
+        self._out_host = {}
+        self._views = {}
+        for g in table.groups.values():
+            self._staging[g.dtype] = _HostRows(sagg._host_for(g.dtype, max_clients, g.ld))
+            bounds = shard_bounds(g.P, len(shards))
+            plan = []
+            for d, sh in enumerate(shards):
+                c0, c1 = bounds[d], bounds[d + 1]
+                if c1 > c0:
+                    plan.append((sh, c0, c1, sh.rows_for(g.dtype, max_clients, c1 - c0), column_chunks(c1 - c0)))
+            self._plan[g.dtype] = plan
+            # the result's pinned buffer and its key views, made while clients
+            # train instead of inside finish() (session.RoundSession.add)
+            self._out_host[g.dtype] = torch.empty(g.P, dtype=g.dtype, pin_memory=True)
+            self._views[g.dtype] = table.unpack(g, self._out_host[g.dtype])
+
+    def add(self, sample_num, state_dict) -> None:
+        """Pack one host client into its pinned row and start every device's
+        shard upload (fedavg_trainer.py:199)."""
+        if self._finished:
+            raise RuntimeError("session already finished")
+        i = len(self.counts)
+        if i >= self.max_clients:
+            raise ValueError(f"more than max_clients={self.max_clients} clients added")
+        t0 = time.perf_counter()
+        if self.table.client_device([state_dict]).type != "cpu":
+            raise TypeError("a ShardedRoundSession streams host clients (device-resident rounds run where they lie)")
+        ptrs, keep = self.table.collect([state_dict], torch.device("cpu"))
+        for g in self.table.groups.values():
+            host = self._staging[g.dtype].host
+            t1 = time.perf_counter()
+            items = self.table.pack_items(g, ptrs, i, g.ld)
+            _lib.check(self._lib.fedavg_pack_rows(items.ctypes.data, items.shape[0], host.data_ptr(),
+                                                  host.element_size(), self._threads), "fedavg_pack_rows")
+            t2 = time.perf_counter()
+            ready = []
+            for sh, c0, c1, rows, chunks in self._plan[g.dtype]:
+                events = []
+                with torch.cuda.device(sh.device), torch.cuda.stream(sh.copy):
+                    for a, b in chunks:  # this device's columns, over its own link
+                        rows[i, a:b].copy_(host[i, c0 + a:c0 + b], non_blocking=True)
+                        ev = torch.cuda.Event()
+                        ev.record(sh.copy)
+                        events.append(ev)
+                ready.append(events)  # each copy stream is FIFO: covers earlier rows too
+            self._ready[g.dtype] = ready
+            t3 = time.perf_counter()
+            self.add_profile["pack_ms"] = self.add_profile.get("pack_ms", 0.0) + (t2 - t1) * 1e3
+            self.add_profile["h2d_issue_ms"] = self.add_profile.get("h2d_issue_ms", 0.0) + (t3 - t2) * 1e3
+        del keep
+        self.counts.append(sample_num)
+        self.dicts.append(state_dict if self.keep_dicts else None)
+        self.add_ms += (time.perf_counter() - t0) * 1e3
+
+    def abandon(self) -> None:
+        if self._finished:
+            return
+        self._finished = True
+        for sh in self.agg._shards:
+            sh.copy.synchronize()
+        self._forget_table()
+
+    def finish(self, w_locals=None, verify=None):
+        """Reduce the added clients over the devices; ``aggregate``'s contract
+        (fedavg_trainer.py:441-458), as RoundSession.finish."""
+        if self._finished:
+            raise RuntimeError("session already finished")
+        self._finished = True
+        if w_locals is not None:
+            if len(w_locals) != len(self.counts):
+                raise ValueError(f"w_locals has {len(w_locals)} clients, session has {len(self.counts)}")
+            for i, ((n, sd), n2, sd2) in enumerate(zip(w_locals, self.counts, self.dicts)):
+                if (verify is None and sd is not sd2) or n != n2:
+                    raise ValueError(f"w_locals[{i}] is not the client added as #{i}")
+        if verify is not None and w_locals is not None:
+            self.dicts = [sd for _, sd in w_locals]
+        if not self.counts:
+            raise ValueError("no clients added (the reference returns the global model then: use aggregate([]))")
+        K = len(self.counts)
+        acc_dict = w_locals[0][1] if w_locals is not None else OrderedDict()
+        from .aggregate import reduce_and_fetch, sample_weights
+
+        weights = sample_weights(self.counts)  # ZeroDivisionError like the reference
+        per_dev = [dict() for _ in self.agg._shards]
+        index = {id(sh): d for d, sh in enumerate(self.agg._shards)}
+        t0 = time.perf_counter()
+        for g in self.table.groups.values():
+            out_host = self._out_host[g.dtype]
+            for (sh, c0, c1, rows, _), ready in zip(self._plan[g.dtype], self._ready[g.dtype]):
+                with torch.cuda.device(sh.device):
+                    cur = torch.cuda.current_stream(sh.device)
+                    w_dev = sh.weights_for(g.dtype, K).upload(weights, cur)
+                    sums = {}
+                    out_dev, _ = reduce_and_fetch(rows[:K], w_dev, c1 - c0, sh.d2h, ready=ready,
+                                                  out_host=out_host[c0:c1], sums=sums)
+                    per_dev[index[id(sh)]][g.dtype] = (rows[:K], out_dev, sums.get(g.dtype), c0, c1)
+        t1 = time.perf_counter()
+        ok = self._verify_now(verify)  # overlaps the GPU work just issued
+        t_v = time.perf_counter()
+        for sh in self.agg._shards:
+            with torch.cuda.device(sh.device):
+                cur = torch.cuda.current_stream(sh.device)
+                sh.d2h.synchronize()
+                cur.synchronize()
+                cur.wait_stream(sh.copy)  # nothing else may reuse the rows before their copies end
+        t2 = time.perf_counter()
+        self.finish_profile = {"issue_ms": (t1 - t0) * 1e3, "verify_ms": (t_v - t1) * 1e3,
+                               "wait_ms": (t2 - t_v) * 1e3, "shards": len(self.agg._shards)}
+        if not ok:
+            self._forget_table()
+            return None
+        for g in self.table.groups.values():
+            self._set_results(acc_dict, self._views[g.dtype])
+        self.finish_profile["unpack_ms"] = (time.perf_counter() - t2) * 1e3
+        self._forget_table()
+        sagg = self.agg
+        sagg._last = {"table": self.table, "K": K, "per_dev": per_dev}
+        try:
+            sagg._last["refs"] = [weakref.ref(sd) for sd in self.dicts]
+            sagg._last["acc"] = weakref.ref(acc_dict)
+        except TypeError:
+            sagg._last = {}
+        sagg.rounds_streamed += 1
+        return acc_dict
+
+    @staticmethod
+    def _verify_now(verify) -> bool:
+        return verify() if verify is not None else True
+
+
+def normalize_device(d) -> torch.device:
+    """``3``, ``"cuda:3"``, ``torch.device("cuda", 3)`` -> ``cuda:3``; a device
+    without an index (``"cuda"``) is the current device, as
+    ``default_aggregator`` takes it.  HIP devices only (no CPU fallback)."""
+    dev = torch.device("cuda", d) if isinstance(d, int) else torch.device(d)
+    if dev.type != "cuda":
+        raise ValueError(f"{dev}: HIP devices only (no CPU fallback)")
+    return torch.device("cuda", dev.index if dev.index is not None else torch.cuda.current_device())
+
+
 def _elem(dtype: torch.dtype) -> int:
     return torch.empty(0, dtype=dtype).element_size()
 
@@ -291,7 +528,7 @@ _sharded_lock = threading.Lock()
 
 def sharded_aggregator(devices: Sequence) -> ShardedAggregator:
     """The process-wide ShardedAggregator for this device list."""
-    key = tuple(int(torch.device(d).index if not isinstance(d, int) else d) for d in devices)
+    key = tuple(normalize_device(d).index for d in devices)
     with _sharded_lock:
         agg = _sharded.get(key)
         if agg is None:

@@ -37,6 +37,10 @@ def main():
     ap.add_argument("--P", type=int, default=25_000_000)
     ap.add_argument("--shards", default="1,2,8")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--pack-threads", default="",
+                    help="also time the packer alone at these thread counts (e.g. 16,32,64): the host rate an "
+                         "N-GPU job with more host cores would get")
+    ap.add_argument("--skip-dropin", action="store_true")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -61,6 +65,20 @@ def main():
     pack_s = float(np.median(ts[1:]))
     print(json.dumps({"leg": "pack_only", "K": K, "P": P, "threads": threads, "ms": round(pack_s * 1e3, 2),
                       "GBps": round(4 * K * P / pack_s / 1e9, 1)}), flush=True)
+    import os
+
+    for nt in [int(x) for x in args.pack_threads.split(",") if x.strip()]:
+        ts = []
+        items = table.pack_items(g, ptrs, 0, g.ld)
+        for _ in range(args.reps + 1):
+            t0 = time.perf_counter()
+            mfl_amd._lib.check(lib.fedavg_pack_rows(items.ctypes.data, items.shape[0], host.data_ptr(), 4, nt),
+                               "pack")
+            ts.append(time.perf_counter() - t0)
+        s_nt = float(np.median(ts[1:]))
+        print(json.dumps({"leg": "pack_threads", "K": K, "P": P, "threads": nt, "ms": round(s_nt * 1e3, 2),
+                          "GBps": round(4 * K * P / s_nt / 1e9, 1), "affinity_cpus": len(os.sched_getaffinity(0)),
+                          "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}), flush=True)
     # single-link rates: the staging rows H2D, the model D2H
     d = torch.empty((K, g.ld), dtype=torch.float32, device=dev)
     out_h = torch.empty(P, dtype=torch.float32, pin_memory=True)
@@ -76,7 +94,7 @@ def main():
         print(json.dumps({"leg": what, "ms": round(s * 1e3, 2), "GBps": round(nbytes / s / 1e9, 1)}), flush=True)
     del d, host
     torch.cuda.empty_cache()
-    for n in [int(x) for x in args.shards.split(",")]:
+    for n in ([] if args.skip_dropin else [int(x) for x in args.shards.split(",")]):
         agg = mfl_amd.default_aggregator(dev) if n == 1 else mfl_amd.ShardedAggregator([0] * n)
         times, prof = [], None
         for r in range(args.reps + 1):

@@ -39,6 +39,10 @@ def main():
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--delay-ms", type=float, default=20.0)
     ap.add_argument("--keys", type=int, default=1, help="split P over this many keys")
+    ap.add_argument("--shards", default="1",
+                    help="streaming legs over N column shards (install(devices=[0]*N): every shard on cuda:0 "
+                         "here, one PCIe link -- a rehearsal of the N-GPU finish, not its link rates)")
+    ap.add_argument("--no-plain", action="store_true", help="skip the plain (streaming off) leg")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -59,9 +63,14 @@ def main():
     rounds = [[(counts[(i + r) % K], [clients[i]]) for i in range(K)] for r in range(args.rounds)]
     print(json.dumps({"setup_s": round(time.perf_counter() - t0, 1)}), flush=True)
     legs = {}
-    for leg, stream in (("streaming", True), ("plain", False)):
+    leg_list = [(f"streaming_shards{n}" if n > 1 else "streaming", True, n)
+                for n in (int(x) for x in args.shards.split(","))]
+    if not args.no_plain:
+        leg_list.append(("plain", False, 1))
+    for leg, stream, n_sh in leg_list:
         T, C = fresh_classes()
-        mfl_amd.install(T, device=dev, client_cls=C, stream_clients=stream)
+        mfl_amd.install(T, device=dev, client_cls=C, stream_clients=stream,
+                        devices=[0] * n_sh if n_sh > 1 else None)
         round_stats = []
 
         tr = T(OrderedDict((k, torch.zeros_like(v)) for k, v in clients[0].items()), rounds,
@@ -81,14 +90,15 @@ def main():
         for r, tm in enumerate(tr.timings):
             if feed is not None and r < len(round_stats):
                 tm = dict(tm, feed=round_stats[r])
-            print(json.dumps({"leg": leg, "K": K, "P": P, "keys": args.keys, "round": r,
+            print(json.dumps({"leg": leg, "shards": n_sh, "K": K, "P": P, "keys": args.keys, "round": r,
                               "aggregate_ms": round(tm["aggregate_ms"], 3),
                               "last_train_to_model_ms": round(tm["last_train_to_model_ms"], 3),
                               "delay_ms": args.delay_ms, "feed": tm.get("feed")}), flush=True)
         if feed is not None:
             print(json.dumps({"leg": leg, "feed_stats": feed.stats}), flush=True)
+    names = list(legs)
     same = all(torch.equal(a[k].view(-1).view(torch.int32), b[k].view(-1).view(torch.int32))
-               for a, b in zip(legs["streaming"].results, legs["plain"].results) for k in a)
+               for other in names[1:] for a, b in zip(legs[names[0]].results, legs[other].results) for k in a)
     agg = {leg: float(np.median([t["aggregate_ms"] for t in tr.timings[1:]])) for leg, tr in legs.items()}
     print(json.dumps({"summary": True, "K": K, "P": P, "bit_identical": same,
                       "median_aggregate_ms_after_round0": agg}), flush=True)

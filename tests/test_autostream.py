@@ -316,3 +316,24 @@ def test_single_in_place_edit_falls_back_every_time(plain_calls, seed):
     assert "__streamed__" in tr.results[0] and "__plain__" in tr.results[1]
     assert feed.stats["last_verify"]["status"] == 8
     assert (feed.stats["last_verify"]["client"], feed.stats["last_verify"]["key"]) == where
+
+
+def test_install_devices_streams_into_the_sharded_aggregator(plain_calls, monkeypatch):
+    """install(devices=[...]): the feed's rounds open on the devices'
+    ShardedAggregator (multi.ShardedRoundSession), not on the first device."""
+    agg = _FakeAgg()
+    asked = []
+
+    def fake_sharded(devs):
+        asked.append(list(devs))
+        return agg
+
+    monkeypatch.setattr("mfl_amd.multi.sharded_aggregator", fake_sharded)
+    monkeypatch.setattr("mfl_amd.autostream.ClientFeed.SMALL_ROUND_BYTES", 0)
+    T, C = fresh_classes()
+    mfl_amd.install(T, stream_clients=True, devices=[0, 1, 2])
+    tr = T({"w": torch.zeros(10)}, _rounds(2))
+    tr.train()
+    assert asked and all(a == [0, 1, 2] for a in asked)
+    assert len(agg.sessions) == 2 and all("__streamed__" in r for r in tr.results)
+    assert plain_calls == []

@@ -28,6 +28,12 @@ DEV = torch.device("cuda", 0)
 RTOL = 1e-5
 
 
+@pytest.fixture(scope="module", autouse=True)
+def _gpu(gpu_available):
+    """A plain ``pytest`` on a GPU-less box skips this module like the other test_gpu_* modules."""
+    yield
+
+
 class _TrackerImpl:
     def __init__(self, meta, init, g2=FO.G2):
         self.t = mfl_amd.FPFTracker(meta["client_num_in_total"], init, meta["comm_round"], device=DEV,
