@@ -271,7 +271,11 @@ def cpu_baseline(K: int, P: int, flat_seconds: float = 6.0, model_seconds: float
         "kind": "port",
         "sample": flat["sample"] + " (value; torch.set_num_threads(len(os.sched_getaffinity(0))), BASELINE.md; "
                                    "threads_from: affinity); reference torch CPU loop restated "
-                                   "(oracle/fedavg_oracle.py aggregate_torch)",
+                                   "(oracle/fedavg_oracle.py aggregate_torch)"
+                  + (f". NOTE: {n_aff} affinity threads oversubscribe this job's {n_omp}-CPU share "
+                     f"(OMP_NUM_THREADS) {n_aff // n_omp}x, so `value` times the scheduler as much as the "
+                     f"reference loop; `value_at_share` ({n_omp} threads) is the reference's speed on this box"
+                     if n_omp else ""),
         "affinity_cpus": n_aff,
         "layouts": layouts,
     }

@@ -138,6 +138,7 @@ class ClientFeed:
         self.broken = False
         self._small = False  # this round fits SMALL_ROUND_BYTES: left to the plain path
         self.fed = []  # sample numbers in feed order
+        self._fed_keys = []  # each fed dict's key objects, in feed order
         self._vplan = None  # verify_rows' table arrays for the open session (worker-made)
         self._graveyard = []  # _Release lists waiting for the next round (worker thread only)
         self._q: Optional[queue.Queue] = None
@@ -165,6 +166,8 @@ class ClientFeed:
             self.broken = self._small = True  # by design: not counted as a fallback
             return
         self.fed.append(sample_num)  # the dict itself goes to the worker only (no round-long reference)
+        # its key objects (the :199 deep copy shares them): verify_rows matches w_locals' keys by identity
+        self._fed_keys.append(tuple(state_dict))
         if self._worker is None:
             self._q = queue.Queue()
             self._worker = threading.Thread(target=self._run, name="mfl-client-feed", daemon=True)
@@ -319,7 +322,7 @@ class ClientFeed:
             ext, names, templ, group, offset, kind, sptr, sld, ses = self._vplan
             st = ext.verify_rows(w_locals, list(self.fed), names, templ, group, offset, kind, sptr, sld, ses,
                                  self.VERIFY_PROBES, random.getrandbits(64), self.VERIFY_FULL_ELEMS,
-                                 deepcopy_version())
+                                 deepcopy_version(), self._fed_keys)
             self.stats["last_verify"] = {"status": int(st[0]), "client": int(st[1]), "key": int(st[2]),
                                          "probes": int(st[3])}
             return st[0] == 0
@@ -332,6 +335,7 @@ class ClientFeed:
             sess.abandon()
         self.session = None
         self.fed = []
+        self._fed_keys = []
         self._vplan = None
         self.broken = self._small = False
         self._err = None

@@ -443,7 +443,8 @@ static py::tuple verify_rows(py::list w_locals, py::list counts, py::list names,
                              const std::vector<int64_t>& group, const std::vector<int64_t>& offset,
                              const std::vector<int64_t>& kind, const std::vector<int64_t>& stage_ptr,
                              const std::vector<int64_t>& stage_ld, const std::vector<int64_t>& stage_esize,
-                             int64_t probes, uint64_t seed, int64_t full_elems, int64_t expect_version) {
+                             int64_t probes, uint64_t seed, int64_t full_elems, int64_t expect_version,
+                             py::object fed_keys) {
   const Py_ssize_t K = PyList_GET_SIZE(w_locals.ptr());
   const Py_ssize_t N = PyList_GET_SIZE(names.ptr());
   auto res = [](int status, Py_ssize_t i, Py_ssize_t j, int64_t n) { return py::make_tuple(status, i, j, n); };
@@ -517,23 +518,38 @@ static py::tuple verify_rows(py::list w_locals, py::list counts, py::list names,
   // the key objects are read -- prefetched with the values).  A dict whose
   // keys are not exact str objects equal to the names in order is redone on
   // this thread with ==.
+  // fed_keys[i] (optional): the key objects of the dict fed as client i,
+  // already matched exactly to the names when it was packed (collect).  The
+  // loop's :199 copy.deepcopy keeps str keys as the same objects, so a key
+  // identical to the fed one is the name without reading the string.
+  std::vector<PyObject* const*> fk(static_cast<size_t>(K), nullptr);
+  if (!fed_keys.is_none()) {
+    if (!PyList_Check(fed_keys.ptr()) || PyList_GET_SIZE(fed_keys.ptr()) != K)
+      throw std::invalid_argument("verify_rows: fed_keys must be a list with one key sequence per client");
+    for (Py_ssize_t i = 0; i < K; ++i) {
+      PyObject* ks = PyList_GET_ITEM(fed_keys.ptr(), i);
+      if (PyTuple_Check(ks) && PyTuple_GET_SIZE(ks) == N) fk[i] = &PyTuple_GET_ITEM(ks, 0);
+    }
+  }
   const auto fill_fast = [&](int64_t i) -> bool {
     Py_ssize_t pos = 0, j = 0;
     PyObject *key, *val;
     Py_hash_t h;
     PyObject** row = &vals[static_cast<size_t>(i) * N];
+    PyObject* const* fed = fk[i];
     thread_local std::vector<PyObject*> keys;
     keys.resize(N);
     while (_PyDict_Next(dicts[i], &pos, &key, &val, &h)) {
       if (j >= N || (key != name_ptr[j] && h != name_hash[j])) return false;
-      keys[j] = key;
+      const bool known = key == name_ptr[j] || (fed && key == fed[j]);
+      keys[j] = known ? nullptr : key;
       row[j++] = val;
-      __builtin_prefetch(key);
+      if (!known) __builtin_prefetch(key);
       __builtin_prefetch(val);
     }
     if (j != N) return false;
     for (Py_ssize_t jj = 0; jj < N; ++jj)
-      if (key_eq(keys[jj], name_ptr[jj]) != KeyEq::kSame) return false;
+      if (keys[jj] && key_eq(keys[jj], name_ptr[jj]) != KeyEq::kSame) return false;
     return true;
   };
   // the VersionCounter object behind a tensor's _version (one more dependent
@@ -551,48 +567,51 @@ static py::tuple verify_rows(py::list w_locals, py::list counts, py::list names,
     // dtype, sizes, host, contiguous, version counter); the pairs probed this
     // round also have elements compared -- every key is probed at one client
     // or more each round (its anchor), so an edit of a key across clients is
-    // always seen by value too.  Prefetches a few keys ahead: the TensorImpl,
-    // then (once it has arrived) its VersionCounter.
+    // always seen by value too.  The objects are cold (made seconds ago, by
+    // the loop's :199 deep copies), so the walk goes in passes, each one a
+    // run of independent loads the core overlaps instead of a chain of
+    // dependent misses per tensor: the TensorImpls (their PyObjects were
+    // prefetched by the dict walk), then every tensor's metadata with its
+    // VersionCounter (and a probed pair's StorageImpl) prefetched, then the
+    // versions and the value probes.
     const auto probed = [&](Py_ssize_t j, uint64_t* hp) {
       const uint64_t h = mix64(seed ^ mix64(static_cast<uint64_t>(i) * 0x100000001B3ull + static_cast<uint64_t>(j)));
       *hp = h;
       return full || h <= thresh ||
              static_cast<int64_t>(mix64(seed + static_cast<uint64_t>(j)) % static_cast<uint64_t>(K)) == i;
     };
-    constexpr Py_ssize_t kImpl = 16, kVer = 8;
-    const auto impl_of = [&](Py_ssize_t j) -> c10::TensorImpl* {
-      return THPVariable_CheckExact(row_vals[j]) ? THPVariable_Unpack(row_vals[j]).unsafeGetTensorImpl() : nullptr;
-    };
-    const auto prefetch_version = [&](Py_ssize_t j) {
-      if (expect_version < 0) return;
-      if (c10::TensorImpl* ti = impl_of(j))
-        if (const void* v = version_obj(ti)) __builtin_prefetch(v);
-    };
-    for (Py_ssize_t j = 0; j < N && j < kImpl; ++j)
-      if (c10::TensorImpl* ti = impl_of(j)) __builtin_prefetch(ti);
-    for (Py_ssize_t j = 0; j < N && j < kVer; ++j) prefetch_version(j);
+    thread_local std::vector<c10::TensorImpl*> impls;
+    impls.resize(N);
+    for (Py_ssize_t j = 0; j < N; ++j) {
+      c10::TensorImpl* ti =
+          THPVariable_CheckExact(row_vals[j]) ? THPVariable_Unpack(row_vals[j]).unsafeGetTensorImpl() : nullptr;
+      impls[j] = ti;
+      if (ti) __builtin_prefetch(ti);
+    }
     for (Py_ssize_t j = 0; j < N && !st; ++j) {
-      if (j + kImpl < N)
-        if (c10::TensorImpl* ti = impl_of(j + kImpl)) __builtin_prefetch(ti);
-      if (j + kVer < N) prefetch_version(j + kVer);
-      PyObject* val = row_vals[j];
-      if (!THPVariable_CheckExact(val)) {  // a Tensor subclass: the plain path decides
+      c10::TensorImpl* ti = impls[j];
+      if (!ti) {  // a Tensor subclass: the plain path decides
         st = (int64_t(6) << 32) | j;
         break;
       }
-      const at::Tensor& ten = THPVariable_Unpack(val);
-      if (ten.scalar_type() != tp[j]->scalar_type() || ten.sizes() != tp[j]->sizes() || !ten.is_cpu() ||
-          !ten.is_contiguous()) {
+      if (ti->dtype() != tp[j]->dtype() || ti->sizes() != tp[j]->sizes() || !ti->is_cpu() || !ti->is_contiguous()) {
         st = (int64_t(6) << 32) | j;
         break;
       }
+      if (expect_version >= 0)
+        if (const void* v = version_obj(ti)) __builtin_prefetch(v);
+      uint64_t h;
+      if (probed(j, &h) && ti->has_storage()) __builtin_prefetch(ti->unsafe_storage().unsafeGetStorageImpl());
+    }
+    for (Py_ssize_t j = 0; j < N && !st; ++j) {
       if (expect_version >= 0) {
-        const c10::VariableVersion& vc = ten.unsafeGetTensorImpl()->version_counter();
+        const c10::VariableVersion& vc = impls[j]->version_counter();
         if (!vc.enabled() || static_cast<int64_t>(vc.current_version()) != expect_version) {
           st = (int64_t(8) << 32) | j;
           break;
         }
       }
+      const at::Tensor& ten = THPVariable_Unpack(row_vals[j]);
       uint64_t h;
       if (!probed(j, &h)) continue;
       const int64_t n = numel[j];
@@ -682,5 +701,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "randomly sampled values)",
         py::arg("w_locals"), py::arg("counts"), py::arg("names"), py::arg("templ"), py::arg("group"),
         py::arg("offset"), py::arg("kind"), py::arg("stage_ptr"), py::arg("stage_ld"), py::arg("stage_esize"),
-        py::arg("probes"), py::arg("seed"), py::arg("full_elems"), py::arg("expect_version") = -1);
+        py::arg("probes"), py::arg("seed"), py::arg("full_elems"), py::arg("expect_version") = -1,
+        py::arg("fed_keys") = py::none());
 }

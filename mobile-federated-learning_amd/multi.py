@@ -464,9 +464,11 @@ class ShardedRoundSession(RoundSession):
         per_dev = [dict() for _ in self.agg._shards]
         index = {id(sh): d for d, sh in enumerate(self.agg._shards)}
         t0 = time.perf_counter()
+        issue = []
         for g in self.table.groups.values():
             out_host = self._out_host[g.dtype]
             for (sh, c0, c1, rows, _), ready in zip(self._plan[g.dtype], self._ready[g.dtype]):
+                issue.append(time.perf_counter())
                 with torch.cuda.device(sh.device):
                     cur = torch.cuda.current_stream(sh.device)
                     w_dev = sh.weights_for(g.dtype, K).upload(weights, cur)
@@ -484,8 +486,10 @@ class ShardedRoundSession(RoundSession):
                 cur.synchronize()
                 cur.wait_stream(sh.copy)  # nothing else may reuse the rows before their copies end
         t2 = time.perf_counter()
+        issue.append(t1)
         self.finish_profile = {"issue_ms": (t1 - t0) * 1e3, "verify_ms": (t_v - t1) * 1e3,
-                               "wait_ms": (t2 - t_v) * 1e3, "shards": len(self.agg._shards)}
+                               "wait_ms": (t2 - t_v) * 1e3, "shards": len(self.agg._shards),
+                               "issue_ms_per_shard": [round((b - a) * 1e3, 3) for a, b in zip(issue, issue[1:])]}
         if not ok:
             self._forget_table()
             return None

@@ -53,8 +53,8 @@ class Round:
                      [x.data_ptr() for x in st], [int(x.stride(0)) for x in st], [x.element_size() for x in st])
         self.counts = list(counts)
 
-    def verify(self, w_locals, seed=1, probes=4096, full_elems=0, expect_version=-1):
-        return ext.verify_rows(w_locals, self.counts, *self.args, probes, seed, full_elems, expect_version)
+    def verify(self, w_locals, seed=1, probes=4096, full_elems=0, expect_version=-1, fed_keys=None):
+        return ext.verify_rows(w_locals, self.counts, *self.args, probes, seed, full_elems, expect_version, fed_keys)
 
 
 def _round(K=8, n_keys=40, numel=40_000, **kw):
@@ -289,3 +289,23 @@ def test_version_walk_cost_resnet56():
         ts.append(time.perf_counter() - t0)
         assert st[0] == 0, st
     assert float(np.median(ts)) < 0.05
+
+
+def test_fed_key_objects_match_by_identity():
+    """fed_keys (autostream: the key objects of each fed dict, which the :199
+    deep copy shares) short-cut the string compare; an equal key that is not
+    the fed object is still compared, and a hash twin still fails."""
+    r, wl = _round(K=4, n_keys=6, numel=100)
+    fed = [tuple(sd) for _, sd in wl]
+    assert r.verify(wl, fed_keys=fed)[0] == 0
+    fresh = [tuple("".join(list(k)) for k in sd) for _, sd in wl]  # equal strings, other objects
+    assert r.verify(wl, fed_keys=fresh)[0] == 0
+    sd = wl[2][1]
+    items = list(sd.items())
+    twin = _HashTwin("layer9.weight")
+    twin.target = items[3][0]
+    items[3] = (twin, items[3][1])
+    wl[2] = (wl[2][0], OrderedDict(items))
+    assert r.verify(wl, fed_keys=fed)[0] == 5
+    with pytest.raises(ValueError):
+        r.verify(wl, fed_keys=fed[:2])
