@@ -755,53 +755,52 @@ def main(argv=None):
     launches_per_call = sched["launches"] if sched else 1
     ev_pairs = []
 
-    # Kernel timing: event pairs attached to the reduce's own launches
-    # (fedavg_reduce_f32_timed / hipExtLaunchKernel: the first launch's start,
-    # the last one's end), handed to ShardedReducer.step per chunk.  A
-    # separate hipEventRecord pair around each call serialises back-to-back
-    # launches (~8 us per call on MI355X), and even launch-attached events
-    # cost ~5 us of wall time per call (profiled dispatch), so calls shorter
-    # than ~1 GB of traffic are timed on a sample: every `sample_every`-th
-    # reduce call of the timed region.  The pool is created and recorded once
-    # before the timed region (torch creates HIP events lazily).
-    bytes_call_est = algorithmic_bytes(K, red.plan.block)
-    sample_every = 1 if bytes_call_est >= 1e9 else (4 if bytes_call_est >= 2.5e8 else 8)
-    n_calls = args.steps * red.plan.chunks * passes
+    # Kernel timing, per reduce pass (one ShardedReducer.step), checked
+    # against rocprofv3's kernel trace (scripts/launch_timing_probe.py,
+    # profiles/r05/launch_timing/ and r05/g3-g4):
+    # * one call per pass (N = 1): events attached to the call's own launches
+    #   (fedavg_reduce_f32_timed / hipExtLaunchKernel: the first launch's
+    #   start, the last one's end) -- 704.2 vs rocprofv3's 702.9 us per
+    #   launch at the target.  A hipEventRecord marker before such a launch
+    #   cost ~20 us of step time per marker (r05/g3: 0.727 ms per launch).
+    # * chunked passes (the per-rank kernel of an N-GPU plan, ~46-90 us per
+    #   chunk): a hipEventRecord pair on the launch stream around the pass's
+    #   chunk launches, which run back to back there (the all-gathers are
+    #   issued after the last one, from a side stream), span / chunks --
+    #   47.1 vs 46.6 us at 4 x 781K; attached events read ~4 us long PER
+    #   CALL (49.9 vs 45.8 us), and a pass spanned by attached events on its
+    #   first and last calls picked up the host's issue gaps between chunks.
+    # The pool is created and recorded once before the timed region (torch
+    # creates HIP events lazily).
+    n_spans = args.steps * passes
     pool = []
     if not rehearsal:
         pool = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                for _ in range(-(-n_calls // sample_every))]
+                for _ in range(n_spans)]
         for a, b in pool:
             a.record()
             b.record()
     _sync(dev)
-    call_no = [0]
     timing_on = [False]
+    attached = red.plan.chunks == 1 and tuned is None
 
-    def timing(c):
-        if not timing_on[0] or rehearsal:
+    def timing(c):  # one call per pass: events attached to its launches
+        if not timing_on[0] or rehearsal or not attached:
             return None
-        i = call_no[0]
-        call_no[0] += 1
-        if i % sample_every:
+        pair = pool[len(ev_pairs)]
+        ev_pairs.append(pair)
+        return pair
+
+    def span():  # chunked passes (and tuning variants): a hipEventRecord pair around the chunk launches
+        if not timing_on[0] or rehearsal or attached:
             return None
         pair = pool[len(ev_pairs)]
         ev_pairs.append(pair)
         return pair
 
     if tuned is not None:
-        # tuning variants (probe library): record pairs around sampled calls
         def local_reduce(clients, w, P, out):
-            if timing_on[0] and call_no[0] % sample_every == 0:
-                st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                st.record()
-                mfl_amd.reduce_packed(clients, w, P, out, tuned=tuned)
-                en.record()
-                ev_pairs.append((st, en))
-            else:
-                mfl_amd.reduce_packed(clients, w, P, out, tuned=tuned)
-            if timing_on[0]:
-                call_no[0] += 1
+            mfl_amd.reduce_packed(clients, w, P, out, tuned=tuned)
         red.local_reduce = local_reduce
 
     if passes > 1:
@@ -813,10 +812,10 @@ def main(argv=None):
         def red_step(w):
             for p in range(passes):
                 red.local_out = red.pass_out[p * red.plan.local_cols:(p + 1) * red.plan.local_cols]
-                red.step(w, timing=timing)
+                red.step(w, timing=timing, span=span())
     else:
         def red_step(w):
-            red.step(w, timing=timing)
+            red.step(w, timing=timing, span=span())
 
     for _ in range(args.warmup):
         red_step(w_dev)
@@ -855,7 +854,7 @@ def main(argv=None):
         calls_per_event = red.plan.chunks * passes
     else:
         timing_on[0] = True
-        calls_per_event = 1
+        calls_per_event = red.plan.chunks  # one span per reduce pass: its chunk calls
     elapsed_max = timed_steps(step, args.steps, dev, use_pg)
     timing_on[0] = False
 
@@ -891,7 +890,12 @@ def main(argv=None):
         value = bytes_step * args.steps / elapsed_max / 1e9
         roofline = None
         if not rehearsal:
-            roofline = roofline_entry(args, K, S, kernel_ms_max, launches_per_call, sched, tuned, sample_every,
+            timing_desc = ("launch-attached HIP events (hipExtLaunchKernel) on the launch stream around every "
+                           "reduce call of the timed region (its first launch's start to its last launch's end)"
+                           if attached else
+                           "hipEventRecord pair on the launch stream around each reduce pass's back-to-back chunk "
+                           "launches, every pass of the timed region, span / chunks")
+            roofline = roofline_entry(args, K, S, kernel_ms_max, launches_per_call, sched, tuned, timing_desc,
                                       len(kernel_ms) * calls_per_event * launches_per_call, world)
         if red.gather:
             exchange = ("rccl" if backend == "nccl" else backend) + " all_gather_into_tensor, overlapped per chunk"
@@ -987,7 +991,7 @@ def main(argv=None):
         dist.destroy_process_group()
 
 
-def roofline_entry(args, K, S, kernel_ms_max, launches_per_call, sched, tuned, sample_every, launches, world):
+def roofline_entry(args, K, S, kernel_ms_max, launches_per_call, sched, tuned, timing_desc, launches, world):
     """The dominant kernel's algorithmic bytes per launch over its average
     launch time (launch-attached HIP events), with the PMC traffic of the
     same launch shape when profiles/ holds it."""
@@ -1011,11 +1015,7 @@ def roofline_entry(args, K, S, kernel_ms_max, launches_per_call, sched, tuned, s
         "bytes_per_launch": bytes_call // launches_per_call,
         "avg_launch_ms": round(kernel_ms_max / launches_per_call, 4),
         "launches": launches,
-        "timing": ("hipGraph replay bracketed by events" if args.graph else
-                   ("hipEventRecord pairs around" if tuned is not None else
-                    "launch-attached HIP events (hipExtLaunchKernel) on the launch stream of")
-                   + (" every reduce call" if sample_every == 1 else f" every {sample_every}th reduce call")
-                   + " of the timed region"),
+        "timing": "hipGraph replay bracketed by events" if args.graph else timing_desc,
     }
     attach_traffic(roofline, args, world)
     return roofline

@@ -494,7 +494,7 @@ class ShardedRoundSession(RoundSession):
             self._forget_table()
             return None
         for g in self.table.groups.values():
-            self._set_results(acc_dict, self._views[g.dtype])
+            self._set_results(acc_dict, self._views[g.dtype], keys_verified=verify is not None)
         self.finish_profile["unpack_ms"] = (time.perf_counter() - t2) * 1e3
         self._forget_table()
         sagg = self.agg

@@ -264,7 +264,8 @@ class RoundSession:
             return None
         for g, out_host in outs:
             views = self._views.get(g.dtype)
-            self._set_results(acc_dict, views if views is not None else self.table.unpack(g, out_host))
+            self._set_results(acc_dict, views if views is not None else self.table.unpack(g, out_host),
+                              keys_verified=self._verify is not None)
         # host-side phases of the finish (ms): issuing weights/reduce/D2H, waiting for them, unpacking
         self.finish_profile = {"issue_ms": (t1 - t0) * 1e3, "verify_ms": (t_v - t1) * 1e3, "wait_ms": (t2 - t_v) * 1e3,
                                "unpack_ms": (time.perf_counter() - t2) * 1e3}
@@ -332,9 +333,12 @@ class RoundSession:
         self._release(list(self.table._template))  # client 0's tensors, held for the native walk's checks
         self.table.forget_tensors()
 
-    def _set_results(self, acc_dict, results) -> None:
-        """acc_dict[name] = result (fedavg_trainer.py:455 replaces client 0's values)."""
-        if len(results) == len(acc_dict) and acc_dict.keys() == results.keys():
+    def _set_results(self, acc_dict, results, keys_verified: bool = False) -> None:
+        """acc_dict[name] = result (fedavg_trainer.py:455 replaces client 0's values).
+        ``keys_verified``: verify_rows has just seen acc_dict hold exactly the
+        table's keys in order, so one group's results replace every value."""
+        if keys_verified and len(self.table.groups) == 1 or (
+                len(results) == len(acc_dict) and acc_dict.keys() == results.keys()):
             # every value replaced (one dtype group): two C-level calls
             old = list(acc_dict.values())
             acc_dict.update(results)
