@@ -624,10 +624,26 @@ __global__ __launch_bounds__(kBlock) void reduce_sqdist_segments_f32_kernel(cons
 constexpr int64_t kSegWinTablePad = 128;
 constexpr int64_t kSegWinMinPerWave = 16;  // windows per wave below which the LDS-DMA tiles keep the round
 
-template <int KMAX, int VEC, int NW, int MINW = win_min_waves(KMAX, VEC)>
+// DESC (round 5): every fast window's K client descriptors come from a
+// descriptor table staged with the key table -- desc[j * KMAX + i] = {client
+// i's address of key j (lo, hi), the key's byte length (0 for padding rows
+// and empty keys), the buffer flags} -- by scalar loads from the constant
+// address space (one s_load_dwordx16 per 4 rows), used in place as the row's
+// buffer resource with the window's start in soffset.  The per-row
+// v_readlane pair and the descriptor's SALU assembly (record count select,
+// flags, mask) of the pointer form -- ~6 of a row's ~20 instructions per
+// window -- are gone.  A window whose next one is ragged (or past the end)
+// reloads from desc[n_keys * KMAX ..], KMAX null descriptors (record count
+// 0: the loads return 0 and touch nothing), and the ragged window is loaded
+// after the squares from the pointer table as before.
+typedef __attribute__((address_space(4))) const u32x4* cdesc_t;
+constexpr uint32_t kWinRsrcFlags = 0x00020000;
+
+template <int KMAX, int VEC, int NW, bool DESC = false, int MINW = win_min_waves(KMAX, VEC)>
 __global__ __launch_bounds__(64 * NW, MINW) void reduce_sqdist_segwin_kernel(
     const SegKey* __restrict__ keys, const int64_t* __restrict__ ptrs, int64_t n_keys, int64_t units, int K,
-    const float* __restrict__ W, float* __restrict__ out, double* __restrict__ partials) {
+    const float* __restrict__ W, float* __restrict__ out, double* __restrict__ partials,
+    const u32x4* __restrict__ desc) {
   typedef typename WinVec<VEC>::T V;
   constexpr int WC = 64 * VEC;
   constexpr int NB = (KMAX + 7) / 8;
@@ -692,6 +708,14 @@ __global__ __launch_bounds__(64 * NW, MINW) void reduce_sqdist_segwin_kernel(
                                           0x00020000),
         voff, soff);
   };
+  // DESC: row i of the window whose descriptors start at `cd`
+  const auto load_desc = [&](cdesc_t cd, int i, uint32_t soff) __attribute__((always_inline)) {
+    const u32x4 d = cd[i];
+    x[i] = win_load<VEC>(
+        __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>((static_cast<uint64_t>(d.y) << 32) | d.x), 0,
+                                          static_cast<int>(d.z), static_cast<int>(d.w)),
+        voff, soff);
+  };
 
   // window / key indices in 32 bits (the host checks units < 2^31): 64-bit
   // compares run on the VALU, and a descriptor built from a VALU result
@@ -711,36 +735,76 @@ __global__ __launch_bounds__(64 * NW, MINW) void reduce_sqdist_segwin_kernel(
     const int w = u - static_cast<int>(key.unit_start);
     c0 = static_cast<int64_t>(w) * WC;
     n = cols_of(key.numel, w);
-    load_ptrs(ptrs + static_cast<int64_t>(j) * K);
+    if (!DESC || n != WC) load_ptrs(ptrs + static_cast<int64_t>(j) * K);  // DESC: slow windows only
     if (n == WC) {
+      if constexpr (DESC) {
+        const cdesc_t cd = (cdesc_t)(desc + static_cast<int64_t>(j) * KMAX);
 #pragma unroll
-      for (int i = 0; i < KMAX; ++i)
-        load_fast(i, static_cast<uint32_t>(c0 * 4), static_cast<uint32_t>((c0 + WC) * 4), K);
+        for (int i = 0; i < KMAX; ++i) {
+          load_desc(cd, i, static_cast<uint32_t>(c0 * 4));
+          if ((i & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < KMAX; ++i)
+          load_fast(i, static_cast<uint32_t>(c0 * 4), static_cast<uint32_t>((c0 + WC) * 4), K);
+      }
     } else {
       load_slow(c0, n, K);
     }
   }
+  // DESC: the current key's output offset and the next-window key's fields
+  // are kept in SGPRs and reloaded only when the scan moves to another key
+  // (next_start: the first window of the key after it), so a window of a
+  // long key issues no scalar load of the key table and waits on none
+  int64_t cur_out = 0, kn_numel = 0;
+  int kn_start = 0, next_start = 0x7fffffff;
+  if (DESC && u < units32) {
+    const SegKey k0 = keys[j];
+    cur_out = k0.out_offset;
+    kn_numel = k0.numel;
+    kn_start = static_cast<int>(k0.unit_start);
+    next_start = j + 1 < nkeys32 ? static_cast<int>(keys[j + 1].unit_start) : 0x7fffffff;
+  }
   for (; u < units32; u += GW32) {
     int Kw = K;
     asm volatile("" : "+s"(Kw));
-    const int64_t out_off = keys[j].out_offset;
+    const int64_t out_off = DESC ? cur_out : keys[j].out_offset;
     // the next window: its key by a forward scan
     const int un = u + GW32;
     int jn = j, nn = 0;
     int64_t c0n = 0;
+    int64_t kn_out = cur_out;
     if (un < units32) {
-      while (jn + 1 < nkeys32 && static_cast<int>(keys[jn + 1].unit_start) <= un) ++jn;
-      const SegKey kn = keys[jn];
-      const int w = un - static_cast<int>(kn.unit_start);
-      c0n = static_cast<int64_t>(w) * WC;
-      nn = cols_of(kn.numel, w);
+      if constexpr (DESC) {
+        while (un >= next_start) {  // keys without windows share their successor's start
+          ++jn;
+          const SegKey kk = keys[jn];
+          kn_numel = kk.numel;
+          kn_start = static_cast<int>(kk.unit_start);
+          kn_out = kk.out_offset;
+          next_start = jn + 1 < nkeys32 ? static_cast<int>(keys[jn + 1].unit_start) : 0x7fffffff;
+        }
+        const int w = un - kn_start;
+        c0n = static_cast<int64_t>(w) * WC;
+        nn = cols_of(kn_numel, w);
+      } else {
+        while (jn + 1 < nkeys32 && static_cast<int>(keys[jn + 1].unit_start) <= un) ++jn;
+        const SegKey kn = keys[jn];
+        const int w = un - static_cast<int>(kn.unit_start);
+        c0n = static_cast<int64_t>(w) * WC;
+        nn = cols_of(kn.numel, w);
+      }
     }
     const bool fastn = un < units32 && nn == WC;
     // the next fast window's soffset and record count; no loads unless it is fast
     const uint32_t soffn = static_cast<uint32_t>(c0n * 4), nrecn = static_cast<uint32_t>((c0n + WC) * 4);
     int Kwn = fastn ? K : 0;
     asm volatile("" : "+s"(Kwn));
-    load_ptrs(ptrs + static_cast<int64_t>(jn) * K);  // the next window's addresses, before the chain
+    // DESC: the next window's descriptors, or the null block when it is not fast
+    const cdesc_t cdn = (cdesc_t)(desc + (fastn ? static_cast<int64_t>(jn) : n_keys) * KMAX);
+    // the next window's addresses, before the chain (DESC: a slow next window only)
+    if (!DESC || (un < units32 && !fastn)) load_ptrs(ptrs + static_cast<int64_t>(jn) * K);
     // the chain (a slow window's columns past its key are 0)
     int wo = 0;
     asm volatile("" : "+v"(wo));
@@ -761,7 +825,11 @@ __global__ __launch_bounds__(64 * NW, MINW) void reduce_sqdist_segwin_kernel(
     }
     float* o = out + out_off + c0 + lane * VEC;
     if (n == WC) {
-      *reinterpret_cast<typename WinVec<VEC>::TA*>(o) = a;  // o: only dword-aligned (key offsets)
+      if constexpr (DESC)  // streamed out, as the rows kernel's output
+        __builtin_nontemporal_store(static_cast<typename WinVec<VEC>::TA>(a),
+                                    reinterpret_cast<typename WinVec<VEC>::TA*>(o));
+      else
+        *reinterpret_cast<typename WinVec<VEC>::TA*>(o) = a;  // o: only dword-aligned (key offsets)
     } else {
 #pragma unroll
       for (int v = 0; v < VEC; ++v)
@@ -769,21 +837,61 @@ __global__ __launch_bounds__(64 * NW, MINW) void reduce_sqdist_segwin_kernel(
     }
     // squares; row i reloaded from the next window right after (a slow next
     // window: empty descriptors here, its element loads after the squares)
+    if constexpr (DESC) {
+      // a batch's 8 descriptors were loaded during the previous batch: the
+      // batch finalises them (their one wait on the scalar loads), issues the
+      // NEXT batch's descriptor loads, then squares and reloads its rows
+      u32x4 dc[8], dn[8];
 #pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      double p[8];
+      for (int r = 0; r < 8; ++r)
+        if (r < KMAX) dc[r] = cdn[r];
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const int i = 8 * b + r;
-        p[r] = 0.0;
-        if (i < KMAX) {
-          p[r] = win_sq<VEC>(x[i] - a);
-          load_fast(i, soffn, nrecn, Kwn);
+      for (int b = 0; b < NB; ++b) {
+        uint32_t hi[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) hi[r] = dc[r].y & 0xffffu;
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+          if (b + 1 < NB && 8 * (b + 1) + r < KMAX) dn[r] = cdn[8 * (b + 1) + r];
+        __builtin_amdgcn_sched_barrier(0);
+        double p[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const int i = 8 * b + r;
+          p[r] = 0.0;
+          if (i < KMAX) {
+            p[r] = win_sq<VEC>(x[i] - a);
+            x[i] = win_load<VEC>(__builtin_amdgcn_make_buffer_rsrc(
+                                     reinterpret_cast<void*>((static_cast<uint64_t>(hi[r]) << 32) | dc[r].x), 0,
+                                     static_cast<int>(dc[r].z), static_cast<int>(dc[r].w)),
+                                 voff, soffn);
+          }
         }
+        const double q01 = fold32(p[0], p[1]), q23 = fold32(p[2], p[3]);
+        const double q45 = fold32(p[4], p[5]), q67 = fold32(p[6], p[7]);
+        acc[64 * b] += fold8(fold16(q01, q23), fold16(q45, q67), upper);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) dc[r] = dn[r];
       }
-      const double q01 = fold32(p[0], p[1]), q23 = fold32(p[2], p[3]);
-      const double q45 = fold32(p[4], p[5]), q67 = fold32(p[6], p[7]);
-      acc[64 * b] += fold8(fold16(q01, q23), fold16(q45, q67), upper);
+    } else {
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        double p[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const int i = 8 * b + r;
+          p[r] = 0.0;
+          if (i < KMAX) {
+            p[r] = win_sq<VEC>(x[i] - a);
+            load_fast(i, soffn, nrecn, Kwn);
+          }
+        }
+        const double q01 = fold32(p[0], p[1]), q23 = fold32(p[2], p[3]);
+        const double q45 = fold32(p[4], p[5]), q67 = fold32(p[6], p[7]);
+        acc[64 * b] += fold8(fold16(q01, q23), fold16(q45, q67), upper);
+      }
     }
     if (un < units32 && !fastn) {
       // a fresh opaque K: with the squares' Kw the compiler kept their KMAX
@@ -796,6 +904,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void reduce_sqdist_segwin_kernel(
     j = jn;
     c0 = c0n;
     n = nn;
+    cur_out = kn_out;
   }
   const int row_in = win_batch_row(lane);
 #pragma unroll
@@ -829,9 +938,9 @@ inline bool segwin_disabled() {
 }
 
 // waves of a zero-copy window launch over `units` windows
-template <int KMAX, int VEC, int NW>
+template <int KMAX, int VEC, int NW, bool DESC = true>
 int64_t segwin_waves(int64_t units) {
-  const int64_t per_cu = resident_blocks(reduce_sqdist_segwin_kernel<KMAX, VEC, NW>, 64 * NW) / cu_count();
+  const int64_t per_cu = resident_blocks(reduce_sqdist_segwin_kernel<KMAX, VEC, NW, DESC>, 64 * NW) / cu_count();
   const int64_t grid = per_cu * cu_count();
   const int64_t need = (units + NW - 1) / NW;
   return (grid < need ? grid : need) * NW;
@@ -1018,7 +1127,8 @@ SegFusedPlan seg_fused_plan(const int64_t* numel, int64_t n_keys, int64_t K, boo
 // The fused launch (+ the sums' finalize) on tables staged with plan.span
 int launch_seg_fused(const SegFusedPlan& p, const SegKey* keys, const int64_t* tptrs, int64_t n_keys, int64_t units,
                      int64_t K, const float* weights, float* out, double* partials, int64_t partial_elems,
-                     double* sumsq, hipStream_t s, const char* what, const int* umap = nullptr) {
+                     double* sumsq, hipStream_t s, const char* what, const int* umap = nullptr,
+                     const u32x4* desc = nullptr) {
   if (units == 0) {
     const hipError_t e = hipMemsetAsync(sumsq, 0, static_cast<size_t>(K) * sizeof(double), s);
     return e == hipSuccess ? FEDAVG_OK : set_error(-static_cast<int>(e), "%s: hipMemsetAsync failed", what);
@@ -1029,28 +1139,21 @@ int launch_seg_fused(const SegFusedPlan& p, const SegKey* keys, const int64_t* t
     if (partial_elems < K * p.waves)
       return set_error(FEDAVG_EINVAL, "%s: partials need %lld doubles", what, (long long)(K * p.waves));
     const dim3 grid(static_cast<unsigned>(p.waves / 4)), block(256);
+#define FEDAVG_SEGWIN(KM, VC)                                                                                       \
+  if (desc)                                                                                                        \
+    hipLaunchKernelGGL((reduce_sqdist_segwin_kernel<KM, VC, 4, true>), grid, block, 0, s, keys, tptrs, n_keys,     \
+                       units, k32, weights, out, partials, desc);                                                  \
+  else                                                                                                             \
+    hipLaunchKernelGGL((reduce_sqdist_segwin_kernel<KM, VC, 4, false>), grid, block, 0, s, keys, tptrs, n_keys,    \
+                       units, k32, weights, out, partials, nullptr);
     switch (p.kmax) {
-      case 48:
-        hipLaunchKernelGGL((reduce_sqdist_segwin_kernel<48, 4, 4>), grid, block, 0, s, keys, tptrs, n_keys, units, k32,
-                           weights, out, partials);
-        break;
-      case 64:
-        hipLaunchKernelGGL((reduce_sqdist_segwin_kernel<64, 2, 4>), grid, block, 0, s, keys, tptrs, n_keys, units, k32,
-                           weights, out, partials);
-        break;
-      case 80:
-        hipLaunchKernelGGL((reduce_sqdist_segwin_kernel<80, 2, 4>), grid, block, 0, s, keys, tptrs, n_keys, units, k32,
-                           weights, out, partials);
-        break;
-      case 100:
-        hipLaunchKernelGGL((reduce_sqdist_segwin_kernel<100, 2, 4>), grid, block, 0, s, keys, tptrs, n_keys, units, k32,
-                           weights, out, partials);
-        break;
-      default:
-        hipLaunchKernelGGL((reduce_sqdist_segwin_kernel<128, 1, 4>), grid, block, 0, s, keys, tptrs, n_keys, units, k32,
-                           weights, out, partials);
-        break;
+      case 48: FEDAVG_SEGWIN(48, 4) break;
+      case 64: FEDAVG_SEGWIN(64, 2) break;
+      case 80: FEDAVG_SEGWIN(80, 2) break;
+      case 100: FEDAVG_SEGWIN(100, 2) break;
+      default: FEDAVG_SEGWIN(128, 1) break;
     }
+#undef FEDAVG_SEGWIN
     nparts = p.waves;
   } else {
     const int S = static_cast<int>(p.span);
@@ -1110,15 +1213,33 @@ struct RoundWs {
 // units (256 KiB; a model of more units at 17-128 clients takes the windows)
 constexpr int64_t kSegUnitMapMax = 65536;
 
+// the windows' descriptor table (reduce_sqdist_segwin_kernel DESC): KMAX
+// entries per key plus KMAX null ones, staged for tables of at most this size
+constexpr int64_t kSegDescMaxBytes = int64_t(4) << 20;
+inline int64_t seg_desc_bytes(int64_t n_keys, int64_t kmax = 128) {
+  return (n_keys + 1) * kmax * static_cast<int64_t>(sizeof(u32x4));
+}
+
+// FEDAVG_SEGWIN_DESC=0 keeps the windows' pointer form (probes, A/B)
+inline bool segwin_desc_disabled() {
+  static const bool off = [] {
+    const char* e = std::getenv("FEDAVG_SEGWIN_DESC");
+    return e && e[0] == '0';
+  }();
+  return off;
+}
+
 inline RoundWs round_ws(int64_t K, int64_t n_keys) {
   RoundWs r;
   r.ptrs = n_keys * static_cast<int64_t>(sizeof(SegKey));
   r.w = round16(r.ptrs + (n_keys * K + kSegWinTablePad) * static_cast<int64_t>(sizeof(int64_t)));
   r.ik = r.w + round16(K * static_cast<int64_t>(sizeof(float)));
   r.isrc = r.ik + round16(n_keys * static_cast<int64_t>(sizeof(IntKey)));
-  // + room for the unit map, placed right after whatever part is used
-  r.end = round16(r.isrc + n_keys * K * static_cast<int64_t>(sizeof(int64_t))) +
-          kSegUnitMapMax * static_cast<int64_t>(sizeof(int));
+  // + room for the tiles' unit map OR the windows' descriptor table (a round
+  // uses one of them), placed right after whatever part is used
+  const int64_t map_bytes = kSegUnitMapMax * static_cast<int64_t>(sizeof(int));
+  const int64_t desc = seg_desc_bytes(n_keys) <= kSegDescMaxBytes ? seg_desc_bytes(n_keys) : 0;
+  r.end = round16(r.isrc + n_keys * K * static_cast<int64_t>(sizeof(int64_t))) + (map_bytes > desc ? map_bytes : desc);
   return r;
 }
 
@@ -1487,12 +1608,32 @@ int fedavg_device_round_f32(const int64_t* client_ptrs, int64_t ptr_ld, const in
       for (int64_t u = hk[j].unit_start; u < u1; ++u) hm[u] = static_cast<int>(j);
     }
   }
+  // the windows' descriptor table: client i's address of key j, the key's
+  // byte length (the range check of every load of that key), the flags;
+  // padding rows and empty keys get a record count of 0, and KMAX null
+  // descriptors follow the last key (the reload target when the next
+  // window is not a full one)
+  const int64_t dbytes = plan.win ? seg_desc_bytes(n_keys, plan.kmax) : 0;
+  const bool with_desc = plan.win && dbytes <= kSegDescMaxBytes && !segwin_desc_disabled();
+  if (with_desc) {
+    auto* hd = reinterpret_cast<u32x4*>(hb + moff);
+    const int64_t km = plan.kmax;
+    for (int64_t j = 0; j <= n_keys; ++j) {
+      const bool live = j < n_keys && key_numel[j] > 0;
+      const uint32_t nrec = live ? static_cast<uint32_t>(key_numel[j] * 4) : 0u;
+      for (int64_t i = 0; i < km; ++i) {
+        const uint64_t p = live && i < K ? static_cast<uint64_t>(hp[j * K + i]) : 0;
+        hd[j * km + i] = u32x4{static_cast<uint32_t>(p), static_cast<uint32_t>(p >> 32), p ? nrec : 0u,
+                               kWinRsrcFlags};
+      }
+    }
+  }
   // the reference's weights n_i / N (fedavg_trainer.py:453) rounded once to
   // fp32 (nearest even, the cast ATen applies to the scalar at :455)
   for (int64_t k = 0; k < K; ++k) hw[k] = static_cast<float>(weights[k]);
   FEDAVG_ROUND_MARK(5);  // plan, key table, weights
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const int64_t bytes = with_map ? moff + units * static_cast<int64_t>(sizeof(int)) : used;
+  const int64_t bytes = with_map ? moff + units * static_cast<int64_t>(sizeof(int)) : (with_desc ? moff + dbytes : used);
   const hipError_t e = hipMemcpyAsync(dev_ws, host_ws, static_cast<size_t>(bytes), hipMemcpyHostToDevice, s);
   if (e != hipSuccess) {
     (void)hipGetLastError();
@@ -1514,7 +1655,8 @@ int fedavg_device_round_f32(const int64_t* client_ptrs, int64_t ptr_ld, const in
   FEDAVG_ROUND_MARK(7);  // the integer keys' launch
   if (fuse) {
     rc = launch_seg_fused(plan, keys, tptrs, n_keys, units, K, dw, out, partials, partial_elems, sumsq, s, what,
-                          with_map ? reinterpret_cast<const int*>(db + moff) : nullptr);
+                          with_map ? reinterpret_cast<const int*>(db + moff) : nullptr,
+                          with_desc ? reinterpret_cast<const u32x4*>(db + moff) : nullptr);
     FEDAVG_ROUND_MARK(8);  // the fused launch and the sums' finalize
     return rc ? rc : FEDAVG_OK;
   }
