@@ -325,6 +325,9 @@ class ClientFeed:
                                  deepcopy_version(), self._fed_keys)
             self.stats["last_verify"] = {"status": int(st[0]), "client": int(st[1]), "key": int(st[2]),
                                          "probes": int(st[3])}
+            if len(st) > 4:  # native phase times (us) and the walk's thread count
+                self.stats["last_verify"].update(prep_us=round(st[4][0], 1), walk_us=round(st[4][1], 1),
+                                                 tail_us=round(st[4][2], 1), threads=int(st[4][3]))
             return st[0] == 0
         except Exception:  # noqa: BLE001
             return False

@@ -21,6 +21,9 @@
 #include <torch/extension.h>
 
 #include <algorithm>
+#include <array>
+#include <atomic>
+#include <chrono>
 #include <cstring>
 #include <vector>
 
@@ -447,7 +450,24 @@ static py::tuple verify_rows(py::list w_locals, py::list counts, py::list names,
                              py::object fed_keys) {
   const Py_ssize_t K = PyList_GET_SIZE(w_locals.ptr());
   const Py_ssize_t N = PyList_GET_SIZE(names.ptr());
-  auto res = [](int status, Py_ssize_t i, Py_ssize_t j, int64_t n) { return py::make_tuple(status, i, j, n); };
+  // (status, client, key, elements compared, (us before the walk, us in the
+  // threaded walk, us after it, intra-op threads)) -- the timings for probes
+  using clk = std::chrono::steady_clock;
+  const auto t_entry = clk::now();
+  auto t_walk0 = t_entry, t_walk1 = t_entry;
+  const auto us = [](clk::time_point a, clk::time_point b) {
+    return std::chrono::duration<double, std::micro>(b - a).count();
+  };
+  // walk_detail: summed us in the dict walks and in the tensor checks, the
+  // slowest thread's us, the parallel chunks
+  std::array<double, 4> walk_detail{0, 0, 0, 0};
+  auto res = [&](int status, Py_ssize_t i, Py_ssize_t j, int64_t n) {
+    const auto t_end = clk::now();
+    return py::make_tuple(status, i, j, n,
+                          py::make_tuple(us(t_entry, t_walk0), us(t_walk0, t_walk1), us(t_walk1, t_end),
+                                         at::get_num_threads(), walk_detail[0], walk_detail[1], walk_detail[2],
+                                         walk_detail[3]));
+  };
   if (K != PyList_GET_SIZE(counts.ptr()) || K == 0) return res(1, -1, -1, 0);
   if (PyList_GET_SIZE(templ.ptr()) != N || static_cast<Py_ssize_t>(group.size()) != N ||
       static_cast<Py_ssize_t>(offset.size()) != N || static_cast<Py_ssize_t>(kind.size()) != N)
@@ -586,7 +606,11 @@ static py::tuple verify_rows(py::list w_locals, py::list counts, py::list names,
       c10::TensorImpl* ti =
           THPVariable_CheckExact(row_vals[j]) ? THPVariable_Unpack(row_vals[j]).unsafeGetTensorImpl() : nullptr;
       impls[j] = ti;
-      if (ti) __builtin_prefetch(ti);
+      if (ti) {  // the fields read below span the TensorImpl's first lines
+        __builtin_prefetch(ti);
+        __builtin_prefetch(reinterpret_cast<const char*>(ti) + 64);
+        __builtin_prefetch(reinterpret_cast<const char*>(ti) + 128);
+      }
     }
     for (Py_ssize_t j = 0; j < N && !st; ++j) {
       c10::TensorImpl* ti = impls[j];
@@ -648,16 +672,34 @@ static py::tuple verify_rows(py::list w_locals, py::list counts, py::list names,
     status[i] = st;
     nprobe[i] += static_cast<int64_t>(todo.size());
   };
+  t_walk0 = clk::now();
+  std::atomic<int64_t> fill_ns{0}, check_ns{0}, max_ns{0}, nchunks{0};
   at::parallel_for(0, K, 1, [&](int64_t i0, int64_t i1) {
     std::vector<Probe> todo;
+    const auto c0 = clk::now();
+    int64_t f = 0, c = 0;
     for (int64_t i = i0; i < i1; ++i) {
-      if (!fill_fast(i)) {
+      const auto a = clk::now();
+      const bool ok = fill_fast(i);
+      const auto b = clk::now();
+      f += std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count();
+      if (!ok) {
         status[i] = kRedo;
         continue;
       }
       check_client(i, todo);
+      c += std::chrono::duration_cast<std::chrono::nanoseconds>(clk::now() - b).count();
+    }
+    const int64_t span = std::chrono::duration_cast<std::chrono::nanoseconds>(clk::now() - c0).count();
+    fill_ns += f;
+    check_ns += c;
+    nchunks += 1;
+    int64_t m = max_ns.load();
+    while (span > m && !max_ns.compare_exchange_weak(m, span)) {
     }
   });
+  t_walk1 = clk::now();
+  walk_detail = {fill_ns.load() / 1e3, check_ns.load() / 1e3, max_ns.load() / 1e3, static_cast<double>(nchunks.load())};
   {  // dicts whose keys are equal but not identical to the names: == on this thread
     std::vector<Probe> todo;
     for (Py_ssize_t i = 0; i < K; ++i) {

@@ -80,7 +80,8 @@ def main():
         def agg_and_snap(self, w_locals, _orig=orig_agg, _rs=round_stats):
             out = _orig(self, w_locals)
             f = self.__dict__.get("_mfl_feed")
-            _rs.append(dict(f.stats["last_round"]) if f is not None else None)
+            _rs.append(dict(f.stats["last_round"], verify=dict(f.stats.get("last_verify", {})))
+                       if f is not None else None)
             return out
 
         T.aggregate = agg_and_snap
