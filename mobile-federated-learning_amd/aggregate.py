@@ -1026,13 +1026,31 @@ def default_aggregator(device: Optional[torch.device] = None) -> DeviceAggregato
 
 def _devices_arg(device, devices):
     """The device list a functional call routes to: ``devices`` when given,
-    else FEDAVG_DEVICES when no single ``device`` was named; None = one GPU."""
+    else FEDAVG_DEVICES when no single ``device`` was named; None = one GPU
+    (``_single_device`` names it)."""
     if devices is None and device is None:
         from .multi import devices_from_env
 
         devices = devices_from_env()
     if devices is not None and len(devices) > 1:
         return list(devices)
+    return None
+
+
+def _single_device(device, devices):
+    """The one GPU a call runs on when ``_devices_arg`` gives no list: ``device``,
+    else the single entry of ``devices`` / FEDAVG_DEVICES, else None (the
+    current device, or where device-resident clients lie)."""
+    if device is not None:
+        return device
+    if devices is None:
+        from .multi import devices_from_env
+
+        devices = devices_from_env()
+    if devices is not None and len(devices) == 1:
+        from .multi import normalize_device
+
+        return normalize_device(devices[0])
     return None
 
 
@@ -1048,6 +1066,7 @@ def aggregate(w_locals, model_global=None, device: Optional[torch.device] = None
         from .multi import sharded_aggregator
 
         return sharded_aggregator(devs).aggregate(w_locals, model_global=model_global)
+    device = _single_device(device, devices)
     if device is None:  # device-resident clients are reduced on their own device
         first = next(iter(w_locals[0][1].values()))
         if isinstance(first, torch.Tensor) and first.is_cuda:
@@ -1062,7 +1081,7 @@ def client_distances(w_locals, w_glob, device: Optional[torch.device] = None, de
         from .multi import sharded_aggregator
 
         return sharded_aggregator(devs).client_distances(w_locals, w_glob)
-    return default_aggregator(device).client_distances(w_locals, w_glob)
+    return default_aggregator(_single_device(device, devices)).client_distances(w_locals, w_glob)
 
 
 def estimate_delta(w_locals, w_glob, lr, device: Optional[torch.device] = None, devices=None):
@@ -1143,6 +1162,8 @@ def install(trainer_cls, device: Optional[torch.device] = None, client_cls=None,
     # every call, so a later install(stream_clients=False) stops the feed
     # instead of leaving wrappers that upload clients nobody reduces
     devs = _devices_arg(device, devices)
+    if devs is None:
+        device = _single_device(device, devices)  # install(devices=[3]) runs on cuda:3
     trainer_cls._mfl_stream_on = streaming
     trainer_cls._mfl_stream_device = device
     trainer_cls._mfl_stream_devices = devs

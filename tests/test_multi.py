@@ -32,3 +32,33 @@ def test_devices_from_env(monkeypatch):
 def test_sharded_aggregator_refuses_cpu_devices():
     with pytest.raises(ValueError):
         mfl_amd.ShardedAggregator([torch.device("cpu")])
+
+
+def test_single_entry_device_list_names_that_device(monkeypatch):
+    """install(devices=[3]) / FEDAVG_DEVICES=3 run on cuda:3, not on the current device."""
+    from mfl_amd.aggregate import _devices_arg, _single_device
+    from loop_replay import fresh_classes
+
+    monkeypatch.delenv("FEDAVG_DEVICES", raising=False)
+    assert _devices_arg(None, [3]) is None and _single_device(None, [3]) == torch.device("cuda", 3)
+    assert _single_device(torch.device("cuda", 1), [3]) == torch.device("cuda", 1)
+    assert _single_device(None, None) is None
+    monkeypatch.setenv("FEDAVG_DEVICES", "5")
+    assert _single_device(None, None) == torch.device("cuda", 5)
+    monkeypatch.delenv("FEDAVG_DEVICES")
+    T, C = fresh_classes()
+    mfl_amd.install(T, client_cls=C, devices=[3])
+    assert T._mfl_stream_device == torch.device("cuda", 3) and T._mfl_stream_devices is None
+    T2, C2 = fresh_classes()
+    mfl_amd.install(T2, client_cls=C2, devices=[0, 1])
+    assert T2._mfl_stream_devices == [0, 1]
+
+
+def test_normalize_device_forms():
+    from mfl_amd.multi import normalize_device
+
+    assert normalize_device(2) == torch.device("cuda", 2)
+    assert normalize_device("cuda:4") == torch.device("cuda", 4)
+    assert normalize_device(torch.device("cuda", 1)) == torch.device("cuda", 1)
+    with pytest.raises(ValueError):
+        normalize_device("cpu")
