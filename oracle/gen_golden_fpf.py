@@ -3,7 +3,7 @@
 Test infrastructure, run by hand in the build container only (the reference is
 not present on the GPU box):
 
-    python oracle/gen_golden_fpf.py        # writes tests/golden/fpf/*.npz
+    python oracle/gen_golden_fpf.py [scenario ...]   # writes tests/golden/fpf/*.npz
 
 The FPF2 state (``local_w_diffs``, ``A_mat``, ``G_mat``, ``local_itr_lst`` /
 ``LRU_itr_lst``; fedavg_trainer.py:108-119, :210, :271-278, :314-327) lives in
@@ -66,14 +66,28 @@ ROUNDS = [  # (client_indexes, local_itr) returned by the scheduler each round
     ([], 1),                    # empty round: A_mat -> NaN (:319), kept as-is
     ([4, 9], 2),
 ]
-SCENARIOS = [("lr_full", "lr", None), ("bn_full", "bn", None), ("lr_lru", "lr", 64)]
+SCENARIOS = [("lr_full", "lr", None), ("bn_full", "bn", None), ("lr_lru", "lr", 64),
+             # round 5: models whose keys are not all fp32 (torch.cat's promotion
+             # in :210 and :291, A_mat / the index in the promoted dtype)
+             # (a bf16 model cannot run the reference's train(): :112 calls .numpy()
+             # on every key, which raises TypeError for bfloat16)
+             ("lr64_full", "lr64", None), ("lr16_full", "lr16", None),
+             ("bnmix64_full", "bnmix64", None), ("lr64_lru", "lr64", 64)]
+ONLY = set(sys.argv[2:])  # scenario names to (re)generate; all when empty
 
 
 def make_model(kind):
     torch.manual_seed(1234)
     if kind == "lr":
         return torch.nn.Linear(100, 10)
-    return torch.nn.Sequential(torch.nn.Linear(16, 8), torch.nn.BatchNorm1d(8))
+    if kind == "lr64":
+        return torch.nn.Linear(100, 10).double()
+    if kind == "lr16":
+        return torch.nn.Linear(100, 10).half()
+    m = torch.nn.Sequential(torch.nn.Linear(16, 8), torch.nn.BatchNorm1d(8))
+    if kind == "bnmix64":  # fp32 Linear, fp64 BatchNorm (its int64 counter stays int64)
+        m[1].double()
+    return m
 
 
 state = {"round": -1}
@@ -103,8 +117,8 @@ class StubClient:
         for k, v in w.items():
             if v.dtype == torch.int64:
                 w[k] = v + local_iteration
-            else:
-                w[k] = v + 0.01 * (1 + self.ds) * torch.randn(v.shape, generator=g)
+            else:  # the noise in the key's own dtype (fp32 keys: unchanged from round 1)
+                w[k] = v + (0.01 * (1 + self.ds) * torch.randn(v.shape, generator=g)).to(v.dtype)
         record[(r, self.slot)] = {k: v.clone() for k, v in w.items()}
         return w, 0.1 * (1 + self.ds), 0.5, 0.5, 0.5, 1
 
@@ -149,18 +163,20 @@ def run(name, kind, threshold):
             "keys": [{"name": k, "shape": list(v.shape), "dtype": str(v.dtype).replace("torch.", "")}
                      for k, v in init.items()]}
     arrays = {"meta": np.frombuffer(json.dumps(meta).encode(), dtype=np.uint8), "fpf": fpf}
+    raw = lambda v: v.view(torch.int16).numpy() if v.dtype == torch.bfloat16 else v.numpy()  # numpy has no bf16
     for k, v in init.items():
-        arrays[f"init__{k}"] = v.numpy()
+        arrays[f"init__{k}"] = raw(v)
     for (r, j), w in record.items():
         for k, v in w.items():
-            arrays[f"w__r{r}__i{j}__{k}"] = v.numpy()
+            arrays[f"w__r{r}__i{j}__{k}"] = raw(v)
     np.savez_compressed(os.path.join(out_dir, name + ".npz"), **arrays)
     print(name, "P =", weight_size, "full =", meta["full"], "nonzero fpf per round:",
           [int(np.count_nonzero(r)) for r in fpf])
 
 
 for name, kind, threshold in SCENARIOS:
-    run(name, kind, threshold)
+    if not ONLY or name in ONLY:
+        run(name, kind, threshold)
 '''
 
 
@@ -184,7 +200,7 @@ def main() -> int:
         env["PYTHONPATH"] = f"{stubs}:{REF_SRC}"
         env["PYTHONDONTWRITEBYTECODE"] = "1"
         env["CUDA_VISIBLE_DEVICES"] = ""
-        proc = subprocess.run([sys.executable, str(child), str(OUT_DIR)], cwd=run, env=env)
+        proc = subprocess.run([sys.executable, str(child), str(OUT_DIR), *sys.argv[1:]], cwd=run, env=env)
         return proc.returncode
 
 

@@ -37,10 +37,16 @@ def load_case(name: str) -> FPFCase:
     z = np.load(FPF_DIR / f"{name}.npz", allow_pickle=False)
     meta = json.loads(bytes(z["meta"]).decode())
     keys = [k["name"] for k in meta["keys"]]
-    init = OrderedDict((k, torch.from_numpy(z[f"init__{k}"].copy())) for k in keys)
+    bf16 = {k["name"] for k in meta["keys"] if k["dtype"] == "bfloat16"}  # stored as int16 bits
+
+    def tensor(arr, k):
+        t = torch.from_numpy(arr.copy())
+        return t.view(torch.bfloat16) if k in bf16 else t
+
+    init = OrderedDict((k, tensor(z[f"init__{k}"], k)) for k in keys)
     states = []
     for t, rd in enumerate(meta["rounds"]):
-        states.append([OrderedDict((k, torch.from_numpy(z[f"w__r{t}__i{j}__{k}"].copy())) for k in keys)
+        states.append([OrderedDict((k, tensor(z[f"w__r{t}__i{j}__{k}"], k)) for k in keys)
                        for j in range(len(rd["client_indexes"]))])
     return FPFCase(meta, init, states, z["fpf"])
 
@@ -65,6 +71,8 @@ def replay(case: FPFCase, impl, record_after_aggregate: bool = False) -> np.ndar
             impl.record_round(idx, w_locals, w_glob)
         for k in model_state:  # :219 load_state_dict (copy_ casts into the buffer's dtype)
             model_state[k].copy_(w_glob[k])
-        rows.append(np.asarray(impl.fpf_index(), dtype=np.float32))  # :272-278
+        # :272-278, in the index's own dtype: fp32, or fp64 once A_mat has
+        # become fp64 (a model with an fp64 key, torch.cat's promotion at :319)
+        rows.append(np.asarray(impl.fpf_index()))
         impl.end_round(t, idx, itr, w_glob, last_w)  # :314-327
     return np.stack(rows)

@@ -153,7 +153,7 @@ def test_fpf_oracle_matches_reference_loop(name):
     got = fpf_replay.replay(case, _OracleImpl(case))
     assert got.shape == case.fpf.shape
     assert np.array_equal(got.astype(np.float64), case.fpf)
-    assert case.meta["full"] == (name != "lr_lru")
+    assert case.meta["full"] == (not name.endswith("_lru"))
     if case.meta["full"]:
         # empty round 6 -> A_mat NaN (0/0 at :319) -> every later index scrubbed to 0
         assert np.count_nonzero(case.fpf[6]) > 0 and not np.any(case.fpf[7])
