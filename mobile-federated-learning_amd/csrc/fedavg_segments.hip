@@ -483,8 +483,16 @@ constexpr int kSegFusedRowsPerThread = 8;  // ceil(K * S / 4 / 256) slots per th
 // loads at 350 keys) and, at a key change, for its client addresses before
 // its data loads can start: four dependent latencies per tile, and a small
 // model's tiles change key almost every time.
-template <int S, bool MAP = false>
-__global__ __launch_bounds__(kBlock) void reduce_sqdist_segments_f32_kernel(const SegKey* __restrict__ keys,
+// LADDR (round 5, with MAP): the current key's K client addresses live in
+// LDS (after the tile and its average) instead of 8 + 8 int64 registers per
+// thread (this slot's row address and the next key's): each slot reads its
+// row's address with one ds_read_b64 when it issues the tile's loads, and at
+// a key change threads 0..K-1 load the next key's addresses behind the tile's
+// loads and write them to LDS after the tile's load barrier (every slot has
+// read the old ones by then).  114 -> ~80 VGPRs: 6 workgroups per CU (the
+// LDS bound, as the rows kernel's tiles) instead of 4.
+template <int S, bool MAP = false, bool LADDR = false>
+__global__ __launch_bounds__(kBlock, LADDR && S != 32 ? 6 : 1) void reduce_sqdist_segments_f32_kernel(const SegKey* __restrict__ keys,
                                                                             const int64_t* __restrict__ ptrs,
                                                                             int64_t n_keys, int64_t units, int K,
                                                                             const float* __restrict__ W,
@@ -510,12 +518,19 @@ __global__ __launch_bounds__(kBlock) void reduce_sqdist_segments_f32_kernel(cons
   int64_t u = blockIdx.x;
   int64_t j = 0;
   SegKey key{};
+  static_assert(!LADDR || MAP, "LDS addresses come with the unit map");
+  int64_t* addr = reinterpret_cast<int64_t*>(gs + S);  // LADDR: [K] client addresses of the current key
   if constexpr (MAP) {
     if (u < units) {
       j = umap[u];
       key = keys[j];
       if (key.kind == kRaw) {
-        load_src(ptrs + j * K, src);
+        if constexpr (LADDR) {
+          if (threadIdx.x < K) addr[threadIdx.x] = ptrs[j * K + threadIdx.x];
+          __syncthreads();
+        } else {
+          load_src(ptrs + j * K, src);
+        }
         cur_key = j;
       }
     }
@@ -536,6 +551,17 @@ __global__ __launch_bounds__(kBlock) void reduce_sqdist_segments_f32_kernel(cons
         }
       }
       const int nfull = n >> 2;  // whole 16-B slices of this unit
+      // LADDR: every slot's row address is read from LDS BEFORE the first
+      // LDS-DMA is issued -- a ds_read after one would wait for it to land
+      // (the compiler cannot tell the address block from the tile's bytes),
+      // which serialised the slots (round 5: 71 us against the rows kernel's
+      // 49 on the same bytes, SQ_WAIT_ANY 1.7x)
+      int64_t base[kSegFusedRowsPerThread];
+#pragma unroll
+      for (int m = 0; m < kSegFusedRowsPerThread; ++m) {
+        const int i = wave * 64 + m * kBlock + lane;
+        base[m] = LADDR ? (i < nload ? addr[i / V] : 0) : src[m];
+      }
 #pragma unroll
       for (int m = 0; m < kSegFusedRowsPerThread; ++m) {
         const int i0 = wave * 64 + m * kBlock;
@@ -543,12 +569,12 @@ __global__ __launch_bounds__(kBlock) void reduce_sqdist_segments_f32_kernel(cons
         const int row = i / V;
         const int c = (i % V) ^ (row & 7);
         if (i0 < nload && i < nload && c < nfull)
-          __builtin_amdgcn_global_load_lds((fused_gbl_t)(reinterpret_cast<const float*>(src[m]) + c0 + 4 * c),
+          __builtin_amdgcn_global_load_lds((fused_gbl_t)(reinterpret_cast<const float*>(base[m]) + c0 + 4 * c),
                                            (fused_lds_t)(tile + 4 * i0), 16, 0, 2 /* nt */);
       }
       if (n & 3) {  // the key's ragged last slice, element by element (never past the tensor's end)
         for (int row = threadIdx.x; row < K; row += kBlock) {
-          const gptr<float> x = to_global<float>(reinterpret_cast<const void*>(P[row]));
+          const gptr<float> x = to_global<float>(reinterpret_cast<const void*>(LADDR ? addr[row] : P[row]));
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int col = 4 * nfull + e;
@@ -567,19 +593,27 @@ __global__ __launch_bounds__(kBlock) void reduce_sqdist_segments_f32_kernel(cons
     int64_t jn = j;
     SegKey keyn = key;
     bool fresh = false;
-    int64_t srcn[kSegFusedRowsPerThread];
+    int64_t srcn[LADDR ? 1 : kSegFusedRowsPerThread];
+    int64_t addr_next = 0;
     if constexpr (MAP) {
       const int64_t un = u + gridDim.x;
       if (un < units) {
         jn = umap[un];
         keyn = keys[jn];
         if (keyn.kind == kRaw && jn != cur_key) {
-          load_src(ptrs + jn * K, srcn);
+          if constexpr (LADDR) {
+            if (threadIdx.x < K) addr_next = ptrs[jn * K + threadIdx.x];
+          } else {
+            load_src(ptrs + jn * K, srcn);
+          }
           fresh = true;
         }
       }
     }
     barrier_loads();
+    if constexpr (LADDR) {  // every slot has read this key's addresses: the next key's replace them
+      if (fresh && threadIdx.x < K) addr[threadIdx.x] = addr_next;
+    }
     fused_average<S>(tile, gs, K, W, n, out + key.out_offset + c0);
     barrier_lds();
     fused_squares<S, 1, true>(tile, gs, K, n, acc);  // full tiles unmasked (same VGPRs, round 4)
@@ -588,8 +622,10 @@ __global__ __launch_bounds__(kBlock) void reduce_sqdist_segments_f32_kernel(cons
       j = jn;
       key = keyn;
       if (fresh) {
+        if constexpr (!LADDR) {
 #pragma unroll
-        for (int m = 0; m < kSegFusedRowsPerThread; ++m) src[m] = srcn[m];
+          for (int m = 0; m < kSegFusedRowsPerThread; ++m) src[m] = srcn[m];
+        }
         cur_key = jn;
       }
     }
@@ -973,12 +1009,21 @@ constexpr int kSegFusedMaxK = kBlock;
 // 64, 128 up to 64, 256 up to 16); every width keeps <= 8 load slots per thread
 inline int seg_fused_cols(int64_t K) { return K > 128 ? 32 : (K > 64 ? 64 : (K > 16 ? 128 : 256)); }
 
-inline int64_t seg_fused_lds_bytes(int64_t K, int S) {
-  const int64_t b = (K + 1) * S * 4;
+inline int64_t seg_fused_lds_bytes(int64_t K, int S, bool laddr = false) {
+  const int64_t b = (K + 1) * S * 4 + (laddr ? K * 8 : 0);  // LADDR: + the key's K client addresses
   return b > kBlock * 8 ? b : kBlock * 8;
 }
 
-template <int S, bool MAP = false>
+// FEDAVG_SEG_LADDR=0 keeps the tiles' client addresses in registers (probes, A/B)
+inline bool seg_laddr_disabled() {
+  static const bool off = [] {
+    const char* e = std::getenv("FEDAVG_SEG_LADDR");
+    return e && e[0] == '0';
+  }();
+  return off;
+}
+
+template <int S, bool MAP = false, bool LADDR = false>
 int seg_fused_per_cu(int64_t K) {
   static std::mutex mu;
   static std::map<std::pair<int, int64_t>, int> cache;
@@ -987,8 +1032,8 @@ int seg_fused_per_cu(int64_t K) {
   std::lock_guard<std::mutex> lk(mu);
   auto it = cache.find({dev, K});
   if (it != cache.end()) return it->second;
-  const auto kern = reduce_sqdist_segments_f32_kernel<S, MAP>;
-  const int64_t lds = seg_fused_lds_bytes(K, S);
+  const auto kern = reduce_sqdist_segments_f32_kernel<S, MAP, LADDR>;
+  const int64_t lds = seg_fused_lds_bytes(K, S, LADDR);
   int per_cu = 0;
   if (lds > 65536 && hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                          hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1003,17 +1048,19 @@ int seg_fused_per_cu(int64_t K) {
   return per_cu;
 }
 
-template <int S, bool MAP = false>
+template <int S, bool MAP = false, bool LADDR = false>
 int64_t seg_fused_grid(int64_t K, int64_t units) {
-  const int64_t g = static_cast<int64_t>(seg_fused_per_cu<S, MAP>(K)) * cu_count();
+  const int64_t g = static_cast<int64_t>(seg_fused_per_cu<S, MAP, LADDR>(K)) * cu_count();
   return units < g ? units : g;
 }
 
-// resident workgroups per CU of either tile kernel (the partials' bound)
+// resident workgroups per CU of any tile kernel form (the partials' bound)
 template <int S>
 int seg_fused_per_cu_max(int64_t K) {
-  const int a = seg_fused_per_cu<S, false>(K), b = seg_fused_per_cu<S, true>(K);
-  return a > b ? a : b;
+  const int a = seg_fused_per_cu<S, false>(K), b = seg_fused_per_cu<S, true>(K),
+            c = seg_fused_per_cu<S, true, true>(K);
+  const int ab = a > b ? a : b;
+  return ab > c ? ab : c;
 }
 
 int64_t units_of(const int64_t* numel, int64_t n_keys, int64_t span = kSegSpan) {
@@ -1159,12 +1206,19 @@ int launch_seg_fused(const SegFusedPlan& p, const SegKey* keys, const int64_t* t
     const int S = static_cast<int>(p.span);
 #define FEDAVG_SEG_FUSED(C)                                                                                        \
   if (S == C) {                                                                                                    \
-    if ((umap ? seg_fused_per_cu<C, true>(K) : seg_fused_per_cu<C>(K)) <= 0)                                      \
+    const bool la = umap && !seg_laddr_disabled();                                                                 \
+    if ((la ? seg_fused_per_cu<C, true, true>(K) : (umap ? seg_fused_per_cu<C, true>(K) : seg_fused_per_cu<C>(K))) \
+        <= 0)                                                                                                      \
       return set_error(FEDAVG_EMODE, "%s: tile does not fit LDS", what);                                           \
-    nparts = umap ? seg_fused_grid<C, true>(K, units) : seg_fused_grid<C>(K, units);                               \
+    nparts = la ? seg_fused_grid<C, true, true>(K, units)                                                          \
+                : (umap ? seg_fused_grid<C, true>(K, units) : seg_fused_grid<C>(K, units));                        \
     if (partial_elems < K * nparts)                                                                                \
       return set_error(FEDAVG_EINVAL, "%s: partials need %lld doubles", what, (long long)(K * nparts));             \
-    if (umap)                                                                                                      \
+    if (la)                                                                                                        \
+      hipLaunchKernelGGL((reduce_sqdist_segments_f32_kernel<C, true, true>), dim3(static_cast<unsigned>(nparts)),   \
+                         dim3(kBlock), static_cast<unsigned>(seg_fused_lds_bytes(K, C, true)), s, keys, tptrs,      \
+                         n_keys, units, k32, weights, out, partials, umap);                                         \
+    else if (umap)                                                                                                 \
       hipLaunchKernelGGL((reduce_sqdist_segments_f32_kernel<C, true>), dim3(static_cast<unsigned>(nparts)),         \
                          dim3(kBlock), static_cast<unsigned>(seg_fused_lds_bytes(K, C)), s, keys, tptrs, n_keys,    \
                          units, k32, weights, out, partials, umap);                                                 \

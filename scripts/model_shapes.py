@@ -67,6 +67,9 @@ CONFIGS = {
     "resnet56": (100, resnet56_shapes()),
     "resnet18_gn": (500, resnet18_gn_shapes()),
     "target_flat": (100, [("w", (25_000_000,))]),
+    # resnet56's fp32 element count as ONE key (tile / window probes: the
+    # per-key cost against the same bytes)
+    "resnet56_flat": (100, [("w", (600_372 - 58,))]),
 }
 
 
