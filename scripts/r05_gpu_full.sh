@@ -21,6 +21,7 @@ for MPW in 16 1; do
     FEDAVG_SEGWIN_MIN_PER_WAVE=$MPW timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
         -d "$OUT/r56_${L}_mpw$MPW" -o run -- python scripts/segwin_layout_probe.py --layout $L --config resnet56 --calls 30 \
         > "$OUT/r56_${L}_mpw$MPW.log" 2>&1
+    find "$OUT/r56_${L}_mpw$MPW" -name "*kernel_trace.csv" -delete  # 35,000 copies per run: over the 64 MiB merge cap
     log "resnet56 $L mpw=$MPW: $(grep -h '"layout"' "$OUT/r56_${L}_mpw$MPW.log" | cut -c1-300)"
   done
 done
