@@ -773,6 +773,7 @@ class DeviceAggregator:
         g = table.groups[torch.float32]
         if K > st.K or K * g.ld * 4 > self.SMALL_ROUND_BYTES or self._session_open():
             return None
+        t0 = time.perf_counter()
         with self._lock:
             stream = torch.cuda.current_stream(self.device).cuda_stream
             status, out_dev, out_host = fast["ext"].small_round(
@@ -782,6 +783,8 @@ class DeviceAggregator:
         if status == 1:
             return None
         _lib.check(status, "fedavg_round_f32")
+        # the whole round is one native call (walk, pack, H2D, reduce, D2H, views)
+        self.last_profile = {"pack_issue_ms": 0.0, "h2d_kernel_d2h_ms": (time.perf_counter() - t0) * 1e3}
         acc = w_locals[0][1]
         self.fast_rounds += 1
         self._last = {"table": table, "K": K, "dev": {torch.float32: (st.dev[:K], out_dev)}}
