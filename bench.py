@@ -969,9 +969,14 @@ def main(argv=None):
                 out["round_with_distances"] = fused_round(red, w_dev)
             except Exception as e:  # noqa: BLE001
                 out["round_with_distances"] = {"error": f"{type(e).__name__}: {e}"}
-        if not args.no_cpu_baseline:
-            # at every N, on rank 0 after the timed region and the parity
-            # checks (the other ranks wait at the barrier below): the
+        if not args.no_cpu_baseline and world > 1:
+            # the bench contract times the CPU baseline on rank 0 at N = 1 only:
+            # an N-GPU line points at that run instead of spending 10-30 s of
+            # the job's host time on the same number again
+            out["cpu_baseline"] = {"value": None, "n_gpus_in_run": world,
+                                   "note": "timed at N = 1 only (rank 0 of the 1-GPU run's line)"}
+        elif not args.no_cpu_baseline:
+            # on rank 0 after the timed region and the parity checks: the
             # workload's own K x P while its rows fit a bounded host sample
             # (<= 10 GB: the target); cfg5's 400 GB is timed on a P-slice
             try:

@@ -184,13 +184,13 @@ def test_as_rank_plans_one_shard_of_a_larger_world():
 
 
 @pytest.mark.parametrize("n", [2, 8])
-def test_cpu_rehearsal_line_has_chunk_sweep_and_cpu_baseline(n):
+def test_cpu_rehearsal_line_has_chunk_sweep(n):
     """``bench.py --gpus N --cpu-rehearsal``: the whole N > 1 bench path on CPU
     with gloo (a torch stand-in for the kernel).  Rank 0's one JSON line
     carries the warm-up chunk sweep (the chosen depth is the fastest step of
-    the candidates), the parity checks of the gathered model, and the CPU
-    baseline timed on rank 0 after the timed region while the other ranks
-    wait -- the same line the driver's N-GPU run prints."""
+    the candidates) and the parity checks of the gathered model -- the same
+    line the driver's N-GPU run prints.  The CPU baseline is timed at N = 1
+    only (the bench contract); the N-GPU line says so."""
     r = _run_bench("--gpus", str(n), "--cpu-rehearsal", "--steps", "2", "--warmup", "1", timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -204,7 +204,18 @@ def test_cpu_rehearsal_line_has_chunk_sweep_and_cpu_baseline(n):
     assert out["config"]["chunks_from"].startswith("warm-up step sweep")
     assert out["parity"]["ok"] and out["parity"]["ranks"] == n and out["parity"]["reassembly_checksums_ok"]
     cb = out["cpu_baseline"]
-    assert cb["value"] > 0 and cb["n_gpus_in_run"] == n and cb["value_at_share"] > 0
+    assert cb["value"] is None and cb["n_gpus_in_run"] == n and "N = 1 only" in cb["note"]
+
+
+def test_cpu_rehearsal_one_rank_times_the_cpu_baseline():
+    """At N = 1 rank 0 times the reference's CPU loop after the timed region:
+    both layouts, the affinity-thread value and the value at the job's share."""
+    r = _run_bench("--gpus", "1", "--cpu-rehearsal", "--steps", "2", "--warmup", "1", timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    cb = json.loads(lines[0])["cpu_baseline"]
+    assert cb["value"] > 0 and cb["n_gpus_in_run"] == 1 and cb["value_at_share"] > 0
     assert {lay["layout"] for lay in cb["layouts"]} >= {"flat", "model-shaped (mnist_lr)"}
 
 
