@@ -33,9 +33,12 @@ path (178.8 ms).
   :199 and :217 (clipping, noise, ``copy_``, slice assignment: any in-place
   op) a deterministic fallback whatever elements they touch; a replaced
   tensor object fails the same check (a fresh tensor's counter is not a deep
-  copy's).  What the counter cannot see -- writes through ``.data``/numpy
-  views or raw pointers, which bypass autograd's bookkeeping -- is left to
-  the value probes.
+  copy's).  An in-place edit of a ``Client.train`` result between :189 and
+  its :199 deep copy is seen on the fed dict itself: the worker keeps the
+  last packed dict with its counters and re-reads them when the next client
+  arrives (status 9 at :217 for the round's last client).  What the counter
+  cannot see -- writes through ``.data``/numpy views or raw pointers, which
+  bypass autograd's bookkeeping -- is left to the value probes.
 
 Anything else falls back to the plain drop-in on ``w_locals`` (same bits,
 the reference's exceptions): a count or sample-number mismatch, a retried
@@ -139,6 +142,13 @@ class ClientFeed:
         self._small = False  # this round fits SMALL_ROUND_BYTES: left to the plain path
         self.fed = []  # sample numbers in feed order
         self._fed_keys = []  # each fed dict's key objects, in feed order
+        # the last packed client's dict and its version counters at packing:
+        # re-read when the next client arrives (the loop's :199 copy of this
+        # one is done by then) and, for the round's last client, inside the
+        # :217 check -- an in-place edit of a Client.train result between
+        # :189 and :199 after the worker packed it is a fallback (the loop's
+        # deep copy would hold the edited values with a fresh counter)
+        self._prev = None
         self._vplan = None  # verify_rows' table arrays for the open session (worker-made)
         self._graveyard = []  # _Release lists waiting for the next round (worker thread only)
         self._q: Optional[queue.Queue] = None
@@ -215,6 +225,10 @@ class ClientFeed:
             try:
                 if not self.broken and self._err is None:
                     n, sd, vers = item
+                    prev, self._prev = self._prev, None
+                    if prev is not None and [v._version for v in prev[0].values()] != prev[1]:
+                        raise RuntimeError("a fed client's tensors changed after they were packed")
+                    prev = None
                     if self.session is None:
                         self.session = self._aggregator_fn().begin_round(sd, self.max_clients)
                         self.session.keep_dicts = False
@@ -223,10 +237,12 @@ class ClientFeed:
                     self.session.add(n, sd)
                     if [v._version for v in sd.values()] != vers:
                         raise RuntimeError("a client's tensors changed while they were packed")
+                    self._prev = (sd, vers)  # until the next client (the loop's `w` holds it as long)
             except BaseException as e:  # noqa: BLE001 -- any failure means: fall back at aggregate
                 self._err = e
+                self._prev = None
             finally:
-                item = n = sd = vers = None  # drop the client's tensors now (the loop holds its own copy)
+                item = n = sd = vers = prev = None  # no other reference to the client's tensors
                 t1 = time.perf_counter()
                 self._add_ms.append((t1 - t0) * 1e3)
                 self._t_done = t1
@@ -319,6 +335,11 @@ class ClientFeed:
         round's GPU work is in flight, and anything unexpected means the
         round is not the fed one."""
         try:
+            prev, self._prev = self._prev, None  # the last client's dict as fed (the worker is drained)
+            if prev is None or [v._version for v in prev[0].values()] != prev[1]:
+                self.stats["last_verify"] = {"status": 9, "client": len(self.fed) - 1, "key": -1, "probes": 0}
+                return False
+            prev = None
             ext, names, templ, group, offset, kind, sptr, sld, ses = self._vplan
             st = ext.verify_rows(w_locals, list(self.fed), names, templ, group, offset, kind, sptr, sld, ses,
                                  self.VERIFY_PROBES, random.getrandbits(64), self.VERIFY_FULL_ELEMS,
@@ -344,6 +365,7 @@ class ClientFeed:
             self._defer_release(self._fed_keys)
         self._fed_keys = []
         self._vplan = None
+        self._prev = None
         self.broken = self._small = False
         self._err = None
         self._add_ms = []

@@ -50,7 +50,8 @@ class Client:
 class FedAvgTrainer:
     client_cls = Client
 
-    def __init__(self, model_state, rounds, n_clients=None, train_delay_s=0.0, after_append=None):
+    def __init__(self, model_state, rounds, n_clients=None, train_delay_s=0.0, after_append=None,
+                 before_append=None):
         self.model_global = _Model(model_state)
         self.rounds = rounds
         n = n_clients or max((len(r) for r in rounds), default=1)
@@ -58,6 +59,7 @@ class FedAvgTrainer:
         for c in self.client_list:
             c.train_delay_s = train_delay_s
         self.after_append = after_append  # test hook: (round, w_locals) -> None, e.g. a mutation
+        self.before_append = before_append  # test hook: (round, client, w) -> None, between :190 and :199
         self.results = []
         self.timings = []
 
@@ -76,6 +78,8 @@ class FedAvgTrainer:
                     w, loss, beta, rho, acc, cyc = client.train(net=None, local_iteration=1)  # :189
                     if loss is not None and beta is not None and rho is not None and acc is not None:  # :190
                         break
+                if self.before_append is not None:
+                    self.before_append(r, idx, w)
                 t_last = time.perf_counter()
                 w_locals.append((client.get_sample_number(), copy.deepcopy(w)))  # :199
             if self.after_append is not None:

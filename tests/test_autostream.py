@@ -318,6 +318,44 @@ def test_single_in_place_edit_falls_back_every_time(plain_calls, seed):
     assert (feed.stats["last_verify"]["client"], feed.stats["last_verify"]["key"]) == where
 
 
+@pytest.mark.parametrize("which", ["middle", "last"])
+def test_fed_dict_edited_before_its_deep_copy_falls_back(plain_calls, which):
+    """A Client.train result edited in place AFTER the worker packed it and
+    BEFORE the loop's :199 deep copy: w_locals then holds the edited values
+    under fresh deep-copy counters, so only the fed dict itself shows the
+    edit.  The worker re-reads the last packed dict's counters when the next
+    client arrives (a middle client: the feed breaks) and :217 re-reads the
+    round's last one (verify status 9)."""
+    K = 6
+    g = torch.Generator().manual_seed(3)
+    specs = [(i + 1, [OrderedDict((f"k{j}", torch.randn(200, generator=g)) for j in range(4))]) for i in range(K)]
+    rounds = [specs, specs]
+    target = 2 if which == "middle" else K - 1
+    feeds = []
+
+    def edit(r, idx, w):
+        if r == 1 and idx == target:
+            feeds[0]._drain()  # the worker has packed this client: the edit comes after
+            w["k1"][7] += 1e-3
+
+    T, C = fresh_classes()
+    mfl_amd.install(T, stream_clients=True)
+    tr = T({"k0": torch.zeros(200)}, rounds, before_append=edit)
+    agg = _FakeAgg()
+    from mfl_amd.autostream import ClientFeed
+
+    feed = ClientFeed(lambda: agg, K)
+    feed.SMALL_ROUND_BYTES = 0
+    feeds.append(feed)
+    tr.__dict__["_mfl_feed"] = feed
+    tr.train()
+    assert "__streamed__" in tr.results[0] and "__plain__" in tr.results[1]
+    if which == "last":
+        assert feed.stats["last_verify"]["status"] == 9
+    else:
+        assert "changed after they were packed" in feed.stats["last_fallback"]
+
+
 def test_install_devices_streams_into_the_sharded_aggregator(plain_calls, monkeypatch):
     """install(devices=[...]): the feed's rounds open on the devices'
     ShardedAggregator (multi.ShardedRoundSession), not on the first device."""
