@@ -270,3 +270,32 @@ def test_drop_in_device_round_all_empty_keys():
     assert glob["a"].device.type == "cuda"
     d = agg.client_distances(wl, glob)
     assert np.array_equal(d, np.zeros(K))
+
+
+def test_device_round_resnet56_doubling_property():
+    """resnet56 x 100 (350 keys, 58 int64 buffers) through the zero-copy
+    tiles (the LDS-address form): against the reference's torch loop bit for
+    bit, then every client doubled in place -- powers of two commute with
+    every rounding step, so the average must come out exactly 2x and each
+    client's fp64 sum of squares exactly 4x (the sums' order is the same
+    grid, so the property is bit-exact)."""
+    import sys
+    from pathlib import Path
+
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "scripts"))
+    from model_shapes import CONFIGS
+
+    K, shapes = CONFIGS["resnet56"]
+    specs = [(s, torch.int64 if n.endswith("num_batches_tracked") else torch.float32) for n, s in shapes]
+    counts, dicts = _clients(K, specs, seed=56)
+    r = _Round(counts, dicts)
+    rc, out, sumsq = r.run()
+    assert rc == 0
+    assert_bits(out.cpu(), _expected(counts, dicts, r.g), "resnet56 device round")
+    for sd in dicts:
+        for t in sd.values():
+            t.mul_(2)
+    rc2, out2, sumsq2 = r.run()
+    assert rc2 == 0
+    assert torch.equal(out2.view(torch.int32), (out * 2.0).view(torch.int32))
+    assert torch.equal(sumsq2, sumsq * 4.0)

@@ -528,6 +528,17 @@ def test_target_size_sampled_parity():
         ref64 += x[k, :P].double() * float(np.float32(w[k]))
     rel = (out.double() - ref64).norm() / ref64.norm()
     assert rel < 1e-6
+    # the fused aggregate + :291 pass at full size: the same average bits, and
+    # an exact scaling property of the whole vector -- doubling every client
+    # doubles every product, sum and fp32 difference exactly (powers of two
+    # commute with rounding away from overflow / subnormals), so the average
+    # must come out exactly 2x and every client's fp64 sum of squares 4x
+    out_f, sums = mfl_amd.reduce_with_sqdist(x, _w(w), P)
+    assert torch.equal(out_f.view(torch.int32), out.view(torch.int32))
+    x.mul_(2.0)
+    out2, sums2 = mfl_amd.reduce_with_sqdist(x, _w(w), P)
+    assert torch.equal(out2.view(torch.int32), (out * 2.0).view(torch.int32))
+    assert torch.equal(sums2, sums * 4.0)
     del x
 
 
