@@ -502,7 +502,8 @@ def fused_round(red, w_dev, reps: int = 10) -> dict:
     kind, tile, slots = plan // 1000000, (plan // 100) % 10000, plan % 100
     kernel = {0: "two passes", 1: f"reduce_sqdist_f32_kernel<S={tile}> (LDS-DMA tiles)",
               2: f"reduce_sqdist_rs_kernel<S={tile},SLOTS={slots}> (register-staged tiles)",
-              3: f"reduce_sqdist_win_kernel<KMAX={tile},VEC={slots}> (wave-owned windows)"}.get(kind, str(plan))
+              3: f"reduce_sqdist_win_kernel<KMAX={tile},VEC={slots}> (wave-owned windows)",
+              4: f"reduce_sqdist_winn_kernel<KH={tile},VEC=1,NSMAX={slots}> (split-row windows)"}.get(kind, str(plan))
     return {"what": "aggregate + :291 sums of squares over the same resident rows (fedavg_trainer.py:217, :291)",
             "two_pass_ms": round(ms["two_pass"], 4), "fused_ms": round(ms["fused"], 4),
             "speedup": round(ms["two_pass"] / ms["fused"], 3),
@@ -963,7 +964,7 @@ def main(argv=None):
             out["clock_mhz"] = clk["clock_mhz"]
             if roofline is not None:
                 roofline["clock"] = clk["clock"]
-        if (not rehearsal and world == 1 and passes == 1 and plan_world == 1 and K <= 512
+        if (not rehearsal and world == 1 and passes == 1 and plan_world == 1 and K <= 1024
                 and red.plan.chunks == 1):
             try:  # a side measurement: never the reason the bench line is missing
                 out["round_with_distances"] = fused_round(red, w_dev)

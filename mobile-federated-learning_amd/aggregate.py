@@ -164,7 +164,7 @@ def column_chunks(P: int) -> List[Tuple[int, int]]:
 # The reference runs :291 after every aggregate with clients (fedavg_trainer.py
 # :289-291), so the drop-in fuses by default; FEDAVG_FUSE_DISTANCES=0 keeps
 # the reduce alone.
-FUSED_MAX_K = 512  # rows kernels (fedavg_reduce_sqdist_f32's fused_plan; more clients: the two passes are faster)
+FUSED_MAX_K = 1024  # rows kernels (fedavg_reduce_sqdist_f32's fused_plan; more clients: the two passes)
 FUSED_SEGMENTS_MAX_K = 256  # device-resident clients' own tensors (fedavg_reduce_sqdist_segments_f32)
 FUSE_DISTANCES = os.environ.get("FEDAVG_FUSE_DISTANCES", "1") != "0"
 

@@ -28,6 +28,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <tuple>
 #include <mutex>
 #include <utility>
 
@@ -352,10 +353,10 @@ void launch_f32x4(const float* clients, int K, int64_t ld, int64_t P, const floa
 template <typename Kern>
 int64_t resident_blocks(Kern kernel, int block = kBlock) {
   static std::mutex mu;
-  static std::map<std::pair<int, const void*>, int64_t> cache;
+  static std::map<std::tuple<int, const void*, int>, int64_t> cache;  // per device, kernel and block size
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 1024;
-  const auto key = std::make_pair(dev, reinterpret_cast<const void*>(kernel));
+  const auto key = std::make_tuple(dev, reinterpret_cast<const void*>(kernel), block);
   {
     std::lock_guard<std::mutex> lk(mu);
     auto it = cache.find(key);

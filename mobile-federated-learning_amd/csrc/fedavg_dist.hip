@@ -1136,6 +1136,189 @@ int launch_fused_win(const float* clients, int64_t K, int64_t P, int64_t ld, con
   return launch_status(what);
 }
 
+// ---------------------------------------------------------------------------
+// Split-row windows (round 5) for 369-1024 rows.  The register-staged tiles
+// ran 500 x 11.2M at 5.4 ms (52 % of HBM peak; a tile's K-step chain runs on
+// 32 lanes only) and the two passes took over beyond 512 rows.  A workgroup of ns = ceil(K / KH) <=
+// NSMAX waves owns a window of 64 x VEC columns; wave h holds rows h*KH ..
+// h*KH + KH - 1 in registers.  The chain keeps the reference's order: wave 0
+// runs its rows, hands its fp32 partial over LDS to wave 1, ... wave ns-1
+// ends it and stores the average; then every wave squares its own rows
+// against it and reloads them from the next window (as reduce_sqdist_win2).
+// Rows past K load through an empty descriptor (+0) with weight -0.0, which
+// leaves every chain value unchanged.
+// ---------------------------------------------------------------------------
+template <int KH, int VEC, int NSMAX>
+__global__ __launch_bounds__(64 * NSMAX, win_min_waves(KH, VEC)) void reduce_sqdist_winn_kernel(
+    const float* __restrict__ X, int K, int64_t ld, int64_t P, int64_t nwin, const float* __restrict__ W,
+    float* __restrict__ out, double* __restrict__ partials) {
+  typedef typename WinVec<VEC>::T V;
+  constexpr int WC = 64 * VEC;
+  constexpr int NB = (KH + 7) / 8;
+  constexpr int KP = (KH + 3) & ~3;
+  const int lane = threadIdx.x & 63;
+  const int h = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int ns = __builtin_amdgcn_readfirstlane(static_cast<int>(blockDim.x >> 6));
+  const int r0 = h * KH;
+  const int64_t G = gridDim.x;
+  const uint32_t voff = static_cast<uint32_t>(lane) * VEC * 4;
+  const int64_t P4 = (P + 3) & ~static_cast<int64_t>(3);
+  const int64_t row_bytes = ld * 4;
+  const bool upper = (lane & 8) != 0;
+  const auto win_bytes = [&](int64_t w) -> int {
+    if (w >= nwin) return 0;
+    const int64_t n = P4 - w * WC;
+    return static_cast<int>((n < WC ? n : WC) * 4);
+  };
+  __shared__ __attribute__((aligned(16))) float wl[NSMAX][KP];
+  __shared__ double accl[NSMAX][NB][64];
+  __shared__ __attribute__((aligned(16))) V xa[64];
+  for (int i = threadIdx.x; i < ns * KP; i += blockDim.x) {
+    const int hh = i / KP, j = i % KP, row = hh * KH + j;
+    wl[hh][j] = (j < KH && row < K) ? W[row] : -0.0f;
+  }
+  double* acc = &accl[h][0][lane];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) acc[64 * b] = 0.0;
+  __syncthreads();
+  V x[KH];
+  {
+    int Kw = K;
+    asm volatile("" : "+s"(Kw));
+    const int nb = win_bytes(blockIdx.x);
+    const char* rp = reinterpret_cast<const char*>(X + static_cast<int64_t>(blockIdx.x) * WC) + r0 * row_bytes;
+#pragma unroll
+    for (int i = 0; i < KH; ++i) {
+      asm volatile("" : "+s"(rp));
+      x[i] = win_load<VEC>(
+          __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(rp), 0, r0 + i < Kw ? nb : 0, 0x00020000), voff);
+      rp += row_bytes;
+    }
+  }
+  const auto chain = [&](V& a, bool first) {
+    int wo = h * KP;  // opaque: the weights are re-read per window, not held in registers
+    asm volatile("" : "+v"(wo));
+    const float* wp = &wl[0][0] + wo;
+#pragma unroll
+    for (int q = 0; q < KP / 4; ++q) {
+      const f32x4 w4 = *reinterpret_cast<const f32x4*>(wp + 4 * q);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int i = 4 * q + j;
+        if (i >= KH) continue;
+        if (first && i == 0) {
+          a = x[0] * w4[0];
+        } else {
+          const V t = x[i] * w4[j];
+          a = a + t;
+        }
+      }
+    }
+  };
+  for (int64_t w = blockIdx.x; w < nwin; w += G) {
+    int Kw = K;
+    asm volatile("" : "+s"(Kw));
+    const int64_t c0 = w * WC;
+    const int64_t cl = c0 + lane * VEC;
+    const int nbn = win_bytes(w + G);
+    const char* rp = reinterpret_cast<const char*>(X + (w + G) * WC) + r0 * row_bytes;
+    const bool ragged = c0 + WC > P;
+    if (ragged) {
+#pragma unroll
+      for (int i = 0; i < KH; ++i) {
+#pragma unroll
+        for (int v = 0; v < VEC; ++v)
+          if (cl + v >= P) x[i][v] = 0.f;
+      }
+    }
+    V a;
+    for (int st = 0; st < ns; ++st) {  // the chain, wave by wave in row order
+      if (h == st) {
+        if (st > 0) a = xa[lane];
+        chain(a, st == 0);
+        xa[lane] = a;
+        if (st == ns - 1) {
+          if (!ragged) {
+            __builtin_nontemporal_store(static_cast<typename WinVec<VEC>::TA>(a),
+                                        reinterpret_cast<typename WinVec<VEC>::TA*>(out + cl));
+          } else {
+#pragma unroll
+            for (int v = 0; v < VEC; ++v)
+              if (cl + v < P) out[cl + v] = a[v];
+          }
+        }
+      }
+      __syncthreads();
+    }
+    if (h != ns - 1) a = xa[lane];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      double p[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = 8 * b + j;
+        p[j] = 0.0;
+        if (i < KH) {
+          p[j] = win_sq<VEC>(x[i] - a);
+          asm volatile("" : "+s"(rp));
+          x[i] = win_load<VEC>(
+              __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(rp), 0, r0 + i < Kw ? nbn : 0, 0x00020000), voff);
+          rp += row_bytes;
+        }
+      }
+      const double q01 = fold32(p[0], p[1]), q23 = fold32(p[2], p[3]);
+      const double q45 = fold32(p[4], p[5]), q67 = fold32(p[6], p[7]);
+      acc[64 * b] += fold8(fold16(q01, q23), fold16(q45, q67), upper);
+    }
+    __syncthreads();  // xa is read by every wave before the next window's chain rewrites it
+  }
+  const int row_in = win_batch_row(lane);
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    double s = acc[64 * b];
+    s += dpp_move_f64<0xB1, 0xF>(s);
+    s += dpp_move_f64<0x4E, 0xF>(s);
+    s += dpp_move_f64<0x141, 0xF>(s);
+    const int row = 8 * b + row_in;
+    if ((lane & 7) == 0 && row < KH && r0 + row < K) partials[static_cast<int64_t>(r0 + row) * G + blockIdx.x] = s;
+  }
+}
+
+// workgroups of the split window launch: the resident ones (ceil(K / KH)
+// waves each), at most one per window
+template <int KH, int VEC, int NSMAX>
+int64_t fused_winn_grid(int64_t K, int64_t P, int blocks_per_cu) {
+  const int ns = static_cast<int>((K + KH - 1) / KH);
+  const int64_t per_cu = blocks_per_cu > 0 ? blocks_per_cu
+                                           : resident_blocks(reduce_sqdist_winn_kernel<KH, VEC, NSMAX>, 64 * ns) /
+                                                 cu_count();
+  const int64_t nwin = (P + 64 * VEC - 1) / (64 * VEC);
+  const int64_t grid = per_cu * cu_count();
+  return grid < nwin ? grid : nwin;
+}
+
+template <int KH, int VEC, int NSMAX>
+int launch_fused_winn(const float* clients, int64_t K, int64_t P, int64_t ld, const float* weights, float* out,
+                      double* partials, int64_t partial_elems, double* sumsq, int blocks_per_cu, hipStream_t s,
+                      const char* what) {
+  if (K > NSMAX * KH) return set_error(FEDAVG_EMODE, "%s: this split window kernel covers K <= %d", what, NSMAX * KH);
+  const int ns = static_cast<int>((K + KH - 1) / KH);
+  const int64_t nwin = (P + 64 * VEC - 1) / (64 * VEC);
+  const int64_t grid = fused_winn_grid<KH, VEC, NSMAX>(K, P, blocks_per_cu);
+  if (grid <= 0) return set_error(FEDAVG_EMODE, "%s: the split window kernel is not resident", what);
+  if (partial_elems < K * grid)
+    return set_error(FEDAVG_EINVAL, "%s: workspace needs %lld doubles", what, (long long)(K * grid));
+  hipLaunchKernelGGL((reduce_sqdist_winn_kernel<KH, VEC, NSMAX>), dim3(static_cast<unsigned>(grid)),
+                     dim3(static_cast<unsigned>(64 * ns)), 0, s, clients, static_cast<int>(K), ld, P, nwin, weights,
+                     out, partials);
+  int rc = launch_status(what);
+  if (rc) return rc;
+  hipLaunchKernelGGL(client_sqdist_finalize_kernel, dim3(static_cast<unsigned>(K)), dim3(kBlock), 0, s, partials,
+                     grid, sumsq);
+  return launch_status(what);
+}
+
+
 #ifdef FEDAVG_TUNING
 // ---------------------------------------------------------------------------
 // Probe (round 3): split-row windows.  With K = 100 rows in one wave the
@@ -1337,12 +1520,20 @@ int launch_fused_win2(const float* clients, int64_t K, int64_t P, int64_t ld, co
 //              0.857 at 32 columns; the LDS-DMA kernel 0.829)
 //   K <= 320   register-staged, 32 columns, 10 slots (224 x 4.5M 0.728 vs
 //              1.03 at 64; 300 x 5M 1.08 vs 1.41 LDS-DMA vs 1.98 two passes)
-//   K <= 512   register-staged, 32 columns, 16 slots (500 x 11.2M 5.41 vs
-//              6.88 ms for the two passes; 512 x 5M 2.58 vs 3.22)
-// Beyond 512 rows the two passes are faster (640 x 3M: 2.37 vs 3.32 ms;
-// 1000 x 12.5M: 15.2 vs 20.0): each tile's K-step chain grows with K.
-constexpr int kFusedNone = 0, kFusedLds = 1, kFusedRs = 2, kFusedWin = 3;
-constexpr int64_t kFusedRowsMaxK = 512;
+//   K <= 368   register-staged, 32 columns, 16 slots (round 3: 500 x 11.2M
+//              5.41 vs 6.88 ms for the two passes; 512 x 5M 2.58 vs 3.22)
+//   K <= 1024  split-row windows (round 5, below: kFusedWinnMinK)
+// Beyond 1024 rows the two passes (a workgroup holds at most 16 x 64 rows).
+constexpr int kFusedNone = 0, kFusedLds = 1, kFusedRs = 2, kFusedWin = 3, kFusedWinn = 4;
+constexpr int64_t kFusedRowsMaxK = 1024;
+// split-row windows (reduce_sqdist_winn_kernel, 64 rows per wave, 64 columns)
+// from 369 rows (round 5, scripts/fused_probe.py, profiles/r05/winn/, ms:
+// 384 x 5M 1.455 vs 1.494 register-staged; 448 x 5M 1.60 vs 2.30; 500 x
+// 11.2M 3.71 vs 5.37; 500 x 1.4M 0.54 vs 0.72; 512 x 5M 1.69 vs 2.59; but
+// 352 x 5M 1.42 vs 1.36 and 300 x 5M 1.10 vs 1.05), up to 8 waves per
+// workgroup to 512 rows, 16 beyond (640 x 3M 1.77 vs 2.46 for the two
+// passes; 1000 x 12.5M 9.99 vs 15.05; 520 x 5M 2.71 vs 3.34)
+constexpr int64_t kFusedWinnMinK = 369;
 constexpr int64_t kWinMinPerWave = 16;  // windows per wave below which the tile kernels keep the round
 // ... except in the LDS-DMA tiles' weak band, 65-96 rows, where the windows
 // win down to ~400K columns (profiles/r03/win/short_rows_*.jsonl, ms, tiles
@@ -1395,7 +1586,8 @@ inline FusedPlan fused_plan(int64_t K, int64_t P) {
   if (K <= 128) return {kFusedLds, 64, 0};
   if (K <= 192) return {kFusedRs, 64, 16};
   if (K <= 320) return {kFusedRs, 32, 10};
-  return {kFusedRs, 32, 16};
+  if (K < kFusedWinnMinK) return {kFusedRs, 32, 16};
+  return {kFusedWinn, 64, K <= 512 ? 8 : 16};  // S = rows per wave, slots = waves per workgroup (max)
 }
 
 // Global-pointer schedule (the fp64/fp16/bf16 passes and the probe
@@ -1712,6 +1904,8 @@ int64_t fedavg_reduce_sqdist_workspace(int64_t K, int64_t P) {
     if (pl.S == 64) fused = K * fused_grid<64>(K, P, 0);
     if (pl.S == 128) fused = K * fused_grid<128>(K, P, 0);
     if (pl.S == 256) fused = K * fused_grid<256>(K, P, 0);
+  } else if (pl.kind == kFusedWinn) {
+    fused = K * (pl.slots == 8 ? fused_winn_grid<64, 1, 8>(K, P, 0) : fused_winn_grid<64, 1, 16>(K, P, 0));
   } else if (pl.kind == kFusedRs) {
     switch (pl.S * 100 + pl.slots) {
       case 25608: fused = K * fused_rs_grid<256, 8, 0>(K, P, 0); break;
@@ -1761,6 +1955,13 @@ int fedavg_reduce_sqdist_f32(const float* clients, int64_t K, int64_t P, int64_t
                                              what);
       }
     }
+    if (pl.kind == kFusedWinn) {
+      if (pl.slots == 8)
+        return launch_fused_winn<64, 1, 8>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq, 0, s,
+                                           what);
+      return launch_fused_winn<64, 1, 16>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq, 0, s,
+                                          what);
+    }
     if (pl.kind == kFusedLds) {
       if (pl.S == 64)
         return launch_fused<64>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq, 0, s, what);
@@ -1786,7 +1987,8 @@ int fedavg_reduce_sqdist_f32(const float* clients, int64_t K, int64_t P, int64_t
 
 // the production plan of fedavg_reduce_sqdist_f32 for K x P: kind x
 // 1000000 + S x 100 + slots (kind 0 two passes, 1 LDS-DMA tiles, 2
-// register-staged tiles, 3 wave-owned windows with S = KMAX, slots = VEC)
+// register-staged tiles, 3 wave-owned windows with S = KMAX, slots = VEC,
+// 4 split-row windows with S = rows per wave, slots = most waves per group)
 int64_t fedavg_fused_plan_of(int64_t K, int64_t P) {
   const FusedPlan pl = fused_plan(K, P);
   return static_cast<int64_t>(pl.kind) * 1000000 + pl.S * 100 + pl.slots;
@@ -1949,6 +2151,18 @@ int fedavg_reduce_sqdist_f32_variant(const float* clients, int64_t K, int64_t P,
     FEDAVG_WIN2_CASE(60, 2)
     FEDAVG_WIN2_CASE(50, 4)
 #undef FEDAVG_WIN2_CASE
+    // split-row windows over ceil(K / KH) <= NSMAX waves (reduce_sqdist_winn_kernel):
+    // 85000000 + NSMAX * 10000 + KH * 10 + VEC
+#define FEDAVG_WINN_CASE(KH, VEC, NSMAX)                                                                          \
+  case 85000000 + NSMAX * 10000 + KH * 10 + VEC:                                                                 \
+    return launch_fused_winn<KH, VEC, NSMAX>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq,  \
+                                             blocks_per_cu, s, what);
+    FEDAVG_WINN_CASE(64, 1, 8)
+    FEDAVG_WINN_CASE(64, 2, 8)
+    FEDAVG_WINN_CASE(32, 2, 16)
+    FEDAVG_WINN_CASE(128, 1, 4)
+    FEDAVG_WINN_CASE(64, 1, 16)
+#undef FEDAVG_WINN_CASE
     default: return set_error(FEDAVG_EMODE, "%s: cols must be 32, 64, 128 or 256 (+1000: double-buffered)", what);
   }
 }

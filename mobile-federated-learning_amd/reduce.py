@@ -270,7 +270,7 @@ def reduce_with_sqdist(clients: torch.Tensor, weights: torch.Tensor, P: Optional
     squares in one pass over fp32 rows: returns ``(out, sumsq)`` with ``out``
     the bits of ``reduce_packed(clients, weights, P)`` and ``sumsq`` [K]
     float64 device sums as ``client_sqdist(clients, out, P)`` forms them.
-    K <= 512 reads the rows once (fedavg_reduce_sqdist_f32); larger K runs
+    K <= 1024 reads the rows once (fedavg_reduce_sqdist_f32); larger K runs
     the two passes inside the same call."""
     K, ld, P, dtype, out = _check_packed(clients, weights, P, out)
     if dtype != torch.float32:

@@ -68,9 +68,9 @@ def test_fused_many_clients_vs_oracle(K, P):
     assert rel < 1e-12, rel
 
 
-@pytest.mark.parametrize("K,P", [(513, 5003), (1300, 2001)])
+@pytest.mark.parametrize("K,P", [(1025, 5003), (1300, 2001)])
 def test_fused_large_k_takes_two_passes(K, P):
-    """K > 512: the same entry runs the two production passes; same bits."""
+    """K > 1024: the same entry runs the two production passes; same bits."""
     x, ld, weights = _rows(K, P, K + P)
     w = mfl_amd.weights_tensor(weights, torch.float32, DEV)
     out, sumsq = mfl_amd.reduce_with_sqdist(x, w, P)
@@ -78,12 +78,13 @@ def test_fused_large_k_takes_two_passes(K, P):
     assert torch.equal(sumsq, mfl_amd.client_sqdist(x, out, P))
 
 
-@pytest.mark.parametrize("K", [16, 17, 32, 33, 64, 65, 128, 129, 192, 193, 320, 321, 512])
+@pytest.mark.parametrize("K", [16, 17, 32, 33, 64, 65, 128, 129, 192, 193, 320, 321, 368, 369, 512, 513, 1024])
 def test_fused_plan_boundaries_bit_exact(K):
     """Both sides of every switch of fused_plan (register-staged 256 / 128
     columns, LDS-DMA 128 / 64, register-staged 64 / 32 columns with 16 / 10 /
-    16 slots): the reduce's bits, sums within 1e-12 of the two-pass sums, on
-    a ragged P (NaN padding) and a P that leaves some workgroups no tile."""
+    16 slots, split-row windows of up to 8 / 16 waves): the reduce's bits,
+    sums within 1e-12 of the two-pass sums, on a ragged P (NaN padding) and a
+    P that leaves some workgroups no tile."""
     for P in (64 * 1000 + 3, 12_345):
         x, ld, weights = _rows(K, P, K * 31 + P)
         w = mfl_amd.weights_tensor(weights, torch.float32, DEV)
@@ -191,11 +192,11 @@ def _host_round(K, shapes, seed):
     return w_locals
 
 
-@pytest.mark.parametrize("K", [1, 9, 100, 128, 300, 512, 513])
+@pytest.mark.parametrize("K", [1, 9, 100, 128, 300, 512, 513, 1025])
 def test_dropin_distances_from_the_fused_pass(K):
     """aggregate (host state_dicts) leaves the fused :291 sums; client_distances
     returns the reference's norms (torch.norm of the fp32 differences) from
-    them -- client 0 (aliased to w_glob, :449) gets 0.  K = 513 takes the
+    them -- client 0 (aliased to w_glob, :449) gets 0.  K = 1025 takes the
     two-pass route and gives the same norms."""
     import copy
 
@@ -207,7 +208,7 @@ def test_dropin_distances_from_the_fused_pass(K):
     agg.SMALL_ROUND_BYTES = 0  # the pipelined host path even for a few clients (small rounds: one native call)
     w_glob = agg.aggregate(w_locals)
     fused = agg._last.get("sumsq", {})
-    assert (torch.float32 in fused) == (K <= 512)
+    assert (torch.float32 in fused) == (K <= 1024)
     norms = agg.client_distances(w_locals, w_glob)
     keys = list(shapes)
     exp = []

@@ -20,6 +20,7 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
 INSTANCES = [(16, 4), (32, 4), (48, 4), (64, 2), (80, 2), (100, 2), (128, 1)]
 KIND_WIN = 3
+KIND_WINN = 4
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -120,6 +121,61 @@ def test_window_negative_zero_and_nonfinite(kmax, vec):
     assert torch.equal(torch.isnan(s), torch.isnan(ref))
 
 
+@pytest.mark.parametrize("K", [369, 400, 448, 512, 513, 640, 1024])
+def test_split_windows_vs_oracle(K):
+    """369-1024 clients take the split-row windows (ceil(K / 64) waves per
+    64-column window, the chain handed from wave to wave): the average bit for
+    bit against the oracle and the row reduce, the sums within 1e-12 of plain
+    torch in fp64, deterministic -- one window, a ragged last window, more
+    windows than workgroups."""
+    lib = mfl_amd._lib.load_probe()
+    for P in (1, 3, 64 + 5, 50_003):
+        plan = lib.fedavg_fused_plan_of(K, P)
+        assert plan // 1000000 == KIND_WINN and plan % 100 == (8 if K <= 512 else 16), plan
+        x, ld, weights = _rows(K, P, K * 13 + P)
+        w = mfl_amd.weights_tensor(weights, torch.float32, DEV)
+        out, s = mfl_amd.reduce_with_sqdist(x, w, P)
+        exp = O.reduce_f32(x[:, :P].cpu().numpy(), np.array([np.float32(v) for v in weights], dtype=np.float32))
+        assert out.cpu().numpy().tobytes() == exp.tobytes(), (K, P)
+        assert torch.equal(out.view(torch.int32), mfl_amd.reduce_packed(x, w, P).view(torch.int32))
+        ref = _sumsq_ref(x, out, P)
+        rel = ((s - ref).abs() / ref.clamp_min(1e-300)).max().item()
+        assert rel < 1e-12, (K, P, rel)
+        _, again = mfl_amd.reduce_with_sqdist(x, w, P)
+        assert torch.equal(s, again)
+
+
+def test_split_windows_cfg4_shard_and_nonfinite():
+    """cfg4's per-rank shape at N = 8 (500 x 1.4M): sampled windows against
+    the oracle, sums against torch fp64; then -0.0 and inf / NaN through the
+    split windows as through the one-wave windows."""
+    K, P = 500, 1_403_477
+    x, ld, weights = _rows(K, P, 4)
+    w = mfl_amd.weights_tensor(weights, torch.float32, DEV)
+    out, s = mfl_amd.reduce_with_sqdist(x, w, P)
+    _oracle_windows(x, out, weights, P, seed=4)
+    ref = _sumsq_torch64(x, out, P)
+    assert ((s - ref).abs() / ref).max().item() < 1e-12
+    del x
+    K, P = 400, 64 * 3 + 1
+    x, ld, weights = _rows(K, P, 5)
+    x[:, :P] = -0.0
+    w = mfl_amd.weights_tensor(weights, torch.float32, DEV)
+    out, s = mfl_amd.reduce_with_sqdist(x, w, P)
+    assert torch.all(out.view(torch.int32) == torch.tensor(-0.0).view(torch.int32).item())
+    assert torch.all(s == 0)
+    x, ld, weights = _rows(K, P, 6)
+    x[1, 17] = float("inf")
+    x[300, P - 1] = float("nan")
+    w = mfl_amd.weights_tensor(weights, torch.float32, DEV)
+    out, s = mfl_amd.reduce_with_sqdist(x, w, P)
+    exp = O.reduce_f32(x[:, :P].cpu().numpy(), np.array([np.float32(v) for v in weights], dtype=np.float32))
+    got = out.cpu().numpy()
+    assert np.array_equal(np.isnan(got), np.isnan(exp))
+    assert np.array_equal(got[~np.isnan(got)], exp[~np.isnan(exp)])
+    assert torch.equal(torch.isnan(s), torch.isnan(_sumsq_ref(x, out, P)))
+
+
 def _oracle_windows(x, out, weights, P, n=6, width=2053, seed=0):
     """Sampled column windows of the fused output, bit for bit against the
     oracle (fedavg_trainer.py:450-457 restated) on host copies of the same
@@ -201,7 +257,13 @@ def test_window_plan_short_rows_and_other_k():
     assert lib.fedavg_fused_plan_of(100, 25_000_000) == KIND_WIN * 1000000 + 100 * 100 + 2
     for K in (1, 16, 129, 300, 512):
         assert lib.fedavg_fused_plan_of(K, 25_000_000) // 1000000 != KIND_WIN
-    assert lib.fedavg_fused_plan_of(513, 25_000_000) == 0
+    # split-row windows from 369 rows: up to 8 waves per group to 512, 16 to 1024; then two passes
+    assert lib.fedavg_fused_plan_of(368, 25_000_000) // 1000000 == 2
+    assert lib.fedavg_fused_plan_of(369, 25_000_000) == KIND_WINN * 1000000 + 64 * 100 + 8
+    assert lib.fedavg_fused_plan_of(512, 25_000_000) == KIND_WINN * 1000000 + 64 * 100 + 8
+    assert lib.fedavg_fused_plan_of(513, 25_000_000) == KIND_WINN * 1000000 + 64 * 100 + 16
+    assert lib.fedavg_fused_plan_of(1024, 1_000) == KIND_WINN * 1000000 + 64 * 100 + 16
+    assert lib.fedavg_fused_plan_of(1025, 25_000_000) == 0
     # the LDS-DMA tiles' weak band (65-96 rows) keeps the windows down to 400K columns
     assert lib.fedavg_fused_plan_of(70, 600_000) == KIND_WIN * 1000000 + 80 * 100 + 2
     assert lib.fedavg_fused_plan_of(90, 400_000) == KIND_WIN * 1000000 + 100 * 100 + 2

@@ -383,15 +383,15 @@ def test_client_arena_layout_is_detected_on_host_pointers():
 
 def test_fused_distance_eligibility(monkeypatch):
     """Which row reductions also form the :291 sums (fedavg_reduce_sqdist_f32):
-    16-B aligned fp32 rows of 1..512 clients, with FEDAVG_FUSE_DISTANCES on
+    16-B aligned fp32 rows of 1..1024 clients, with FEDAVG_FUSE_DISTANCES on
     (the default)."""
     import sys
 
     A = sys.modules[mfl_amd.DeviceAggregator.__module__]
-    assert A.FUSE_DISTANCES and A.FUSED_MAX_K == 512 and A.FUSED_SEGMENTS_MAX_K == 256
+    assert A.FUSE_DISTANCES and A.FUSED_MAX_K == 1024 and A.FUSED_SEGMENTS_MAX_K == 256
     assert A.fuse_eligible(torch.empty((1, 64)))
-    assert A.fuse_eligible(torch.empty((512, 64)))
-    assert not A.fuse_eligible(torch.empty((513, 64)))
+    assert A.fuse_eligible(torch.empty((1024, 64)))
+    assert not A.fuse_eligible(torch.empty((1025, 64)))
     rows = torch.empty((10, 72))
     assert A.fuse_eligible(rows[:, :64]) and not A.fuse_eligible(rows[:, 1:65])  # unaligned start
     assert not A.fuse_eligible(torch.empty((10, 66))[:, :64])  # row stride 66 floats
