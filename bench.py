@@ -566,9 +566,11 @@ def _rehearsal_reduce(clients, weights, P, out):
     out[:P].copy_(acc)
 
 
-def timed_steps(step, n: int, dev, use_pg: bool) -> float:
+def timed_steps(step, n: int, dev, use_pg: bool, region=None) -> float:
     """``n`` steps bracketed by barrier + synchronize on both sides; the
-    MAX over ranks of the wall time (seconds)."""
+    MAX over ranks of the wall time (seconds).  ``region`` (optional): a
+    (start, stop) event pair recorded on the current stream right after the
+    opening synchronize and right after the last step's launches."""
     import torch
     import torch.distributed as dist
 
@@ -577,8 +579,12 @@ def timed_steps(step, n: int, dev, use_pg: bool) -> float:
         dist.barrier()
     _sync(dev)
     t0 = time.perf_counter()
+    if region is not None:
+        region[0].record()
     for _ in range(n):
         step()
+    if region is not None:
+        region[1].record()
     _sync(dev)
     if use_pg:
         dist.barrier()
@@ -756,14 +762,18 @@ def main(argv=None):
     launches_per_call = sched["launches"] if sched else 1
     ev_pairs = []
 
-    # Kernel timing, per reduce pass (one ShardedReducer.step), checked
-    # against rocprofv3's kernel trace (scripts/launch_timing_probe.py,
-    # profiles/r05/launch_timing/ and r05/g3-g4):
-    # * one call per pass (N = 1): events attached to the call's own launches
-    #   (fedavg_reduce_f32_timed / hipExtLaunchKernel: the first launch's
-    #   start, the last one's end) -- 704.2 vs rocprofv3's 702.9 us per
-    #   launch at the target.  A hipEventRecord marker before such a launch
-    #   cost ~20 us of step time per marker (r05/g3: 0.727 ms per launch).
+    # Kernel timing, checked against rocprofv3's kernel trace
+    # (scripts/launch_timing_probe.py, profiles/r05/launch_timing/ and
+    # r05/g3-g4):
+    # * one call per pass (N = 1): ONE event pair on the launch stream around
+    #   the whole timed region, divided by its launches -- per-launch kernel
+    #   time including the back-to-back launch boundaries (~1.7 us each).
+    #   Events attached to every launch (fedavg_reduce_f32_timed,
+    #   hipExtLaunchKernel: round 5's first form, 704.2 vs rocprofv3's 702.9
+    #   us) cost ~4.7 us of GPU time per launch (scripts/step_host_probe.py:
+    #   FEMNIST x 10 12.2 vs 7.5 us per call), i.e. ~10 us of every target
+    #   step and half of a cache-resident model's; a hipEventRecord marker
+    #   before each launch cost ~20 us of step time (r05/g3).
     # * chunked passes (the per-rank kernel of an N-GPU plan, ~46-90 us per
     #   chunk): a hipEventRecord pair on the launch stream around the pass's
     #   chunk launches, which run back to back there (the all-gathers are
@@ -783,17 +793,13 @@ def main(argv=None):
             b.record()
     _sync(dev)
     timing_on = [False]
-    attached = red.plan.chunks == 1 and tuned is None
+    whole = red.plan.chunks == 1 and tuned is None and not rehearsal  # one pair around the timed region
 
-    def timing(c):  # one call per pass: events attached to its launches
-        if not timing_on[0] or rehearsal or not attached:
-            return None
-        pair = pool[len(ev_pairs)]
-        ev_pairs.append(pair)
-        return pair
+    def timing(c):  # per-launch attached events: not used in the timed region (their cost, above)
+        return None
 
     def span():  # chunked passes (and tuning variants): a hipEventRecord pair around the chunk launches
-        if not timing_on[0] or rehearsal or attached:
+        if not timing_on[0] or rehearsal or whole:
             return None
         pair = pool[len(ev_pairs)]
         ev_pairs.append(pair)
@@ -853,10 +859,16 @@ def main(argv=None):
         torch.cuda.synchronize()
         ev_pairs.clear()
         calls_per_event = red.plan.chunks * passes
+        region = None
     else:
         timing_on[0] = True
         calls_per_event = red.plan.chunks  # one span per reduce pass: its chunk calls
-    elapsed_max = timed_steps(step, args.steps, dev, use_pg)
+        region = None
+        if whole:
+            region = pool[0]
+            ev_pairs.append(region)
+            calls_per_event = args.steps * passes  # every reduce call of the timed region
+    elapsed_max = timed_steps(step, args.steps, dev, use_pg, region=region)
     timing_on[0] = False
 
     kernel_ms = [s.elapsed_time(e) / calls_per_event for s, e in ev_pairs]
@@ -891,9 +903,10 @@ def main(argv=None):
         value = bytes_step * args.steps / elapsed_max / 1e9
         roofline = None
         if not rehearsal:
-            timing_desc = ("launch-attached HIP events (hipExtLaunchKernel) on the launch stream around every "
-                           "reduce call of the timed region (its first launch's start to its last launch's end)"
-                           if attached else
+            timing_desc = ("one HIP event pair on the launch stream around the whole timed region (recorded "
+                           "after the opening barrier + synchronize and after the last step's launches), divided "
+                           "by the region's reduce launches: kernel time incl. the back-to-back launch boundaries"
+                           if whole else
                            "hipEventRecord pair on the launch stream around each reduce pass's back-to-back chunk "
                            "launches, every pass of the timed region, span / chunks")
             roofline = roofline_entry(args, K, S, kernel_ms_max, launches_per_call, sched, tuned, timing_desc,
@@ -999,8 +1012,8 @@ def main(argv=None):
 
 def roofline_entry(args, K, S, kernel_ms_max, launches_per_call, sched, tuned, timing_desc, launches, world):
     """The dominant kernel's algorithmic bytes per launch over its average
-    launch time (launch-attached HIP events), with the PMC traffic of the
-    same launch shape when profiles/ holds it."""
+    launch time (HIP events on the launch stream, ``timing_desc``), with the
+    PMC traffic of the same launch shape when profiles/ holds it."""
     bytes_call = algorithmic_bytes(K, S)
     achieved = bytes_call / (kernel_ms_max * 1e-3) / 1e9
     if sched:
