@@ -70,6 +70,10 @@ WORKLOADS = {
     "rehearsal_small": (8, 200_003, "CPU rehearsal of the multi-rank machinery (8 x 200,003; --cpu-rehearsal)"),
 }
 
+# chunked passes: every SPAN_EVERY-th pass of the timed region is bracketed by
+# an event pair for the per-launch kernel time (the markers' own cost, above)
+SPAN_EVERY = 8
+
 # One rank's client rows may take this much HBM (MI355X: 288 GB); a larger
 # single-GPU workload (cfg5 at N = 1: 400 GB) runs as P-chunked passes over
 # one resident buffer ("each pass device-resident; time = sum").
@@ -626,6 +630,8 @@ def main(argv=None):
     ap.add_argument("--traffic-json", default="", help="PMC traffic summary (profiles/*.json) to attach")
     ap.add_argument("--host-out", action="store_true",
                     help="host consumer (SURVEY 8e): D2H each rank's shard into pinned host memory, no collective")
+    ap.add_argument("--no-kernel-timing", action="store_true",
+                    help="diagnostic: no HIP events in the timed region (no roofline): the events' own cost on the step")
     ap.add_argument("--shard-of", type=int, default=0,
                     help="N=1 only: reduce rank 0's shard of an N-GPU strong-scaled plan (its chunks, no exchange) "
                          "-- the per-rank kernel at the N-GPU geometry, measured on one GPU")
@@ -798,8 +804,19 @@ def main(argv=None):
     def timing(c):  # per-launch attached events: not used in the timed region (their cost, above)
         return None
 
-    def span():  # chunked passes (and tuning variants): a hipEventRecord pair around the chunk launches
-        if not timing_on[0] or rehearsal or whole:
+    # chunked passes (and tuning variants): a hipEventRecord pair around the
+    # chunk launches of every SPAN_EVERY-th pass (the last one when fewer):
+    # a marked pass costs ~8 us of step at the N = 8 rank shape (0.190 vs
+    # 0.182 ms, profiles/r05/span_cost/), so the timed region carries few
+    n_passes = args.steps * passes
+    span_seen = [0]
+
+    def span():
+        if not timing_on[0] or rehearsal or whole or args.no_kernel_timing:
+            return None
+        i = span_seen[0]
+        span_seen[0] += 1
+        if i % SPAN_EVERY != SPAN_EVERY - 1 and not (i == n_passes - 1 and not ev_pairs):
             return None
         pair = pool[len(ev_pairs)]
         ev_pairs.append(pair)
@@ -864,7 +881,7 @@ def main(argv=None):
         timing_on[0] = True
         calls_per_event = red.plan.chunks  # one span per reduce pass: its chunk calls
         region = None
-        if whole:
+        if whole and not args.no_kernel_timing:
             region = pool[0]
             ev_pairs.append(region)
             calls_per_event = args.steps * passes  # every reduce call of the timed region
@@ -902,13 +919,14 @@ def main(argv=None):
         bytes_step = algorithmic_bytes(K, P_done)
         value = bytes_step * args.steps / elapsed_max / 1e9
         roofline = None
-        if not rehearsal:
+        if not rehearsal and not args.no_kernel_timing:
             timing_desc = ("one HIP event pair on the launch stream around the whole timed region (recorded "
                            "after the opening barrier + synchronize and after the last step's launches), divided "
                            "by the region's reduce launches: kernel time incl. the back-to-back launch boundaries"
                            if whole else
-                           "hipEventRecord pair on the launch stream around each reduce pass's back-to-back chunk "
-                           "launches, every pass of the timed region, span / chunks")
+                           f"hipEventRecord pair on the launch stream around a reduce pass's back-to-back chunk "
+                           f"launches, every {SPAN_EVERY}th pass of the timed region ({len(ev_pairs)} of "
+                           f"{args.steps * passes}), span / chunks")
             roofline = roofline_entry(args, K, S, kernel_ms_max, launches_per_call, sched, tuned, timing_desc,
                                       len(kernel_ms) * calls_per_event * launches_per_call, world)
         if red.gather:
