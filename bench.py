@@ -799,7 +799,10 @@ def main(argv=None):
             b.record()
     _sync(dev)
     timing_on = [False]
-    whole = red.plan.chunks == 1 and tuned is None and not rehearsal  # one pair around the timed region
+    # one pair around the timed region: only where the region holds nothing but the reduce launches
+    # (no exchange, no D2H) -- otherwise the sampled per-pass spans below
+    whole = (red.plan.chunks == 1 and tuned is None and not rehearsal and world == 1 and not red.gather
+             and host_out is None)
 
     def timing(c):  # per-launch attached events: not used in the timed region (their cost, above)
         return None
