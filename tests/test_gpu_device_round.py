@@ -130,7 +130,7 @@ def _exact_sums(dicts, g, glob):
     return np.array(sums)
 
 
-@pytest.mark.parametrize("K", [1, 5, 40, 100, 130])
+@pytest.mark.parametrize("K", [1, 5, 16, 17, 40, 64, 65, 100, 128, 129, 130, 256])
 def test_device_round_fused_bit_exact(K):
     counts, dicts = _clients(K, _SPECS, seed=K)
     r = _Round(counts, dicts, extra_cols=3)
@@ -156,12 +156,13 @@ def test_device_round_misaligned_source_reduces_only():
     assert bool((sumsq == -1.0).all())
 
 
-def test_device_round_many_clients_reduce_only():
-    counts, dicts = _clients(300, [((300,), torch.float32), ((), torch.int64)], seed=9)
+@pytest.mark.parametrize("K", [257, 300])
+def test_device_round_many_clients_reduce_only(K):
+    counts, dicts = _clients(K, [((300,), torch.float32), ((), torch.int64)], seed=9)
     r = _Round(counts, dicts)
     rc, out, sumsq = r.run()
     assert rc == 1
-    assert_bits(out.cpu(), _expected(counts, dicts, r.g), "K=300 device round")
+    assert_bits(out.cpu(), _expected(counts, dicts, r.g), f"K={K} device round")
 
 
 def test_device_round_long_model_windows():
