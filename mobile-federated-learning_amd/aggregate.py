@@ -165,7 +165,9 @@ def column_chunks(P: int) -> List[Tuple[int, int]]:
 # :289-291), so the drop-in fuses by default; FEDAVG_FUSE_DISTANCES=0 keeps
 # the reduce alone.
 FUSED_MAX_K = 1024  # rows kernels (fedavg_reduce_sqdist_f32's fused_plan; more clients: the two passes)
-FUSED_SEGMENTS_MAX_K = 256  # device-resident clients' own tensors (fedavg_reduce_sqdist_segments_f32)
+# device-resident clients' own tensors (fedavg_device_round_f32): LDS-DMA tiles to 256
+# clients, split-row windows to 1024 (round 5)
+FUSED_SEGMENTS_MAX_K = 1024
 FUSE_DISTANCES = os.environ.get("FEDAVG_FUSE_DISTANCES", "1") != "0"
 
 
@@ -515,7 +517,7 @@ class DeviceAggregator:
         """The fp32 group of a device-resident round from the clients' own
         tensors in ONE native call (fedavg_device_round_f32): the walk's
         address table, the reference's weights and the key table go in; the
-        averaged group and -- fused by default (K <= 256, 16-B aligned fp32
+        averaged group and -- fused by default (K <= 1024, 16-B aligned fp32
         sources) -- the round's :291 sums come out.  Integer keys of a fused
         round are converted into a device scratch first (held here until the
         launches that read it are issued: freed earlier, the caching allocator

@@ -954,6 +954,181 @@ __global__ __launch_bounds__(64 * NW, MINW) void reduce_sqdist_segwin_kernel(
   }
 }
 
+// Zero-copy split-row windows (round 5): fedavg_dist.hip's
+// reduce_sqdist_winn_kernel on the key / pointer tables, for 257-1024
+// device-resident clients (the tiles stop at 256).  A workgroup of ns =
+// ceil(K / 64) waves owns a window of 64 columns of one key; wave h holds
+// clients 64h .. 64h + 63 in registers, one dword per lane.  The chain runs
+// wave by wave in client order, handed over LDS; the last wave stores the
+// average, then every wave squares its rows against it and reloads them from
+// the next window (its 64 client addresses: one vector load per wave, read
+// per row with v_readlane, as the pointer form of the one-wave windows).  A
+// key's ragged last window loads element by element through descriptors
+// ranged to the key.  fp32 keys only (integer keys arrive as fp32 scratch).
+// ---------------------------------------------------------------------------
+template <int NSMAX>
+__global__ __launch_bounds__(64 * NSMAX, win_min_waves(64, 1)) void reduce_sqdist_segwinn_kernel(
+    const SegKey* __restrict__ keys, const int64_t* __restrict__ ptrs, int64_t n_keys, int64_t units, int K,
+    const float* __restrict__ W, float* __restrict__ out, double* __restrict__ partials) {
+  constexpr int KH = 64, WC = 64, NB = 8;
+  const int lane = threadIdx.x & 63;
+  const int h = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int ns = __builtin_amdgcn_readfirstlane(static_cast<int>(blockDim.x >> 6));
+  const int r0 = h * KH;
+  const int G = static_cast<int>(gridDim.x);
+  const uint32_t voff = static_cast<uint32_t>(lane) * 4;
+  const bool upper = (lane & 8) != 0;
+  __shared__ __attribute__((aligned(16))) float wl[NSMAX][KH];
+  __shared__ double accl[NSMAX][NB][64];
+  __shared__ float xa[64];
+  for (int i = threadIdx.x; i < ns * KH; i += blockDim.x) wl[i / KH][i % KH] = i < K ? W[i] : -0.0f;
+  double* acc = &accl[h][0][lane];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) acc[64 * b] = 0.0;
+  __syncthreads();
+
+  float x[KH];
+  int64_t pv = 0;  // lane l: client r0 + l's address of the window's key
+  const auto load_ptrs = [&](const int64_t* P) __attribute__((always_inline)) {
+    const gptr<int64_t> q = to_global<int64_t>(P);
+    pv = r0 + lane < K ? q[r0 + lane] : 0;
+  };
+  const auto ptr_of = [&](int i) __attribute__((always_inline)) {
+    int li = i;
+    asm volatile("" : "+s"(li));
+    const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(pv), li);
+    const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(static_cast<uint64_t>(pv) >> 32), li);
+    return reinterpret_cast<const float*>((static_cast<uint64_t>(hi) << 32) | lo);
+  };
+  // a full window: the client's address as the base, the window's start in
+  // soffset, the window's end byte as the record count (0: client >= K)
+  const auto load_fast = [&](int i, uint32_t soff, uint32_t nrec, int Kw) __attribute__((always_inline)) {
+    x[i] = __builtin_bit_cast(
+        float, __builtin_amdgcn_raw_buffer_load_b32(
+                   __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(ptr_of(i)), 0,
+                                                     r0 + i < Kw ? static_cast<int>(nrec) : 0, 0x00020000),
+                   static_cast<int>(voff), static_cast<int>(soff), 2));
+  };
+  // a key's ragged last window: the descriptor's range is the client's part of it
+  const auto load_slow = [&](int64_t c0, int n, int Kw) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < KH; ++i) {
+      const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(ptr_of(i) + c0), 0,
+                                                                         r0 + i < Kw ? n * 4 : 0, 0x00020000);
+      x[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, static_cast<int>(voff), 0, 2));
+    }
+  };
+  const int units32 = static_cast<int>(units), nkeys32 = static_cast<int>(n_keys);
+  const auto cols_of = [&](int64_t numel, int w) __attribute__((always_inline)) {
+    const int64_t left = numel - static_cast<int64_t>(w) * WC;
+    return (left >> 31) != 0 ? WC : (static_cast<int>(left) < WC ? static_cast<int>(left) : WC);
+  };
+  int u = static_cast<int>(blockIdx.x), j = 0, n = 0;
+  int64_t c0 = 0;
+  if (u < units32) {
+    j = __builtin_amdgcn_readfirstlane(static_cast<int>(find_key(keys, n_keys, u)));
+    const SegKey key = keys[j];
+    const int w = u - static_cast<int>(key.unit_start);
+    c0 = static_cast<int64_t>(w) * WC;
+    n = cols_of(key.numel, w);
+    load_ptrs(ptrs + static_cast<int64_t>(j) * K);
+    if (n == WC) {
+#pragma unroll
+      for (int i = 0; i < KH; ++i) load_fast(i, static_cast<uint32_t>(c0 * 4), static_cast<uint32_t>((c0 + WC) * 4), K);
+    } else {
+      load_slow(c0, n, K);
+    }
+  }
+  for (; u < units32; u += G) {
+    const int64_t out_off = keys[j].out_offset;
+    const int un = u + G;
+    int jn = j, nn = 0;
+    int64_t c0n = 0;
+    if (un < units32) {
+      while (jn + 1 < nkeys32 && static_cast<int>(keys[jn + 1].unit_start) <= un) ++jn;
+      const SegKey kn = keys[jn];
+      const int w = un - static_cast<int>(kn.unit_start);
+      c0n = static_cast<int64_t>(w) * WC;
+      nn = cols_of(kn.numel, w);
+    }
+    const bool fastn = un < units32 && nn == WC;
+    const uint32_t soffn = static_cast<uint32_t>(c0n * 4), nrecn = static_cast<uint32_t>((c0n + WC) * 4);
+    int Kwn = fastn ? K : 0;
+    asm volatile("" : "+s"(Kwn));
+    if (un < units32) load_ptrs(ptrs + static_cast<int64_t>(jn) * K);  // this window's rows are loaded
+    float a = 0.f;
+    for (int st = 0; st < ns; ++st) {  // the chain, wave by wave in client order
+      if (h == st) {
+        int wo = h * KH;
+        asm volatile("" : "+v"(wo));
+        const float* wp = &wl[0][0] + wo;
+        if (st > 0) a = xa[lane];
+#pragma unroll
+        for (int q = 0; q < KH / 4; ++q) {
+          const f32x4 w4 = *reinterpret_cast<const f32x4*>(wp + 4 * q);
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            const int i = 4 * q + jj;
+            if (st == 0 && i == 0) {
+              a = x[0] * w4[0];
+            } else {
+              const float t = x[i] * w4[jj];
+              a = a + t;
+            }
+          }
+        }
+        xa[lane] = a;
+        if (st == ns - 1 && lane < n) out[out_off + c0 + lane] = a;
+      }
+      __syncthreads();
+    }
+    if (h != ns - 1) a = xa[lane];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      double p[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int i = 8 * b + r;
+        const double d = static_cast<double>(x[i] - a);  // fp32 difference, as the reference forms it
+        p[r] = d * d;
+        load_fast(i, soffn, nrecn, Kwn);
+      }
+      const double q01 = fold32(p[0], p[1]), q23 = fold32(p[2], p[3]);
+      const double q45 = fold32(p[4], p[5]), q67 = fold32(p[6], p[7]);
+      acc[64 * b] += fold8(fold16(q01, q23), fold16(q45, q67), upper);
+    }
+    if (un < units32 && !fastn) {
+      int Ks = K;
+      asm volatile("" : "+s"(Ks));
+      load_slow(c0n, nn, Ks);
+    }
+    __syncthreads();  // every wave has read xa before the next window's chain rewrites it
+    j = jn;
+    c0 = c0n;
+    n = nn;
+  }
+  const int row_in = win_batch_row(lane);
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    double sm = acc[64 * b];
+    sm += dpp_move_f64<0xB1, 0xF>(sm);
+    sm += dpp_move_f64<0x4E, 0xF>(sm);
+    sm += dpp_move_f64<0x141, 0xF>(sm);
+    const int row = 8 * b + row_in;
+    if ((lane & 7) == 0 && r0 + row < K) partials[static_cast<int64_t>(r0 + row) * G + blockIdx.x] = sm;
+  }
+}
+
+constexpr int64_t kSegSplitMaxK = 1024;  // the split-row windows' reach (16 waves of 64 clients)
+
+// workgroups of the split-row window launch over `units` windows (0: not resident)
+inline int64_t segwinn_blocks(int64_t K, int64_t units) {
+  const int ns = static_cast<int>((K + 63) / 64);
+  const int64_t res = ns <= 8 ? resident_blocks(reduce_sqdist_segwinn_kernel<8>, 64 * ns)
+                              : resident_blocks(reduce_sqdist_segwinn_kernel<16>, 64 * ns);
+  return units < res ? units : res;
+}
+
 // windows per wave below which the LDS-DMA tiles keep the round
 // (kSegWinMinPerWave; FEDAVG_SEGWIN_MIN_PER_WAVE overrides it for probes)
 inline int64_t segwin_min_per_wave() {
@@ -1153,8 +1328,26 @@ struct SegFusedPlan {
   int64_t span, waves;
 };
 
+// 257-1024 clients fuse only on the split-row windows: 32-bit buffer offsets
+// per key, window indices in 32 bits
+inline bool seg_split_ok(const int64_t* numel, int64_t n_keys) {
+  if (!numel || n_keys <= 0 || n_keys >= (int64_t(1) << 31)) return false;
+  for (int64_t j = 0; j < n_keys; ++j)
+    if (numel[j] < 0 || numel[j] >= (int64_t(1) << 30)) return false;
+  return units_of(numel, n_keys, 64) < (int64_t(1) << 31);
+}
+
 SegFusedPlan seg_fused_plan(const int64_t* numel, int64_t n_keys, int64_t K, bool all_raw) {
   SegFusedPlan p{false, segwin_kmax(K), seg_fused_cols(K), 0};
+  if (K > kSegFusedMaxK) {  // kmax -1: the split-row windows (the caller checked seg_split_ok)
+    if (K <= kSegSplitMaxK && all_raw && seg_split_ok(numel, n_keys)) {
+      p.win = true;
+      p.kmax = -1;
+      p.span = 64;
+      p.waves = segwinn_blocks(K, units_of(numel, n_keys, 64));
+    }
+    return p;
+  }
   // the windows address a key's bytes with 32-bit buffer offsets
   bool small_keys = numel != nullptr;
   for (int64_t j = 0; small_keys && j < n_keys; ++j) small_keys = numel[j] < (int64_t(1) << 30);
@@ -1182,7 +1375,21 @@ int launch_seg_fused(const SegFusedPlan& p, const SegKey* keys, const int64_t* t
   }
   const int k32 = static_cast<int>(K);
   int64_t nparts = 0;
-  if (p.win) {
+  if (p.win && p.kmax < 0) {  // split-row windows: p.waves workgroups of ceil(K / 64) waves
+    if (p.waves <= 0) return set_error(FEDAVG_EMODE, "%s: the split window kernel is not resident", what);
+    if (partial_elems < K * p.waves)
+      return set_error(FEDAVG_EINVAL, "%s: partials need %lld doubles", what, (long long)(K * p.waves));
+    const int ns = static_cast<int>((K + 63) / 64);
+    if (ns <= 8)
+      hipLaunchKernelGGL((reduce_sqdist_segwinn_kernel<8>), dim3(static_cast<unsigned>(p.waves)),
+                         dim3(static_cast<unsigned>(64 * ns)), 0, s, keys, tptrs, n_keys, units, k32, weights, out,
+                         partials);
+    else
+      hipLaunchKernelGGL((reduce_sqdist_segwinn_kernel<16>), dim3(static_cast<unsigned>(p.waves)),
+                         dim3(static_cast<unsigned>(64 * ns)), 0, s, keys, tptrs, n_keys, units, k32, weights, out,
+                         partials);
+    nparts = p.waves;
+  } else if (p.win) {
     if (partial_elems < K * p.waves)
       return set_error(FEDAVG_EINVAL, "%s: partials need %lld doubles", what, (long long)(K * p.waves));
     const dim3 grid(static_cast<unsigned>(p.waves / 4)), block(256);
@@ -1418,7 +1625,8 @@ int fedavg_client_sqdist_segments_f32(const int64_t* client_ptrs, const int64_t*
 // fedavg_reduce_segments_f32, sumsq as fedavg_client_sqdist_segments_f32 on
 // that out.  partials : fedavg_reduce_sqdist_segments_partials(K) doubles.
 int64_t fedavg_reduce_sqdist_segments_partials(int64_t K) {
-  if (K <= 0 || K > kSegFusedMaxK) return 0;
+  if (K <= 0 || K > kSegSplitMaxK) return 0;
+  if (K > kSegFusedMaxK) return K * segwinn_blocks(K, INT64_MAX / 2);  // the split-row windows (device round)
   const int S = seg_fused_cols(K);
   const int per_cu = S == 32 ? seg_fused_per_cu_max<32>(K)
                      : (S == 64 ? seg_fused_per_cu_max<64>(K)
@@ -1539,7 +1747,7 @@ int fedavg_device_round_f32(const int64_t* client_ptrs, int64_t ptr_ld, const in
   }
   const int64_t ld = ptr_ld;
   if (S >= (int64_t(1) << 31)) return set_error(FEDAVG_EINVAL, "%s: integer keys too large", what);
-  bool fuse = sumsq != nullptr && K <= kSegFusedMaxK;
+  bool fuse = sumsq != nullptr && (K <= kSegFusedMaxK || (K <= kSegSplitMaxK && seg_split_ok(key_numel, n_keys)));
   // a fused round takes its integer keys as fp32 scratch columns: the window
   // kernels read fp32 only, and the tiles' in-kernel conversion (element by
   // element, one tile per key and client block) made resnet56 x 100's fused
@@ -1667,8 +1875,8 @@ int fedavg_device_round_f32(const int64_t* client_ptrs, int64_t ptr_ld, const in
   // padding rows and empty keys get a record count of 0, and KMAX null
   // descriptors follow the last key (the reload target when the next
   // window is not a full one)
-  const int64_t dbytes = plan.win ? seg_desc_bytes(n_keys, plan.kmax) : 0;
-  const bool with_desc = plan.win && dbytes <= kSegDescMaxBytes && !segwin_desc_disabled();
+  const int64_t dbytes = plan.win && plan.kmax > 0 ? seg_desc_bytes(n_keys, plan.kmax) : 0;
+  const bool with_desc = plan.win && plan.kmax > 0 && dbytes <= kSegDescMaxBytes && !segwin_desc_disabled();
   if (with_desc) {
     auto* hd = reinterpret_cast<u32x4*>(hb + moff);
     const int64_t km = plan.kmax;

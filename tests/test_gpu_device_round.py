@@ -90,7 +90,7 @@ class _Round:
     def run(self, sums=True, scratch=True):
         lib, K, n = self.lib, self.K, self.n
         out = torch.full((self.g.P,), float("nan"), device=DEV)
-        partials = torch.empty(max(1, lib.fedavg_reduce_sqdist_segments_partials(max(1, min(K, 256)))),
+        partials = torch.empty(max(1, lib.fedavg_reduce_sqdist_segments_partials(max(1, min(K, 1024)))),
                                dtype=torch.float64, device=DEV)
         sumsq = torch.full((K,), -1.0, dtype=torch.float64, device=DEV) if sums else None
         n_s = lib.fedavg_device_round_scratch(self.numel.ctypes.data, self.kind.ctypes.data, n, K)
@@ -156,7 +156,26 @@ def test_device_round_misaligned_source_reduces_only():
     assert bool((sumsq == -1.0).all())
 
 
-@pytest.mark.parametrize("K", [257, 300])
+@pytest.mark.parametrize("K", [257, 300, 513, 1024])
+def test_device_round_split_windows_bit_exact(K):
+    """257-1024 clients fuse on the zero-copy split-row windows (ceil(K / 64)
+    waves per 64-column window): every key kind of _SPECS (integer and bool
+    keys through the fp32 scratch, an empty key, keys shorter than a window
+    and ragged last windows), the reference's bits and the exact sums."""
+    counts, dicts = _clients(K, _SPECS, seed=K)
+    r = _Round(counts, dicts, extra_cols=2)
+    rc, out, sumsq = r.run()
+    assert rc == 0
+    exp = _expected(counts, dicts, r.g)
+    assert_bits(out.cpu(), exp, f"split-row device round K={K}")
+    got = sumsq.cpu().numpy()
+    ref = _exact_sums(dicts, r.g, exp)
+    assert np.allclose(got, ref, rtol=1e-11, atol=0.0), (got[:4], ref[:4])
+    _, _, again = r.run()
+    assert torch.equal(sumsq, again)  # deterministic
+
+
+@pytest.mark.parametrize("K", [1025])
 def test_device_round_many_clients_reduce_only(K):
     counts, dicts = _clients(K, [((300,), torch.float32), ((), torch.int64)], seed=9)
     r = _Round(counts, dicts)

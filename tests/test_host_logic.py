@@ -388,7 +388,7 @@ def test_fused_distance_eligibility(monkeypatch):
     import sys
 
     A = sys.modules[mfl_amd.DeviceAggregator.__module__]
-    assert A.FUSE_DISTANCES and A.FUSED_MAX_K == 1024 and A.FUSED_SEGMENTS_MAX_K == 256
+    assert A.FUSE_DISTANCES and A.FUSED_MAX_K == 1024 and A.FUSED_SEGMENTS_MAX_K == 1024
     assert A.fuse_eligible(torch.empty((1, 64)))
     assert A.fuse_eligible(torch.empty((1024, 64)))
     assert not A.fuse_eligible(torch.empty((1025, 64)))
