@@ -1467,7 +1467,7 @@ struct IntKey {
 inline int64_t round16(int64_t b) { return (b + 15) & ~int64_t(15); }
 
 struct RoundWs {
-  int64_t ptrs, w, ik, isrc, end;
+  int64_t ptrs, w, ik, isrc, end, desc_room;  // desc_room: the unit map's / descriptor table's reserved bytes
 };
 
 // the tile kernel's unit -> key map is staged for rounds of at most this many
@@ -1500,7 +1500,8 @@ inline RoundWs round_ws(int64_t K, int64_t n_keys) {
   // uses one of them), placed right after whatever part is used
   const int64_t map_bytes = kSegUnitMapMax * static_cast<int64_t>(sizeof(int));
   const int64_t desc = seg_desc_bytes(n_keys) <= kSegDescMaxBytes ? seg_desc_bytes(n_keys) : 0;
-  r.end = round16(r.isrc + n_keys * K * static_cast<int64_t>(sizeof(int64_t))) + (map_bytes > desc ? map_bytes : desc);
+  r.desc_room = map_bytes > desc ? map_bytes : desc;
+  r.end = round16(r.isrc + n_keys * K * static_cast<int64_t>(sizeof(int64_t))) + r.desc_room;
   return r;
 }
 
@@ -1876,7 +1877,10 @@ int fedavg_device_round_f32(const int64_t* client_ptrs, int64_t ptr_ld, const in
   // descriptors follow the last key (the reload target when the next
   // window is not a full one)
   const int64_t dbytes = plan.win && plan.kmax > 0 ? seg_desc_bytes(n_keys, plan.kmax) : 0;
-  const bool with_desc = plan.win && plan.kmax > 0 && dbytes <= kSegDescMaxBytes && !segwin_desc_disabled();
+  // (within the room round_ws reserved: a table of more than 2,047 keys at
+  // KMAX 128 reserves none, and a smaller KMAX's table must not overrun it)
+  const bool with_desc =
+      plan.win && plan.kmax > 0 && dbytes <= kSegDescMaxBytes && dbytes <= L.desc_room && !segwin_desc_disabled();
   if (with_desc) {
     auto* hd = reinterpret_cast<u32x4*>(hb + moff);
     const int64_t km = plan.kmax;

@@ -319,3 +319,20 @@ def test_device_round_resnet56_doubling_property():
     assert rc2 == 0
     assert torch.equal(out2.view(torch.int32), (out * 2.0).view(torch.int32))
     assert torch.equal(sumsq2, sumsq * 4.0)
+
+
+def test_device_round_many_keys_window_plan():
+    """A model of 2,100 keys at 20 clients on the one-wave windows (48-row
+    instance): its descriptor table (2,101 x 48 entries) is larger than the
+    room the workspace reserves when a 128-row table would not fit, so the
+    round takes the pointer form -- same bits, exact sums (round 5 fix: the
+    table was written past the workspace before)."""
+    specs = [((4500,), torch.float32)] * 2100
+    counts, dicts = _clients(20, specs, seed=21)
+    r = _Round(counts, dicts)
+    rc, out, sumsq = r.run()
+    assert rc == 0
+    exp = _expected(counts, dicts, r.g)
+    assert_bits(out.cpu(), exp, "2,100-key device round")
+    ref = _exact_sums(dicts, r.g, exp)
+    assert np.allclose(sumsq.cpu().numpy(), ref, rtol=1e-11, atol=0.0)
