@@ -249,12 +249,13 @@ def _device_round(K, shapes, seed, misalign=False):
 
 
 @pytest.mark.parametrize("K,misalign", [(1, False), (7, False), (100, False), (129, False), (256, False), (12, True),
-                                       (257, False)])
+                                       (257, False), (600, False), (1025, False)])
 def test_device_round_fused_segments(K, misalign):
     """Device-resident clients (separate tensors, an int64 buffer, ragged key
     sizes): the zero-copy round's average keeps the oracle's bits and the
-    fused :291 sums give the reference's norms.  A misaligned client tensor
-    or K > 256 takes the two-pass route with the same results."""
+    fused :291 sums give the reference's norms (tiles to 256 clients, split-row
+    windows to 1024).  A misaligned client tensor or K > 1024 takes the
+    two-pass route with the same results."""
     import copy
 
     shapes = {"conv.weight": (16, 3, 3, 3), "conv.bias": (16,), "bn.num_batches_tracked": (),
@@ -268,7 +269,7 @@ def test_device_round_fused_segments(K, misalign):
         got, exp = w_glob[k].cpu(), ref[k]
         assert got.dtype == exp.dtype, k
         assert torch.equal(got.reshape(-1).view(torch.int32), exp.reshape(-1).view(torch.int32)), k
-    assert (torch.float32 in agg._last.get("sumsq", {})) == (K <= 256 and not misalign)
+    assert (torch.float32 in agg._last.get("sumsq", {})) == (K <= 1024 and not misalign)
     norms = agg.client_distances(w_locals, w_glob)
     keys = list(shapes)
     # :291's fp32 differences (int64 buffers promote to fp32), squared and summed exactly
