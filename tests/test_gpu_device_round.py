@@ -147,12 +147,16 @@ def test_device_round_fused_bit_exact(K):
     assert_bits(out1.cpu(), exp, f"device round reduce-only K={K}")
 
 
-def test_device_round_misaligned_source_reduces_only():
-    counts, dicts = _clients(20, _SPECS, seed=3, misalign_client=7)
+@pytest.mark.parametrize("K", [20, 600])
+def test_device_round_misaligned_source_reduces_only(K):
+    """A 4-B aligned fp32 source (the tiles' LDS-DMA and the split windows'
+    loads need 16 B) sends the round to the reduce alone: same bits, sums
+    untouched (the caller then runs the :291 pass)."""
+    counts, dicts = _clients(K, _SPECS, seed=3, misalign_client=7)
     r = _Round(counts, dicts)
     rc, out, sumsq = r.run()
     assert rc == 1
-    assert_bits(out.cpu(), _expected(counts, dicts, r.g), "misaligned device round")
+    assert_bits(out.cpu(), _expected(counts, dicts, r.g), f"misaligned device round K={K}")
     assert bool((sumsq == -1.0).all())
 
 
