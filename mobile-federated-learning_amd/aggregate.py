@@ -139,8 +139,9 @@ def _trivial(w_locals, model_global=None):
 # chunk c's copy to pinned host memory overlaps the reduce of chunk c+1 (the
 # copy, ~50 GB/s over PCIe, is the slower of the two).  Chunks of >= 2M
 # columns keep every launch a full-chip one; all schedules give the same bits.
-D2H_CHUNK_MIN_COLS = 2 << 20
-D2H_MAX_CHUNKS = 8
+# (FEDAVG_D2H_MAX_CHUNKS / FEDAVG_D2H_CHUNK_MIN_COLS override them for measurements)
+D2H_CHUNK_MIN_COLS = int(os.environ.get("FEDAVG_D2H_CHUNK_MIN_COLS", str(2 << 20)))
+D2H_MAX_CHUNKS = int(os.environ.get("FEDAVG_D2H_MAX_CHUNKS", "8"))
 # D2H engine of fedavg_copy_to_host: 0 = the runtime's DMA copy (production:
 # a streaming round's finish at K=100 x P=25M measured 2.67 ms in steady state
 # vs 3.0-3.1 ms for the 64-workgroup zero-copy kernel),
