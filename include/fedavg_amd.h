@@ -124,9 +124,10 @@ int fedavg_client_sqdist_f32(const float* clients, int64_t K, int64_t P, int64_t
  * Needs 16-B aligned rows and ld % 4 == 0 (FEDAVG_EALIGN otherwise, before
  * any work: fedavg_reduce_f32 alone takes unaligned rows).  K <= 1024 runs
  * a fused kernel: for 17-128 clients on long rows one wave per window of
- * 64 x VEC columns x all K rows in registers; from 369 clients a workgroup
- * of ceil(K / 64) waves per 64-column window, 64 rows per wave, the chain
- * handed from wave to wave in row order; otherwise tiles of K rows x 32-256
+ * 64 x VEC columns x all K rows in registers; from 369 clients (and at
+ * 161-256 and 289-368 clients on long rows) a workgroup of ceil(K / 64)
+ * waves per 64-column window, 64 rows per wave, the chain handed from wave
+ * to wave in row order; otherwise tiles of K rows x 32-256
  * columns staged in LDS per workgroup (by LDS-DMA or through registers);
  * K > 1024 runs the two passes back to back (fedavg_fused_plan_of says
  * which).  workspace : fedavg_reduce_sqdist_workspace(K, P) doubles of
@@ -139,7 +140,8 @@ int64_t fedavg_reduce_sqdist_workspace(int64_t K, int64_t P);
  * `slots` 16-B slots per thread; 3: wave-owned windows of KMAX = S rows and
  * VEC = slots columns per lane (17-128 clients on rows of >= 16 windows per
  * wave); 4: split-row windows of S = 64 rows per wave, at most `slots` waves
- * per workgroup (369-1024 clients). */
+ * per workgroup (369-1024 clients; 161-256 and 289-368 on rows of >= 24
+ * windows per workgroup). */
 int64_t fedavg_fused_plan_of(int64_t K, int64_t P);
 int fedavg_reduce_sqdist_f32(const float* clients, int64_t K, int64_t P, int64_t ld,
                              const float* weights, float* out, double* workspace,

@@ -26,6 +26,7 @@
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <tuple>
@@ -738,6 +739,17 @@ __device__ __forceinline__ double win_sq(typename WinVec<VEC>::T d) {
 // __launch_bounds__'s second argument is waves per SIMD: the window's KMAX x
 // VEC registers (+ a quarter more at VEC 1: one square per row per lane
 // before the folds) and ~40 others within 512 / waves
+// rows of the next window the split-row window kernels prefetch while the
+// chain runs (reduce_sqdist_winn_kernel, reduce_sqdist_segwinn_kernel);
+// FEDAVG_SPLIT_PREFETCH=0 turns it off (A/B)
+inline int split_prefetch_rows() {
+  static const int v = [] {
+    const char* e = std::getenv("FEDAVG_SPLIT_PREFETCH");
+    return e && e[0] == '0' ? 0 : 8;
+  }();
+  return v;
+}
+
 constexpr int win_min_waves(int kmax, int vec) {
   const int regs = kmax * vec + (vec == 1 ? kmax / 4 : 0);
   return regs <= 88 ? 4 : (regs <= 128 ? 3 : (regs <= 216 ? 2 : 1));

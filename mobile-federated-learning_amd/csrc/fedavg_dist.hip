@@ -1147,8 +1147,13 @@ int launch_fused_win(const float* clients, int64_t K, int64_t P, int64_t ld, con
 // against it and reloads them from the next window (as reduce_sqdist_win2).
 // Rows past K load through an empty descriptor (+0) with weight -0.0, which
 // leaves every chain value unchanged.
+// PF > 0: the first PF rows of the next window are loaded into spare
+// registers as the window starts, so HBM has work while the chain runs (at
+// one workgroup per CU nothing else is in flight then: the reloads wait for
+// the squares, the squares for the chain's last wave); after squaring row
+// i < PF the wave takes the prefetched row instead of reloading it.
 // ---------------------------------------------------------------------------
-template <int KH, int VEC, int NSMAX>
+template <int KH, int VEC, int NSMAX, int PF = 0>
 __global__ __launch_bounds__(64 * NSMAX, win_min_waves(KH, VEC)) void reduce_sqdist_winn_kernel(
     const float* __restrict__ X, int K, int64_t ld, int64_t P, int64_t nwin, const float* __restrict__ W,
     float* __restrict__ out, double* __restrict__ partials) {
@@ -1182,6 +1187,7 @@ __global__ __launch_bounds__(64 * NSMAX, win_min_waves(KH, VEC)) void reduce_sqd
   for (int b = 0; b < NB; ++b) acc[64 * b] = 0.0;
   __syncthreads();
   V x[KH];
+  V xp[PF > 0 ? PF : 1];
   {
     int Kw = K;
     asm volatile("" : "+s"(Kw));
@@ -1222,6 +1228,15 @@ __global__ __launch_bounds__(64 * NSMAX, win_min_waves(KH, VEC)) void reduce_sqd
     const int64_t cl = c0 + lane * VEC;
     const int nbn = win_bytes(w + G);
     const char* rp = reinterpret_cast<const char*>(X + (w + G) * WC) + r0 * row_bytes;
+    if constexpr (PF > 0) {
+#pragma unroll
+      for (int i = 0; i < PF; ++i) {
+        asm volatile("" : "+s"(rp));
+        xp[i] = win_load<VEC>(
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(rp), 0, r0 + i < Kw ? nbn : 0, 0x00020000), voff);
+        rp += row_bytes;
+      }
+    }
     const bool ragged = c0 + WC > P;
     if (ragged) {
 #pragma unroll
@@ -1260,10 +1275,14 @@ __global__ __launch_bounds__(64 * NSMAX, win_min_waves(KH, VEC)) void reduce_sqd
         p[j] = 0.0;
         if (i < KH) {
           p[j] = win_sq<VEC>(x[i] - a);
-          asm volatile("" : "+s"(rp));
-          x[i] = win_load<VEC>(
-              __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(rp), 0, r0 + i < Kw ? nbn : 0, 0x00020000), voff);
-          rp += row_bytes;
+          if (i < PF) {
+            x[i] = xp[i < PF ? i : 0];
+          } else {
+            asm volatile("" : "+s"(rp));
+            x[i] = win_load<VEC>(
+                __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(rp), 0, r0 + i < Kw ? nbn : 0, 0x00020000), voff);
+            rp += row_bytes;
+          }
         }
       }
       const double q01 = fold32(p[0], p[1]), q23 = fold32(p[2], p[3]);
@@ -1285,30 +1304,34 @@ __global__ __launch_bounds__(64 * NSMAX, win_min_waves(KH, VEC)) void reduce_sqd
 }
 
 // workgroups of the split window launch: the resident ones (ceil(K / KH)
-// waves each), at most one per window
-template <int KH, int VEC, int NSMAX>
+// waves each) rounded down to a power of two per CU -- 3 workgroups of 5
+// waves on a CU ran 12-15 % slower than 2 (profiles/r05/prefetch/) --, at
+// most one per window
+template <int KH, int VEC, int NSMAX, int PF = 0>
 int64_t fused_winn_grid(int64_t K, int64_t P, int blocks_per_cu) {
   const int ns = static_cast<int>((K + KH - 1) / KH);
-  const int64_t per_cu = blocks_per_cu > 0 ? blocks_per_cu
-                                           : resident_blocks(reduce_sqdist_winn_kernel<KH, VEC, NSMAX>, 64 * ns) /
-                                                 cu_count();
+  int64_t per_cu = blocks_per_cu;
+  if (per_cu <= 0) {
+    const int64_t r = resident_blocks(reduce_sqdist_winn_kernel<KH, VEC, NSMAX, PF>, 64 * ns) / cu_count();
+    for (per_cu = r > 0 ? 1 : 0; per_cu * 2 <= r;) per_cu *= 2;
+  }
   const int64_t nwin = (P + 64 * VEC - 1) / (64 * VEC);
   const int64_t grid = per_cu * cu_count();
   return grid < nwin ? grid : nwin;
 }
 
-template <int KH, int VEC, int NSMAX>
+template <int KH, int VEC, int NSMAX, int PF = 0>
 int launch_fused_winn(const float* clients, int64_t K, int64_t P, int64_t ld, const float* weights, float* out,
                       double* partials, int64_t partial_elems, double* sumsq, int blocks_per_cu, hipStream_t s,
                       const char* what) {
   if (K > NSMAX * KH) return set_error(FEDAVG_EMODE, "%s: this split window kernel covers K <= %d", what, NSMAX * KH);
   const int ns = static_cast<int>((K + KH - 1) / KH);
   const int64_t nwin = (P + 64 * VEC - 1) / (64 * VEC);
-  const int64_t grid = fused_winn_grid<KH, VEC, NSMAX>(K, P, blocks_per_cu);
+  const int64_t grid = fused_winn_grid<KH, VEC, NSMAX, PF>(K, P, blocks_per_cu);
   if (grid <= 0) return set_error(FEDAVG_EMODE, "%s: the split window kernel is not resident", what);
   if (partial_elems < K * grid)
     return set_error(FEDAVG_EINVAL, "%s: workspace needs %lld doubles", what, (long long)(K * grid));
-  hipLaunchKernelGGL((reduce_sqdist_winn_kernel<KH, VEC, NSMAX>), dim3(static_cast<unsigned>(grid)),
+  hipLaunchKernelGGL((reduce_sqdist_winn_kernel<KH, VEC, NSMAX, PF>), dim3(static_cast<unsigned>(grid)),
                      dim3(static_cast<unsigned>(64 * ns)), 0, s, clients, static_cast<int>(K), ld, P, nwin, weights,
                      out, partials);
   int rc = launch_status(what);
@@ -1534,6 +1557,17 @@ constexpr int64_t kFusedRowsMaxK = 1024;
 // workgroup to 512 rows, 16 beyond (640 x 3M 1.77 vs 2.46 for the two
 // passes; 1000 x 12.5M 9.99 vs 15.05; 520 x 5M 2.71 vs 3.34)
 constexpr int64_t kFusedWinnMinK = 369;
+constexpr int kFusedWinnPF = 8;  // rows of the next window prefetched (split_prefetch_rows)
+// With the prefetch the split windows also beat the register-staged tiles at
+// 161-256 and 289-368 rows on long rows (profiles/r05/prefetch/, ms, tiles vs
+// split: 170 x 5M 0.606 vs 0.593; 192 x 5M 0.725 vs 0.661; 240 x 5M 0.897 vs
+// 0.822; 256 x 12M 2.53 vs 2.19; 290 x 5M 1.026 vs 0.998; 310 x 5M 1.092 vs
+// 1.033; 352 x 5M 1.347 vs 1.178; 368 x 5M 1.427 vs 1.228), not at 140 x 5M
+// (0.493 vs 0.529) or 270 x 5M (0.933 vs 0.981), and tie at 200 x 1.2M (18
+// windows per workgroup): below 369 rows they take rounds of >= 24 windows
+// per workgroup, and only with the prefetch on
+constexpr int64_t kFusedWinnLowMinK = 161, kFusedWinnGapMinK = 257, kFusedWinnGapMaxK = 288;
+constexpr int64_t kFusedWinnLowMinPerBlock = 24;
 constexpr int64_t kWinMinPerWave = 16;  // windows per wave below which the tile kernels keep the round
 // ... except in the LDS-DMA tiles' weak band, 65-96 rows, where the windows
 // win down to ~400K columns (profiles/r03/win/short_rows_*.jsonl, ms, tiles
@@ -1584,6 +1618,11 @@ inline FusedPlan fused_plan(int64_t K, int64_t P) {
   if (K <= 48) return {kFusedLds, 256, 0};
   if (K <= 64) return {kFusedLds, 128, 0};
   if (K <= 128) return {kFusedLds, 64, 0};
+  if (K >= kFusedWinnLowMinK && K < kFusedWinnMinK && (K < kFusedWinnGapMinK || K > kFusedWinnGapMaxK) &&
+      split_prefetch_rows() > 0) {
+    const int64_t grid = fused_winn_grid<64, 1, 8, kFusedWinnPF>(K, P, 0);
+    if (grid > 0 && (P + 63) / 64 >= kFusedWinnLowMinPerBlock * grid) return {kFusedWinn, 64, 8};
+  }
   if (K <= 192) return {kFusedRs, 64, 16};
   if (K <= 320) return {kFusedRs, 32, 10};
   if (K < kFusedWinnMinK) return {kFusedRs, 32, 16};
@@ -1905,7 +1944,10 @@ int64_t fedavg_reduce_sqdist_workspace(int64_t K, int64_t P) {
     if (pl.S == 128) fused = K * fused_grid<128>(K, P, 0);
     if (pl.S == 256) fused = K * fused_grid<256>(K, P, 0);
   } else if (pl.kind == kFusedWinn) {
-    fused = K * (pl.slots == 8 ? fused_winn_grid<64, 1, 8>(K, P, 0) : fused_winn_grid<64, 1, 16>(K, P, 0));
+    const bool pf = split_prefetch_rows() > 0;
+    fused = K * (pl.slots == 8 ? (pf ? fused_winn_grid<64, 1, 8, kFusedWinnPF>(K, P, 0) : fused_winn_grid<64, 1, 8>(K, P, 0))
+                               : (pf ? fused_winn_grid<64, 1, 16, kFusedWinnPF>(K, P, 0)
+                                     : fused_winn_grid<64, 1, 16>(K, P, 0)));
   } else if (pl.kind == kFusedRs) {
     switch (pl.S * 100 + pl.slots) {
       case 25608: fused = K * fused_rs_grid<256, 8, 0>(K, P, 0); break;
@@ -1956,9 +1998,16 @@ int fedavg_reduce_sqdist_f32(const float* clients, int64_t K, int64_t P, int64_t
       }
     }
     if (pl.kind == kFusedWinn) {
+      const bool pf = split_prefetch_rows() > 0;
+      if (pl.slots == 8 && pf)
+        return launch_fused_winn<64, 1, 8, kFusedWinnPF>(clients, K, P, ld, weights, out, workspace, workspace_elems,
+                                                         sumsq, 0, s, what);
       if (pl.slots == 8)
         return launch_fused_winn<64, 1, 8>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq, 0, s,
                                            what);
+      if (pf)
+        return launch_fused_winn<64, 1, 16, kFusedWinnPF>(clients, K, P, ld, weights, out, workspace, workspace_elems,
+                                                          sumsq, 0, s, what);
       return launch_fused_winn<64, 1, 16>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq, 0, s,
                                           what);
     }
@@ -2163,6 +2212,25 @@ int fedavg_reduce_sqdist_f32_variant(const float* clients, int64_t K, int64_t P,
     FEDAVG_WINN_CASE(128, 1, 4)
     FEDAVG_WINN_CASE(64, 1, 16)
 #undef FEDAVG_WINN_CASE
+    // the same (64 rows per wave, one column per lane) with PF rows of the next
+    // window prefetched: 87000000 + PF * 100 + NSMAX
+#define FEDAVG_WINNPF_CASE(NSMAX, PF)                                                                             \
+  case 87000000 + PF * 100 + NSMAX:                                                                              \
+    return launch_fused_winn<64, 1, NSMAX, PF>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq, \
+                                               blocks_per_cu, s, what);
+    FEDAVG_WINNPF_CASE(8, 4)
+    FEDAVG_WINNPF_CASE(8, 8)
+    FEDAVG_WINNPF_CASE(8, 12)
+    FEDAVG_WINNPF_CASE(8, 16)
+    FEDAVG_WINNPF_CASE(16, 2)
+    FEDAVG_WINNPF_CASE(16, 4)
+    FEDAVG_WINNPF_CASE(16, 6)
+    FEDAVG_WINNPF_CASE(16, 8)
+    FEDAVG_WINNPF_CASE(16, 10)
+    FEDAVG_WINNPF_CASE(16, 12)
+    FEDAVG_WINNPF_CASE(16, 16)
+    FEDAVG_WINNPF_CASE(16, 24)
+#undef FEDAVG_WINNPF_CASE
     default: return set_error(FEDAVG_EMODE, "%s: cols must be 32, 64, 128 or 256 (+1000: double-buffered)", what);
   }
 }

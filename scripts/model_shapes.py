@@ -67,6 +67,8 @@ CONFIGS = {
     "resnet56": (100, resnet56_shapes()),
     "resnet18_gn": (500, resnet18_gn_shapes()),
     "target_flat": (100, [("w", (25_000_000,))]),
+    "flat_640x3m": (640, [("w", (3_000_000,))]),      # split-row zero-copy windows, 16 waves
+    "flat_1000x5m": (1000, [("w", (5_000_000,))]),
     # resnet56's fp32 element count as ONE key (tile / window probes: the
     # per-key cost against the same bytes)
     "resnet56_flat": (100, [("w", (600_372 - 58,))]),

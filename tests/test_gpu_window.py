@@ -145,6 +145,28 @@ def test_split_windows_vs_oracle(K):
         assert torch.equal(s, again)
 
 
+@pytest.mark.parametrize("K", [161, 192, 256, 289, 320, 368])
+def test_split_windows_low_band(K):
+    """161-256 and 289-368 clients on long rows take the split-row windows too
+    (prefetching the next window's first 8 rows per wave): sampled windows of
+    the average bit-exact against the oracle, the whole average equal to the
+    row reduce's bits, the sums within 1e-12 of plain torch in fp64."""
+    lib = mfl_amd._lib.load_probe()
+    P = 1_700_003
+    plan = lib.fedavg_fused_plan_of(K, P)
+    assert plan == KIND_WINN * 1000000 + 64 * 100 + 8, plan
+    x, ld, weights = _rows(K, P, K * 7)
+    w = mfl_amd.weights_tensor(weights, torch.float32, DEV)
+    out, s = mfl_amd.reduce_with_sqdist(x, w, P)
+    _oracle_windows(x, out, weights, P, seed=K)
+    assert torch.equal(out.view(torch.int32), mfl_amd.reduce_packed(x, w, P).view(torch.int32))
+    ref = _sumsq_torch64(x, out, P)
+    assert ((s - ref).abs() / ref).max().item() < 1e-12
+    _, again = mfl_amd.reduce_with_sqdist(x, w, P)
+    assert torch.equal(s, again)
+    del x
+
+
 def test_split_windows_cfg4_shard_and_nonfinite():
     """cfg4's per-rank shape at N = 8 (500 x 1.4M): sampled windows against
     the oracle, sums against torch fp64; then -0.0 and inf / NaN through the
@@ -258,8 +280,14 @@ def test_window_plan_short_rows_and_other_k():
     for K in (1, 16, 129, 300, 512):
         assert lib.fedavg_fused_plan_of(K, 25_000_000) // 1000000 != KIND_WIN
     # split-row windows from 369 rows: up to 8 waves per group to 512, 16 to 1024; then two passes
-    assert lib.fedavg_fused_plan_of(368, 25_000_000) // 1000000 == 2
     assert lib.fedavg_fused_plan_of(369, 25_000_000) == KIND_WINN * 1000000 + 64 * 100 + 8
+    assert lib.fedavg_fused_plan_of(369, 1_000) == KIND_WINN * 1000000 + 64 * 100 + 8
+    # ... and (with the next window's rows prefetched) 161-256 and 289-368 rows on long rows
+    for K in (161, 200, 256, 289, 320, 368):
+        assert lib.fedavg_fused_plan_of(K, 25_000_000) == KIND_WINN * 1000000 + 64 * 100 + 8, K
+        assert lib.fedavg_fused_plan_of(K, 600_000) // 1000000 == 2, K  # < 24 windows per workgroup
+    for K in (129, 160, 257, 288):
+        assert lib.fedavg_fused_plan_of(K, 25_000_000) // 1000000 == 2, K
     assert lib.fedavg_fused_plan_of(512, 25_000_000) == KIND_WINN * 1000000 + 64 * 100 + 8
     assert lib.fedavg_fused_plan_of(513, 25_000_000) == KIND_WINN * 1000000 + 64 * 100 + 16
     assert lib.fedavg_fused_plan_of(1024, 1_000) == KIND_WINN * 1000000 + 64 * 100 + 16
