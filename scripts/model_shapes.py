@@ -69,6 +69,7 @@ CONFIGS = {
     "target_flat": (100, [("w", (25_000_000,))]),
     "flat_640x3m": (640, [("w", (3_000_000,))]),      # split-row zero-copy windows, 16 waves
     "flat_1000x5m": (1000, [("w", (5_000_000,))]),
+    "flat_300x5m": (300, [("w", (5_000_000,))]),
     # resnet56's fp32 element count as ONE key (tile / window probes: the
     # per-key cost against the same bytes)
     "resnet56_flat": (100, [("w", (600_372 - 58,))]),
