@@ -739,9 +739,10 @@ __device__ __forceinline__ double win_sq(typename WinVec<VEC>::T d) {
 // __launch_bounds__'s second argument is waves per SIMD: the window's KMAX x
 // VEC registers (+ a quarter more at VEC 1: one square per row per lane
 // before the folds) and ~40 others within 512 / waves
-// rows of the next window the split-row window kernels prefetch while the
-// chain runs (reduce_sqdist_winn_kernel, reduce_sqdist_segwinn_kernel);
-// FEDAVG_SPLIT_PREFETCH=0 turns it off (A/B)
+// rows of the next window the split-row window kernel on packed rows
+// prefetches while the chain runs (reduce_sqdist_winn_kernel; the zero-copy
+// form gained nothing from it); FEDAVG_SPLIT_PREFETCH=0 turns it
+// off and gives 161-368 rows back to the tiles (A/B)
 inline int split_prefetch_rows() {
   static const int v = [] {
     const char* e = std::getenv("FEDAVG_SPLIT_PREFETCH");
