@@ -504,10 +504,11 @@ def fused_round(red, w_dev, reps: int = 10) -> dict:
     rel = float(((sums["fused"] - sums["two_pass"]).abs() / sums["two_pass"].abs().clamp_min(1e-300)).max())
     plan = int(mfl_amd._lib.load().fedavg_fused_plan_of(K, P))
     kind, tile, slots = plan // 1000000, (plan // 100) % 10000, plan % 100
+    pf = 0 if os.environ.get("FEDAVG_SPLIT_PREFETCH", "") == "0" else 8  # csrc/common.hpp split_prefetch_rows
     kernel = {0: "two passes", 1: f"reduce_sqdist_f32_kernel<S={tile}> (LDS-DMA tiles)",
               2: f"reduce_sqdist_rs_kernel<S={tile},SLOTS={slots}> (register-staged tiles)",
               3: f"reduce_sqdist_win_kernel<KMAX={tile},VEC={slots}> (wave-owned windows)",
-              4: f"reduce_sqdist_winn_kernel<KH={tile},VEC=1,NSMAX={slots}> (split-row windows)"}.get(kind, str(plan))
+              4: f"reduce_sqdist_winn_kernel<KH={tile},VEC=1,NSMAX={slots},PF={pf}> (split-row windows)"}.get(kind, str(plan))
     return {"what": "aggregate + :291 sums of squares over the same resident rows (fedavg_trainer.py:217, :291)",
             "two_pass_ms": round(ms["two_pass"], 4), "fused_ms": round(ms["fused"], 4),
             "speedup": round(ms["two_pass"] / ms["fused"], 3),
