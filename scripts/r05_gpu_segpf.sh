@@ -1,6 +1,8 @@
 #!/bin/bash
 # Zero-copy split windows with the same-key prefetch: device-round parity,
-# then rocprofv3 kernel stats with the prefetch off and on.
+# then rocprofv3 kernel stats with the prefetch off and on.  (The measured
+# form was not adopted -- DESIGN §5 -- so in the current tree the switch only
+# reaches the packed-row kernel and this A/B compares two equal runs.)
 set -o pipefail
 O=gpurun_out/r05/g51
 mkdir -p $O
