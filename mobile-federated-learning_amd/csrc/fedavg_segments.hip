@@ -1124,8 +1124,18 @@ constexpr int64_t kSegSplitMaxK = 1024;  // the split-row windows' reach (16 wav
 // workgroups of the split-row window launch over `units` windows (0: not resident)
 inline int64_t segwinn_blocks(int64_t K, int64_t units) {
   const int ns = static_cast<int>((K + 63) / 64);
-  const int64_t res = ns <= 8 ? resident_blocks(reduce_sqdist_segwinn_kernel<8>, 64 * ns)
-                              : resident_blocks(reduce_sqdist_segwinn_kernel<16>, 64 * ns);
+  int64_t res = ns <= 8 ? resident_blocks(reduce_sqdist_segwinn_kernel<8>, 64 * ns)
+                        : resident_blocks(reduce_sqdist_segwinn_kernel<16>, 64 * ns);
+  // 5 waves per workgroup (257-320 clients): 4 resident workgroups per CU
+  // ran 8-11 % slower than 3 (260 x 8M 1.97 vs 1.77 ms, 300 x 5M 1.32 vs
+  // 1.18, 320 x 3M 0.87 vs 0.80, host-inclusive; profiles/r05/seg_layout_cfg4/
+  // wgs_per_cu_*); FEDAVG_SEGWINN_PER_CU caps it for probes
+  static const int64_t per_cu_env = [] {
+    const char* e = std::getenv("FEDAVG_SEGWINN_PER_CU");
+    return e && e[0] ? static_cast<int64_t>(std::atoll(e)) : int64_t(0);
+  }();
+  const int64_t per_cu = per_cu_env > 0 ? per_cu_env : (ns == 5 ? 3 : 0);
+  if (per_cu > 0 && per_cu * cu_count() < res) res = per_cu * cu_count();
   return units < res ? units : res;
 }
 

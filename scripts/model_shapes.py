@@ -70,6 +70,8 @@ CONFIGS = {
     "flat_640x3m": (640, [("w", (3_000_000,))]),      # split-row zero-copy windows, 16 waves
     "flat_1000x5m": (1000, [("w", (5_000_000,))]),
     "flat_300x5m": (300, [("w", (5_000_000,))]),
+    "flat_260x8m": (260, [("w", (8_000_000,))]),
+    "flat_320x3m": (320, [("w", (3_000_000,))]),
     # resnet56's fp32 element count as ONE key (tile / window probes: the
     # per-key cost against the same bytes)
     "resnet56_flat": (100, [("w", (600_372 - 58,))]),
