@@ -1132,6 +1132,20 @@ def _feed_of(trainer):
     return feed
 
 
+def stream_distinct_ok(devs) -> bool:
+    """Whether ``install(devices=devs)`` streams: always for one distinct
+    device (N shards on one GPU, the rehearsed form); for several distinct
+    GPUs only with ``FEDAVG_STREAM_DISTINCT_DEVICES=1`` -- streaming over
+    distinct devices (several DMA engines reading one pinned staging block,
+    per-device event waits, one pinned output filled by several D2H streams)
+    is parity-unpinned until a multi-GPU node runs tests/test_gpu_multi.py."""
+    from .multi import normalize_device
+
+    if len({normalize_device(d) for d in devs}) <= 1:
+        return True
+    return os.environ.get("FEDAVG_STREAM_DISTINCT_DEVICES", "0") == "1"
+
+
 def install(trainer_cls, device: Optional[torch.device] = None, client_cls=None, stream_clients: Optional[bool] = None,
             devices=None):
     """Patch ``trainer_cls.aggregate`` (e.g. the reference ``FedAvgTrainer``) in place.
@@ -1145,10 +1159,12 @@ def install(trainer_cls, device: Optional[torch.device] = None, client_cls=None,
     ``w_locals`` is not what was streamed).
 
     ``devices`` (or FEDAVG_DEVICES=0,1,... when ``device`` is None): host
-    rounds run over those GPUs by columns, one PCIe link each -- streamed
-    rounds (multi.ShardedRoundSession: each client's column shards uploaded
-    to every device as it arrives) and plain ones (multi.ShardedAggregator)
-    alike, with the single-GPU bits.
+    rounds run over those GPUs by columns, one PCIe link each, with the
+    single-GPU bits (multi.ShardedAggregator).  Streaming over them
+    (multi.ShardedRoundSession: each client's column shards uploaded to every
+    device as it arrives) has only run as same-GPU rehearsals, so a list of
+    DISTINCT devices streams only with ``FEDAVG_STREAM_DISTINCT_DEVICES=1``;
+    otherwise its rounds take the plain sharded path at :217.
 
     GPU initialisation is eager: install() creates every listed device's
     streams and runs each first-use kernel and copy once (warm_up), before
@@ -1170,6 +1186,8 @@ def install(trainer_cls, device: Optional[torch.device] = None, client_cls=None,
     devs = _devices_arg(device, devices)
     if devs is None:
         device = _single_device(device, devices)  # install(devices=[3]) runs on cuda:3
+    elif streaming and not stream_distinct_ok(devs):
+        streaming = False  # plain sharded rounds (multi.ShardedAggregator) until distinct GPUs have run it
     trainer_cls._mfl_stream_on = streaming
     trainer_cls._mfl_stream_device = device
     trainer_cls._mfl_stream_devices = devs

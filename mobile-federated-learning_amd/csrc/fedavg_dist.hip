@@ -1313,7 +1313,9 @@ int64_t fused_winn_grid(int64_t K, int64_t P, int blocks_per_cu) {
   int64_t per_cu = blocks_per_cu;
   if (per_cu <= 0) {
     const int64_t r = resident_blocks(reduce_sqdist_winn_kernel<KH, VEC, NSMAX, PF>, 64 * ns) / cu_count();
-    for (per_cu = r > 0 ? 1 : 0; per_cu * 2 <= r;) per_cu *= 2;
+    per_cu = 0;  // none resident: the caller reports it (grid 0)
+    if (r >= 1)
+      for (per_cu = 1; per_cu * 2 <= r;) per_cu *= 2;
   }
   const int64_t nwin = (P + 64 * VEC - 1) / (64 * VEC);
   const int64_t grid = per_cu * cu_count();

@@ -1383,6 +1383,10 @@ int launch_seg_fused(const SegFusedPlan& p, const SegKey* keys, const int64_t* t
     const hipError_t e = hipMemsetAsync(sumsq, 0, static_cast<size_t>(K) * sizeof(double), s);
     return e == hipSuccess ? FEDAVG_OK : set_error(-static_cast<int>(e), "%s: hipMemsetAsync failed", what);
   }
+  // beyond kSegFusedMaxK clients only the split-row windows fuse: the tile
+  // kernel loads at most kBlock client addresses per workgroup
+  if (K > kSegFusedMaxK && !(p.win && p.kmax < 0))
+    return set_error(FEDAVG_EMODE, "%s: K = %lld fuses only on the split-row windows", what, (long long)K);
   const int k32 = static_cast<int>(K);
   int64_t nparts = 0;
   if (p.win && p.kmax < 0) {  // split-row windows: p.waves workgroups of ceil(K / 64) waves

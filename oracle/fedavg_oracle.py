@@ -226,3 +226,35 @@ def delta_from_norms(sample_nums, norms, lr):
     """fedavg_trainer.py:293."""
     sample_nums = np.asarray(sample_nums)
     return np.sum(sample_nums * np.asarray(norms)) / np.sum(sample_nums) / lr
+
+
+THRESHOLD_RHO = 1000  # config.py:85
+THRESHOLD_BETA = 1000  # config.py:86
+
+
+def round_stats_update(stats, sample_nums, norms, rho_locals, beta_locals, lr, have_losses=True):
+    """fedavg_trainer.py:289-305: the loop's scheduler statistics after a round.
+
+    ``stats`` = ``(delta, rho, beta, rho_flag, beta_flag)`` as they stood
+    (:107 draws the first three, both flags True); ``norms`` = the round's
+    :291 distances (one per ``w_locals`` entry).  Returns the updated tuple:
+    ``delta`` replaced by :293 when finite; ``rho`` / ``beta`` by their
+    sample-weighted means when larger (or on the first update) and finite
+    and below THRESHOLD_RHO / THRESHOLD_BETA, which also clears the flag.
+    Nothing changes for an empty round (:289)."""
+    delta, rho, beta, rho_flag, beta_flag = stats
+    if not (len(sample_nums) and have_losses):
+        return stats
+    sample_nums = np.array(sample_nums)
+    delta_tmp = np.sum(sample_nums * np.asarray(norms)) / np.sum(sample_nums) / lr
+    if not np.isnan(delta_tmp) and not np.isinf(delta_tmp):
+        delta = delta_tmp
+    rho_tmp = np.sum(sample_nums * np.array(rho_locals)) / np.sum(sample_nums)
+    if rho_tmp > rho or rho_flag:
+        if (not np.isnan(rho_tmp) and not np.isinf(rho_tmp)) and rho_tmp < THRESHOLD_RHO:
+            rho, rho_flag = rho_tmp, False
+    beta_tmp = np.sum(sample_nums * np.array(beta_locals)) / np.sum(sample_nums)
+    if beta_tmp > beta or beta_flag:
+        if (not np.isnan(beta_tmp) and not np.isinf(beta_tmp)) and beta_tmp < THRESHOLD_BETA:
+            beta, beta_flag = beta_tmp, False
+    return delta, rho, beta, rho_flag, beta_flag

@@ -9,11 +9,12 @@ compared with the reference's own CSV rows (``case.fpf``).
 from __future__ import annotations
 
 import copy
+import hashlib
 import json
 from collections import OrderedDict
 from dataclasses import dataclass
 from pathlib import Path
-from typing import List
+from typing import List, Optional
 
 import numpy as np
 import torch
@@ -25,17 +26,62 @@ FPF_DIR = Path(__file__).resolve().parent / "golden" / "fpf"
 class FPFCase:
     meta: dict
     init: "OrderedDict[str, torch.Tensor]"
-    client_states: List[List["OrderedDict[str, torch.Tensor]"]]  # [round][j]
+    client_states: Optional[List[List["OrderedDict[str, torch.Tensor]"]]]  # [round][j]; None: regenerated
     fpf: np.ndarray  # [rounds, client_num_in_total], the reference's CSV values
+    stats: Optional[np.ndarray] = None  # [rounds, (rho, beta, delta)] after each round's :289-305 update
+
+    def client_state(self, t: int, j: int, model_state) -> "OrderedDict[str, torch.Tensor]":
+        """Client ``j``'s returned state in round ``t``: the stored one, or --
+        for a scenario stored as digests (``meta["inputs"] == "sha256"``) --
+        rebuilt from ``model_state`` (the model the round's clients start
+        from) by the generator's stub ``Client.train`` recipe
+        (oracle/gen_golden_fpf.py) and checked against the reference input's
+        sha256."""
+        if self.client_states is not None:
+            return self.client_states[t][j]
+        rd = self.meta["rounds"][t]
+        ds = rd["client_indexes"][j]
+        g = torch.Generator().manual_seed(1000 * t + ds)
+        w = OrderedDict()
+        for k, v in model_state.items():
+            v = v.detach().cpu()
+            if v.dtype == torch.int64:
+                w[k] = v + rd["local_itr"]
+            else:
+                w[k] = v + (0.01 * (1 + ds) * torch.randn(v.shape, generator=g)).to(v.dtype)
+        want = self.meta["client_sha256"][f"r{t}_i{j}"]
+        assert _digest(w) == want, f"regenerated client r{t} i{j} differs from the reference's input"
+        return w
 
 
-def case_names():
-    return sorted(p.stem for p in FPF_DIR.glob("*.npz"))
+def _digest(sd) -> str:
+    h = hashlib.sha256()
+    for v in sd.values():
+        h.update(v.numpy().tobytes())
+    return h.hexdigest()
+
+
+def big_init() -> "OrderedDict[str, torch.Tensor]":
+    """The ``big`` scenario's initial model: the generator's ``make_model("big")``."""
+    torch.manual_seed(1234)
+    return OrderedDict((k, v.detach().clone()) for k, v in torch.nn.Linear(1000, 1000).state_dict().items())
+
+
+def case_names(stats_only: bool = False):
+    """Scenario names; ``stats_only=False`` leaves out the regenerated
+    (digest-only) scenarios, whose replay costs seconds per round."""
+    names = sorted(p.stem for p in FPF_DIR.glob("*.npz"))
+    return names if stats_only else [n for n in names if not n.startswith("big")]
 
 
 def load_case(name: str) -> FPFCase:
     z = np.load(FPF_DIR / f"{name}.npz", allow_pickle=False)
     meta = json.loads(bytes(z["meta"]).decode())
+    stats = z["stats"] if "stats" in z.files else None
+    if meta.get("inputs") == "sha256":
+        init = big_init()
+        assert _digest(init) == meta["init_sha256"], "the regenerated initial model differs from the reference's"
+        return FPFCase(meta, init, None, z["fpf"], stats)
     keys = [k["name"] for k in meta["keys"]]
     bf16 = {k["name"] for k in meta["keys"] if k["dtype"] == "bfloat16"}  # stored as int16 bits
 
@@ -48,7 +94,7 @@ def load_case(name: str) -> FPFCase:
     for t, rd in enumerate(meta["rounds"]):
         states.append([OrderedDict((k, tensor(z[f"w__r{t}__i{j}__{k}"], k)) for k in keys)
                        for j in range(len(rd["client_indexes"]))])
-    return FPFCase(meta, init, states, z["fpf"])
+    return FPFCase(meta, init, states, z["fpf"], stats)
 
 
 def replay(case: FPFCase, impl, record_after_aggregate: bool = False) -> np.ndarray:
@@ -62,7 +108,7 @@ def replay(case: FPFCase, impl, record_after_aggregate: bool = False) -> np.ndar
         idx, itr = rd["client_indexes"], rd["local_itr"]
         last_w = copy.deepcopy(model_state)  # :165
         impl.begin_round(last_w)
-        w_locals = [(n, copy.deepcopy(sd)) for n, sd in zip(rd["sample_nums"], case.client_states[t])]
+        w_locals = [(n, copy.deepcopy(case.client_state(t, j, model_state))) for j, n in enumerate(rd["sample_nums"])]
         if not record_after_aggregate:
             for c, (_, w) in zip(idx, w_locals):
                 impl.record_client(c, w, last_w)  # :210, before aggregate aliases w_locals[0][1]
@@ -76,3 +122,29 @@ def replay(case: FPFCase, impl, record_after_aggregate: bool = False) -> np.ndar
         rows.append(np.asarray(impl.fpf_index()))
         impl.end_round(t, idx, itr, w_glob, last_w)  # :314-327
     return np.stack(rows)
+
+
+def replay_stats(case: FPFCase, aggregate, norms):
+    """Drive the rounds through the loop's :217 aggregate and the :289-305
+    statistics.  ``aggregate(w_locals, model_state)`` -> ``w_glob``;
+    ``norms(w_locals, w_glob)`` -> the round's :291 distances.  Returns
+    ``(stats, norms_per_round)``: ``stats`` [rounds, (rho, beta, delta)] after
+    each round's update, comparable with ``case.stats`` (the reference's)."""
+    import fedavg_oracle as O
+
+    rho0, beta0, delta0 = case.meta["stats_init"]
+    st = (delta0, rho0, beta0, True, True)  # :107
+    lr = case.meta["lr"]
+    model_state = OrderedDict((k, v.clone()) for k, v in case.init.items())
+    out, all_norms = [], []
+    for t, rd in enumerate(case.meta["rounds"]):
+        w_locals = [(n, copy.deepcopy(case.client_state(t, j, model_state))) for j, n in enumerate(rd["sample_nums"])]
+        w_glob = aggregate(w_locals, model_state)  # :217
+        for k in model_state:  # :219
+            model_state[k].copy_(w_glob[k])
+        nrm = np.asarray(norms(w_locals, w_glob)) if w_locals else np.zeros(0)  # :291
+        all_norms.append(nrm)
+        st = O.round_stats_update(st, rd["sample_nums"], nrm, rd["rhos"], rd["betas"], lr,
+                                  have_losses=bool(rd["losses"]))
+        out.append((st[1], st[2], st[0]))
+    return np.array(out, dtype=np.float64), all_norms

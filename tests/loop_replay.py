@@ -43,6 +43,8 @@ class Client:
             time.sleep(self.train_delay_s)  # the client's local training
         if self._attempt is None:  # diverged (client.py:71-73)
             return OrderedDict(), None, None, None, None, None
+        if callable(self._attempt):  # a result computed from the round's global model
+            return self._attempt(net)
         w = OrderedDict((k, v.clone()) for k, v in self._attempt.items())  # net.cpu().state_dict(): fresh tensors
         return w, 0.25, 0.5, 0.75, 0.9, 100.0
 
@@ -51,7 +53,7 @@ class FedAvgTrainer:
     client_cls = Client
 
     def __init__(self, model_state, rounds, n_clients=None, train_delay_s=0.0, after_append=None,
-                 before_append=None):
+                 before_append=None, after_aggregate=None):
         self.model_global = _Model(model_state)
         self.rounds = rounds
         n = n_clients or max((len(r) for r in rounds), default=1)
@@ -60,6 +62,8 @@ class FedAvgTrainer:
             c.train_delay_s = train_delay_s
         self.after_append = after_append  # test hook: (round, w_locals) -> None, e.g. a mutation
         self.before_append = before_append  # test hook: (round, client, w) -> None, between :190 and :199
+        # test hook: (round, w_locals, w_glob, train results) -> None after :219, where :289-305 run
+        self.after_aggregate = after_aggregate
         self.results = []
         self.timings = []
 
@@ -68,16 +72,17 @@ class FedAvgTrainer:
 
     def train(self):  # fedavg_trainer.py:95
         for r, specs in enumerate(self.rounds):
-            w_locals = []
+            w_locals, trained = [], []
             t_last = time.perf_counter()
             for idx, (n, attempts) in enumerate(specs):  # :172
                 client = self.client_list[idx]
                 tries = iter(attempts)
                 while True:  # :181-195
                     client.update_local_dataset(idx, next(tries), n)
-                    w, loss, beta, rho, acc, cyc = client.train(net=None, local_iteration=1)  # :189
+                    w, loss, beta, rho, acc, cyc = client.train(net=self.model_global, local_iteration=1)  # :189
                     if loss is not None and beta is not None and rho is not None and acc is not None:  # :190
                         break
+                trained.append((loss, beta, rho))
                 if self.before_append is not None:
                     self.before_append(r, idx, w)
                 t_last = time.perf_counter()
@@ -88,6 +93,8 @@ class FedAvgTrainer:
             w_glob = self.aggregate(w_locals)  # :217
             t1 = time.perf_counter()
             self.model_global.load_state_dict(w_glob)  # :219
+            if self.after_aggregate is not None:
+                self.after_aggregate(r, w_locals, w_glob, trained)
             self.results.append(OrderedDict((k, v.clone()) for k, v in w_glob.items()))
             self.timings.append({"aggregate_ms": (t1 - t0) * 1e3, "last_train_to_model_ms": (t1 - t_last) * 1e3})
 

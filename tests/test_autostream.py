@@ -368,6 +368,7 @@ def test_install_devices_streams_into_the_sharded_aggregator(plain_calls, monkey
 
     monkeypatch.setattr("mfl_amd.multi.sharded_aggregator", fake_sharded)
     monkeypatch.setattr("mfl_amd.autostream.ClientFeed.SMALL_ROUND_BYTES", 0)
+    monkeypatch.setenv("FEDAVG_STREAM_DISTINCT_DEVICES", "1")  # distinct devices stream only when opted in
     T, C = fresh_classes()
     mfl_amd.install(T, stream_clients=True, devices=[0, 1, 2])
     tr = T({"w": torch.zeros(10)}, _rounds(2))
@@ -375,3 +376,22 @@ def test_install_devices_streams_into_the_sharded_aggregator(plain_calls, monkey
     assert asked and all(a == [0, 1, 2] for a in asked)
     assert len(agg.sessions) == 2 and all("__streamed__" in r for r in tr.results)
     assert plain_calls == []
+
+
+def test_install_distinct_devices_do_not_stream_by_default(monkeypatch):
+    """Streaming over distinct GPUs is opt-in (FEDAVG_STREAM_DISTINCT_DEVICES=1):
+    without it install(devices=[0, 1]) keeps the wrappers off and :217 runs
+    the plain sharded path; N shards on one device (the rehearsed form) stream."""
+    from mfl_amd.aggregate import stream_distinct_ok
+
+    monkeypatch.delenv("FEDAVG_STREAM_DISTINCT_DEVICES", raising=False)
+    monkeypatch.setattr(mfl_amd.DeviceAggregator, "WARMUP", False)
+    assert not stream_distinct_ok([0, 1]) and stream_distinct_ok([0, 0, 0]) and stream_distinct_ok(["cuda:2"])
+    T, C = fresh_classes()
+    mfl_amd.install(T, stream_clients=True, devices=[0, 1])
+    assert T._mfl_stream_on is False and T._mfl_stream_devices == [0, 1]
+    T2, C2 = fresh_classes()
+    mfl_amd.install(T2, stream_clients=True, devices=[0, 0])
+    assert T2._mfl_stream_on is True
+    monkeypatch.setenv("FEDAVG_STREAM_DISTINCT_DEVICES", "1")
+    assert stream_distinct_ok([0, 1])

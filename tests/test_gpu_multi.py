@@ -260,6 +260,7 @@ def test_distinct_devices_stream_and_plain_bit_exact(monkeypatch):
     from loop_replay import fresh_classes
 
     T, C = fresh_classes()
+    monkeypatch.setenv("FEDAVG_STREAM_DISTINCT_DEVICES", "1")  # streaming over distinct GPUs is opt-in
     mfl_amd.install(T, client_cls=C, devices=devs)
     tr = T(OrderedDict((k, torch.zeros_like(v)) for k, v in w_locals[0][1].items()),
            [[(c, [sd]) for c, sd in w_locals]])

@@ -46,6 +46,9 @@ def test_single_entry_device_list_names_that_device(monkeypatch):
     monkeypatch.setenv("FEDAVG_DEVICES", "5")
     assert _single_device(None, None) == torch.device("cuda", 5)
     monkeypatch.delenv("FEDAVG_DEVICES")
+    # install() warms the listed devices up eagerly when a GPU is visible; this
+    # checks the routing only (a one-GPU box has no cuda:1 or cuda:3)
+    monkeypatch.setattr(mfl_amd.DeviceAggregator, "WARMUP", False)
     T, C = fresh_classes()
     mfl_amd.install(T, client_cls=C, devices=[3])
     assert T._mfl_stream_device == torch.device("cuda", 3) and T._mfl_stream_devices is None

@@ -177,3 +177,35 @@ def test_distance_oracles_agree_other_dtypes(name):
     eps = torch.finfo(d).eps
     assert t[0] == 0.0 and e[0] == 0.0
     assert np.allclose(t, e, rtol=2 * eps, atol=0), (t, e)
+
+
+# ---------------------------------------------------------------------------
+# The loop's scheduler statistics (fedavg_trainer.py:289-305): delta from the
+# :291 norms, rho and beta -- the reference's own values from its train()
+STATS_CASES = [n for n in fpf_replay.case_names(stats_only=True) if "stats" in np.load(
+    fpf_replay.FPF_DIR / f"{n}.npz").files]
+
+
+def test_stats_golden_present():
+    assert {"lr_full", "big_lru"} <= set(STATS_CASES)
+
+
+@pytest.mark.parametrize("name", STATS_CASES)
+def test_round_stats_oracle_matches_reference_loop(name):
+    """The restatement (aggregate_torch, client_distances_torch, round_stats_update)
+    reproduces the reference's delta / rho / beta after every round bit for bit:
+    same torch CPU expressions on the same inputs.  ``big_lru`` (P = 1,001,000)
+    also checks that its regenerated client states are the reference's inputs
+    (sha256 per client, in FPFCase.client_state)."""
+    case = fpf_replay.load_case(name)
+    agg = lambda wl, ms: copy.deepcopy(ms) if not wl else O.aggregate_torch(wl)  # noqa: E731
+    got, _ = fpf_replay.replay_stats(case, agg, O.client_distances_torch)
+    assert got.shape == case.stats.shape
+    assert np.array_equal(got, case.stats), (got - case.stats)
+
+
+def test_big_lru_fpf_rows_match_reference():
+    case = fpf_replay.load_case("big_lru")
+    assert case.meta["weight_size"] == 1_001_000 and not case.meta["full"]
+    got = fpf_replay.replay(case, _OracleImpl(case))
+    assert np.array_equal(got.astype(np.float64), case.fpf)
