@@ -31,9 +31,16 @@ path (178.8 ms).
   against the pinned staging rows the GPU reduces (converted as the packer
   converts).  The version counter makes in-place edits of w_locals between
   :199 and :217 (clipping, noise, ``copy_``, slice assignment: any in-place
-  op) a deterministic fallback whatever elements they touch; a replaced
-  tensor object fails the same check (a fresh tensor's counter is not a deep
-  copy's).  An in-place edit of a ``Client.train`` result between :189 and
+  op) a deterministic fallback whatever elements they touch.  A replaced
+  tensor object is one too: every fed (Ordered)dict gets a one-shot
+  ``__deepcopy__`` hook that records the tensors of the loop's :199 deep copy
+  (``_hook_deepcopy``), and each ``w_locals`` value must BE one of them -- so
+  a replacement by another ``copy.deepcopy`` (whose version counter is a
+  deep copy's as well) is caught without any probe landing on it.  The hook
+  is an instance attribute between ``Client.train``'s return and that deep
+  copy (pickling the result in that window would fail on it); a plain
+  ``dict`` result (no instance attributes) gets no hook, and its
+  replacements are left to the value probes.  An in-place edit of a ``Client.train`` result between :189 and
   its :199 deep copy is seen on the fed dict itself: the worker keeps the
   last packed dict with its counters and re-reads them when the next client
   arrives (status 9 at :217 for the round's last client).  What the counter
@@ -58,11 +65,13 @@ model) keeps it.
 """
 from __future__ import annotations
 
+import copy
 import os
 import queue
 import random
 import threading
 import time
+import weakref
 from typing import Optional
 
 import torch
@@ -142,6 +151,10 @@ class ClientFeed:
         self._small = False  # this round fits SMALL_ROUND_BYTES: left to the plain path
         self.fed = []  # sample numbers in feed order
         self._fed_keys = []  # each fed dict's key objects, in feed order
+        # per fed client: the values of the loop's :199 deep copy of it (recorded
+        # by _hook_deepcopy), or None; the round generation the hooks belong to
+        self._copies = []
+        self._gen = 0
         # the last packed client's dict and its version counters at packing:
         # re-read when the next client arrives (the loop's :199 copy of this
         # one is done by then) and, for the round's last client, inside the
@@ -178,6 +191,8 @@ class ClientFeed:
         self.fed.append(sample_num)  # the dict itself goes to the worker only (no round-long reference)
         # its key objects (the :199 deep copy shares them): verify_rows matches w_locals' keys by identity
         self._fed_keys.append(tuple(state_dict))
+        self._copies.append(None)
+        self._hook_deepcopy(state_dict, len(self.fed) - 1)
         if self._worker is None:
             self._q = queue.Queue()
             self._worker = threading.Thread(target=self._run, name="mfl-client-feed", daemon=True)
@@ -187,6 +202,35 @@ class ClientFeed:
         # worker re-reads them after packing (an in-place update meanwhile
         # means the packed row may mix two states)
         self._q.put((sample_num, state_dict, [v._version for v in state_dict.values()]))
+
+    def _hook_deepcopy(self, sd, slot: int) -> None:
+        """Give the fed dict a one-shot ``__deepcopy__`` (an instance
+        attribute: ``copy.deepcopy`` looks it up on an OrderedDict instance)
+        that makes the standard deep copy -- the hook removes itself first, so
+        the copy and its ``__dict__`` are exactly what ``copy.deepcopy`` gives
+        without it -- and records the copy's tensors as fed client ``slot``'s
+        :199 copy.  At :217 ``verify_rows`` then requires every ``w_locals``
+        value to BE one of those tensors: a tensor replaced between :199 and
+        :217, even by another deep copy, is a deterministic fallback.  Plain
+        ``dict`` results (no instance attributes) and dicts the loop never
+        deep-copies keep ``None`` (version counters and value probes only)."""
+        if type(sd) in copy._deepcopy_dispatch or not hasattr(sd, "__dict__") or "__deepcopy__" in sd.__dict__:
+            return
+        ref, feed_ref, gen = weakref.ref(sd), weakref.ref(self), self._gen
+
+        def hook(memo):
+            d = ref()
+            d.__dict__.pop("__deepcopy__", None)  # one shot: the copy below is the plain one
+            y = copy.deepcopy(d, memo)
+            feed = feed_ref()
+            if feed is not None and feed._gen == gen and slot < len(feed._copies):
+                feed._copies[slot] = tuple(y.values()) if isinstance(y, dict) else None
+            return y
+
+        try:
+            sd.__deepcopy__ = hook
+        except (AttributeError, TypeError):
+            pass
 
     def refuse(self, why: str) -> None:
         """This round is not streamed (the plain drop-in runs at :217)."""
@@ -343,7 +387,7 @@ class ClientFeed:
             ext, names, templ, group, offset, kind, sptr, sld, ses = self._vplan
             st = ext.verify_rows(w_locals, list(self.fed), names, templ, group, offset, kind, sptr, sld, ses,
                                  self.VERIFY_PROBES, random.getrandbits(64), self.VERIFY_FULL_ELEMS,
-                                 deepcopy_version(), self._fed_keys)
+                                 deepcopy_version(), self._fed_keys, list(self._copies))
             self.stats["last_verify"] = {"status": int(st[0]), "client": int(st[1]), "key": int(st[2]),
                                          "probes": int(st[3])}
             if len(st) > 4:  # native phase times (us) and the walk's thread count
@@ -363,7 +407,11 @@ class ClientFeed:
             # 35,000 key references at resnet56 x 100: their decrefs (cold
             # objects, ~0.2 ms) go to the worker, off the :217 call
             self._defer_release(self._fed_keys)
+        if self._copies:
+            self._defer_release(self._copies)
         self._fed_keys = []
+        self._copies = []
+        self._gen += 1  # hooks of dicts fed in this round (not yet deep-copied) record nothing now
         self._vplan = None
         self._prev = None
         self.broken = self._small = False

@@ -407,9 +407,17 @@ static py::tuple small_round(py::list w_locals, py::list names, py::list templ, 
 //     fedavg_host.cpp).  Equal converted values reduce to the same bits, so
 //     a match is exactly the reduction's criterion at that element.
 // The per-client walks run on torch's intra-op threads (see below).
+//   * with `copies` (optional, one entry per client): where copies[i] is a
+//     tuple, every value of client i IS (object identity) the tensor at that
+//     position of the dict the loop's :199 copy.deepcopy returned for fed
+//     client i (autostream records it in a one-shot __deepcopy__ hook).  A
+//     tensor replaced between :199 and :217 -- by a fresh tensor or by
+//     another deep copy, whose version counter is a deep copy's too -- is
+//     caught deterministically; None entries skip the check.
 // status 0: all checks passed; 1 count; 2 sample number; 3 not a (n, dict)
 // pair; 4 repeated dict; 5 keys; 6 tensor metadata; 7 value (client, key);
-// 8 version counter (client, key).
+// 8 version counter (client, key); 10 not the :199 deep copy's tensor
+// (client, key).
 namespace {
 inline uint64_t mix64(uint64_t x) {
   x += 0x9E3779B97F4A7C15ull;
@@ -447,7 +455,7 @@ static py::tuple verify_rows(py::list w_locals, py::list counts, py::list names,
                              const std::vector<int64_t>& kind, const std::vector<int64_t>& stage_ptr,
                              const std::vector<int64_t>& stage_ld, const std::vector<int64_t>& stage_esize,
                              int64_t probes, uint64_t seed, int64_t full_elems, int64_t expect_version,
-                             py::object fed_keys) {
+                             py::object fed_keys, py::object copies) {
   const Py_ssize_t K = PyList_GET_SIZE(w_locals.ptr());
   const Py_ssize_t N = PyList_GET_SIZE(names.ptr());
   // (status, client, key, elements compared, (us before the walk, us in the
@@ -551,6 +559,17 @@ static py::tuple verify_rows(py::list w_locals, py::list counts, py::list names,
       if (PyTuple_Check(ks) && PyTuple_GET_SIZE(ks) == N) fk[i] = &PyTuple_GET_ITEM(ks, 0);
     }
   }
+  std::vector<PyObject* const*> ck(static_cast<size_t>(K), nullptr);
+  if (!copies.is_none()) {
+    if (!PyList_Check(copies.ptr()) || PyList_GET_SIZE(copies.ptr()) != K)
+      throw std::invalid_argument("verify_rows: copies must be a list with one entry per client");
+    for (Py_ssize_t i = 0; i < K; ++i) {
+      PyObject* cs = PyList_GET_ITEM(copies.ptr(), i);
+      if (cs == Py_None) continue;
+      if (!PyTuple_Check(cs) || PyTuple_GET_SIZE(cs) != N) return res(10, i, -1, 0);  // the copy had other keys
+      ck[i] = &PyTuple_GET_ITEM(cs, 0);
+    }
+  }
   const auto fill_fast = [&](int64_t i) -> bool {
     Py_ssize_t pos = 0, j = 0;
     PyObject *key, *val;
@@ -600,6 +619,13 @@ static py::tuple verify_rows(py::list w_locals, py::list counts, py::list names,
       return full || h <= thresh ||
              static_cast<int64_t>(mix64(seed + static_cast<uint64_t>(j)) % static_cast<uint64_t>(K)) == i;
     };
+    if (PyObject* const* cp = ck[i]) {  // the values the loop's :199 deep copy made (pointer compares)
+      for (Py_ssize_t j = 0; j < N; ++j)
+        if (row_vals[j] != cp[j]) {
+          status[i] = (int64_t(10) << 32) | j;
+          return;
+        }
+    }
     thread_local std::vector<c10::TensorImpl*> impls;
     impls.resize(N);
     for (Py_ssize_t j = 0; j < N; ++j) {
@@ -744,5 +770,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("w_locals"), py::arg("counts"), py::arg("names"), py::arg("templ"), py::arg("group"),
         py::arg("offset"), py::arg("kind"), py::arg("stage_ptr"), py::arg("stage_ld"), py::arg("stage_esize"),
         py::arg("probes"), py::arg("seed"), py::arg("full_elems"), py::arg("expect_version") = -1,
-        py::arg("fed_keys") = py::none());
+        py::arg("fed_keys") = py::none(), py::arg("copies") = py::none());
 }

@@ -356,6 +356,97 @@ def test_fed_dict_edited_before_its_deep_copy_falls_back(plain_calls, which):
         assert "changed after they were packed" in feed.stats["last_fallback"]
 
 
+@pytest.mark.parametrize("hooked", [True, False], ids=["ordered_dict", "plain_dict"])
+@pytest.mark.parametrize("seed", range(6))
+def test_tensor_replaced_by_a_deep_copy_falls_back(plain_calls, seed, hooked):
+    """A w_locals tensor REPLACED between :199 and :217 by another deep copy
+    (``w_locals[i] = (n, copy.deepcopy(edited))``, one element changed at an
+    unsampled-in-general position): its version counter is a deep copy's and
+    its keys are the same objects, so counters cannot see it.  For the
+    reference's OrderedDict state_dicts the feed recorded the loop's own :199
+    deep copies (autostream._hook_deepcopy) and verify_rows requires identity
+    with them: a deterministic fallback (status 10) every time.  A plain
+    ``dict`` result carries no hook; there only the ~4,096 value probes can
+    see it, so the streamed result is returned unless a probe lands on the
+    element (this round has 64 x 130 x 300 elements: it rarely does)."""
+    import copy
+
+    g = torch.Generator().manual_seed(100 + seed)
+    K, n_keys = 64, 130
+    specs = []
+    for i in range(K):
+        sd = OrderedDict((f"k{j}", torch.randn(300, generator=g)) for j in range(n_keys))
+        if hooked:
+            specs.append((i + 1, [sd]))
+        else:  # Client.train returning a plain dict of fresh tensors
+            specs.append((i + 1, [lambda net, sd=sd: (dict((k, v.clone()) for k, v in sd.items()),
+                                                      0.25, 0.5, 0.75, 0.9, 100.0)]))
+    rounds = [specs, specs]
+    where = torch.randint(0, K, (1,), generator=g).item(), torch.randint(0, n_keys, (1,), generator=g).item()
+    pos = torch.randint(0, 300, (1,), generator=g).item()
+
+    def replace(r, w_locals):
+        if r == 1:
+            n, sd = w_locals[where[0]]
+            edited = copy.deepcopy(sd)
+            edited[f"k{where[1]}"][pos] += 1e-3
+            w_locals[where[0]] = (n, copy.deepcopy(edited))  # fresh deep copies: version 1, same key objects
+
+    T, C = fresh_classes()
+    mfl_amd.install(T, stream_clients=True)
+    tr = T({"k0": torch.zeros(300)}, rounds, after_append=replace)
+    agg = _FakeAgg()
+    from mfl_amd.autostream import ClientFeed
+
+    feed = ClientFeed(lambda: agg, K)
+    feed.SMALL_ROUND_BYTES = 0
+    feed.VERIFY_FULL_ELEMS = 0
+    tr.__dict__["_mfl_feed"] = feed
+    tr.train()
+    assert "__streamed__" in tr.results[0]
+    if hooked:
+        assert "__plain__" in tr.results[1]
+        assert feed.stats["last_verify"]["status"] == 10
+        assert feed.stats["last_verify"]["client"] == where[0] and feed.stats["last_verify"]["key"] == 0
+    else:  # the documented limit: caught only when a value probe hits the edited element
+        st = feed.stats["last_verify"]["status"]
+        assert st in (0, 7)
+        assert ("__plain__" in tr.results[1]) == (st == 7)
+
+
+def test_deepcopy_hook_leaves_the_copy_unchanged():
+    """The one-shot hook's deep copy is the plain one: same type, same
+    ``_metadata`` attribute, no hook carried over; the hook is gone from the
+    fed dict after it fired and a second deep copy is plain."""
+    import copy
+
+    from mfl_amd.autostream import ClientFeed
+
+    sd = torch.nn.Linear(3, 2).state_dict()  # an OrderedDict with _metadata, as client.py:96 returns
+    feed = ClientFeed(lambda: None, 4)
+    feed.fed.append(1)
+    feed._copies.append(None)
+    feed._hook_deepcopy(sd, 0)
+    assert "__deepcopy__" in sd.__dict__
+    y = copy.deepcopy(sd)
+    assert "__deepcopy__" not in sd.__dict__ and "__deepcopy__" not in y.__dict__
+    assert type(y) is type(sd) and y._metadata == sd._metadata and list(y) == list(sd)
+    assert all(torch.equal(a, b) and a is not b for a, b in zip(y.values(), sd.values()))
+    assert feed._copies[0] is not None and all(a is b for a, b in zip(feed._copies[0], y.values()))
+    y2 = copy.deepcopy(sd)
+    assert all(a is not b for a, b in zip(y2.values(), y.values()))
+    feed._reset()
+    sd2 = torch.nn.Linear(3, 2).state_dict()
+    feed.fed.append(1)
+    feed._copies.append(None)
+    feed._hook_deepcopy(sd2, 0)
+    gen = feed._gen
+    feed._reset()  # the round ended before the loop's deep copy: the hook records nothing
+    assert feed._gen == gen + 1
+    copy.deepcopy(sd2)
+    assert feed._copies == []
+
+
 def test_install_devices_streams_into_the_sharded_aggregator(plain_calls, monkeypatch):
     """install(devices=[...]): the feed's rounds open on the devices'
     ShardedAggregator (multi.ShardedRoundSession), not on the first device."""

@@ -53,8 +53,9 @@ class Round:
                      [x.data_ptr() for x in st], [int(x.stride(0)) for x in st], [x.element_size() for x in st])
         self.counts = list(counts)
 
-    def verify(self, w_locals, seed=1, probes=4096, full_elems=0, expect_version=-1, fed_keys=None):
-        return ext.verify_rows(w_locals, self.counts, *self.args, probes, seed, full_elems, expect_version, fed_keys)
+    def verify(self, w_locals, seed=1, probes=4096, full_elems=0, expect_version=-1, fed_keys=None, copies=None):
+        return ext.verify_rows(w_locals, self.counts, *self.args, probes, seed, full_elems, expect_version, fed_keys,
+                               copies)
 
 
 def _round(K=8, n_keys=40, numel=40_000, **kw):
@@ -309,3 +310,26 @@ def test_fed_key_objects_match_by_identity():
     assert r.verify(wl, fed_keys=fed)[0] == 5
     with pytest.raises(ValueError):
         r.verify(wl, fed_keys=fed[:2])
+
+
+def test_copies_identity_catches_a_replacement_by_a_deep_copy():
+    """``copies[i]``: the values of the loop's :199 deep copy of client i.  A
+    value that is not that object -- here one key replaced by a deep copy
+    with equal values and a deep copy's version counter -- is status 10 at
+    (client, key); None entries skip the check; a tuple of the wrong length
+    is status 10 with key -1."""
+    r, wl = _round(K=5, n_keys=6, numel=1000)
+    copies = [tuple(d.values()) for _, d in wl]
+    assert r.verify(wl, copies=copies)[0] == 0
+    n, d = wl[3]
+    d2 = OrderedDict(d)
+    k = list(d2)[4]
+    d2[k] = copy.deepcopy(d2[k])  # same values, version counter of a deep copy
+    wl[3] = (n, d2)
+    assert r.verify(wl, expect_version=1)[0] == 0  # counters and values cannot see it
+    st = r.verify(wl, expect_version=1, copies=copies)
+    assert (st[0], st[1], st[2]) == (10, 3, 4)
+    copies[3] = None
+    assert r.verify(wl, expect_version=1, copies=copies)[0] == 0
+    copies[3] = copies[2][:2]
+    assert r.verify(wl, copies=copies)[:3] == (10, 3, -1)
