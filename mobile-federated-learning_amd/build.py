@@ -35,6 +35,7 @@ HIP_SOURCES = [CSRC_DIR / "fedavg_reduce.hip", CSRC_DIR / "fedavg_dist.hip",
 PROBE_SOURCES = [CSRC_DIR / "fedavg_variants.hip"]  # probe library only
 CSRC_HOST = CSRC_DIR / "fedavg_host.cpp"
 CSRC_COMMON = CSRC_DIR / "common.hpp"
+CSRC_STAGING = CSRC_DIR / "staging.hpp"  # host-side staged layouts (also g++-built by tests/native)
 CSRC_COLLECT = CSRC_DIR / "fedavg_collect_ext.cpp"
 COLLECT_NAME = "fedavg_collect_ext"
 INCLUDE = REPO_DIR / "include"
@@ -65,7 +66,7 @@ def hipcc_path() -> str:
 
 
 def sources():
-    return [*HIP_SOURCES, *PROBE_SOURCES, CSRC_HOST, CSRC_COMMON, INCLUDE / "fedavg_amd.h",
+    return [*HIP_SOURCES, *PROBE_SOURCES, CSRC_HOST, CSRC_COMMON, CSRC_STAGING, INCLUDE / "fedavg_amd.h",
             INCLUDE / "fedavg_amd_tuning.h", Path(__file__)]
 
 

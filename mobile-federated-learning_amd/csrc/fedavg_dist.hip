@@ -867,7 +867,9 @@ int launch_fused_rs(const float* clients, int64_t K, int64_t P, int64_t ld, cons
 // slice (num_records 0 past the last window: the tail's reloads are dropped
 // in the address unit, no traffic), columns past P inside the last slice are
 // zeroed before the chain.
-// MODE 1: loads only (a traffic probe: wrong results).
+// MODE 1: loads only (a traffic probe: wrong results).  MODE 4 (probe):
+// squares in fp32 (the VEC columns' fl32(d*d) summed in fp32, widened once
+// per row): the fp64 VALU stream's share of time and clock, measured.
 // ---------------------------------------------------------------------------
 // (window helpers: WinVec, fold32/16/8, win_batch_row, win_load, win_sq in common.hpp)
 
@@ -1002,12 +1004,12 @@ __global__ __launch_bounds__(64 * NW, MINW) void reduce_sqdist_win_kernel(
                            voff);
       rp += row_bytes;
     };
-    if constexpr (MODE == 1) {
+    if constexpr ((MODE & 1) != 0) {
 #pragma unroll
       for (int i = 0; i < KMAX; ++i) {
 #pragma unroll
         for (int v = 0; v < VEC; ++v) probe += x[i][v];
-        reload(i);
+        if (i >= E) reload(i);
       }
       continue;
     }
@@ -1072,7 +1074,15 @@ __global__ __launch_bounds__(64 * NW, MINW) void reduce_sqdist_win_kernel(
         const int i = 8 * b + j;
         p[j] = 0.0;
         if (i < KMAX) {
-          p[j] = win_sq<VEC>(x[i] - a);
+          if constexpr ((MODE & 4) != 0) {  // probe: fp32 squares
+            const V d = x[i] - a;
+            float sq = d[0] * d[0];
+#pragma unroll
+            for (int v = 1; v < VEC; ++v) sq = sq + d[v] * d[v];
+            p[j] = static_cast<double>(sq);
+          } else {
+            p[j] = win_sq<VEC>(x[i] - a);
+          }
           if (i >= E) reload(i);
         }
       }
@@ -1086,7 +1096,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void reduce_sqdist_win_kernel(
     }
     if constexpr ((MODE & 2) != 0) __builtin_amdgcn_s_setprio(0);
   }
-  if constexpr (MODE == 1) {
+  if constexpr ((MODE & 1) != 0) {
     if (probe == 12345.f) out[0] = probe;  // keep the loads
     return;
   }
@@ -1130,7 +1140,7 @@ int launch_fused_win(const float* clients, int64_t K, int64_t P, int64_t ld, con
   hipLaunchKernelGGL((reduce_sqdist_win_kernel<KMAX, VEC, NW, MODE, MINW>), dim3(static_cast<unsigned>(waves / NW)),
                      dim3(64 * NW), 0, s, clients, static_cast<int>(K), ld, P, nwin, weights, out, partials);
   int rc = launch_status(what);
-  if (rc || MODE == 1) return rc;
+  if (rc || (MODE & 1) != 0) return rc;
   hipLaunchKernelGGL(client_sqdist_finalize_kernel, dim3(static_cast<unsigned>(K)), dim3(kBlock), 0, s, partials,
                      waves, sumsq);
   return launch_status(what);
@@ -1152,8 +1162,16 @@ int launch_fused_win(const float* clients, int64_t K, int64_t P, int64_t ld, con
 // one workgroup per CU nothing else is in flight then: the reloads wait for
 // the squares, the squares for the chain's last wave); after squaring row
 // i < PF the wave takes the prefetched row instead of reloading it.
+// LE > 0 (round 6 probe): rows PF .. PF+LE-1 of the next window go to LDS by
+// LDS-DMA as the window starts (no registers: the row loads stream through
+// the chain), and are read back in the squares in place of their reloads.
+// MODE (probe, timing only): 1 = no chain (every wave takes x[0] as the
+// average, no hand-offs), 2 = no squares (rows reloaded, nothing summed).
 // ---------------------------------------------------------------------------
-template <int KH, int VEC, int NSMAX, int PF = 0>
+// s_waitcnt vmcnt(0) expcnt(7) lgkmcnt(15) (gfx9 encoding: vmcnt in [3:0] and [15:14])
+constexpr int kWaitVmcnt0 = 0x0F70;
+
+template <int KH, int VEC, int NSMAX, int PF = 0, int LE = 0, int MODE = 0>
 __global__ __launch_bounds__(64 * NSMAX, win_min_waves(KH, VEC)) void reduce_sqdist_winn_kernel(
     const float* __restrict__ X, int K, int64_t ld, int64_t P, int64_t nwin, const float* __restrict__ W,
     float* __restrict__ out, double* __restrict__ partials) {
@@ -1178,6 +1196,9 @@ __global__ __launch_bounds__(64 * NSMAX, win_min_waves(KH, VEC)) void reduce_sqd
   __shared__ __attribute__((aligned(16))) float wl[NSMAX][KP];
   __shared__ double accl[NSMAX][NB][64];
   __shared__ __attribute__((aligned(16))) V xa[64];
+  static_assert(LE == 0 || VEC == 1, "LDS rows: 256-B row segments");
+  static_assert(PF + LE <= KH, "prefetched rows");
+  __shared__ __attribute__((aligned(16))) float rowl[LE > 0 ? NSMAX : 1][LE > 0 ? LE : 1][64];
   for (int i = threadIdx.x; i < ns * KP; i += blockDim.x) {
     const int hh = i / KP, j = i % KP, row = hh * KH + j;
     wl[hh][j] = (j < KH && row < K) ? W[row] : -0.0f;
@@ -1229,11 +1250,30 @@ __global__ __launch_bounds__(64 * NSMAX, win_min_waves(KH, VEC)) void reduce_sqd
     const int nbn = win_bytes(w + G);
     const char* rp = reinterpret_cast<const char*>(X + (w + G) * WC) + r0 * row_bytes;
     if constexpr (PF > 0) {
+      // this window's rows (reloaded in the last window's squares) first: a
+      // pre-existing wait the compiler's waitcnt pass accounts for, so the
+      // chain's uses of x[] need no wait on the prefetches issued below (it
+      // otherwise entered the turn loop with vmcnt(0): every wave waited for
+      // its prefetched rows of the NEXT window before its turn)
+      __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
 #pragma unroll
       for (int i = 0; i < PF; ++i) {
         asm volatile("" : "+s"(rp));
         xp[i] = win_load<VEC>(
             __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(rp), 0, r0 + i < Kw ? nbn : 0, 0x00020000), voff);
+        rp += row_bytes;
+      }
+    }
+    if constexpr (LE > 0) {
+      // the last window's LDS rows have been read out (their ds_reads done)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      typedef __attribute__((address_space(3))) void* lds_ptr_t;
+#pragma unroll
+      for (int i = 0; i < LE; ++i) {
+        asm volatile("" : "+s"(rp));
+        const __amdgpu_buffer_rsrc_t r =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(rp), 0, r0 + PF + i < Kw ? nbn : 0, 0x00020000);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)&rowl[h][i][0], 4, lane * 4, 0, 0, 2);
         rp += row_bytes;
       }
     }
@@ -1247,6 +1287,9 @@ __global__ __launch_bounds__(64 * NSMAX, win_min_waves(KH, VEC)) void reduce_sqd
       }
     }
     V a;
+    if constexpr ((MODE & 1) != 0) {  // probe: no chain
+      a = x[0];
+    } else
     for (int st = 0; st < ns; ++st) {  // the chain, wave by wave in row order
       if (h == st) {
         if (st > 0) a = xa[lane];
@@ -1265,7 +1308,9 @@ __global__ __launch_bounds__(64 * NSMAX, win_min_waves(KH, VEC)) void reduce_sqd
       }
       __syncthreads();
     }
-    if (h != ns - 1) a = xa[lane];
+    if constexpr ((MODE & 1) == 0) {
+      if (h != ns - 1) a = xa[lane];
+    }
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       double p[8];
@@ -1274,9 +1319,11 @@ __global__ __launch_bounds__(64 * NSMAX, win_min_waves(KH, VEC)) void reduce_sqd
         const int i = 8 * b + j;
         p[j] = 0.0;
         if (i < KH) {
-          p[j] = win_sq<VEC>(x[i] - a);
+          if constexpr ((MODE & 2) == 0) p[j] = win_sq<VEC>(x[i] - a);
           if (i < PF) {
             x[i] = xp[i < PF ? i : 0];
+          } else if (i < PF + LE) {
+            x[i][0] = rowl[h][i - PF < LE ? i - PF : 0][lane];
           } else {
             asm volatile("" : "+s"(rp));
             x[i] = win_load<VEC>(
@@ -1307,12 +1354,12 @@ __global__ __launch_bounds__(64 * NSMAX, win_min_waves(KH, VEC)) void reduce_sqd
 // waves each) rounded down to a power of two per CU -- 3 workgroups of 5
 // waves on a CU ran 12-15 % slower than 2 (profiles/r05/prefetch/) --, at
 // most one per window
-template <int KH, int VEC, int NSMAX, int PF = 0>
+template <int KH, int VEC, int NSMAX, int PF = 0, int LE = 0, int MODE = 0>
 int64_t fused_winn_grid(int64_t K, int64_t P, int blocks_per_cu) {
   const int ns = static_cast<int>((K + KH - 1) / KH);
   int64_t per_cu = blocks_per_cu;
   if (per_cu <= 0) {
-    const int64_t r = resident_blocks(reduce_sqdist_winn_kernel<KH, VEC, NSMAX, PF>, 64 * ns) / cu_count();
+    const int64_t r = resident_blocks(reduce_sqdist_winn_kernel<KH, VEC, NSMAX, PF, LE, MODE>, 64 * ns) / cu_count();
     per_cu = 0;  // none resident: the caller reports it (grid 0)
     if (r >= 1)
       for (per_cu = 1; per_cu * 2 <= r;) per_cu *= 2;
@@ -1322,18 +1369,18 @@ int64_t fused_winn_grid(int64_t K, int64_t P, int blocks_per_cu) {
   return grid < nwin ? grid : nwin;
 }
 
-template <int KH, int VEC, int NSMAX, int PF = 0>
+template <int KH, int VEC, int NSMAX, int PF = 0, int LE = 0, int MODE = 0>
 int launch_fused_winn(const float* clients, int64_t K, int64_t P, int64_t ld, const float* weights, float* out,
                       double* partials, int64_t partial_elems, double* sumsq, int blocks_per_cu, hipStream_t s,
                       const char* what) {
   if (K > NSMAX * KH) return set_error(FEDAVG_EMODE, "%s: this split window kernel covers K <= %d", what, NSMAX * KH);
   const int ns = static_cast<int>((K + KH - 1) / KH);
   const int64_t nwin = (P + 64 * VEC - 1) / (64 * VEC);
-  const int64_t grid = fused_winn_grid<KH, VEC, NSMAX, PF>(K, P, blocks_per_cu);
+  const int64_t grid = fused_winn_grid<KH, VEC, NSMAX, PF, LE, MODE>(K, P, blocks_per_cu);
   if (grid <= 0) return set_error(FEDAVG_EMODE, "%s: the split window kernel is not resident", what);
   if (partial_elems < K * grid)
     return set_error(FEDAVG_EINVAL, "%s: workspace needs %lld doubles", what, (long long)(K * grid));
-  hipLaunchKernelGGL((reduce_sqdist_winn_kernel<KH, VEC, NSMAX, PF>), dim3(static_cast<unsigned>(grid)),
+  hipLaunchKernelGGL((reduce_sqdist_winn_kernel<KH, VEC, NSMAX, PF, LE, MODE>), dim3(static_cast<unsigned>(grid)),
                      dim3(static_cast<unsigned>(64 * ns)), 0, s, clients, static_cast<int>(K), ld, P, nwin, weights,
                      out, partials);
   int rc = launch_status(what);
@@ -2174,6 +2221,8 @@ int fedavg_reduce_sqdist_f32_variant(const float* clients, int64_t K, int64_t P,
     FEDAVG_WIN_CASE(2, 1, 64)
     FEDAVG_WIN_CASE(2, 2, 64)
     FEDAVG_WIN_CASE(2, 4, 128)
+    FEDAVG_WIN_CASE(2, 4, 65)  // LDS rows, loads only (round 6 clock attribution)
+    FEDAVG_WIN_CASE(2, 4, 68)  // LDS rows, fp32 squares
     case 60000000 + 192 * 1000000 + 42:  // LDS rows + 8-row descriptors
       return launch_fused_win<100, 2, 4, 192>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq,
                                               blocks_per_cu, s, what);
@@ -2233,6 +2282,36 @@ int fedavg_reduce_sqdist_f32_variant(const float* clients, int64_t K, int64_t P,
     FEDAVG_WINNPF_CASE(16, 16)
     FEDAVG_WINNPF_CASE(16, 24)
 #undef FEDAVG_WINNPF_CASE
+    // round 6: 128 rows per wave (2 waves per SIMD: 256 registers), half the
+    // chain's hand-offs of the 64-row form and room for a deep prefetch:
+    // 89000000 + PF * 100 + NSMAX
+#define FEDAVG_WINN128_CASE(NSMAX, PF)                                                                            \
+  case 89000000 + PF * 100 + NSMAX:                                                                              \
+    return launch_fused_winn<128, 1, NSMAX, PF>(clients, K, P, ld, weights, out, workspace, workspace_elems,       \
+                                                sumsq, blocks_per_cu, s, what);
+    FEDAVG_WINN128_CASE(8, 0)
+    FEDAVG_WINN128_CASE(8, 16)
+    FEDAVG_WINN128_CASE(8, 32)
+    FEDAVG_WINN128_CASE(8, 48)
+    FEDAVG_WINN128_CASE(8, 64)
+    FEDAVG_WINN128_CASE(8, 80)
+#undef FEDAVG_WINN128_CASE
+    // round 6: 64-row split windows with LE rows of the next window in LDS
+    // (LDS-DMA through the chain) and timing modes: 88000000 + MODE * 100000
+    // + LE * 100 + PF (NSMAX 16)
+#define FEDAVG_WINNLE_CASE(PF, LE, MODE)                                                                         \
+  case 88000000 + MODE * 100000 + LE * 100 + PF:                                                                 \
+    return launch_fused_winn<64, 1, 16, PF, LE, MODE>(clients, K, P, ld, weights, out, workspace, workspace_elems, \
+                                                      sumsq, blocks_per_cu, s, what);
+    FEDAVG_WINNLE_CASE(8, 0, 1)
+    FEDAVG_WINNLE_CASE(8, 0, 2)
+    FEDAVG_WINNLE_CASE(8, 0, 3)
+    FEDAVG_WINNLE_CASE(8, 8, 0)
+    FEDAVG_WINNLE_CASE(8, 16, 0)
+    FEDAVG_WINNLE_CASE(8, 22, 0)
+    FEDAVG_WINNLE_CASE(0, 22, 0)
+    FEDAVG_WINNLE_CASE(16, 22, 0)
+#undef FEDAVG_WINNLE_CASE
     default: return set_error(FEDAVG_EMODE, "%s: cols must be 32, 64, 128 or 256 (+1000: double-buffered)", what);
   }
 }

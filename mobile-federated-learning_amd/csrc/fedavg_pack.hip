@@ -26,6 +26,7 @@
 // items are copied as bit patterns (NaN payloads kept).  HBM-bound: per
 // element, the source bytes read + elem_size bytes written.
 #include "common.hpp"
+#include "staging.hpp"
 
 namespace {
 using namespace fedavg_impl;
@@ -179,15 +180,15 @@ __global__ __launch_bounds__(kPackThreads) void pack_small_items_kernel(const fe
 constexpr int64_t kSmallItemAvg = 64;
 constexpr int64_t kSmallItemMax = 4096;
 
-int64_t items_bytes(int64_t n_items) { return n_items * static_cast<int64_t>(sizeof(fedavg_pack_item)); }
+// the staged items | starts layout: staging.hpp (g++-built for the sanitizer fuzz)
+int64_t items_bytes(int64_t n_items) { return fedavg_staging::pack_items_bytes(n_items); }
 
 }  // namespace
 
 extern "C" {
 
 int64_t fedavg_pack_rows_device_workspace(int64_t n_items) {
-  if (n_items < 0) return -1;
-  return items_bytes(n_items) + (n_items + 1) * static_cast<int64_t>(sizeof(int64_t));
+  return fedavg_staging::pack_rows_device_workspace_bytes(n_items);
 }
 
 int fedavg_pack_rows_device(const fedavg_pack_item* items, int64_t n_items, void* dst_base, int64_t elem_size,
@@ -205,26 +206,13 @@ int fedavg_pack_rows_device(const fedavg_pack_item* items, int64_t n_items, void
   if (!is_device_memory(dst_base) || !is_device_memory(dev_ws))
     return set_error(FEDAVG_EINVAL, "%s: dst_base and dev_ws must be device memory", what);
   if (!is_pinned_host_memory(host_ws)) return set_error(FEDAVG_EINVAL, "%s: host_ws is not pinned host memory", what);
-  auto* h_items = static_cast<fedavg_pack_item*>(host_ws);
-  auto* h_start = reinterpret_cast<int64_t*>(static_cast<char*>(host_ws) + items_bytes(n_items));
-  int64_t total = 0, max_numel = 0;
-  const void* first_src = nullptr;
-  const void* last_src = nullptr;
-  for (int64_t i = 0; i < n_items; ++i) {
-    const fedavg_pack_item& it = items[i];
-    if (it.numel < 0 || it.dst_offset < 0 || it.kind < kRaw || it.kind > kBool || (it.numel > 0 && !it.src) ||
-        (it.kind != kRaw && elem_size != 4))
-      return set_error(FEDAVG_EINVAL, "%s: bad item %lld", what, (long long)i);
-    h_items[i] = it;
-    h_start[i] = total;
-    total += it.numel;
-    if (it.numel > max_numel) max_numel = it.numel;
-    if (it.numel > 0) {
-      if (!first_src) first_src = reinterpret_cast<const void*>(it.src);
-      last_src = reinterpret_cast<const void*>(it.src);
-    }
-  }
-  h_start[n_items] = total;
+  fedavg_staging::PackOut st;
+  fedavg_staging::Msg msg;
+  if (const int rc = fedavg_staging::stage_pack_items(items, n_items, elem_size, host_ws, ws_bytes, &st, &msg))
+    return set_error(rc, "%s: %s", what, msg.text);
+  const int64_t total = st.total, max_numel = st.max_numel;
+  const void* first_src = st.first_src;
+  const void* last_src = st.last_src;
   if (total == 0) return FEDAVG_OK;
   const int64_t blocks = (total + kPackBlockElems - 1) / kPackBlockElems;
   if (blocks > INT32_MAX) return set_error(FEDAVG_EINVAL, "%s: %lld elements exceed one launch", what, (long long)total);

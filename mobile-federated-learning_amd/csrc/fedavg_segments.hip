@@ -19,12 +19,32 @@
 // key-major in round-split launches of 3 x CUs workgroups, so a launch streams
 // one compact window of every client's tensors, like the row-major reduce.
 #include "common.hpp"
+#include "staging.hpp"
 
 #include <chrono>
 #include <vector>
 
 namespace {
 using namespace fedavg_impl;
+// the host-side staged layouts (key table, pointer table, descriptor table,
+// workspace sizes): staging.hpp, which g++ also builds for the sanitizer fuzz
+using fedavg_staging::kBool;
+using fedavg_staging::kI16;
+using fedavg_staging::kI32;
+using fedavg_staging::kI64;
+using fedavg_staging::kI8;
+using fedavg_staging::kRaw;
+using fedavg_staging::kSegDescMaxBytes;
+using fedavg_staging::kSegUnitMapMax;
+using fedavg_staging::kSegWinTablePad;
+using fedavg_staging::kU8;
+using fedavg_staging::kWinRsrcFlags;
+using fedavg_staging::IntKey;
+using fedavg_staging::round16;
+using fedavg_staging::round_ws;
+using fedavg_staging::RoundWs;
+using fedavg_staging::seg_desc_bytes;
+using fedavg_staging::SegKey;
 
 typedef f32x4 f32x4_a4 __attribute__((aligned(4)));  // dword-aligned 16-B vector (client tensors, outputs)
 
@@ -69,11 +89,6 @@ constexpr int kSegDistC = 8;
 constexpr int64_t kSegDistSpan = static_cast<int64_t>(kBlock) * kSegDistC * 4;
 constexpr int64_t kSegSpanMaxBytes = static_cast<int64_t>(kBlock) * 16 * 16;  // widest unit (C = 16), bytes
 
-enum : int64_t { kRaw = 0, kI64 = 1, kI32 = 2, kI16 = 3, kI8 = 4, kU8 = 5, kBool = 6 };
-
-struct SegKey {
-  int64_t numel, out_offset, kind, unit_start;
-};
 
 // the key owning unit u (keys without units share their successor's start
 // and lose the tie)
@@ -657,7 +672,6 @@ __global__ __launch_bounds__(kBlock, LADDR && S != 32 ? 6 : 1) void reduce_sqdis
 // pointer table is padded by kSegWinTablePad entries so every group's 8
 // addresses load unconditionally (a padding row's is never dereferenced).
 // ---------------------------------------------------------------------------
-constexpr int64_t kSegWinTablePad = 128;
 constexpr int64_t kSegWinMinPerWave = 16;  // windows per wave below which the LDS-DMA tiles keep the round
 
 // DESC (round 5): every fast window's K client descriptors come from a
@@ -673,7 +687,6 @@ constexpr int64_t kSegWinMinPerWave = 16;  // windows per wave below which the L
 // 0: the loads return 0 and touch nothing), and the ragged window is loaded
 // after the squares from the pointer table as before.
 typedef __attribute__((address_space(4))) const u32x4* cdesc_t;
-constexpr uint32_t kWinRsrcFlags = 0x00020000;
 
 template <int KMAX, int VEC, int NW, bool DESC = false, int MINW = win_min_waves(KMAX, VEC)>
 __global__ __launch_bounds__(64 * NW, MINW) void reduce_sqdist_segwin_kernel(
@@ -1277,32 +1290,16 @@ int64_t stage_tables(const char* what, const int64_t* client_ptrs, const int64_t
   if (!aligned16(host_ws) || !aligned16(dev_ws)) return set_error(FEDAVG_EALIGN, "%s: workspaces must be 16-B aligned", what);
   if (!is_pinned_host_memory(host_ws)) return set_error(FEDAVG_EINVAL, "%s: host_ws is not pinned host memory", what);
   if (!is_device_memory(dev_ws)) return set_error(FEDAVG_EINVAL, "%s: dev_ws must be device memory", what);
-  auto* hk = static_cast<SegKey*>(host_ws);
-  auto* hp = reinterpret_cast<int64_t*>(static_cast<char*>(host_ws) + n_keys * static_cast<int64_t>(sizeof(SegKey)));
-  int64_t units = 0;
-  const void* first_src = nullptr;
-  const void* last_src = nullptr;
-  for (int64_t j = 0; j < n_keys; ++j) {
-    if (numel[j] < 0 || offset[j] < 0 || kind[j] < kRaw || kind[j] > kBool)
-      return set_error(FEDAVG_EINVAL, "%s: bad key %lld", what, (long long)j);
-    hk[j] = SegKey{numel[j], offset[j], kind[j], units};
-    units += (numel[j] + span - 1) / span;
-    for (int64_t k = 0; k < K; ++k) {
-      const int64_t p = client_ptrs[k * n_keys + j];
-      if (numel[j] > 0) {
-        if (p == 0 || (kind[j] == kRaw && (p & 3) != 0))
-          return set_error(FEDAVG_EINVAL, "%s: client %lld key %lld: null or misaligned source", what, (long long)k,
-                           (long long)j);
-        if (!first_src) first_src = reinterpret_cast<const void*>(p);
-        last_src = reinterpret_cast<const void*>(p);
-      }
-      hp[j * K + k] = p;
-    }
-  }
+  fedavg_staging::TablesOut st;
+  fedavg_staging::Msg msg;
+  if (const int rc = fedavg_staging::stage_segment_tables(client_ptrs, numel, offset, kind, n_keys, K, host_ws, ws_bytes,
+                                                          span, &st, &msg))
+    return set_error(rc, "%s: %s", what, msg.text);
+  const int64_t units = st.units;
   if (units == 0) return 0;
   // a host address would fault the kernels: spot check of the first and last
   // source (the Python layer checks every tensor's device)
-  if (!is_device_memory(first_src) || !is_device_memory(last_src))
+  if (!is_device_memory(st.first_src) || !is_device_memory(st.last_src))
     return set_error(FEDAVG_EINVAL, "%s: client sources must be device memory", what);
   const hipError_t e = hipMemcpyAsync(dev_ws, host_ws, static_cast<size_t>(fedavg_segments_workspace(K, n_keys)),
                                       hipMemcpyHostToDevice, s);
@@ -1474,26 +1471,9 @@ int launch_seg_fused(const SegFusedPlan& p, const SegKey* keys, const int64_t* t
 //   SegKey[n_keys] | int64 ptrs[n_keys * K + kSegWinTablePad] | float w[K] |
 //   IntKey[n_keys] | int64 int_src[n_keys * K]
 // ---------------------------------------------------------------------------
-struct IntKey {
-  int64_t numel, kind, col;  // col: the key's first column in a client's scratch row
-};
-
-inline int64_t round16(int64_t b) { return (b + 15) & ~int64_t(15); }
-
-struct RoundWs {
-  int64_t ptrs, w, ik, isrc, end, desc_room;  // desc_room: the unit map's / descriptor table's reserved bytes
-};
-
-// the tile kernel's unit -> key map is staged for rounds of at most this many
-// units (256 KiB; a model of more units at 17-128 clients takes the windows)
-constexpr int64_t kSegUnitMapMax = 65536;
-
-// the windows' descriptor table (reduce_sqdist_segwin_kernel DESC): KMAX
-// entries per key plus KMAX null ones, staged for tables of at most this size
-constexpr int64_t kSegDescMaxBytes = int64_t(4) << 20;
-inline int64_t seg_desc_bytes(int64_t n_keys, int64_t kmax = 128) {
-  return (n_keys + 1) * kmax * static_cast<int64_t>(sizeof(u32x4));
-}
+// (IntKey, RoundWs / round_ws, the unit map's and the descriptor table's
+// limits: staging.hpp; a tile round of more than kSegUnitMapMax units at
+// 17-128 clients takes the windows)
 
 // FEDAVG_SEGWIN_DESC=0 keeps the windows' pointer form (probes, A/B)
 inline bool segwin_desc_disabled() {
@@ -1504,20 +1484,6 @@ inline bool segwin_desc_disabled() {
   return off;
 }
 
-inline RoundWs round_ws(int64_t K, int64_t n_keys) {
-  RoundWs r;
-  r.ptrs = n_keys * static_cast<int64_t>(sizeof(SegKey));
-  r.w = round16(r.ptrs + (n_keys * K + kSegWinTablePad) * static_cast<int64_t>(sizeof(int64_t)));
-  r.ik = r.w + round16(K * static_cast<int64_t>(sizeof(float)));
-  r.isrc = r.ik + round16(n_keys * static_cast<int64_t>(sizeof(IntKey)));
-  // + room for the tiles' unit map OR the windows' descriptor table (a round
-  // uses one of them), placed right after whatever part is used
-  const int64_t map_bytes = kSegUnitMapMax * static_cast<int64_t>(sizeof(int));
-  const int64_t desc = seg_desc_bytes(n_keys) <= kSegDescMaxBytes ? seg_desc_bytes(n_keys) : 0;
-  r.desc_room = map_bytes > desc ? map_bytes : desc;
-  r.end = round16(r.isrc + n_keys * K * static_cast<int64_t>(sizeof(int64_t))) + r.desc_room;
-  return r;
-}
 
 // a fused round's integer / bool keys as fp32 columns of the [K, S] scratch:
 // one wave per (key, client) item, the packers' static_cast (fedavg_pack.hip)
@@ -1537,9 +1503,7 @@ __global__ __launch_bounds__(64) void int_keys_to_f32_kernel(const IntKey* __res
 extern "C" {
 
 int64_t fedavg_segments_workspace(int64_t K, int64_t n_keys) {
-  if (K <= 0 || n_keys <= 0) return 0;
-  return n_keys * static_cast<int64_t>(sizeof(SegKey)) +
-         (n_keys * K + kSegWinTablePad) * static_cast<int64_t>(sizeof(int64_t));
+  return fedavg_staging::segments_workspace_bytes(K, n_keys);
 }
 
 int64_t fedavg_segments_partials(const int64_t* key_numel, int64_t n_keys, int64_t K) {
@@ -1742,117 +1706,49 @@ int fedavg_device_round_f32(const int64_t* client_ptrs, int64_t ptr_ld, const in
   if (sumsq && (!is_device_memory(sumsq) || !is_device_memory(partials)))
     return set_error(FEDAVG_EINVAL, "%s: partials and sumsq must be device memory", what);
   FEDAVG_ROUND_MARK(1);  // argument and pointer-attribute checks
-  char* hb = static_cast<char*>(host_ws);
-  auto* hk = reinterpret_cast<SegKey*>(hb);
-  auto* hp = reinterpret_cast<int64_t*>(hb + L.ptrs);
-  auto* hw = reinterpret_cast<float*>(hb + L.w);
-  auto* hik = reinterpret_cast<IntKey*>(hb + L.ik);
-  auto* hsrc = reinterpret_cast<int64_t*>(hb + L.isrc);
-  // keys: validation, the integer keys' scratch columns
-  int64_t S = 0, n_int = 0;
-  for (int64_t j = 0; j < n_keys; ++j) {
-    const int64_t col = key_index ? key_index[j] : j;
-    if (key_numel[j] < 0 || key_offset[j] < 0 || key_kind[j] < kRaw || key_kind[j] > kBool || col < 0 ||
-        (key_index && col >= ptr_ld))
-      return set_error(FEDAVG_EINVAL, "%s: bad key %lld", what, (long long)j);
-    if (key_kind[j] != kRaw && key_numel[j] > 0) {
-      S += (key_numel[j] + 3) & ~int64_t(3);
-      ++n_int;
-    }
-  }
-  const int64_t ld = ptr_ld;
-  if (S >= (int64_t(1) << 31)) return set_error(FEDAVG_EINVAL, "%s: integer keys too large", what);
-  bool fuse = sumsq != nullptr && (K <= kSegFusedMaxK || (K <= kSegSplitMaxK && seg_split_ok(key_numel, n_keys)));
+  const bool fuse_req = sumsq != nullptr && (K <= kSegFusedMaxK || (K <= kSegSplitMaxK && seg_split_ok(key_numel, n_keys)));
   // a fused round takes its integer keys as fp32 scratch columns: the window
   // kernels read fp32 only, and the tiles' in-kernel conversion (element by
   // element, one tile per key and client block) made resnet56 x 100's fused
   // tile kernel 104 us against 77 + 4.7 us with the conversion launch
   // (profiles/r04/segwin_layout/); the two-pass reduce converts in-kernel
-  if (fuse && n_int > 0 &&
-      (!int_scratch || scratch_elems < K * S || !aligned16(int_scratch) || !is_device_memory(int_scratch)))
-    return set_error(FEDAVG_EINVAL, "%s: integer keys need an aligned device scratch of %lld floats", what,
-                     (long long)(K * S));
-  FEDAVG_ROUND_MARK(2);  // key validation
-  // the pointer table, key-major; fused rounds need 16-B aligned fp32 sources
-  // (a misaligned one sends the round to the reduce alone, rewritten below).
-  // Client-major walk: the walk's table was just written by other threads
-  // (fedavg_collect_ext), and read row by row -- the order the hardware
-  // prefetcher follows -- the call took 73-78 us right after a resnet56 x 100
-  // walk, against 182-200 us filling key-major and 79-86 us in blocks of 8
-  // clients; with the checks branch-free per row, 63-65 us, 44 of them the
-  // fill (scripts/device_round_call_probe.py, profiles/r04/device_round/).
-  const void* first_src = nullptr;
-  const void* last_src = nullptr;
-  // per key: table column, the masks its sources are checked with (a
-  // non-empty key needs a non-null source; fp32 sources 4-B aligned, 16-B
-  // for the fused pass), and for a converted integer key its int_src row and
-  // scratch column
-  struct KeyFill {
-    int64_t col, need, align, fuse_mask;
-  };
-  thread_local std::vector<KeyFill> kf;
-  thread_local std::vector<int64_t> conv_j, conv_col;
-  kf.resize(static_cast<size_t>(n_keys));
-  for (int64_t j = 0; j < n_keys; ++j) {
-    const bool live = key_numel[j] > 0, raw = key_kind[j] == kRaw;
-    kf[j] = KeyFill{key_index ? key_index[j] : j, live ? 1 : 0, live && raw ? 3 : 0, live && raw ? 15 : 0};
+  if (fuse_req && int_scratch) {
+    int64_t n_int = 0;
+    fedavg_staging::int_scratch_cols(key_numel, key_kind, n_keys, &n_int);
+    if (n_int > 0 && !is_device_memory(int_scratch))
+      return set_error(FEDAVG_EINVAL, "%s: the integer keys' scratch must be device memory", what);
   }
-  const auto fill = [&](bool convert) -> int {
-    // every entry as is, branch-free checks accumulated per client row ...
-    int64_t fuse_bits = 0;
-    for (int64_t k = 0; k < K; ++k) {
-      const int64_t* row = client_ptrs + k * ld;
-      int64_t bad = 0;
-      for (int64_t j = 0; j < n_keys; ++j) {
-        const KeyFill f = kf[j];
-        const int64_t p = row[f.col];
-        hp[j * K + k] = p;
-        bad |= (f.need & static_cast<int64_t>(p == 0)) | (p & f.align);
-        fuse_bits |= p & f.fuse_mask;
-      }
-      if (bad) {
-        for (int64_t j = 0; j < n_keys; ++j) {
-          const int64_t p = row[kf[j].col];
-          if ((kf[j].need && p == 0) || (p & kf[j].align))
-            return set_error(FEDAVG_EINVAL, "%s: client %lld key %lld: null or misaligned source", what,
-                             (long long)k, (long long)j);
-        }
-      }
+  FEDAVG_ROUND_MARK(2);  // key validation
+  // Everything the host writes before the tables' H2D (staging.hpp): the key
+  // validation, the pointer table (client-major walk: the walk's table was
+  // just written by other threads in fedavg_collect_ext and read row by row
+  // -- the order the hardware prefetcher follows -- the call took 73-78 us
+  // right after a resnet56 x 100 walk, against 182-200 us filling key-major;
+  // branch-free checks per row: 63-65 us, scripts/device_round_call_probe.py,
+  // profiles/r04/device_round/), the integer keys' scratch columns, the plan,
+  // the key table, the tiles' unit map or the windows' descriptor table, the
+  // weights.
+  SegFusedPlan plan{false, 0, 0, 0};
+  const auto plan_fn = [&](bool fuse, bool all_raw) -> fedavg_staging::RoundPlan {
+    if (fuse) {
+      plan = seg_fused_plan(key_numel, n_keys, K, all_raw);
+      return fedavg_staging::RoundPlan{plan.win, plan.kmax, plan.span, false};
     }
-    if (fuse_bits) fuse = false;
-    // ... then the converted integer keys pointed at their scratch columns
-    conv_j.clear();
-    conv_col.clear();
-    if (convert && fuse) {
-      int64_t soff = 0;
-      for (int64_t j = 0; j < n_keys; ++j)
-        if (key_kind[j] != kRaw && key_numel[j] > 0) {
-          hik[conv_j.size()] = IntKey{key_numel[j], key_kind[j], soff};
-          conv_j.push_back(j);
-          conv_col.push_back(soff);
-          soff += (key_numel[j] + 3) & ~int64_t(3);
-        }
-      for (size_t q = 0; q < conv_j.size(); ++q) {
-        const int64_t j = conv_j[q];
-        for (int64_t k = 0; k < K; ++k) {
-          hsrc[static_cast<int64_t>(q) * K + k] = hp[j * K + k];
-          hp[j * K + k] = reinterpret_cast<int64_t>(int_scratch + k * S + conv_col[q]);
-        }
-      }
-    }
-    // the spot-checked sources: client 0's first and client K-1's last non-empty key
-    for (int64_t j = 0; j < n_keys && !first_src; ++j)
-      if (kf[j].need) first_src = reinterpret_cast<const void*>(client_ptrs[kf[j].col]);
-    for (int64_t j = n_keys - 1; j >= 0 && !last_src; --j)
-      if (kf[j].need) last_src = reinterpret_cast<const void*>(client_ptrs[(K - 1) * ld + kf[j].col]);
-    return FEDAVG_OK;
+    const bool small = segments_small(key_numel, n_keys);
+    return fedavg_staging::RoundPlan{false, 0, small ? kSegSmallSpan : kSegSpan, small};
   };
-  const bool convert = fuse && n_int > 0;
-  int rc = fill(convert);  // a misaligned fp32 source clears `fuse`: the integer keys then stay as they are
-  if (rc) return rc;
-  const bool converted = convert && fuse;
+  const fedavg_staging::RoundIn rin{client_ptrs, ptr_ld, key_index, key_numel, key_offset, key_kind, n_keys, K,
+                                    weights, reinterpret_cast<int64_t>(int_scratch), int_scratch ? scratch_elems : 0,
+                                    fuse_req, segwin_desc_disabled()};
+  fedavg_staging::RoundOut st;
+  fedavg_staging::Msg msg;
+  int rc = fedavg_staging::stage_device_round(rin, host_ws, ws_bytes, plan_fn, &st, &msg);
+  if (rc) return set_error(rc, "%s: %s", what, msg.text);
   FEDAVG_ROUND_MARK(3);  // the pointer-table fill
-  if (!first_src) {  // every key empty
+  const bool fuse = st.fuse, converted = st.converted, small = st.plan.small;
+  const int64_t units = st.units, S = st.S, n_int = st.n_int, moff = st.moff;
+  const bool with_map = st.with_map, with_desc = st.with_desc;
+  if (!st.first_src) {  // every key empty
     if (sumsq) {
       const hipError_t e = hipMemsetAsync(sumsq, 0, static_cast<size_t>(K) * sizeof(double), static_cast<hipStream_t>(stream));
       if (e != hipSuccess) return set_error(-static_cast<int>(e), "%s: hipMemsetAsync failed", what);
@@ -1861,60 +1757,12 @@ int fedavg_device_round_f32(const int64_t* client_ptrs, int64_t ptr_ld, const in
   }
   // a host address would fault the kernels: spot check of the first and last
   // source (the Python layer checks every tensor's device)
-  if (!is_device_memory(first_src) || !is_device_memory(last_src))
+  if (!is_device_memory(st.first_src) || !is_device_memory(st.last_src))
     return set_error(FEDAVG_EINVAL, "%s: client sources must be device memory", what);
   FEDAVG_ROUND_MARK(4);  // the sources' spot check
-  // the unit width, then the key table
-  const bool all_raw = converted || n_int == 0;
-  const SegFusedPlan plan = fuse ? seg_fused_plan(key_numel, n_keys, K, all_raw) : SegFusedPlan{false, 0, 0, 0};
-  const bool small = !fuse && segments_small(key_numel, n_keys);
-  const int64_t span = fuse ? plan.span : (small ? kSegSmallSpan : kSegSpan);
-  int64_t units = 0;
-  for (int64_t j = 0; j < n_keys; ++j) {
-    hk[j] = SegKey{key_numel[j], key_offset[j], converted ? kRaw : key_kind[j], units};
-    units += (key_numel[j] + span - 1) / span;
-  }
-  // the tiles' unit -> key map (reduce_sqdist_segments_f32_kernel MAP)
-  const int64_t used = converted ? L.isrc + n_int * K * static_cast<int64_t>(sizeof(int64_t)) : L.ik;
-  const int64_t moff = round16(used);
-  const bool with_map = fuse && !plan.win && units > 0 && units <= kSegUnitMapMax;
-  if (with_map) {
-    int* hm = reinterpret_cast<int*>(hb + moff);
-    for (int64_t j = 0; j < n_keys; ++j) {
-      const int64_t u1 = j + 1 < n_keys ? hk[j + 1].unit_start : units;
-      for (int64_t u = hk[j].unit_start; u < u1; ++u) hm[u] = static_cast<int>(j);
-    }
-  }
-  // the windows' descriptor table: client i's address of key j, the key's
-  // byte length (the range check of every load of that key), the flags;
-  // padding rows and empty keys get a record count of 0, and KMAX null
-  // descriptors follow the last key (the reload target when the next
-  // window is not a full one)
-  const int64_t dbytes = plan.win && plan.kmax > 0 ? seg_desc_bytes(n_keys, plan.kmax) : 0;
-  // (within the room round_ws reserved: a table of more than 2,047 keys at
-  // KMAX 128 reserves none, and a smaller KMAX's table must not overrun it)
-  const bool with_desc =
-      plan.win && plan.kmax > 0 && dbytes <= kSegDescMaxBytes && dbytes <= L.desc_room && !segwin_desc_disabled();
-  if (with_desc) {
-    auto* hd = reinterpret_cast<u32x4*>(hb + moff);
-    const int64_t km = plan.kmax;
-    for (int64_t j = 0; j <= n_keys; ++j) {
-      const bool live = j < n_keys && key_numel[j] > 0;
-      const uint32_t nrec = live ? static_cast<uint32_t>(key_numel[j] * 4) : 0u;
-      for (int64_t i = 0; i < km; ++i) {
-        const uint64_t p = live && i < K ? static_cast<uint64_t>(hp[j * K + i]) : 0;
-        hd[j * km + i] = u32x4{static_cast<uint32_t>(p), static_cast<uint32_t>(p >> 32), p ? nrec : 0u,
-                               kWinRsrcFlags};
-      }
-    }
-  }
-  // the reference's weights n_i / N (fedavg_trainer.py:453) rounded once to
-  // fp32 (nearest even, the cast ATen applies to the scalar at :455)
-  for (int64_t k = 0; k < K; ++k) hw[k] = static_cast<float>(weights[k]);
-  FEDAVG_ROUND_MARK(5);  // plan, key table, weights
+  FEDAVG_ROUND_MARK(5);  // plan, key table, weights (staged above)
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const int64_t bytes = with_map ? moff + units * static_cast<int64_t>(sizeof(int)) : (with_desc ? moff + dbytes : used);
-  const hipError_t e = hipMemcpyAsync(dev_ws, host_ws, static_cast<size_t>(bytes), hipMemcpyHostToDevice, s);
+  const hipError_t e = hipMemcpyAsync(dev_ws, host_ws, static_cast<size_t>(st.bytes), hipMemcpyHostToDevice, s);
   if (e != hipSuccess) {
     (void)hipGetLastError();
     return set_error(-static_cast<int>(e), "%s: hipMemcpyAsync failed: %s", what, hipGetErrorString(e));

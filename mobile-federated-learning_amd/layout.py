@@ -21,8 +21,10 @@ Each group's row stride ``ld`` is its element count rounded up to
 """
 from __future__ import annotations
 
+import os
 from collections import OrderedDict
 from dataclasses import dataclass, field
+from pathlib import Path
 from typing import Dict, List, Mapping, Optional, Sequence, Tuple
 
 import numpy as np
@@ -97,7 +99,9 @@ def _collect_ext():
 
             from .build import collect_ext_path
 
-            path = collect_ext_path()
+            # FEDAVG_COLLECT_EXT_PATH: a sanitizer build of the same source
+            # (tests/test_native_sanitized.py); the in-tree build otherwise
+            path = Path(os.environ.get("FEDAVG_COLLECT_EXT_PATH") or collect_ext_path())
             if path.exists():
                 spec = importlib.util.spec_from_file_location("fedavg_collect_ext", path)
                 mod = importlib.util.module_from_spec(spec)
