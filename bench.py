@@ -992,6 +992,9 @@ def main(argv=None):
             out["dtype"] = "f32"
         if diagnostics is not None:
             out["diagnostics"] = diagnostics
+        if world > 1 or plan_world > 1:
+            out["north_star"] = north_star_block(args.workload, plan_world, roofline, out["step_frac_of_node_hbm"],
+                                                 args.scaling, measured_world=world)
         if not rehearsal and world == 1 and passes == 1:
             # the shader clock the chip held under the timed kernel's load (same launches, after
             # the timed region): box-to-box spread in GB/s vs DVFS, by measurement
@@ -1030,6 +1033,50 @@ def main(argv=None):
         # when the gloo side group exists: rank 0's CPU baseline runs 10-30 s)
         dist.barrier(group=cpu_group)
         dist.destroy_process_group()
+
+
+NORTH_STAR_BAR = 0.70  # BASELINE.json north_star: >= 70 % of per-GPU HBM-read roofline at 1 and 8 GPUs
+PREDICTION = ROOT / "profiles" / "r06" / "scale_prediction.json"  # scripts/predict_scale.py
+
+
+def north_star_block(workload: str, n: int, roofline, step_frac: float, scaling: str, measured_world: int) -> dict:
+    """north_star's bar against this line: the per-rank kernel fraction (each
+    GPU's reduce launch against its own 8 TB/s -- the quantity the bar is
+    met on) and the whole step against the node's N x 8 TB/s (which a
+    strong-scaled step cannot reach once the RCCL all-gather over xGMI is
+    longer than the per-rank reduce), next to the written prediction for this
+    workload and N (profiles/r06/scale_prediction.json)."""
+    kfrac = roofline.get("frac") if roofline else None
+    block = {
+        "bar": NORTH_STAR_BAR,
+        "met_on": "per_rank_kernel_frac",
+        "per_rank_kernel_frac": kfrac,
+        "per_rank_kernel_meets_bar": None if kfrac is None else bool(kfrac >= NORTH_STAR_BAR),
+        "step_frac_of_node_hbm": step_frac,
+        "step_meets_bar": bool(step_frac >= NORTH_STAR_BAR) if step_frac is not None else None,
+        "why_step_differs": ("strong scaling: every rank reduces P/N columns (HBM-bound, the per-rank kernel) and "
+                             "receives (N-1)/N x 4P bytes in the RCCL all-gather over xGMI; at the target's N = 8 "
+                             "that exchange (87.5 MB in per rank) is longer than the 0.18 ms reduce, so the step is "
+                             "exchange-bound and its node-HBM fraction is not the bar's quantity"),
+    }
+    if scaling == "strong" and PREDICTION.exists():
+        try:
+            pred = json.loads(PREDICTION.read_text())["workloads"].get(workload, {}).get(str(n))
+        except (ValueError, OSError):
+            pred = None
+        if pred is not None:
+            block["prediction"] = {"per_rank_kernel_frac": pred["per_rank_kernel_frac"],
+                                   "bound": pred["bound"],
+                                   "step_ms": [pred["predicted"]["high"]["step_ms"], pred["predicted"]["low"]["step_ms"]],
+                                   "value_GBps": [pred["predicted"]["low"]["value_GBps"],
+                                                  pred["predicted"]["high"]["value_GBps"]],
+                                   "step_frac_of_node_hbm": [pred["predicted"]["low"]["step_frac_of_node_hbm"],
+                                                             pred["predicted"]["high"]["step_frac_of_node_hbm"]],
+                                   "source": "profiles/r06/scale_prediction.json (xGMI in-rate 153 GB/s .. "
+                                             "0.75 x (N-1) x 153 GB/s per rank; DESIGN.md section 7)"}
+    if measured_world != n:
+        block["note"] = f"--shard-of {n} rehearsal on {measured_world} GPU: no exchange, so the step fraction is the reduce's"
+    return block
 
 
 def roofline_entry(args, K, S, kernel_ms_max, launches_per_call, sched, tuned, timing_desc, launches, world):

@@ -43,6 +43,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--reps", type=int, default=6)
     ap.add_argument("--clock-calls", type=int, default=30)
+    ap.add_argument("--clock-passes", type=int, default=5)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -87,7 +88,7 @@ def main():
                 times[n].append((a, b))
         torch.cuda.synchronize()
     clocks = {}
-    for _ in range(2):  # two interleaved passes of the clock probe
+    for _ in range(args.clock_passes):  # interleaved passes of the clock probe
         for n, fn in runs.items():
             clocks.setdefault(n, []).append(bench.shader_clock_mhz(fn, calls=args.clock_calls)["clock_mhz"])
     alg = 4 * K * P + 4 * P + 4 * K

@@ -205,6 +205,27 @@ def test_cpu_rehearsal_line_has_chunk_sweep(n):
     assert out["parity"]["ok"] and out["parity"]["ranks"] == n and out["parity"]["reassembly_checksums_ok"]
     cb = out["cpu_baseline"]
     assert cb["value"] is None and cb["n_gpus_in_run"] == n and "N = 1 only" in cb["note"]
+    ns = out["north_star"]  # the bar, the quantity it is met on, and the step fraction beside it
+    assert ns["bar"] == 0.70 and ns["met_on"] == "per_rank_kernel_frac"
+    assert ns["per_rank_kernel_frac"] is None  # the rehearsal has no kernel timing
+    assert ns["step_frac_of_node_hbm"] == out["step_frac_of_node_hbm"] and "exchange" in ns["why_step_differs"]
+
+
+def test_north_star_block_carries_the_written_prediction():
+    """At the target's N = 8 the block holds DESIGN.md section 7's prediction
+    (profiles/r06/scale_prediction.json): the per-rank kernel above the bar,
+    the step exchange-bound, its node-HBM fraction as a range below 0.70."""
+    roof = {"frac": 0.851}
+    ns = bench.north_star_block("target", 8, roof, 0.40, "strong", measured_world=8)
+    assert ns["per_rank_kernel_meets_bar"] is True and ns["step_meets_bar"] is False
+    pred = ns["prediction"]
+    assert pred["bound"] == "exchange" and pred["per_rank_kernel_frac"] > 0.70
+    lo, hi = pred["step_frac_of_node_hbm"]
+    assert 0 < lo <= hi < 0.70
+    assert pred["value_GBps"][0] <= pred["value_GBps"][1]
+    assert "prediction" in bench.north_star_block("resnet18_gn", 4, roof, 0.8, "strong", 4)
+    assert "prediction" not in bench.north_star_block("target", 8, roof, 0.4, "weak", 8)
+    assert "note" in bench.north_star_block("target", 8, roof, 0.8, "strong", measured_world=1)
 
 
 def test_cpu_rehearsal_one_rank_times_the_cpu_baseline():
