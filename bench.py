@@ -460,8 +460,11 @@ def shader_clock_mhz(fn, lead: int = 3, calls: int = 30, window_ms: float = 0.0)
         fn()
     mfl_amd._lib.check(lib.fedavg_probe_clock(out.data_ptr(), blocks, samples, interval_us, side.cuda_stream),
                        "fedavg_probe_clock", lib)
+    c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    c0.record()
     for _ in range(calls):
         fn()
+    c1.record()
     torch.cuda.synchronize()
     st = out.view(blocks, samples + 1, 2).cpu().numpy().astype(np.float64)
     dc, dr = st[:, -1, 0] - st[:, 0, 0], st[:, -1, 1] - st[:, 0, 1]
@@ -469,6 +472,8 @@ def shader_clock_mhz(fn, lead: int = 3, calls: int = 30, window_ms: float = 0.0)
     return {"clock_mhz": round(float(np.median(mhz)), 1), "min": round(float(mhz.min()), 1),
             "max": round(float(mhz.max()), 1), "window_ms": round(float(np.median(dr)) / 1e5, 3),
             "call_ms": round(call_ms, 4), "calls_after_probe": calls,
+            # the same calls' own time: clock and time from one window (cycles = ms x MHz)
+            "ms_per_call_in_window": round(c0.elapsed_time(c1) / calls, 4),
             "method": "d(s_memtime)/d(s_memrealtime) x 100 MHz, 8 one-wave probe workgroups on a side stream "
                       "beside back-to-back calls; median over workgroups"}
 

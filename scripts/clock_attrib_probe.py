@@ -10,10 +10,12 @@ Variants (all on the same resident [K, ld] rows):
   fp32_squares  the same kernel with its squares in fp32 (MODE 4 + 64, probe: sums differ)
   loads_only    the same grid and loads, no chain, no squares (MODE 1 + 64, probe: wrong results)
 
-Per variant: median ms over rounds x reps (HIP events around each call),
-the clock the chip holds under back-to-back calls (bench.shader_clock_mhz:
-d(s_memtime)/d(s_memrealtime) on a side stream), cycles per call = ms x MHz,
-and the fp32-squares sums' max relative difference from the fp64 ones.
+Per variant: median ms over rounds x reps (HIP events around each call);
+then, in interleaved passes, the clock the chip holds under back-to-back
+calls (bench.shader_clock_mhz: d(s_memtime)/d(s_memrealtime) on a side
+stream) together with those same calls' time, so every pass gives one
+(time, clock) pair from one window and cycles per call = ms x MHz of that
+pair; and the fp32-squares sums' max relative difference from the fp64 ones.
 One JSON line per variant, then a summary line.
 """
 from __future__ import annotations
@@ -87,28 +89,34 @@ def main():
                 b.record()
                 times[n].append((a, b))
         torch.cuda.synchronize()
-    clocks = {}
-    for _ in range(args.clock_passes):  # interleaved passes of the clock probe
+    clocks, pair_ms = {}, {}
+    for _ in range(args.clock_passes):  # interleaved passes of the clock probe, each timing its own calls
         for n, fn in runs.items():
-            clocks.setdefault(n, []).append(bench.shader_clock_mhz(fn, calls=args.clock_calls)["clock_mhz"])
+            c = bench.shader_clock_mhz(fn, calls=args.clock_calls)
+            clocks.setdefault(n, []).append(c["clock_mhz"])
+            pair_ms.setdefault(n, []).append(c["ms_per_call_in_window"])
     alg = 4 * K * P + 4 * P + 4 * K
     ref = outs["reduce"].view(torch.int32)
     summary = {}
     for n in runs:
         ms = float(np.median([a.elapsed_time(b) for a, b in times[n]]))
         mhz = float(np.median(clocks[n]))
+        # cycles from (time, clock) pairs measured over the same window of calls
+        cyc = [m * c / 1e3 for m, c in zip(pair_ms[n], clocks[n])]
         rec = {"K": K, "P": P, "variant": n, "ms_median": round(ms, 4), "GBps": round(alg / ms / 1e6, 1),
                "frac_of_8TBps": round(alg / ms / 1e6 / 8000.0, 4), "clock_mhz": mhz, "clock_samples": clocks[n],
-               "mcycles_per_call": round(ms * mhz / 1e3, 3),
+               "window_ms_samples": pair_ms[n], "mcycles_per_call": round(float(np.median(cyc)), 3),
+               "mcycles_samples": [round(x, 3) for x in cyc],
                "out_bits_equal_reduce": bool(torch.equal(outs[n].view(torch.int32), ref))}
         if n in sums and n not in ("fused", "loads_only"):
             rec["sums_max_rel_vs_fused"] = float(((sums[n] - sums["fused"]).abs() / sums["fused"].abs()).max())
-        summary[n] = (ms, mhz)
+        summary[n] = (float(np.median(pair_ms[n])), mhz, float(np.median(cyc)))
         print(json.dumps(rec), flush=True)
-    base_ms, base_mhz = summary["reduce"]
-    print(json.dumps({"summary": {n: {"ms_over_reduce": round(ms / base_ms, 4), "clock_over_reduce": round(mhz / base_mhz, 4),
-                                      "cycles_over_reduce": round(ms * mhz / (base_ms * base_mhz), 4)}
-                                  for n, (ms, mhz) in summary.items()}}), flush=True)
+    base_ms, base_mhz, base_cyc = summary["reduce"]
+    print(json.dumps({"summary": {n: {"window_ms_over_reduce": round(ms / base_ms, 4),
+                                      "clock_over_reduce": round(mhz / base_mhz, 4),
+                                      "cycles_over_reduce": round(cyc / base_cyc, 4)}
+                                  for n, (ms, mhz, cyc) in summary.items()}}), flush=True)
 
 
 if __name__ == "__main__":

@@ -61,17 +61,31 @@ def _digest(sd) -> str:
     return h.hexdigest()
 
 
-def big_init() -> "OrderedDict[str, torch.Tensor]":
-    """The ``big`` scenario's initial model: the generator's ``make_model("big")``."""
+# the digest-only scenarios' models (the generator's make_model): P = 1,001,000 and 25,005,000
+_DIGEST_MODELS = {"big": (1000, 1000), "target": (5000, 5000)}
+
+
+def big_init(kind: str = "big") -> "OrderedDict[str, torch.Tensor]":
+    """A digest-only scenario's initial model: the generator's ``make_model(kind)``."""
     torch.manual_seed(1234)
-    return OrderedDict((k, v.detach().clone()) for k, v in torch.nn.Linear(1000, 1000).state_dict().items())
+    return OrderedDict((k, v.detach().clone()) for k, v in torch.nn.Linear(*_DIGEST_MODELS[kind]).state_dict().items())
 
 
-def case_names(stats_only: bool = False):
+def case_names(stats_only: bool = False, max_p: Optional[int] = None):
     """Scenario names; ``stats_only=False`` leaves out the regenerated
-    (digest-only) scenarios, whose replay costs seconds per round."""
+    (digest-only) scenarios, whose replay costs seconds per round;
+    ``max_p`` leaves out scenarios with more parameters."""
     names = sorted(p.stem for p in FPF_DIR.glob("*.npz"))
-    return names if stats_only else [n for n in names if not n.startswith("big")]
+    if not stats_only:
+        names = [n for n in names if not n.startswith(("big", "target"))]
+    if max_p is not None:
+        names = [n for n in names if _weight_size(n) <= max_p]
+    return names
+
+
+def _weight_size(name: str) -> int:
+    z = np.load(FPF_DIR / f"{name}.npz", allow_pickle=False)
+    return int(json.loads(bytes(z["meta"]).decode())["weight_size"])
 
 
 def load_case(name: str) -> FPFCase:
@@ -79,7 +93,7 @@ def load_case(name: str) -> FPFCase:
     meta = json.loads(bytes(z["meta"]).decode())
     stats = z["stats"] if "stats" in z.files else None
     if meta.get("inputs") == "sha256":
-        init = big_init()
+        init = big_init(meta["model"])
         assert _digest(init) == meta["init_sha256"], "the regenerated initial model differs from the reference's"
         return FPFCase(meta, init, None, z["fpf"], stats)
     keys = [k["name"] for k in meta["keys"]]

@@ -187,7 +187,7 @@ STATS_CASES = [n for n in fpf_replay.case_names(stats_only=True) if "stats" in n
 
 
 def test_stats_golden_present():
-    assert {"lr_full", "big_lru"} <= set(STATS_CASES)
+    assert {"lr_full", "big_lru", "target_lru"} <= set(STATS_CASES)
 
 
 @pytest.mark.parametrize("name", STATS_CASES)
@@ -195,8 +195,9 @@ def test_round_stats_oracle_matches_reference_loop(name):
     """The restatement (aggregate_torch, client_distances_torch, round_stats_update)
     reproduces the reference's delta / rho / beta after every round bit for bit:
     same torch CPU expressions on the same inputs.  ``big_lru`` (P = 1,001,000)
-    also checks that its regenerated client states are the reference's inputs
-    (sha256 per client, in FPFCase.client_state)."""
+    and ``target_lru`` (P = 25,005,000, ~15 s) also check that their regenerated
+    client states are the reference's inputs (sha256 per client, in
+    FPFCase.client_state)."""
     case = fpf_replay.load_case(name)
     agg = lambda wl, ms: copy.deepcopy(ms) if not wl else O.aggregate_torch(wl)  # noqa: E731
     got, _ = fpf_replay.replay_stats(case, agg, O.client_distances_torch)
