@@ -214,7 +214,10 @@ class ClientFeed:
         :217, even by another deep copy, is a deterministic fallback.  Plain
         ``dict`` results (no instance attributes) and dicts the loop never
         deep-copies keep ``None`` (version counters and value probes only)."""
-        if type(sd) in copy._deepcopy_dispatch or not hasattr(sd, "__dict__") or "__deepcopy__" in sd.__dict__:
+        # copy.deepcopy dispatches on the exact type first (dict, list, ...): those never reach an
+        # instance __deepcopy__, and objects without a __dict__ cannot carry one
+        if (type(sd) in getattr(copy, "_deepcopy_dispatch", {dict: None}) or not hasattr(sd, "__dict__")
+                or "__deepcopy__" in sd.__dict__):
             return
         ref, feed_ref, gen = weakref.ref(sd), weakref.ref(self), self._gen
 
