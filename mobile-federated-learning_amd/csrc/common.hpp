@@ -147,6 +147,88 @@ __device__ __forceinline__ int64_t wave_search_last_le(Start start, int64_t n, i
 // round trip per step, 12 per fp64 sum) serialises ~6 LDS latencies per sum;
 // the per-client sums of the :291 pass do one per client row.  Same addends,
 // fixed order: deterministic, but not the shfl tree's bits.
+// f(std::integral_constant<int, I>{}) for I = 0 .. N-1, unrolled at compile
+// time (DPP controls must be constants)
+template <class F, int... Is>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, Is...>) {
+  (f(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// The sequential fp32 chain a = fl32(a + fl32(w_i x_i)) over 8 rows whose
+// weights are lanes of one register: row i's weight is lane 16r + i % 16 of w,
+// broadcast over its 16-lane row r by the multiply's own DPP operand
+// (row_newbcast).  Software-pipelined by hand: the product of the block's
+// first row arrives in tc, each add reads a product issued two instructions
+// earlier, and tc leaves with the product of the next block's first row
+// (lane 0 or 8, of wn when the next row starts a new 16).  The compiler's DPP
+// combiner keeps row_newbcast as a separate v_mov_b32_dpp (and an s_nop after
+// every inline v_mul), so the block is written out.  H = 0: rows of lanes
+// 0..7, H = 1: lanes 8..15; LAST: no next row.
+template <int H, bool LAST>
+__device__ __forceinline__ void chain8_row_bcast(float& a, float& tc, float w, float wn, const float* x) {
+  float t1;
+#define FEDAVG_C8_MUL(T, X, L) "v_mul_f32_dpp " T ", %[w], " X " row_newbcast:" #L " row_mask:0xf bank_mask:0xf\n\t"
+#define FEDAVG_C8_ADD(T) "v_add_f32_e32 %[a], %[a], " T "\n\t"
+  if constexpr (H == 0) {
+    if constexpr (LAST) {
+      asm(FEDAVG_C8_MUL("%[t1]", "%[x1]", 1) FEDAVG_C8_ADD("%[tc]") FEDAVG_C8_MUL("%[tc]", "%[x2]", 2)
+              FEDAVG_C8_ADD("%[t1]") FEDAVG_C8_MUL("%[t1]", "%[x3]", 3) FEDAVG_C8_ADD("%[tc]")
+                  FEDAVG_C8_MUL("%[tc]", "%[x4]", 4) FEDAVG_C8_ADD("%[t1]") FEDAVG_C8_MUL("%[t1]", "%[x5]", 5)
+                      FEDAVG_C8_ADD("%[tc]") FEDAVG_C8_MUL("%[tc]", "%[x6]", 6) FEDAVG_C8_ADD("%[t1]")
+                          FEDAVG_C8_MUL("%[t1]", "%[x7]", 7) FEDAVG_C8_ADD("%[tc]") FEDAVG_C8_ADD("%[t1]")
+          : [a] "+v"(a), [tc] "+v"(tc), [t1] "=&v"(t1)
+          : [w] "v"(w), [x1] "v"(x[1]), [x2] "v"(x[2]), [x3] "v"(x[3]), [x4] "v"(x[4]), [x5] "v"(x[5]),
+            [x6] "v"(x[6]), [x7] "v"(x[7]));
+    } else {
+      asm(FEDAVG_C8_MUL("%[t1]", "%[x1]", 1) FEDAVG_C8_ADD("%[tc]") FEDAVG_C8_MUL("%[tc]", "%[x2]", 2)
+              FEDAVG_C8_ADD("%[t1]") FEDAVG_C8_MUL("%[t1]", "%[x3]", 3) FEDAVG_C8_ADD("%[tc]")
+                  FEDAVG_C8_MUL("%[tc]", "%[x4]", 4) FEDAVG_C8_ADD("%[t1]") FEDAVG_C8_MUL("%[t1]", "%[x5]", 5)
+                      FEDAVG_C8_ADD("%[tc]") FEDAVG_C8_MUL("%[tc]", "%[x6]", 6) FEDAVG_C8_ADD("%[t1]")
+                          FEDAVG_C8_MUL("%[t1]", "%[x7]", 7) FEDAVG_C8_ADD("%[tc]")
+                              FEDAVG_C8_MUL("%[tc]", "%[x8]", 8) FEDAVG_C8_ADD("%[t1]")
+          : [a] "+v"(a), [tc] "+v"(tc), [t1] "=&v"(t1)
+          : [w] "v"(w), [x1] "v"(x[1]), [x2] "v"(x[2]), [x3] "v"(x[3]), [x4] "v"(x[4]), [x5] "v"(x[5]),
+            [x6] "v"(x[6]), [x7] "v"(x[7]), [x8] "v"(x[8]));
+    }
+  } else {
+    if constexpr (LAST) {
+      asm(FEDAVG_C8_MUL("%[t1]", "%[x1]", 9) FEDAVG_C8_ADD("%[tc]") FEDAVG_C8_MUL("%[tc]", "%[x2]", 10)
+              FEDAVG_C8_ADD("%[t1]") FEDAVG_C8_MUL("%[t1]", "%[x3]", 11) FEDAVG_C8_ADD("%[tc]")
+                  FEDAVG_C8_MUL("%[tc]", "%[x4]", 12) FEDAVG_C8_ADD("%[t1]") FEDAVG_C8_MUL("%[t1]", "%[x5]", 13)
+                      FEDAVG_C8_ADD("%[tc]") FEDAVG_C8_MUL("%[tc]", "%[x6]", 14) FEDAVG_C8_ADD("%[t1]")
+                          FEDAVG_C8_MUL("%[t1]", "%[x7]", 15) FEDAVG_C8_ADD("%[tc]") FEDAVG_C8_ADD("%[t1]")
+          : [a] "+v"(a), [tc] "+v"(tc), [t1] "=&v"(t1)
+          : [w] "v"(w), [x1] "v"(x[1]), [x2] "v"(x[2]), [x3] "v"(x[3]), [x4] "v"(x[4]), [x5] "v"(x[5]),
+            [x6] "v"(x[6]), [x7] "v"(x[7]));
+    } else {
+      asm(FEDAVG_C8_MUL("%[t1]", "%[x1]", 9) FEDAVG_C8_ADD("%[tc]") FEDAVG_C8_MUL("%[tc]", "%[x2]", 10)
+              FEDAVG_C8_ADD("%[t1]") FEDAVG_C8_MUL("%[t1]", "%[x3]", 11) FEDAVG_C8_ADD("%[tc]")
+                  FEDAVG_C8_MUL("%[tc]", "%[x4]", 12) FEDAVG_C8_ADD("%[t1]") FEDAVG_C8_MUL("%[t1]", "%[x5]", 13)
+                      FEDAVG_C8_ADD("%[tc]") FEDAVG_C8_MUL("%[tc]", "%[x6]", 14) FEDAVG_C8_ADD("%[t1]")
+                          FEDAVG_C8_MUL("%[t1]", "%[x7]", 15) FEDAVG_C8_ADD("%[tc]")
+                              "v_mul_f32_dpp %[tc], %[wn], %[x8] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+                                  FEDAVG_C8_ADD("%[t1]")
+          : [a] "+v"(a), [tc] "+v"(tc), [t1] "=&v"(t1)
+          : [w] "v"(w), [wn] "v"(wn), [x1] "v"(x[1]), [x2] "v"(x[2]), [x3] "v"(x[3]), [x4] "v"(x[4]),
+            [x5] "v"(x[5]), [x6] "v"(x[6]), [x7] "v"(x[7]), [x8] "v"(x[8]));
+    }
+  }
+#undef FEDAVG_C8_MUL
+#undef FEDAVG_C8_ADD
+}
+
+// fl32(w[16r + I % 16] * x) by the same broadcast (the chain's first product)
+template <int I>
+__device__ __forceinline__ float mul_row_bcast(float w, float x) {
+  float r;
+  asm("v_mul_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(w), "v"(x), "n"(I % 16));
+  return r;
+}
+
 template <int CTRL, int ROW_MASK>
 __device__ __forceinline__ double dpp_move_f64(double v) {
   const uint64_t u = __builtin_bit_cast(uint64_t, v);

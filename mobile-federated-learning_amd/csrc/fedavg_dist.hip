@@ -1166,10 +1166,19 @@ int launch_fused_win(const float* clients, int64_t K, int64_t P, int64_t ld, con
 // LDS-DMA as the window starts (no registers: the row loads stream through
 // the chain), and are read back in the squares in place of their reloads.
 // MODE (probe, timing only): 1 = no chain (every wave takes x[0] as the
-// average, no hand-offs), 2 = no squares (rows reloaded, nothing summed).
+// average, no hand-offs), 2 = no squares (rows reloaded, nothing summed),
+// 16 = the chain's weights by DPP broadcast: lane 16r + j of wv[k] holds row
+// 16k + j's weight (every r), read once per launch, and row_newbcast:j hands
+// it to the v_mul (no LDS reads and no lgkmcnt waits inside a turn),
+// 8 = timeline: lane 0 of every wave of the first kStampBlocks workgroups
+// stores s_memtime at five points of its first kStampWins windows, after the
+// K x G partials (winn_stamp_elems; scripts/winn_timeline.py reads them).
 // ---------------------------------------------------------------------------
 // s_waitcnt vmcnt(0) expcnt(7) lgkmcnt(15) (gfx9 encoding: vmcnt in [3:0] and [15:14])
 constexpr int kWaitVmcnt0 = 0x0F70;
+constexpr int kStampBlocks = 8, kStampWins = 48, kStampSlots = 8;
+constexpr uint64_t kStampMagic = 0x504D415453ull;  // "STAMP"
+inline int64_t winn_stamp_elems(int nsmax) { return 1 + int64_t(kStampBlocks) * nsmax * kStampWins * kStampSlots; }
 
 template <int KH, int VEC, int NSMAX, int PF = 0, int LE = 0, int MODE = 0>
 __global__ __launch_bounds__(64 * NSMAX, win_min_waves(KH, VEC)) void reduce_sqdist_winn_kernel(
@@ -1199,6 +1208,19 @@ __global__ __launch_bounds__(64 * NSMAX, win_min_waves(KH, VEC)) void reduce_sqd
   static_assert(LE == 0 || VEC == 1, "LDS rows: 256-B row segments");
   static_assert(PF + LE <= KH, "prefetched rows");
   __shared__ __attribute__((aligned(16))) float rowl[LE > 0 ? NSMAX : 1][LE > 0 ? LE : 1][64];
+  uint64_t* const stamps = reinterpret_cast<uint64_t*>(partials + static_cast<int64_t>(K) * G);
+  int wi = 0;  // window count (timeline probe)
+  const auto stamp = [&](int ph) __attribute__((always_inline)) {
+    if constexpr ((MODE & 8) != 0) {
+      if (blockIdx.x < kStampBlocks && wi < kStampWins) {
+        const uint64_t t = __builtin_amdgcn_s_memtime();
+        if (lane == 0) stamps[1 + ((int64_t(blockIdx.x) * NSMAX + h) * kStampWins + wi) * kStampSlots + ph] = t;
+      }
+    }
+  };
+  if constexpr ((MODE & 8) != 0) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) stamps[0] = kStampMagic;
+  }
   for (int i = threadIdx.x; i < ns * KP; i += blockDim.x) {
     const int hh = i / KP, j = i % KP, row = hh * KH + j;
     wl[hh][j] = (j < KH && row < K) ? W[row] : -0.0f;
@@ -1207,6 +1229,16 @@ __global__ __launch_bounds__(64 * NSMAX, win_min_waves(KH, VEC)) void reduce_sqd
 #pragma unroll
   for (int b = 0; b < NB; ++b) acc[64 * b] = 0.0;
   __syncthreads();
+  constexpr bool kBcastW = (MODE & 16) != 0;
+  constexpr int NWV = kBcastW ? (KP + 15) / 16 : 1;
+  float wv[NWV];
+  if constexpr (kBcastW) {
+#pragma unroll
+    for (int k = 0; k < NWV; ++k) {
+      const int j = 16 * k + (lane & 15);
+      wv[k] = j < KP ? wl[h][j < KP ? j : 0] : 0.f;
+    }
+  }
   V x[KH];
   V xp[PF > 0 ? PF : 1];
   {
@@ -1223,6 +1255,22 @@ __global__ __launch_bounds__(64 * NSMAX, win_min_waves(KH, VEC)) void reduce_sqd
     }
   }
   const auto chain = [&](V& a, bool first) {
+    if constexpr (kBcastW) {
+      static_assert(VEC == 1 && KH % 16 == 0, "broadcast weights: one column per lane, 16-row groups");
+      // the first turn starts from -0.0: fl32(-0.0 + p) is p, bit for bit
+      float ac = first ? -0.0f : a[0];
+      float tc = mul_row_bcast<0>(wv[0], x[0][0]);
+      float xs[KH];
+#pragma unroll
+      for (int i = 0; i < KH; ++i) xs[i] = x[i][0];
+      static_for<KH / 8>([&](auto bc) {
+        constexpr int b = decltype(bc)::value;
+        constexpr bool last = b == KH / 8 - 1;
+        chain8_row_bcast<b % 2, last>(ac, tc, wv[b / 2], wv[last ? b / 2 : (b + 1) / 2], xs + 8 * b);
+      });
+      a[0] = ac;
+      return;
+    }
     int wo = h * KP;  // opaque: the weights are re-read per window, not held in registers
     asm volatile("" : "+v"(wo));
     const float* wp = &wl[0][0] + wo;
@@ -1249,6 +1297,7 @@ __global__ __launch_bounds__(64 * NSMAX, win_min_waves(KH, VEC)) void reduce_sqd
     const int64_t cl = c0 + lane * VEC;
     const int nbn = win_bytes(w + G);
     const char* rp = reinterpret_cast<const char*>(X + (w + G) * WC) + r0 * row_bytes;
+    stamp(0);
     if constexpr (PF > 0) {
       // this window's rows (reloaded in the last window's squares) first: a
       // pre-existing wait the compiler's waitcnt pass accounts for, so the
@@ -1256,6 +1305,7 @@ __global__ __launch_bounds__(64 * NSMAX, win_min_waves(KH, VEC)) void reduce_sqd
       // otherwise entered the turn loop with vmcnt(0): every wave waited for
       // its prefetched rows of the NEXT window before its turn)
       __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
+      stamp(1);
 #pragma unroll
       for (int i = 0; i < PF; ++i) {
         asm volatile("" : "+s"(rp));
@@ -1292,9 +1342,11 @@ __global__ __launch_bounds__(64 * NSMAX, win_min_waves(KH, VEC)) void reduce_sqd
     } else
     for (int st = 0; st < ns; ++st) {  // the chain, wave by wave in row order
       if (h == st) {
+        stamp(2);
         if (st > 0) a = xa[lane];
         chain(a, st == 0);
         xa[lane] = a;
+        stamp(3);
         if (st == ns - 1) {
           if (!ragged) {
             __builtin_nontemporal_store(static_cast<typename WinVec<VEC>::TA>(a),
@@ -1336,7 +1388,10 @@ __global__ __launch_bounds__(64 * NSMAX, win_min_waves(KH, VEC)) void reduce_sqd
       const double q45 = fold32(p[4], p[5]), q67 = fold32(p[6], p[7]);
       acc[64 * b] += fold8(fold16(q01, q23), fold16(q45, q67), upper);
     }
+    stamp(4);
     __syncthreads();  // xa is read by every wave before the next window's chain rewrites it
+    stamp(5);
+    ++wi;
   }
   const int row_in = win_batch_row(lane);
 #pragma unroll
@@ -1378,8 +1433,9 @@ int launch_fused_winn(const float* clients, int64_t K, int64_t P, int64_t ld, co
   const int64_t nwin = (P + 64 * VEC - 1) / (64 * VEC);
   const int64_t grid = fused_winn_grid<KH, VEC, NSMAX, PF, LE, MODE>(K, P, blocks_per_cu);
   if (grid <= 0) return set_error(FEDAVG_EMODE, "%s: the split window kernel is not resident", what);
-  if (partial_elems < K * grid)
-    return set_error(FEDAVG_EINVAL, "%s: workspace needs %lld doubles", what, (long long)(K * grid));
+  const int64_t need = K * grid + ((MODE & 8) != 0 ? winn_stamp_elems(NSMAX) : 0);
+  if (partial_elems < need)
+    return set_error(FEDAVG_EINVAL, "%s: workspace needs %lld doubles", what, (long long)need);
   hipLaunchKernelGGL((reduce_sqdist_winn_kernel<KH, VEC, NSMAX, PF, LE, MODE>), dim3(static_cast<unsigned>(grid)),
                      dim3(static_cast<unsigned>(64 * ns)), 0, s, clients, static_cast<int>(K), ld, P, nwin, weights,
                      out, partials);
@@ -1390,6 +1446,252 @@ int launch_fused_winn(const float* clients, int64_t K, int64_t P, int64_t ld, co
   return launch_status(what);
 }
 
+
+// ---------------------------------------------------------------------------
+// Split-row windows with point-to-point hand-offs (round 6).  The same work as
+// reduce_sqdist_winn_kernel<64, 1, NSMAX, PF> -- wave h holds rows 64h ..
+// 64h + 63 of a 64-column window, the chain runs wave by wave in row order,
+// then every wave squares its rows against the average and reloads them from
+// the next window -- without a workgroup barrier anywhere in the window loop:
+//   * wave h > 0 starts its turn when wave h - 1's partial for this window is
+//     in LDS (part[h - 1], flag[h - 1] = the window's sequence number), wave
+//     ns - 1 publishes the average (avg, flag[NSMAX]); every other wave waits
+//     for it before its squares;
+//   * a wave's own rows are waited for at its turn (the compiler's vmcnt(PF):
+//     the prefetched rows of the next window stay in flight), not at the
+//     window's start;
+//   * the squares and reloads run at a priority by wave (waves 0-3 first), so
+//     the first waves' rows of the next window arrive first and their turns
+//     start while the later waves' rows are still streaming.
+// The timeline probe (winn, MODE 8) measured the barrier form's window as
+// chain (14.4k cycles with the broadcast weights) + reload phase (9-12k)
+// end to end: every turn waited at a barrier for the slowest wave's reloads.
+// Hand-off safety: wave h writes part[h] for window s + 1 only after its
+// squares of window s, i.e. after the average of s, i.e. after wave h + 1
+// read part[h] for s; wave ns - 1 writes avg for s + 1 only after every other
+// wave's turn of s + 1, each after its squares of s read avg.  Every wave runs
+// the same windows, so every flag a wave waits for is set; the polls are
+// bounded (kHandoffSpinMax) so a broken protocol ends in wrong sums (the parity
+// tests), never in a hung grid.  Weights by row broadcast (chain8_row_bcast).
+// MODE 8: the timeline stamps of the winn kernel.
+// ---------------------------------------------------------------------------
+constexpr int kHandoffSpinMax = 1 << 16;  // x s_sleep 1 (64 clocks): ~1.7 ms, a window is ~13 us
+
+template <int NSMAX, int PF, int MODE = 0>
+__global__ __launch_bounds__(64 * NSMAX, win_min_waves(64, 1)) void reduce_sqdist_winf_kernel(
+    const float* __restrict__ X, int K, int64_t ld, int64_t P, int64_t nwin, const float* __restrict__ W,
+    float* __restrict__ out, double* __restrict__ partials) {
+  constexpr int KH = 64, WC = 64, NB = 8, NWV = 4;
+  static_assert(PF >= 1 && PF <= KH, "prefetched rows");
+  const int lane = threadIdx.x & 63;
+  const int h = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int ns = __builtin_amdgcn_readfirstlane(static_cast<int>(blockDim.x >> 6));
+  const int r0 = h * KH;
+  const int64_t G = gridDim.x;
+  const uint32_t voff = static_cast<uint32_t>(lane) * 4;
+  const int64_t P4 = (P + 3) & ~static_cast<int64_t>(3);
+  const int64_t row_bytes = ld * 4;
+  const bool upper = (lane & 8) != 0;
+  const auto win_bytes = [&](int64_t w) -> int {
+    if (w >= nwin) return 0;
+    const int64_t n = P4 - w * WC;
+    return static_cast<int>((n < WC ? n : WC) * 4);
+  };
+  __shared__ double accl[NSMAX][NB][64];
+  __shared__ float part[NSMAX][64];
+  __shared__ float avg[64];
+  __shared__ int flag[NSMAX + 1];
+  uint64_t* const stamps = reinterpret_cast<uint64_t*>(partials + static_cast<int64_t>(K) * G);
+  int wi = 0;
+  const auto stamp = [&](int ph) __attribute__((always_inline)) {
+    if constexpr ((MODE & 8) != 0) {
+      if (blockIdx.x < kStampBlocks && wi < kStampWins) {
+        const uint64_t t = __builtin_amdgcn_s_memtime();
+        if (lane == 0) stamps[1 + ((int64_t(blockIdx.x) * NSMAX + h) * kStampWins + wi) * kStampSlots + ph] = t;
+      }
+    }
+  };
+  if constexpr ((MODE & 8) != 0) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) stamps[0] = kStampMagic;
+  }
+  double* acc = &accl[h][0][lane];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) acc[64 * b] = 0.0;
+  if (threadIdx.x <= NSMAX) flag[threadIdx.x] = -1;
+  float wv[NWV];  // lane 16r + j of wv[k]: row 16k + j's weight (-0.0 past K)
+#pragma unroll
+  for (int k = 0; k < NWV; ++k) {
+    const int row = r0 + 16 * k + (lane & 15);
+    wv[k] = row < K ? W[row] : -0.0f;
+  }
+  __syncthreads();
+  // LDS pointers spelled out: a volatile access through a generic pointer is a
+  // flat_load, whose wait is vmcnt(0) -- every row load of the wave
+  typedef __attribute__((address_space(3))) volatile int lds_flag_t;
+  const auto wait_flag = [&](int idx, int seq) __attribute__((always_inline)) {
+    lds_flag_t* f = (lds_flag_t*)&flag[idx];
+    for (int it = 0; __builtin_amdgcn_readfirstlane(*f) != seq && it < kHandoffSpinMax; ++it)
+      __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
+  };
+  const auto publish = [&](int idx, int seq) __attribute__((always_inline)) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the payload's ds_write is done
+    *(lds_flag_t*)&flag[idx] = seq;
+  };
+  float x[KH];
+  float xp[PF];
+  {
+    int Kw = K;
+    asm volatile("" : "+s"(Kw));
+    const int nb = win_bytes(blockIdx.x);
+    const char* rp = reinterpret_cast<const char*>(X + static_cast<int64_t>(blockIdx.x) * WC) + r0 * row_bytes;
+#pragma unroll
+    for (int i = 0; i < KH; ++i) {
+      asm volatile("" : "+s"(rp));
+      x[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                           __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(rp), 0,
+                                                                             r0 + i < Kw ? nb : 0, 0x00020000),
+                                           static_cast<int>(voff), 0, 2));
+      rp += row_bytes;
+    }
+  }
+  int seq = 0;
+  for (int64_t w = blockIdx.x; w < nwin; w += G, ++seq) {
+    int Kw = K;
+    asm volatile("" : "+s"(Kw));
+    const int64_t c0 = w * WC;
+    const int64_t cl = c0 + lane;
+    const int nbn = win_bytes(w + G);
+    const char* rp = reinterpret_cast<const char*>(X + (w + G) * WC) + r0 * row_bytes;
+    stamp(0);
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {  // the next window's first rows, in flight through the turn
+      asm volatile("" : "+s"(rp));
+      xp[i] = __builtin_bit_cast(
+          float, __builtin_amdgcn_raw_buffer_load_b32(
+                     __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(rp), 0, r0 + i < Kw ? nbn : 0, 0x00020000),
+                     static_cast<int>(voff), 0, 2));
+      rp += row_bytes;
+    }
+    const bool ragged = c0 + WC > P;
+    if (ragged) {
+#pragma unroll
+      for (int i = 0; i < KH; ++i)
+        if (cl >= P) x[i] = 0.f;
+    }
+    // the turn
+    float a = -0.0f;  // fl32(-0.0 + p) is p, bit for bit: wave 0 starts the chain from it
+    if (h > 0) {
+      wait_flag(h - 1, seq);
+      a = part[h - 1][lane];
+    }
+    stamp(2);
+    __builtin_amdgcn_s_setprio(3);
+    {
+      float tc = mul_row_bcast<0>(wv[0], x[0]);
+      static_for<KH / 8>([&](auto bc) {
+        constexpr int b = decltype(bc)::value;
+        constexpr bool last = b == KH / 8 - 1;
+        chain8_row_bcast<b % 2, last>(a, tc, wv[b / 2], wv[last ? b / 2 : (b + 1) / 2], x + 8 * b);
+      });
+    }
+    if (h < ns - 1) {
+      part[h][lane] = a;
+      publish(h, seq);
+    } else {
+      avg[lane] = a;
+      publish(NSMAX, seq);
+      if (!ragged) {
+        __builtin_nontemporal_store(a, out + cl);
+      } else if (cl < P) {
+        out[cl] = a;
+      }
+    }
+    stamp(3);
+    if (h < ns - 1) {
+      __builtin_amdgcn_s_setprio(0);
+      wait_flag(NSMAX, seq);
+      a = avg[lane];
+    }
+    // the squares, the next window's rows reloaded behind them: waves 0-3 first
+    if (h < 4)
+      __builtin_amdgcn_s_setprio(2);
+    else if (h < 8)
+      __builtin_amdgcn_s_setprio(1);
+    else
+      __builtin_amdgcn_s_setprio(0);
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      double p[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = 8 * b + j;
+        const double d = static_cast<double>(x[i] - a);  // fp32 difference, as the reference forms it
+        p[j] = d * d;
+        if (i < PF) {
+          x[i] = xp[i < PF ? i : 0];
+        } else {
+          asm volatile("" : "+s"(rp));
+          x[i] = __builtin_bit_cast(
+              float, __builtin_amdgcn_raw_buffer_load_b32(
+                         __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(rp), 0, r0 + i < Kw ? nbn : 0, 0x00020000),
+                         static_cast<int>(voff), 0, 2));
+          rp += row_bytes;
+        }
+      }
+      const double q01 = fold32(p[0], p[1]), q23 = fold32(p[2], p[3]);
+      const double q45 = fold32(p[4], p[5]), q67 = fold32(p[6], p[7]);
+      acc[64 * b] += fold8(fold16(q01, q23), fold16(q45, q67), upper);
+    }
+    __builtin_amdgcn_s_setprio(0);
+    stamp(4);
+    ++wi;
+  }
+  const int row_in = win_batch_row(lane);
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    double sm = acc[64 * b];
+    sm += dpp_move_f64<0xB1, 0xF>(sm);
+    sm += dpp_move_f64<0x4E, 0xF>(sm);
+    sm += dpp_move_f64<0x141, 0xF>(sm);
+    const int row = 8 * b + row_in;
+    if ((lane & 7) == 0 && r0 + row < K) partials[static_cast<int64_t>(r0 + row) * G + blockIdx.x] = sm;
+  }
+}
+
+template <int NSMAX, int PF, int MODE = 0>
+int64_t fused_winf_grid(int64_t K, int64_t P) {
+  const int ns = static_cast<int>((K + 63) / 64);
+  const int64_t r = resident_blocks(reduce_sqdist_winf_kernel<NSMAX, PF, MODE>, 64 * ns) / cu_count();
+  int64_t per_cu = 0;
+  if (r >= 1)
+    for (per_cu = 1; per_cu * 2 <= r;) per_cu *= 2;
+  const int64_t nwin = (P + 63) / 64;
+  const int64_t grid = per_cu * cu_count();
+  return grid < nwin ? grid : nwin;
+}
+
+template <int NSMAX, int PF, int MODE = 0>
+int launch_fused_winf(const float* clients, int64_t K, int64_t P, int64_t ld, const float* weights, float* out,
+                      double* partials, int64_t partial_elems, double* sumsq, hipStream_t s, const char* what) {
+  if (K > NSMAX * 64 || K < 2)
+    return set_error(FEDAVG_EMODE, "%s: these split windows cover 2 <= K <= %d", what, NSMAX * 64);
+  const int ns = static_cast<int>((K + 63) / 64);
+  const int64_t nwin = (P + 63) / 64;
+  const int64_t grid = fused_winf_grid<NSMAX, PF, MODE>(K, P);
+  if (grid <= 0) return set_error(FEDAVG_EMODE, "%s: the split window kernel is not resident", what);
+  const int64_t need = K * grid + ((MODE & 8) != 0 ? winn_stamp_elems(NSMAX) : 0);
+  if (partial_elems < need)
+    return set_error(FEDAVG_EINVAL, "%s: workspace needs %lld doubles", what, (long long)need);
+  hipLaunchKernelGGL((reduce_sqdist_winf_kernel<NSMAX, PF, MODE>), dim3(static_cast<unsigned>(grid)),
+                     dim3(static_cast<unsigned>(64 * ns)), 0, s, clients, static_cast<int>(K), ld, P, nwin, weights,
+                     out, partials);
+  int rc = launch_status(what);
+  if (rc) return rc;
+  hipLaunchKernelGGL(client_sqdist_finalize_kernel, dim3(static_cast<unsigned>(K)), dim3(kBlock), 0, s, partials,
+                     grid, sumsq);
+  return launch_status(what);
+}
 
 #ifdef FEDAVG_TUNING
 // ---------------------------------------------------------------------------
@@ -1606,7 +1908,15 @@ constexpr int64_t kFusedRowsMaxK = 1024;
 // workgroup to 512 rows, 16 beyond (640 x 3M 1.77 vs 2.46 for the two
 // passes; 1000 x 12.5M 9.99 vs 15.05; 520 x 5M 2.71 vs 3.34)
 constexpr int64_t kFusedWinnMinK = 369;
-constexpr int kFusedWinnPF = 8;  // rows of the next window prefetched (split_prefetch_rows)
+// (round 5: the barrier form with 8 prefetched rows, split_prefetch_rows)
+// Round 6: the split windows run reduce_sqdist_winf_kernel (point-to-point
+// hand-offs, broadcast weights) with 8 prefetched rows at <= 8 waves and 16
+// beyond (profiles/r06/winf/, ms, barrier form vs winf: 1000 x 12.5M 9.06 vs
+// 8.02; 999 x 10M+3 7.75 vs 6.44; 600 x 10M 5.13 vs 4.28; 513 x 3M 1.48 vs
+// 1.26; 500 x 11.2M 3.66 vs 3.57; 400 x 10M 2.73 vs 2.60; 370 x 5M 1.25 vs
+// 1.18; every output bit-identical).  FEDAVG_SPLIT_PREFETCH=0 keeps the
+// barrier form without prefetch (A/B).
+constexpr int kWinfPF8 = 8, kWinfPF16 = 16;
 // With the prefetch the split windows also beat the register-staged tiles at
 // 161-256 and 289-368 rows on long rows (profiles/r05/prefetch/, ms, tiles vs
 // split: 170 x 5M 0.606 vs 0.593; 192 x 5M 0.725 vs 0.661; 240 x 5M 0.897 vs
@@ -1669,7 +1979,7 @@ inline FusedPlan fused_plan(int64_t K, int64_t P) {
   if (K <= 128) return {kFusedLds, 64, 0};
   if (K >= kFusedWinnLowMinK && K < kFusedWinnMinK && (K < kFusedWinnGapMinK || K > kFusedWinnGapMaxK) &&
       split_prefetch_rows() > 0) {
-    const int64_t grid = fused_winn_grid<64, 1, 8, kFusedWinnPF>(K, P, 0);
+    const int64_t grid = fused_winf_grid<8, kWinfPF8>(K, P);
     if (grid > 0 && (P + 63) / 64 >= kFusedWinnLowMinPerBlock * grid) return {kFusedWinn, 64, 8};
   }
   if (K <= 192) return {kFusedRs, 64, 16};
@@ -1994,9 +2304,8 @@ int64_t fedavg_reduce_sqdist_workspace(int64_t K, int64_t P) {
     if (pl.S == 256) fused = K * fused_grid<256>(K, P, 0);
   } else if (pl.kind == kFusedWinn) {
     const bool pf = split_prefetch_rows() > 0;
-    fused = K * (pl.slots == 8 ? (pf ? fused_winn_grid<64, 1, 8, kFusedWinnPF>(K, P, 0) : fused_winn_grid<64, 1, 8>(K, P, 0))
-                               : (pf ? fused_winn_grid<64, 1, 16, kFusedWinnPF>(K, P, 0)
-                                     : fused_winn_grid<64, 1, 16>(K, P, 0)));
+    fused = K * (pl.slots == 8 ? (pf ? fused_winf_grid<8, kWinfPF8>(K, P) : fused_winn_grid<64, 1, 8>(K, P, 0))
+                               : (pf ? fused_winf_grid<16, kWinfPF16>(K, P) : fused_winn_grid<64, 1, 16>(K, P, 0)));
   } else if (pl.kind == kFusedRs) {
     switch (pl.S * 100 + pl.slots) {
       case 25608: fused = K * fused_rs_grid<256, 8, 0>(K, P, 0); break;
@@ -2049,14 +2358,14 @@ int fedavg_reduce_sqdist_f32(const float* clients, int64_t K, int64_t P, int64_t
     if (pl.kind == kFusedWinn) {
       const bool pf = split_prefetch_rows() > 0;
       if (pl.slots == 8 && pf)
-        return launch_fused_winn<64, 1, 8, kFusedWinnPF>(clients, K, P, ld, weights, out, workspace, workspace_elems,
-                                                         sumsq, 0, s, what);
+        return launch_fused_winf<8, kWinfPF8>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq, s,
+                                              what);
       if (pl.slots == 8)
         return launch_fused_winn<64, 1, 8>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq, 0, s,
                                            what);
       if (pf)
-        return launch_fused_winn<64, 1, 16, kFusedWinnPF>(clients, K, P, ld, weights, out, workspace, workspace_elems,
-                                                          sumsq, 0, s, what);
+        return launch_fused_winf<16, kWinfPF16>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq, s,
+                                                what);
       return launch_fused_winn<64, 1, 16>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq, 0, s,
                                           what);
     }
@@ -2311,7 +2620,25 @@ int fedavg_reduce_sqdist_f32_variant(const float* clients, int64_t K, int64_t P,
     FEDAVG_WINNLE_CASE(8, 22, 0)
     FEDAVG_WINNLE_CASE(0, 22, 0)
     FEDAVG_WINNLE_CASE(16, 22, 0)
+    FEDAVG_WINNLE_CASE(8, 0, 8)
+    FEDAVG_WINNLE_CASE(0, 0, 8)
+    FEDAVG_WINNLE_CASE(16, 0, 8)
+    FEDAVG_WINNLE_CASE(8, 0, 16)
+    FEDAVG_WINNLE_CASE(8, 0, 24)
+    FEDAVG_WINNLE_CASE(16, 0, 16)
 #undef FEDAVG_WINNLE_CASE
+    // round 6: split-row windows with point-to-point hand-offs
+    // (reduce_sqdist_winf_kernel): 91000000 + MODE * 10000 + PF * 100 + NSMAX
+#define FEDAVG_WINF_CASE(NSMAX, PF, MODE)                                                                        \
+  case 91000000 + MODE * 10000 + PF * 100 + NSMAX:                                                              \
+    return launch_fused_winf<NSMAX, PF, MODE>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq, s, \
+                                              what);
+    FEDAVG_WINF_CASE(16, 8, 0)
+    FEDAVG_WINF_CASE(16, 16, 0)
+    FEDAVG_WINF_CASE(16, 8, 8)
+    FEDAVG_WINF_CASE(8, 8, 0)
+    FEDAVG_WINF_CASE(8, 16, 0)
+#undef FEDAVG_WINF_CASE
     default: return set_error(FEDAVG_EMODE, "%s: cols must be 32, 64, 128 or 256 (+1000: double-buffered)", what);
   }
 }

@@ -1132,13 +1132,238 @@ __global__ __launch_bounds__(64 * NSMAX, win_min_waves(64, 1)) void reduce_sqdis
   }
 }
 
+// Zero-copy split-row windows with point-to-point hand-offs (round 6): the
+// segwinn work on fedavg_dist.hip's reduce_sqdist_winf_kernel protocol -- no
+// workgroup barrier in the window loop (wave h > 0 takes wave h - 1's partial
+// from LDS behind a flag, the last wave publishes the average behind another),
+// a wave waits for its own rows at its turn, the weights come by row
+// broadcast, the squares and reloads run at a priority by wave, and the first
+// PF rows of the next window are in flight through the turn.  The client
+// addresses of the window after next load at the start of the squares, ahead
+// of the reloads, so the next prefetch waits on them with the reloads still in
+// flight (vmcnt counts in issue order); the key table is read through the
+// constant address space (scalar loads: the key walk never waits on vmcnt).
+// Hand-off safety and the bounded polls: see the rows kernel.
+template <int NSMAX, int PF>
+__global__ __launch_bounds__(64 * NSMAX, win_min_waves(64, 1)) void reduce_sqdist_segwinf_kernel(
+    const SegKey* __restrict__ keys, const int64_t* __restrict__ ptrs, int64_t n_keys, int64_t units, int K,
+    const float* __restrict__ W, float* __restrict__ out, double* __restrict__ partials) {
+  constexpr int KH = 64, WC = 64, NB = 8, NWV = 4;
+  static_assert(PF >= 1 && PF <= KH, "prefetched rows");
+  constexpr int kSpinMax = 1 << 16;
+  const int lane = threadIdx.x & 63;
+  const int h = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int ns = __builtin_amdgcn_readfirstlane(static_cast<int>(blockDim.x >> 6));
+  const int r0 = h * KH;
+  const int G = static_cast<int>(gridDim.x);
+  const uint32_t voff = static_cast<uint32_t>(lane) * 4;
+  const bool upper = (lane & 8) != 0;
+  __shared__ double accl[NSMAX][NB][64];
+  __shared__ float part[NSMAX][64];
+  __shared__ float avg[64];
+  __shared__ int flag[NSMAX + 1];
+  double* acc = &accl[h][0][lane];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) acc[64 * b] = 0.0;
+  if (threadIdx.x <= NSMAX) flag[threadIdx.x] = -1;
+  float wv[NWV];  // lane 16r + j of wv[k]: client 16k + j's weight (-0.0 past K)
+#pragma unroll
+  for (int k = 0; k < NWV; ++k) {
+    const int row = r0 + 16 * k + (lane & 15);
+    wv[k] = row < K ? W[row] : -0.0f;
+  }
+  __syncthreads();
+  typedef __attribute__((address_space(3))) volatile int lds_flag_t;
+  const auto wait_flag = [&](int idx, int seq) __attribute__((always_inline)) {
+    lds_flag_t* f = (lds_flag_t*)&flag[idx];
+    for (int it = 0; __builtin_amdgcn_readfirstlane(*f) != seq && it < kSpinMax; ++it) __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
+  };
+  const auto publish = [&](int idx, int seq) __attribute__((always_inline)) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    *(lds_flag_t*)&flag[idx] = seq;
+  };
+  const auto load_ptrs = [&](const int64_t* P) __attribute__((always_inline)) -> int64_t {
+    const gptr<int64_t> q = to_global<int64_t>(P);
+    return r0 + lane < K ? q[r0 + lane] : 0;
+  };
+  const auto ptr_of = [&](int64_t pv, int i) __attribute__((always_inline)) {
+    int li = i;
+    asm volatile("" : "+s"(li));
+    const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(pv), li);
+    const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(static_cast<uint64_t>(pv) >> 32), li);
+    return reinterpret_cast<const float*>((static_cast<uint64_t>(hi) << 32) | lo);
+  };
+  const auto load_fast = [&](int64_t pv, int i, uint32_t soff, uint32_t nrec, int Kw) __attribute__((always_inline)) {
+    return __builtin_bit_cast(
+        float, __builtin_amdgcn_raw_buffer_load_b32(
+                   __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(ptr_of(pv, i)), 0,
+                                                     r0 + i < Kw ? static_cast<int>(nrec) : 0, 0x00020000),
+                   static_cast<int>(voff), static_cast<int>(soff), 2));
+  };
+  float x[KH];
+  float xp[PF];
+  const auto load_slow = [&](int64_t pv, int64_t c0, int n, int Kw) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < KH; ++i) {
+      const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(ptr_of(pv, i) + c0), 0,
+                                                                         r0 + i < Kw ? n * 4 : 0, 0x00020000);
+      x[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, static_cast<int>(voff), 0, 2));
+    }
+  };
+  const int units32 = static_cast<int>(units), nkeys32 = static_cast<int>(n_keys);
+  const auto cols_of = [&](int64_t numel, int w) __attribute__((always_inline)) {
+    const int64_t left = numel - static_cast<int64_t>(w) * WC;
+    return (left >> 31) != 0 ? WC : (static_cast<int>(left) < WC ? static_cast<int>(left) : WC);
+  };
+  typedef __attribute__((address_space(4))) const SegKey ckey_t;
+  ckey_t* const kc = (ckey_t*)keys;
+  // window u_ of key j_ (walked forward from j_): its first column and width
+  const auto locate = [&](int u_, int& j_, int64_t& c0_, int& n_) __attribute__((always_inline)) {
+    while (j_ + 1 < nkeys32 && static_cast<int>(kc[j_ + 1].unit_start) <= u_) ++j_;
+    const int w = u_ - static_cast<int>(kc[j_].unit_start);
+    c0_ = static_cast<int64_t>(w) * WC;
+    n_ = cols_of(kc[j_].numel, w);
+  };
+  int u = static_cast<int>(blockIdx.x), j = 0, n = 0;
+  int64_t c0 = 0;
+  int jn = 0, nn = 0;
+  int64_t c0n = 0, pvn = 0;
+  if (u < units32) {
+    j = __builtin_amdgcn_readfirstlane(static_cast<int>(find_key(keys, n_keys, u)));
+    locate(u, j, c0, n);
+    jn = j;
+    const int64_t pv0 = load_ptrs(ptrs + static_cast<int64_t>(j) * K);
+    // the next window's addresses before this window's rows: the loop's
+    // first prefetch then waits for them with the rows still in flight
+    if (u + G < units32) {
+      locate(u + G, jn, c0n, nn);
+      pvn = load_ptrs(ptrs + static_cast<int64_t>(jn) * K);
+    }
+    if (n == WC) {
+#pragma unroll
+      for (int i = 0; i < KH; ++i)
+        x[i] = load_fast(pv0, i, static_cast<uint32_t>(c0 * 4), static_cast<uint32_t>((c0 + WC) * 4), K);
+    } else {
+      load_slow(pv0, c0, n, K);
+    }
+  }
+  int seq = 0;
+  for (; u < units32; u += G, ++seq) {
+    const int64_t out_off = kc[j].out_offset;
+    const int un = u + G, unn = un + G;
+    const bool fastn = un < units32 && nn == WC;
+    const uint32_t soffn = static_cast<uint32_t>(c0n * 4), nrecn = static_cast<uint32_t>((c0n + WC) * 4);
+    int Kwn = fastn ? K : 0;
+    asm volatile("" : "+s"(Kwn));
+#pragma unroll
+    for (int i = 0; i < PF; ++i) xp[i] = load_fast(pvn, i, soffn, nrecn, Kwn);
+    // the turn
+    float a = -0.0f;  // fl32(-0.0 + p) is p, bit for bit
+    if (h > 0) {
+      wait_flag(h - 1, seq);
+      a = part[h - 1][lane];
+    }
+    __builtin_amdgcn_s_setprio(3);
+    {
+      float tc = mul_row_bcast<0>(wv[0], x[0]);
+      static_for<KH / 8>([&](auto bc) {
+        constexpr int b = decltype(bc)::value;
+        constexpr bool last = b == KH / 8 - 1;
+        chain8_row_bcast<b % 2, last>(a, tc, wv[b / 2], wv[last ? b / 2 : (b + 1) / 2], x + 8 * b);
+      });
+    }
+    if (h < ns - 1) {
+      part[h][lane] = a;
+      publish(h, seq);
+    } else {
+      avg[lane] = a;
+      publish(NSMAX, seq);
+      if (lane < n) out[out_off + c0 + lane] = a;
+    }
+    if (h < ns - 1) {
+      __builtin_amdgcn_s_setprio(0);
+      wait_flag(NSMAX, seq);
+      a = avg[lane];
+    }
+    // the window after next: its key and client addresses, ahead of the reloads
+    int jnn = jn, nnn = 0;
+    int64_t c0nn = 0, pvnn = 0;
+    if (unn < units32) {
+      locate(unn, jnn, c0nn, nnn);
+      pvnn = load_ptrs(ptrs + static_cast<int64_t>(jnn) * K);
+    }
+    if (h < 4)
+      __builtin_amdgcn_s_setprio(2);
+    else if (h < 8)
+      __builtin_amdgcn_s_setprio(1);
+    else
+      __builtin_amdgcn_s_setprio(0);
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      double p[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int i = 8 * b + r;
+        const double d = static_cast<double>(x[i] - a);  // fp32 difference, as the reference forms it
+        p[r] = d * d;
+        if (i < PF)
+          x[i] = xp[i < PF ? i : 0];
+        else
+          x[i] = load_fast(pvn, i, soffn, nrecn, Kwn);
+      }
+      const double q01 = fold32(p[0], p[1]), q23 = fold32(p[2], p[3]);
+      const double q45 = fold32(p[4], p[5]), q67 = fold32(p[6], p[7]);
+      acc[64 * b] += fold8(fold16(q01, q23), fold16(q45, q67), upper);
+    }
+    if (un < units32 && !fastn) {
+      int Ks = K;
+      asm volatile("" : "+s"(Ks));
+      load_slow(pvn, c0n, nn, Ks);
+    }
+    __builtin_amdgcn_s_setprio(0);
+    j = jn;
+    c0 = c0n;
+    n = nn;
+    jn = jnn;
+    c0n = c0nn;
+    nn = nnn;
+    pvn = pvnn;
+  }
+  const int row_in = win_batch_row(lane);
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    double sm = acc[64 * b];
+    sm += dpp_move_f64<0xB1, 0xF>(sm);
+    sm += dpp_move_f64<0x4E, 0xF>(sm);
+    sm += dpp_move_f64<0x141, 0xF>(sm);
+    const int row = 8 * b + row_in;
+    if ((lane & 7) == 0 && r0 + row < K) partials[static_cast<int64_t>(r0 + row) * G + blockIdx.x] = sm;
+  }
+}
+
 constexpr int64_t kSegSplitMaxK = 1024;  // the split-row windows' reach (16 waves of 64 clients)
 
 // workgroups of the split-row window launch over `units` windows (0: not resident)
+constexpr int kSegWinfPF8 = 8, kSegWinfPF16 = 16;  // prefetched rows at <= 8 / 16 waves
+
+// FEDAVG_SEGWINN_BARRIER=1 keeps round 5's barrier form of the zero-copy
+// split windows (A/B); the hand-off form is the default
+inline bool seg_barrier_windows() {
+  static const bool on = [] {
+    const char* e = std::getenv("FEDAVG_SEGWINN_BARRIER");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 inline int64_t segwinn_blocks(int64_t K, int64_t units) {
   const int ns = static_cast<int>((K + 63) / 64);
-  int64_t res = ns <= 8 ? resident_blocks(reduce_sqdist_segwinn_kernel<8>, 64 * ns)
-                        : resident_blocks(reduce_sqdist_segwinn_kernel<16>, 64 * ns);
+  const bool bar = seg_barrier_windows();
+  int64_t res = ns <= 8 ? (bar ? resident_blocks(reduce_sqdist_segwinn_kernel<8>, 64 * ns)
+                               : resident_blocks(reduce_sqdist_segwinf_kernel<8, kSegWinfPF8>, 64 * ns))
+                        : (bar ? resident_blocks(reduce_sqdist_segwinn_kernel<16>, 64 * ns)
+                               : resident_blocks(reduce_sqdist_segwinf_kernel<16, kSegWinfPF16>, 64 * ns));
   // 5 waves per workgroup (257-320 clients): 4 resident workgroups per CU
   // ran 8-11 % slower than 3 (260 x 8M 1.97 vs 1.77 ms, 300 x 5M 1.32 vs
   // 1.18, 320 x 3M 0.87 vs 0.80, host-inclusive; profiles/r05/seg_layout_cfg4/
@@ -1391,14 +1616,23 @@ int launch_seg_fused(const SegFusedPlan& p, const SegKey* keys, const int64_t* t
     if (partial_elems < K * p.waves)
       return set_error(FEDAVG_EINVAL, "%s: partials need %lld doubles", what, (long long)(K * p.waves));
     const int ns = static_cast<int>((K + 63) / 64);
-    if (ns <= 8)
-      hipLaunchKernelGGL((reduce_sqdist_segwinn_kernel<8>), dim3(static_cast<unsigned>(p.waves)),
-                         dim3(static_cast<unsigned>(64 * ns)), 0, s, keys, tptrs, n_keys, units, k32, weights, out,
-                         partials);
-    else
-      hipLaunchKernelGGL((reduce_sqdist_segwinn_kernel<16>), dim3(static_cast<unsigned>(p.waves)),
-                         dim3(static_cast<unsigned>(64 * ns)), 0, s, keys, tptrs, n_keys, units, k32, weights, out,
-                         partials);
+    const dim3 grid(static_cast<unsigned>(p.waves)), block(static_cast<unsigned>(64 * ns));
+    if (K < 2)
+      return set_error(FEDAVG_EMODE, "%s: the split windows take K >= 2", what);
+    if (seg_barrier_windows()) {
+      if (ns <= 8)
+        hipLaunchKernelGGL((reduce_sqdist_segwinn_kernel<8>), grid, block, 0, s, keys, tptrs, n_keys, units, k32,
+                           weights, out, partials);
+      else
+        hipLaunchKernelGGL((reduce_sqdist_segwinn_kernel<16>), grid, block, 0, s, keys, tptrs, n_keys, units, k32,
+                           weights, out, partials);
+    } else if (ns <= 8) {
+      hipLaunchKernelGGL((reduce_sqdist_segwinf_kernel<8, kSegWinfPF8>), grid, block, 0, s, keys, tptrs, n_keys, units,
+                         k32, weights, out, partials);
+    } else {
+      hipLaunchKernelGGL((reduce_sqdist_segwinf_kernel<16, kSegWinfPF16>), grid, block, 0, s, keys, tptrs, n_keys,
+                         units, k32, weights, out, partials);
+    }
     nparts = p.waves;
   } else if (p.win) {
     if (partial_elems < K * p.waves)

@@ -198,6 +198,50 @@ def test_split_windows_cfg4_shard_and_nonfinite():
     assert torch.equal(torch.isnan(s), torch.isnan(_sumsq_ref(x, out, P)))
 
 
+@pytest.mark.parametrize("nsmax,pf,Ks", [(8, 8, (2, 63, 64, 65, 200, 511, 512)), (16, 16, (513, 777, 1024)),
+                                          (16, 8, (70, 640)), (8, 16, (129, 448))])
+def test_split_windows_handoff_kernel_vs_oracle(nsmax, pf, Ks):
+    """reduce_sqdist_winf_kernel (the production split windows: LDS flags
+    instead of barriers, broadcast weights, PF prefetched rows) through the
+    probe entry at every wave count it serves, K below a multiple of 64
+    (padding rows weighted -0.0), one window, a ragged last window and more
+    windows than workgroups: the oracle's bits, sums within 1e-12 of torch
+    fp64, deterministic."""
+    code = 91000000 + pf * 100 + nsmax
+    for K in Ks:
+        for P in (1, 67, 64 * 7 + 3, 2_000_003 if K in (Ks[0], Ks[-1]) else 40_001):
+            x, ld, weights = _rows(K, P, K * 31 + P)
+            w = mfl_amd.weights_tensor(weights, torch.float32, DEV)
+            out, s = _win(x, K, P, ld, w, 0, 0, code=code)
+            if P <= 64 * 7 + 3:
+                exp = O.reduce_f32(x[:, :P].cpu().numpy(), np.array([np.float32(v) for v in weights], dtype=np.float32))
+                assert out.cpu().numpy().view(np.uint32).tobytes() == exp.view(np.uint32).tobytes(), (K, P)
+            else:
+                _oracle_windows(x, out, weights, P, n=3, width=min(2053, P // 4), seed=K)
+            assert torch.equal(out.view(torch.int32), mfl_amd.reduce_packed(x, w, P).view(torch.int32)), (K, P)
+            ref = _sumsq_torch64(x, out, P)
+            rel = ((s - ref).abs() / ref.clamp_min(1e-300)).max().item()
+            assert rel < 1e-12, (K, P, rel)
+            _, again = _win(x, K, P, ld, w, 0, 0, code=code)
+            assert torch.equal(s, again)
+            del x
+
+
+def test_split_windows_handoff_kernel_bounds():
+    """The hand-off kernel refuses K past its waves and K < 2 (EMODE; the
+    probe entry itself refuses K > 1024 first, EINVAL)."""
+    lib = mfl_amd._lib.load_probe()
+    for K, code in ((513, 91000808), (1, 91000808), (1025, 91001616)):
+        x, ld, weights = _rows(K, 100, 1)
+        w = mfl_amd.weights_tensor(weights, torch.float32, DEV)
+        work = torch.empty(K * 8192, dtype=torch.float64, device=DEV)
+        out = torch.empty(100, device=DEV)
+        s = torch.empty(K, dtype=torch.float64, device=DEV)
+        rc = lib.fedavg_reduce_sqdist_f32_variant(x.data_ptr(), K, 100, ld, w.data_ptr(), out.data_ptr(), work.data_ptr(),
+                                                  work.numel(), s.data_ptr(), code, 0, None)
+        assert rc == (mfl_amd._lib.FEDAVG_EINVAL if K > 1024 else mfl_amd._lib.FEDAVG_EMODE), (K, code, rc)
+
+
 def _oracle_windows(x, out, weights, P, n=6, width=2053, seed=0):
     """Sampled column windows of the fused output, bit for bit against the
     oracle (fedavg_trainer.py:450-457 restated) on host copies of the same
