@@ -221,6 +221,154 @@ __device__ __forceinline__ void chain8_row_bcast(float& a, float& tc, float w, f
 #undef FEDAVG_C8_ADD
 }
 
+// chain8_row_bcast for two columns per lane (window VEC 2): the rows' two
+// products by the broadcast weight, then the two columns' adds of the row
+// before (four instructions a row, each add reading a product issued four
+// instructions earlier).  The block text is generated (rows 1..7, + row 8's
+// product unless LAST).
+template <int H, bool LAST, class V2>
+__device__ __forceinline__ void chain8_row_bcast2(float& a0, float& a1, float& tc0, float& tc1, float w, float wn,
+                                                  const V2* x) {
+  float t10, t11;
+  if constexpr (H == 0 && LAST) {
+    asm("v_mul_f32_dpp %[t10], %[w], %[x10] row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+          "v_mul_f32_dpp %[t11], %[w], %[x11] row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+          "v_add_f32_e32 %[a0], %[a0], %[tc0]\n\t"
+          "v_add_f32_e32 %[a1], %[a1], %[tc1]\n\t"
+          "v_mul_f32_dpp %[tc0], %[w], %[x20] row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+          "v_mul_f32_dpp %[tc1], %[w], %[x21] row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+          "v_add_f32_e32 %[a0], %[a0], %[t10]\n\t"
+          "v_add_f32_e32 %[a1], %[a1], %[t11]\n\t"
+          "v_mul_f32_dpp %[t10], %[w], %[x30] row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+          "v_mul_f32_dpp %[t11], %[w], %[x31] row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+          "v_add_f32_e32 %[a0], %[a0], %[tc0]\n\t"
+          "v_add_f32_e32 %[a1], %[a1], %[tc1]\n\t"
+          "v_mul_f32_dpp %[tc0], %[w], %[x40] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+          "v_mul_f32_dpp %[tc1], %[w], %[x41] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+          "v_add_f32_e32 %[a0], %[a0], %[t10]\n\t"
+          "v_add_f32_e32 %[a1], %[a1], %[t11]\n\t"
+          "v_mul_f32_dpp %[t10], %[w], %[x50] row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+          "v_mul_f32_dpp %[t11], %[w], %[x51] row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+          "v_add_f32_e32 %[a0], %[a0], %[tc0]\n\t"
+          "v_add_f32_e32 %[a1], %[a1], %[tc1]\n\t"
+          "v_mul_f32_dpp %[tc0], %[w], %[x60] row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+          "v_mul_f32_dpp %[tc1], %[w], %[x61] row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+          "v_add_f32_e32 %[a0], %[a0], %[t10]\n\t"
+          "v_add_f32_e32 %[a1], %[a1], %[t11]\n\t"
+          "v_mul_f32_dpp %[t10], %[w], %[x70] row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+          "v_mul_f32_dpp %[t11], %[w], %[x71] row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+          "v_add_f32_e32 %[a0], %[a0], %[tc0]\n\t"
+          "v_add_f32_e32 %[a1], %[a1], %[tc1]\n\t"
+          "v_add_f32_e32 %[a0], %[a0], %[t10]\n\t"
+          "v_add_f32_e32 %[a1], %[a1], %[t11]\n\t"
+        : [a0] "+v"(a0), [a1] "+v"(a1), [tc0] "+v"(tc0), [tc1] "+v"(tc1), [t10] "=&v"(t10), [t11] "=&v"(t11)
+        : [w] "v"(w), [x10] "v"(x[1][0]), [x11] "v"(x[1][1]), [x20] "v"(x[2][0]), [x21] "v"(x[2][1]), [x30] "v"(x[3][0]), [x31] "v"(x[3][1]), [x40] "v"(x[4][0]), [x41] "v"(x[4][1]), [x50] "v"(x[5][0]), [x51] "v"(x[5][1]), [x60] "v"(x[6][0]), [x61] "v"(x[6][1]), [x70] "v"(x[7][0]), [x71] "v"(x[7][1]));
+  } else if constexpr (H == 0) {
+    asm("v_mul_f32_dpp %[t10], %[w], %[x10] row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+          "v_mul_f32_dpp %[t11], %[w], %[x11] row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+          "v_add_f32_e32 %[a0], %[a0], %[tc0]\n\t"
+          "v_add_f32_e32 %[a1], %[a1], %[tc1]\n\t"
+          "v_mul_f32_dpp %[tc0], %[w], %[x20] row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+          "v_mul_f32_dpp %[tc1], %[w], %[x21] row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+          "v_add_f32_e32 %[a0], %[a0], %[t10]\n\t"
+          "v_add_f32_e32 %[a1], %[a1], %[t11]\n\t"
+          "v_mul_f32_dpp %[t10], %[w], %[x30] row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+          "v_mul_f32_dpp %[t11], %[w], %[x31] row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+          "v_add_f32_e32 %[a0], %[a0], %[tc0]\n\t"
+          "v_add_f32_e32 %[a1], %[a1], %[tc1]\n\t"
+          "v_mul_f32_dpp %[tc0], %[w], %[x40] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+          "v_mul_f32_dpp %[tc1], %[w], %[x41] row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+          "v_add_f32_e32 %[a0], %[a0], %[t10]\n\t"
+          "v_add_f32_e32 %[a1], %[a1], %[t11]\n\t"
+          "v_mul_f32_dpp %[t10], %[w], %[x50] row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+          "v_mul_f32_dpp %[t11], %[w], %[x51] row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+          "v_add_f32_e32 %[a0], %[a0], %[tc0]\n\t"
+          "v_add_f32_e32 %[a1], %[a1], %[tc1]\n\t"
+          "v_mul_f32_dpp %[tc0], %[w], %[x60] row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+          "v_mul_f32_dpp %[tc1], %[w], %[x61] row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+          "v_add_f32_e32 %[a0], %[a0], %[t10]\n\t"
+          "v_add_f32_e32 %[a1], %[a1], %[t11]\n\t"
+          "v_mul_f32_dpp %[t10], %[w], %[x70] row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+          "v_mul_f32_dpp %[t11], %[w], %[x71] row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+          "v_add_f32_e32 %[a0], %[a0], %[tc0]\n\t"
+          "v_add_f32_e32 %[a1], %[a1], %[tc1]\n\t"
+          "v_mul_f32_dpp %[tc0], %[w], %[x80] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+          "v_mul_f32_dpp %[tc1], %[w], %[x81] row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+          "v_add_f32_e32 %[a0], %[a0], %[t10]\n\t"
+          "v_add_f32_e32 %[a1], %[a1], %[t11]\n\t"
+        : [a0] "+v"(a0), [a1] "+v"(a1), [tc0] "+v"(tc0), [tc1] "+v"(tc1), [t10] "=&v"(t10), [t11] "=&v"(t11)
+        : [w] "v"(w), [x10] "v"(x[1][0]), [x11] "v"(x[1][1]), [x20] "v"(x[2][0]), [x21] "v"(x[2][1]), [x30] "v"(x[3][0]), [x31] "v"(x[3][1]), [x40] "v"(x[4][0]), [x41] "v"(x[4][1]), [x50] "v"(x[5][0]), [x51] "v"(x[5][1]), [x60] "v"(x[6][0]), [x61] "v"(x[6][1]), [x70] "v"(x[7][0]), [x71] "v"(x[7][1]), [x80] "v"(x[8][0]), [x81] "v"(x[8][1]));
+  } else if constexpr (LAST) {
+    asm("v_mul_f32_dpp %[t10], %[w], %[x10] row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+          "v_mul_f32_dpp %[t11], %[w], %[x11] row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+          "v_add_f32_e32 %[a0], %[a0], %[tc0]\n\t"
+          "v_add_f32_e32 %[a1], %[a1], %[tc1]\n\t"
+          "v_mul_f32_dpp %[tc0], %[w], %[x20] row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+          "v_mul_f32_dpp %[tc1], %[w], %[x21] row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+          "v_add_f32_e32 %[a0], %[a0], %[t10]\n\t"
+          "v_add_f32_e32 %[a1], %[a1], %[t11]\n\t"
+          "v_mul_f32_dpp %[t10], %[w], %[x30] row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+          "v_mul_f32_dpp %[t11], %[w], %[x31] row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+          "v_add_f32_e32 %[a0], %[a0], %[tc0]\n\t"
+          "v_add_f32_e32 %[a1], %[a1], %[tc1]\n\t"
+          "v_mul_f32_dpp %[tc0], %[w], %[x40] row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
+          "v_mul_f32_dpp %[tc1], %[w], %[x41] row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
+          "v_add_f32_e32 %[a0], %[a0], %[t10]\n\t"
+          "v_add_f32_e32 %[a1], %[a1], %[t11]\n\t"
+          "v_mul_f32_dpp %[t10], %[w], %[x50] row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
+          "v_mul_f32_dpp %[t11], %[w], %[x51] row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
+          "v_add_f32_e32 %[a0], %[a0], %[tc0]\n\t"
+          "v_add_f32_e32 %[a1], %[a1], %[tc1]\n\t"
+          "v_mul_f32_dpp %[tc0], %[w], %[x60] row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
+          "v_mul_f32_dpp %[tc1], %[w], %[x61] row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
+          "v_add_f32_e32 %[a0], %[a0], %[t10]\n\t"
+          "v_add_f32_e32 %[a1], %[a1], %[t11]\n\t"
+          "v_mul_f32_dpp %[t10], %[w], %[x70] row_newbcast:15 row_mask:0xf bank_mask:0xf\n\t"
+          "v_mul_f32_dpp %[t11], %[w], %[x71] row_newbcast:15 row_mask:0xf bank_mask:0xf\n\t"
+          "v_add_f32_e32 %[a0], %[a0], %[tc0]\n\t"
+          "v_add_f32_e32 %[a1], %[a1], %[tc1]\n\t"
+          "v_add_f32_e32 %[a0], %[a0], %[t10]\n\t"
+          "v_add_f32_e32 %[a1], %[a1], %[t11]\n\t"
+        : [a0] "+v"(a0), [a1] "+v"(a1), [tc0] "+v"(tc0), [tc1] "+v"(tc1), [t10] "=&v"(t10), [t11] "=&v"(t11)
+        : [w] "v"(w), [x10] "v"(x[1][0]), [x11] "v"(x[1][1]), [x20] "v"(x[2][0]), [x21] "v"(x[2][1]), [x30] "v"(x[3][0]), [x31] "v"(x[3][1]), [x40] "v"(x[4][0]), [x41] "v"(x[4][1]), [x50] "v"(x[5][0]), [x51] "v"(x[5][1]), [x60] "v"(x[6][0]), [x61] "v"(x[6][1]), [x70] "v"(x[7][0]), [x71] "v"(x[7][1]));
+  } else {
+    asm("v_mul_f32_dpp %[t10], %[w], %[x10] row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+          "v_mul_f32_dpp %[t11], %[w], %[x11] row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+          "v_add_f32_e32 %[a0], %[a0], %[tc0]\n\t"
+          "v_add_f32_e32 %[a1], %[a1], %[tc1]\n\t"
+          "v_mul_f32_dpp %[tc0], %[w], %[x20] row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+          "v_mul_f32_dpp %[tc1], %[w], %[x21] row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+          "v_add_f32_e32 %[a0], %[a0], %[t10]\n\t"
+          "v_add_f32_e32 %[a1], %[a1], %[t11]\n\t"
+          "v_mul_f32_dpp %[t10], %[w], %[x30] row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+          "v_mul_f32_dpp %[t11], %[w], %[x31] row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+          "v_add_f32_e32 %[a0], %[a0], %[tc0]\n\t"
+          "v_add_f32_e32 %[a1], %[a1], %[tc1]\n\t"
+          "v_mul_f32_dpp %[tc0], %[w], %[x40] row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
+          "v_mul_f32_dpp %[tc1], %[w], %[x41] row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
+          "v_add_f32_e32 %[a0], %[a0], %[t10]\n\t"
+          "v_add_f32_e32 %[a1], %[a1], %[t11]\n\t"
+          "v_mul_f32_dpp %[t10], %[w], %[x50] row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
+          "v_mul_f32_dpp %[t11], %[w], %[x51] row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
+          "v_add_f32_e32 %[a0], %[a0], %[tc0]\n\t"
+          "v_add_f32_e32 %[a1], %[a1], %[tc1]\n\t"
+          "v_mul_f32_dpp %[tc0], %[w], %[x60] row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
+          "v_mul_f32_dpp %[tc1], %[w], %[x61] row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
+          "v_add_f32_e32 %[a0], %[a0], %[t10]\n\t"
+          "v_add_f32_e32 %[a1], %[a1], %[t11]\n\t"
+          "v_mul_f32_dpp %[t10], %[w], %[x70] row_newbcast:15 row_mask:0xf bank_mask:0xf\n\t"
+          "v_mul_f32_dpp %[t11], %[w], %[x71] row_newbcast:15 row_mask:0xf bank_mask:0xf\n\t"
+          "v_add_f32_e32 %[a0], %[a0], %[tc0]\n\t"
+          "v_add_f32_e32 %[a1], %[a1], %[tc1]\n\t"
+          "v_mul_f32_dpp %[tc0], %[wn], %[x80] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+          "v_mul_f32_dpp %[tc1], %[wn], %[x81] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+          "v_add_f32_e32 %[a0], %[a0], %[t10]\n\t"
+          "v_add_f32_e32 %[a1], %[a1], %[t11]\n\t"
+        : [a0] "+v"(a0), [a1] "+v"(a1), [tc0] "+v"(tc0), [tc1] "+v"(tc1), [t10] "=&v"(t10), [t11] "=&v"(t11)
+        : [w] "v"(w), [wn] "v"(wn), [x10] "v"(x[1][0]), [x11] "v"(x[1][1]), [x20] "v"(x[2][0]), [x21] "v"(x[2][1]), [x30] "v"(x[3][0]), [x31] "v"(x[3][1]), [x40] "v"(x[4][0]), [x41] "v"(x[4][1]), [x50] "v"(x[5][0]), [x51] "v"(x[5][1]), [x60] "v"(x[6][0]), [x61] "v"(x[6][1]), [x70] "v"(x[7][0]), [x71] "v"(x[7][1]), [x80] "v"(x[8][0]), [x81] "v"(x[8][1]));
+  }
+}
+
 // fl32(w[16r + I % 16] * x) by the same broadcast (the chain's first product)
 template <int I>
 __device__ __forceinline__ float mul_row_bcast(float w, float x) {

@@ -867,6 +867,9 @@ int launch_fused_rs(const float* clients, int64_t K, int64_t P, int64_t ld, cons
 // slice (num_records 0 past the last window: the tail's reloads are dropped
 // in the address unit, no traffic), columns past P inside the last slice are
 // zeroed before the chain.
+// MODE 256 (probe): the chain's weights by row broadcast (lane 16r + j of
+// wvb[k] = row 16k + j's weight) in hand-pipelined 8-row blocks
+// (chain8_row_bcast2): no v_readlane / LDS weight reads, four VALU a row.
 // MODE 1: loads only (a traffic probe: wrong results).  MODE 4 (probe):
 // squares in fp32 (the VEC columns' fl32(d*d) summed in fp32, widened once
 // per row): the fp64 VALU stream's share of time and clock, measured.
@@ -909,6 +912,16 @@ __global__ __launch_bounds__(64 * NW, MINW) void reduce_sqdist_win_kernel(
   __shared__ double accl[NW][NB][64];
   for (int i = threadIdx.x; i < ((KMAX + 3) & ~3); i += 64 * NW) wl[i] = i < K ? W[i] : -0.0f;
   float wv0 = lane < K ? W[lane] : -0.0f, wv1 = 64 + lane < K ? W[64 + lane] : -0.0f;  // LROWS: lane l = W[l], W[64 + l]
+  constexpr bool BCW = (MODE & 256) != 0;
+  static_assert(!BCW || (VEC == 2 && KMAX >= 16), "broadcast weights: VEC 2, 8-row blocks");
+  float wvb[BCW ? (KMAX + 15) / 16 : 1];
+  if constexpr (BCW) {
+#pragma unroll
+    for (int k = 0; k < (KMAX + 15) / 16; ++k) {
+      const int row = 16 * k + (lane & 15);
+      wvb[k] = row < K ? W[row] : -0.0f;
+    }
+  }
   double* acc = &accl[threadIdx.x >> 6][0][lane];
 #pragma unroll
   for (int b = 0; b < NB; ++b) acc[64 * b] = 0.0;
@@ -1024,7 +1037,30 @@ __global__ __launch_bounds__(64 * NW, MINW) void reduce_sqdist_win_kernel(
     }
     // the reference's chain, per lane: fl32(x_0 w_0), then + fl32(x_i w_i) in client order
     V a;
-    if constexpr (LROWS) {
+    if constexpr (BCW) {
+      float a0 = -0.0f, a1 = -0.0f;  // fl32(-0.0 + p) is p, bit for bit
+      float tc0 = mul_row_bcast<0>(wvb[0], x[0][0]), tc1 = mul_row_bcast<0>(wvb[0], x[0][1]);
+      constexpr int NBLK = KMAX / 8, REM = KMAX % 8;
+      static_for<NBLK>([&](auto bc) {
+        constexpr int b = decltype(bc)::value;
+        constexpr bool last = b == NBLK - 1 && REM == 0;
+        chain8_row_bcast2<b % 2, last>(a0, a1, tc0, tc1, wvb[b / 2], wvb[last ? b / 2 : (b + 1) / 2], x + 8 * b);
+      });
+      static_for<REM>([&](auto rc) {  // the rows past the last 8-row block (tc: row 8 NBLK + r's product)
+        constexpr int i = 8 * NBLK + decltype(rc)::value;
+        float n0 = 0.f, n1 = 0.f;
+        if constexpr (i + 1 < KMAX) {
+          n0 = mul_row_bcast<i + 1>(wvb[(i + 1) / 16], x[i + 1][0]);
+          n1 = mul_row_bcast<i + 1>(wvb[(i + 1) / 16], x[i + 1][1]);
+        }
+        a0 = a0 + tc0;
+        a1 = a1 + tc1;
+        tc0 = n0;
+        tc1 = n1;
+      });
+      a[0] = a0;
+      a[1] = a1;
+    } else if constexpr (LROWS) {
       // weights from VGPR lanes (v_readlane): an LDS read here would wait for
       // the LDS-DMA just issued (the compiler cannot tell the arrays apart)
       asm volatile("" : "+v"(wv0), "+v"(wv1));  // re-read per window: not hoisted into SGPRs
@@ -2532,6 +2568,8 @@ int fedavg_reduce_sqdist_f32_variant(const float* clients, int64_t K, int64_t P,
     FEDAVG_WIN_CASE(2, 4, 128)
     FEDAVG_WIN_CASE(2, 4, 65)  // LDS rows, loads only (round 6 clock attribution)
     FEDAVG_WIN_CASE(2, 4, 68)  // LDS rows, fp32 squares
+    FEDAVG_WIN_CASE(2, 4, 256)  // broadcast weights (round 6)
+    FEDAVG_WIN_CASE(2, 4, 320)  // LDS rows + broadcast weights (round 6)
     case 60000000 + 192 * 1000000 + 42:  // LDS rows + 8-row descriptors
       return launch_fused_win<100, 2, 4, 192>(clients, K, P, ld, weights, out, workspace, workspace_elems, sumsq,
                                               blocks_per_cu, s, what);
