@@ -1509,7 +1509,9 @@ int launch_fused_winn(const float* clients, int64_t K, int64_t P, int64_t ld, co
 // the same windows, so every flag a wave waits for is set; the polls are
 // bounded (kHandoffSpinMax) so a broken protocol ends in wrong sums (the parity
 // tests), never in a hung grid.  Weights by row broadcast (chain8_row_bcast).
-// MODE 8: the timeline stamps of the winn kernel.
+// MODE 8: the timeline stamps of the winn kernel.  Probes: MODE 1 polls
+// without s_sleep, 2 keeps every priority at 0, 4 keeps the turn at the
+// squares' priority.
 // ---------------------------------------------------------------------------
 constexpr int kHandoffSpinMax = 1 << 16;  // x s_sleep 1 (64 clocks): ~1.7 ms, a window is ~13 us
 
@@ -1566,14 +1568,15 @@ __global__ __launch_bounds__(64 * NSMAX, win_min_waves(64, 1)) void reduce_sqdis
   typedef __attribute__((address_space(3))) volatile int lds_flag_t;
   const auto wait_flag = [&](int idx, int seq) __attribute__((always_inline)) {
     lds_flag_t* f = (lds_flag_t*)&flag[idx];
-    for (int it = 0; __builtin_amdgcn_readfirstlane(*f) != seq && it < kHandoffSpinMax; ++it)
-      __builtin_amdgcn_s_sleep(1);
+    for (int it = 0; __builtin_amdgcn_readfirstlane(*f) != seq && it < kHandoffSpinMax * ((MODE & 1) ? 16 : 1); ++it)
+      if constexpr ((MODE & 1) == 0) __builtin_amdgcn_s_sleep(1);
     asm volatile("" ::: "memory");
   };
   const auto publish = [&](int idx, int seq) __attribute__((always_inline)) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the payload's ds_write is done
     *(lds_flag_t*)&flag[idx] = seq;
   };
+  constexpr bool kPrio = (MODE & 2) == 0, kTurnPrio = kPrio && (MODE & 4) == 0;
   float x[KH];
   float xp[PF];
   {
@@ -1622,7 +1625,7 @@ __global__ __launch_bounds__(64 * NSMAX, win_min_waves(64, 1)) void reduce_sqdis
       a = part[h - 1][lane];
     }
     stamp(2);
-    __builtin_amdgcn_s_setprio(3);
+    if constexpr (kTurnPrio) __builtin_amdgcn_s_setprio(3);
     {
       float tc = mul_row_bcast<0>(wv[0], x[0]);
       static_for<KH / 8>([&](auto bc) {
@@ -1645,17 +1648,19 @@ __global__ __launch_bounds__(64 * NSMAX, win_min_waves(64, 1)) void reduce_sqdis
     }
     stamp(3);
     if (h < ns - 1) {
-      __builtin_amdgcn_s_setprio(0);
+      if constexpr (kTurnPrio) __builtin_amdgcn_s_setprio(0);
       wait_flag(NSMAX, seq);
       a = avg[lane];
     }
     // the squares, the next window's rows reloaded behind them: waves 0-3 first
-    if (h < 4)
-      __builtin_amdgcn_s_setprio(2);
-    else if (h < 8)
-      __builtin_amdgcn_s_setprio(1);
-    else
-      __builtin_amdgcn_s_setprio(0);
+    if constexpr (kPrio) {
+      if (h < 4)
+        __builtin_amdgcn_s_setprio(2);
+      else if (h < 8)
+        __builtin_amdgcn_s_setprio(1);
+      else
+        __builtin_amdgcn_s_setprio(0);
+    }
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       double p[8];
@@ -2676,6 +2681,16 @@ int fedavg_reduce_sqdist_f32_variant(const float* clients, int64_t K, int64_t P,
     FEDAVG_WINF_CASE(16, 8, 8)
     FEDAVG_WINF_CASE(8, 8, 0)
     FEDAVG_WINF_CASE(8, 16, 0)
+    FEDAVG_WINF_CASE(16, 16, 1)
+    FEDAVG_WINF_CASE(16, 16, 2)
+    FEDAVG_WINF_CASE(16, 16, 4)
+    FEDAVG_WINF_CASE(16, 24, 0)
+    FEDAVG_WINF_CASE(16, 32, 0)
+    FEDAVG_WINF_CASE(16, 16, 8)
+    FEDAVG_WINF_CASE(16, 16, 9)
+    FEDAVG_WINF_CASE(8, 8, 1)
+    FEDAVG_WINF_CASE(8, 8, 2)
+    FEDAVG_WINF_CASE(8, 16, 1)
 #undef FEDAVG_WINF_CASE
     default: return set_error(FEDAVG_EMODE, "%s: cols must be 32, 64, 128 or 256 (+1000: double-buffered)", what);
   }
