@@ -1510,10 +1510,10 @@ int launch_fused_winn(const float* clients, int64_t K, int64_t P, int64_t ld, co
 // bounded (kHandoffSpinMax) so a broken protocol ends in wrong sums (the parity
 // tests), never in a hung grid.  Weights by row broadcast (chain8_row_bcast).
 // MODE 8: the timeline stamps of the winn kernel.  Probes: MODE 1 polls
-// without s_sleep, 2 keeps every priority at 0, 4 keeps the turn at the
-// squares' priority.
+// with s_sleep 1 (the first form), 2 keeps every priority at 0, 4 keeps the
+// turn at the squares' priority.
 // ---------------------------------------------------------------------------
-constexpr int kHandoffSpinMax = 1 << 16;  // x s_sleep 1 (64 clocks): ~1.7 ms, a window is ~13 us
+constexpr int kHandoffSpinMax = 1 << 16;  // x 16 polls of ~100 clocks (or x s_sleep 1): < 50 ms, a window is ~13 us
 
 template <int NSMAX, int PF, int MODE = 0>
 __global__ __launch_bounds__(64 * NSMAX, win_min_waves(64, 1)) void reduce_sqdist_winf_kernel(
@@ -1568,8 +1568,10 @@ __global__ __launch_bounds__(64 * NSMAX, win_min_waves(64, 1)) void reduce_sqdis
   typedef __attribute__((address_space(3))) volatile int lds_flag_t;
   const auto wait_flag = [&](int idx, int seq) __attribute__((always_inline)) {
     lds_flag_t* f = (lds_flag_t*)&flag[idx];
-    for (int it = 0; __builtin_amdgcn_readfirstlane(*f) != seq && it < kHandoffSpinMax * ((MODE & 1) ? 16 : 1); ++it)
-      if constexpr ((MODE & 1) == 0) __builtin_amdgcn_s_sleep(1);
+    // tight polls (no s_sleep): 600 x 10M 4.20 -> 4.09 ms, 1000 x 12.5M 7.97 -> 7.93
+    // (profiles/r06/winf_modes/); MODE 1 is the s_sleep 1 form
+    for (int it = 0; __builtin_amdgcn_readfirstlane(*f) != seq && it < kHandoffSpinMax * ((MODE & 1) ? 1 : 16); ++it)
+      if constexpr ((MODE & 1) != 0) __builtin_amdgcn_s_sleep(1);
     asm volatile("" ::: "memory");
   };
   const auto publish = [&](int idx, int seq) __attribute__((always_inline)) {
@@ -1966,8 +1968,14 @@ constexpr int kWinfPF8 = 8, kWinfPF16 = 16;
 // (0.493 vs 0.529) or 270 x 5M (0.933 vs 0.981), and tie at 200 x 1.2M (18
 // windows per workgroup): below 369 rows they take rounds of >= 24 windows
 // per workgroup, and only with the prefetch on
-constexpr int64_t kFusedWinnLowMinK = 161, kFusedWinnGapMinK = 257, kFusedWinnGapMaxK = 288;
-constexpr int64_t kFusedWinnLowMinPerBlock = 24;
+// Round 6, the hand-off kernel (profiles/r06/winf_bands/, ms, plan then vs
+// winf): 160 x 5M 0.615 vs 0.547; 260 x 5M 0.913 vs 0.851; 270 x 5M 0.939 vs
+// 0.876; 288 x 5M 0.983 vs 0.923 (the old 257-288 gap); 200 x 1.2M (18
+// windows per workgroup) 0.190 vs 0.182; 200 x 800K (12) 0.144 vs 0.126;
+// 300-368 x 5M equal; below 160 the tiles keep it (150 x 5M 0.526 vs 0.536,
+// 130 x 5M 0.459 vs 0.495)
+constexpr int64_t kFusedWinnLowMinK = 160;
+constexpr int64_t kFusedWinnLowMinPerBlock = 8;
 constexpr int64_t kWinMinPerWave = 16;  // windows per wave below which the tile kernels keep the round
 // ... except in the LDS-DMA tiles' weak band, 65-96 rows, where the windows
 // win down to ~400K columns (profiles/r03/win/short_rows_*.jsonl, ms, tiles
@@ -2018,7 +2026,7 @@ inline FusedPlan fused_plan(int64_t K, int64_t P) {
   if (K <= 48) return {kFusedLds, 256, 0};
   if (K <= 64) return {kFusedLds, 128, 0};
   if (K <= 128) return {kFusedLds, 64, 0};
-  if (K >= kFusedWinnLowMinK && K < kFusedWinnMinK && (K < kFusedWinnGapMinK || K > kFusedWinnGapMaxK) &&
+  if (K >= kFusedWinnLowMinK && K < kFusedWinnMinK &&
       split_prefetch_rows() > 0) {
     const int64_t grid = fused_winf_grid<8, kWinfPF8>(K, P);
     if (grid > 0 && (P + 63) / 64 >= kFusedWinnLowMinPerBlock * grid) return {kFusedWinn, 64, 8};

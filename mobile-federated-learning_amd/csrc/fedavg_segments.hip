@@ -1150,7 +1150,7 @@ __global__ __launch_bounds__(64 * NSMAX, win_min_waves(64, 1)) void reduce_sqdis
     const float* __restrict__ W, float* __restrict__ out, double* __restrict__ partials) {
   constexpr int KH = 64, WC = 64, NB = 8, NWV = 4;
   static_assert(PF >= 1 && PF <= KH, "prefetched rows");
-  constexpr int kSpinMax = 1 << 16;
+  constexpr int kSpinMax = 1 << 20;  // tight polls, as the rows kernel's
   const int lane = threadIdx.x & 63;
   const int h = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int ns = __builtin_amdgcn_readfirstlane(static_cast<int>(blockDim.x >> 6));
@@ -1176,7 +1176,8 @@ __global__ __launch_bounds__(64 * NSMAX, win_min_waves(64, 1)) void reduce_sqdis
   typedef __attribute__((address_space(3))) volatile int lds_flag_t;
   const auto wait_flag = [&](int idx, int seq) __attribute__((always_inline)) {
     lds_flag_t* f = (lds_flag_t*)&flag[idx];
-    for (int it = 0; __builtin_amdgcn_readfirstlane(*f) != seq && it < kSpinMax; ++it) __builtin_amdgcn_s_sleep(1);
+    for (int it = 0; __builtin_amdgcn_readfirstlane(*f) != seq && it < kSpinMax; ++it) {
+    }
     asm volatile("" ::: "memory");
   };
   const auto publish = [&](int idx, int seq) __attribute__((always_inline)) {

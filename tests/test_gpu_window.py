@@ -145,9 +145,9 @@ def test_split_windows_vs_oracle(K):
         assert torch.equal(s, again)
 
 
-@pytest.mark.parametrize("K", [161, 192, 256, 289, 320, 368])
+@pytest.mark.parametrize("K", [160, 192, 256, 270, 289, 320, 368])
 def test_split_windows_low_band(K):
-    """161-256 and 289-368 clients on long rows take the split-row windows too
+    """160-368 clients on long rows take the split-row windows too
     (prefetching the next window's first 8 rows per wave): sampled windows of
     the average bit-exact against the oracle, the whole average equal to the
     row reduce's bits, the sums within 1e-12 of plain torch in fp64."""
@@ -326,11 +326,11 @@ def test_window_plan_short_rows_and_other_k():
     # split-row windows from 369 rows: up to 8 waves per group to 512, 16 to 1024; then two passes
     assert lib.fedavg_fused_plan_of(369, 25_000_000) == KIND_WINN * 1000000 + 64 * 100 + 8
     assert lib.fedavg_fused_plan_of(369, 1_000) == KIND_WINN * 1000000 + 64 * 100 + 8
-    # ... and (with the next window's rows prefetched) 161-256 and 289-368 rows on long rows
-    for K in (161, 200, 256, 289, 320, 368):
+    # ... and (the hand-off kernel, round 6) 160-368 rows when each workgroup gets >= 8 windows
+    for K in (160, 161, 200, 256, 257, 288, 289, 320, 368):
         assert lib.fedavg_fused_plan_of(K, 25_000_000) == KIND_WINN * 1000000 + 64 * 100 + 8, K
-        assert lib.fedavg_fused_plan_of(K, 600_000) // 1000000 == 2, K  # < 24 windows per workgroup
-    for K in (129, 160, 257, 288):
+        assert lib.fedavg_fused_plan_of(K, 100_000) // 1000000 == 2, K  # < 8 windows per workgroup
+    for K in (129, 159):
         assert lib.fedavg_fused_plan_of(K, 25_000_000) // 1000000 == 2, K
     assert lib.fedavg_fused_plan_of(512, 25_000_000) == KIND_WINN * 1000000 + 64 * 100 + 8
     assert lib.fedavg_fused_plan_of(513, 25_000_000) == KIND_WINN * 1000000 + 64 * 100 + 16
