@@ -1570,8 +1570,35 @@ inline bool seg_split_ok(const int64_t* numel, int64_t n_keys) {
   return units_of(numel, n_keys, 64) < (int64_t(1) << 31);
 }
 
+// 129-256 clients take the zero-copy split windows too when every workgroup
+// gets >= kSegSplitMinPerBlock windows (round 6; profiles/r06/seg160/, seg129/,
+// resnet18_gn-shaped device rounds, ms, tiles vs split windows: 129 2.07 vs
+// 1.46; 150 2.29 vs 1.49; 160 2.44 vs 1.43; 200 2.90 vs 1.71; 256 4.12 vs
+// 2.10; the one-wave windows keep <= 128: 100 0.79 vs 1.06, 120 0.97 vs 1.11)
+constexpr int64_t kSegSplitMinK = 129, kSegSplitMinPerBlock = 8;
+// FEDAVG_SEG_SPLIT_MIN_K overrides kSegSplitMinK (probes)
+inline int64_t seg_split_min_k() {
+  static const int64_t v = [] {
+    const char* e = std::getenv("FEDAVG_SEG_SPLIT_MIN_K");
+    return e && e[0] ? static_cast<int64_t>(std::atoll(e)) : kSegSplitMinK;
+  }();
+  return v;
+}
+
 SegFusedPlan seg_fused_plan(const int64_t* numel, int64_t n_keys, int64_t K, bool all_raw) {
   SegFusedPlan p{false, segwin_kmax(K), seg_fused_cols(K), 0};
+  if (K >= seg_split_min_k() && K >= 2 && K <= kSegFusedMaxK && all_raw && !seg_barrier_windows() &&
+      seg_split_ok(numel, n_keys)) {
+    const int64_t units = units_of(numel, n_keys, 64);
+    const int64_t blocks = segwinn_blocks(K, units);
+    if (blocks > 0 && units >= kSegSplitMinPerBlock * blocks) {
+      p.win = true;
+      p.kmax = -1;
+      p.span = 64;
+      p.waves = blocks;
+      return p;
+    }
+  }
   if (K > kSegFusedMaxK) {  // kmax -1: the split-row windows (the caller checked seg_split_ok)
     if (K <= kSegSplitMaxK && all_raw && seg_split_ok(numel, n_keys)) {
       p.win = true;
@@ -1847,7 +1874,9 @@ int64_t fedavg_reduce_sqdist_segments_partials(int64_t K) {
                                 : (S == 128 ? seg_fused_per_cu_max<128>(K) : seg_fused_per_cu_max<256>(K)));
   const int64_t tiles = K * static_cast<int64_t>(per_cu > 0 ? per_cu : 1) * cu_count();
   const int64_t windows = K * segwin_waves_for(segwin_kmax(K), INT64_MAX / 2);  // a full window launch
-  return tiles > windows ? tiles : windows;
+  const int64_t split = K >= seg_split_min_k() ? K * segwinn_blocks(K, INT64_MAX / 2) : 0;  // 129-256: split windows
+  const int64_t need = tiles > windows ? tiles : windows;
+  return need > split ? need : split;
 }
 
 int fedavg_reduce_sqdist_segments_f32(const int64_t* client_ptrs, const int64_t* key_numel, const int64_t* key_offset,

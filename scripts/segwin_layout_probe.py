@@ -90,11 +90,14 @@ def main():
     ap.add_argument("--layout", default="separate", choices=["separate", "arena", "shuffled", "packed"])
     ap.add_argument("--config", default="resnet56")
     ap.add_argument("--calls", type=int, default=30)
+    ap.add_argument("--clients", type=int, default=0, help="the config's first N clients (0: all)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     lib = mfl_amd._lib.load()
     counts, dicts = device_clients(args.config, dev)
+    if args.clients:
+        counts, dicts = counts[:args.clients], dicts[:args.clients]
     dicts, rows = relayout(dicts, args.layout, dev)
     torch.cuda.synchronize()
     table = mfl_amd.KeyTable(dicts[0])

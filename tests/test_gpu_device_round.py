@@ -179,6 +179,24 @@ def test_device_round_split_windows_bit_exact(K):
     assert torch.equal(sumsq, again)  # deterministic
 
 
+@pytest.mark.parametrize("K", [129, 160, 200, 256])
+def test_device_round_split_windows_from_129(K):
+    """129-256 clients on a long enough model (>= 8 windows of 64 columns per
+    workgroup) take the zero-copy split windows too (round 6): every key kind
+    of _SPECS plus a long key, the reference's bits and the exact sums."""
+    specs = _SPECS + [((600_001,), torch.float32)]
+    counts, dicts = _clients(K, specs, seed=K + 1)
+    r = _Round(counts, dicts)
+    rc, out, sumsq = r.run()
+    assert rc == 0
+    exp = _expected(counts, dicts, r.g)
+    assert_bits(out.cpu(), exp, f"split-row device round K={K}")
+    ref = _exact_sums(dicts, r.g, exp)
+    assert np.allclose(sumsq.cpu().numpy(), ref, rtol=1e-10, atol=0.0)
+    _, _, again = r.run()
+    assert torch.equal(sumsq, again)
+
+
 @pytest.mark.parametrize("K", [1025])
 def test_device_round_many_clients_reduce_only(K):
     counts, dicts = _clients(K, [((300,), torch.float32), ((), torch.int64)], seed=9)
