@@ -1365,16 +1365,26 @@ inline int64_t segwinn_blocks(int64_t K, int64_t units) {
                                : resident_blocks(reduce_sqdist_segwinf_kernel<8, kSegWinfPF8>, 64 * ns))
                         : (bar ? resident_blocks(reduce_sqdist_segwinn_kernel<16>, 64 * ns)
                                : resident_blocks(reduce_sqdist_segwinf_kernel<16, kSegWinfPF16>, 64 * ns));
-  // 5 waves per workgroup (257-320 clients): 4 resident workgroups per CU
-  // ran 8-11 % slower than 3 (260 x 8M 1.97 vs 1.77 ms, 300 x 5M 1.32 vs
-  // 1.18, 320 x 3M 0.87 vs 0.80, host-inclusive; profiles/r05/seg_layout_cfg4/
-  // wgs_per_cu_*); FEDAVG_SEGWINN_PER_CU caps it for probes
+  // workgroups per CU: the resident ones rounded down to a power of two, as
+  // the rows kernel's grid (round 6, the hand-off kernel, resnet18_gn-shaped
+  // rounds, profiles/r06/zc_percu/, ms: 257 clients 3 per CU 2.70 vs 2 2.32;
+  // 300 2.83 vs 2.47; 129 clients 5 per CU 1.53 vs 4 1.47; 500 equal; the
+  // barrier form's rule was 3 at 5 waves); FEDAVG_SEGWINN_PER_CU caps it
   static const int64_t per_cu_env = [] {
     const char* e = std::getenv("FEDAVG_SEGWINN_PER_CU");
     return e && e[0] ? static_cast<int64_t>(std::atoll(e)) : int64_t(0);
   }();
-  const int64_t per_cu = per_cu_env > 0 ? per_cu_env : (ns == 5 ? 3 : 0);
-  if (per_cu > 0 && per_cu * cu_count() < res) res = per_cu * cu_count();
+  const int64_t cus = cu_count();
+  int64_t per_cu = per_cu_env;
+  if (per_cu <= 0 && !bar) {
+    const int64_t r = res / cus;
+    per_cu = 0;
+    if (r >= 1)
+      for (per_cu = 1; per_cu * 2 <= r;) per_cu *= 2;
+  } else if (per_cu <= 0) {
+    per_cu = ns == 5 ? 3 : 0;  // the barrier form's rule (round 5)
+  }
+  if (per_cu > 0 && per_cu * cus < res) res = per_cu * cus;
   return units < res ? units : res;
 }
 
