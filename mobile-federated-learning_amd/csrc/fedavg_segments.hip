@@ -1144,7 +1144,13 @@ __global__ __launch_bounds__(64 * NSMAX, win_min_waves(64, 1)) void reduce_sqdis
 // flight (vmcnt counts in issue order); the key table is read through the
 // constant address space (scalar loads: the key walk never waits on vmcnt).
 // Hand-off safety and the bounded polls: see the rows kernel.
-template <int NSMAX, int PF>
+// UNI: every row load takes the client's address + the window's first column
+// as its base and the window's columns as its range, so a key's ragged last
+// window loads through the same instructions as a full one (lanes past it
+// read 0).  Without it a ragged window reloads every row again after the
+// squares (round 5's form), and the compiler, merging the two load paths,
+// waits for all of a wave's rows at the start of its turn.
+template <int NSMAX, int PF, bool UNI = true>
 __global__ __launch_bounds__(64 * NSMAX, win_min_waves(64, 1)) void reduce_sqdist_segwinf_kernel(
     const SegKey* __restrict__ keys, const int64_t* __restrict__ ptrs, int64_t n_keys, int64_t units, int K,
     const float* __restrict__ W, float* __restrict__ out, double* __restrict__ partials) {
@@ -1202,6 +1208,13 @@ __global__ __launch_bounds__(64 * NSMAX, win_min_waves(64, 1)) void reduce_sqdis
                                                      r0 + i < Kw ? static_cast<int>(nrec) : 0, 0x00020000),
                    static_cast<int>(voff), static_cast<int>(soff), 2));
   };
+  const auto load_row = [&](int64_t pv, int i, int64_t c0_, int n_, int Kw) __attribute__((always_inline)) {
+    return __builtin_bit_cast(
+        float, __builtin_amdgcn_raw_buffer_load_b32(
+                   __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(ptr_of(pv, i) + c0_), 0,
+                                                     r0 + i < Kw ? n_ * 4 : 0, 0x00020000),
+                   static_cast<int>(voff), 0, 2));
+  };
   float x[KH];
   float xp[PF];
   const auto load_slow = [&](int64_t pv, int64_t c0, int n, int Kw) __attribute__((always_inline)) {
@@ -1241,7 +1254,10 @@ __global__ __launch_bounds__(64 * NSMAX, win_min_waves(64, 1)) void reduce_sqdis
       locate(u + G, jn, c0n, nn);
       pvn = load_ptrs(ptrs + static_cast<int64_t>(jn) * K);
     }
-    if (n == WC) {
+    if constexpr (UNI) {
+#pragma unroll
+      for (int i = 0; i < KH; ++i) x[i] = load_row(pv0, i, c0, n, K);
+    } else if (n == WC) {
 #pragma unroll
       for (int i = 0; i < KH; ++i)
         x[i] = load_fast(pv0, i, static_cast<uint32_t>(c0 * 4), static_cast<uint32_t>((c0 + WC) * 4), K);
@@ -1249,16 +1265,20 @@ __global__ __launch_bounds__(64 * NSMAX, win_min_waves(64, 1)) void reduce_sqdis
       load_slow(pv0, c0, n, K);
     }
   }
+  // the first window's rows in: without this wait the compiler merges the
+  // prologue's pending row loads into the loop's state and waits for ALL of
+  // a wave's rows at every turn (vmcnt(PF)) instead of row by row
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   int seq = 0;
   for (; u < units32; u += G, ++seq) {
     const int64_t out_off = kc[j].out_offset;
     const int un = u + G, unn = un + G;
     const bool fastn = un < units32 && nn == WC;
     const uint32_t soffn = static_cast<uint32_t>(c0n * 4), nrecn = static_cast<uint32_t>((c0n + WC) * 4);
-    int Kwn = fastn ? K : 0;
+    int Kwn = (UNI ? un < units32 : fastn) ? K : 0;
     asm volatile("" : "+s"(Kwn));
 #pragma unroll
-    for (int i = 0; i < PF; ++i) xp[i] = load_fast(pvn, i, soffn, nrecn, Kwn);
+    for (int i = 0; i < PF; ++i) xp[i] = UNI ? load_row(pvn, i, c0n, nn, Kwn) : load_fast(pvn, i, soffn, nrecn, Kwn);
     // the turn
     float a = -0.0f;  // fl32(-0.0 + p) is p, bit for bit
     if (h > 0) {
@@ -1311,13 +1331,13 @@ __global__ __launch_bounds__(64 * NSMAX, win_min_waves(64, 1)) void reduce_sqdis
         if (i < PF)
           x[i] = xp[i < PF ? i : 0];
         else
-          x[i] = load_fast(pvn, i, soffn, nrecn, Kwn);
+          x[i] = UNI ? load_row(pvn, i, c0n, nn, Kwn) : load_fast(pvn, i, soffn, nrecn, Kwn);
       }
       const double q01 = fold32(p[0], p[1]), q23 = fold32(p[2], p[3]);
       const double q45 = fold32(p[4], p[5]), q67 = fold32(p[6], p[7]);
       acc[64 * b] += fold8(fold16(q01, q23), fold16(q45, q67), upper);
     }
-    if (un < units32 && !fastn) {
+    if (!UNI && un < units32 && !fastn) {
       int Ks = K;
       asm volatile("" : "+s"(Ks));
       load_slow(pvn, c0n, nn, Ks);
@@ -1353,6 +1373,16 @@ constexpr int kSegWinfPF8 = 8, kSegWinfPF16 = 16;  // prefetched rows at <= 8 / 
 inline bool seg_barrier_windows() {
   static const bool on = [] {
     const char* e = std::getenv("FEDAVG_SEGWINN_BARRIER");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
+// FEDAVG_SEGWINF_TWO_PATHS=1: the hand-off kernel with round 5's separate
+// ragged-window reload (A/B against the uniform row loads)
+inline bool seg_split_two_paths() {
+  static const bool on = [] {
+    const char* e = std::getenv("FEDAVG_SEGWINF_TWO_PATHS");
     return e && e[0] == '1';
   }();
   return on;
@@ -1664,6 +1694,13 @@ int launch_seg_fused(const SegFusedPlan& p, const SegKey* keys, const int64_t* t
       else
         hipLaunchKernelGGL((reduce_sqdist_segwinn_kernel<16>), grid, block, 0, s, keys, tptrs, n_keys, units, k32,
                            weights, out, partials);
+    } else if (seg_split_two_paths()) {  // A/B: ragged windows reloaded after the squares
+      if (ns <= 8)
+        hipLaunchKernelGGL((reduce_sqdist_segwinf_kernel<8, kSegWinfPF8, false>), grid, block, 0, s, keys, tptrs,
+                           n_keys, units, k32, weights, out, partials);
+      else
+        hipLaunchKernelGGL((reduce_sqdist_segwinf_kernel<16, kSegWinfPF16, false>), grid, block, 0, s, keys, tptrs,
+                           n_keys, units, k32, weights, out, partials);
     } else if (ns <= 8) {
       hipLaunchKernelGGL((reduce_sqdist_segwinf_kernel<8, kSegWinfPF8>), grid, block, 0, s, keys, tptrs, n_keys, units,
                          k32, weights, out, partials);
