@@ -147,6 +147,14 @@ __device__ __forceinline__ int64_t wave_search_last_le(Start start, int64_t n, i
 // round trip per step, 12 per fp64 sum) serialises ~6 LDS latencies per sum;
 // the per-client sums of the :291 pass do one per client row.  Same addends,
 // fixed order: deterministic, but not the shfl tree's bits.
+// Timeline probes of the split windows (MODE 8): lane 0 of every wave of the
+// first kStampBlocks workgroups stores s_memtime at up to kStampSlots points
+// of its first kStampWins windows, after the K x G partials, behind a magic
+// word (scripts/winn_timeline.py reads them)
+constexpr int kStampBlocks = 8, kStampWins = 48, kStampSlots = 8;
+constexpr uint64_t kStampMagic = 0x504D415453ull;  // "STAMP"
+inline int64_t winn_stamp_elems(int nsmax) { return 1 + int64_t(kStampBlocks) * nsmax * kStampWins * kStampSlots; }
+
 // f(std::integral_constant<int, I>{}) for I = 0 .. N-1, unrolled at compile
 // time (DPP controls must be constants)
 template <class F, int... Is>

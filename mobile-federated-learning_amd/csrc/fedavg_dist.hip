@@ -1212,9 +1212,6 @@ int launch_fused_win(const float* clients, int64_t K, int64_t P, int64_t ld, con
 // ---------------------------------------------------------------------------
 // s_waitcnt vmcnt(0) expcnt(7) lgkmcnt(15) (gfx9 encoding: vmcnt in [3:0] and [15:14])
 constexpr int kWaitVmcnt0 = 0x0F70;
-constexpr int kStampBlocks = 8, kStampWins = 48, kStampSlots = 8;
-constexpr uint64_t kStampMagic = 0x504D415453ull;  // "STAMP"
-inline int64_t winn_stamp_elems(int nsmax) { return 1 + int64_t(kStampBlocks) * nsmax * kStampWins * kStampSlots; }
 
 template <int KH, int VEC, int NSMAX, int PF = 0, int LE = 0, int MODE = 0>
 __global__ __launch_bounds__(64 * NSMAX, win_min_waves(KH, VEC)) void reduce_sqdist_winn_kernel(
@@ -2699,6 +2696,7 @@ int fedavg_reduce_sqdist_f32_variant(const float* clients, int64_t K, int64_t P,
     FEDAVG_WINF_CASE(8, 8, 1)
     FEDAVG_WINF_CASE(8, 8, 2)
     FEDAVG_WINF_CASE(8, 16, 1)
+    FEDAVG_WINF_CASE(8, 8, 8)
 #undef FEDAVG_WINF_CASE
     default: return set_error(FEDAVG_EMODE, "%s: cols must be 32, 64, 128 or 256 (+1000: double-buffered)", what);
   }

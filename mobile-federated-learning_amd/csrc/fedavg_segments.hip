@@ -1150,7 +1150,7 @@ __global__ __launch_bounds__(64 * NSMAX, win_min_waves(64, 1)) void reduce_sqdis
 // read 0).  Without it a ragged window reloads every row again after the
 // squares (round 5's form), and the compiler, merging the two load paths,
 // waits for all of a wave's rows at the start of its turn.
-template <int NSMAX, int PF, bool UNI = true>
+template <int NSMAX, int PF, bool UNI = true, int MODE = 0>
 __global__ __launch_bounds__(64 * NSMAX, win_min_waves(64, 1)) void reduce_sqdist_segwinf_kernel(
     const SegKey* __restrict__ keys, const int64_t* __restrict__ ptrs, int64_t n_keys, int64_t units, int K,
     const float* __restrict__ W, float* __restrict__ out, double* __restrict__ partials) {
@@ -1168,6 +1168,19 @@ __global__ __launch_bounds__(64 * NSMAX, win_min_waves(64, 1)) void reduce_sqdis
   __shared__ float part[NSMAX][64];
   __shared__ float avg[64];
   __shared__ int flag[NSMAX + 1];
+  uint64_t* const stamps = reinterpret_cast<uint64_t*>(partials + static_cast<int64_t>(K) * G);
+  int wi = 0;
+  const auto stamp = [&](int ph) __attribute__((always_inline)) {  // MODE 8: the rows kernel's timeline
+    if constexpr ((MODE & 8) != 0) {
+      if (blockIdx.x < kStampBlocks && wi < kStampWins) {
+        const uint64_t t = __builtin_amdgcn_s_memtime();
+        if (lane == 0) stamps[1 + ((int64_t(blockIdx.x) * NSMAX + h) * kStampWins + wi) * kStampSlots + ph] = t;
+      }
+    }
+  };
+  if constexpr ((MODE & 8) != 0) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) stamps[0] = kStampMagic;
+  }
   double* acc = &accl[h][0][lane];
 #pragma unroll
   for (int b = 0; b < NB; ++b) acc[64 * b] = 0.0;
@@ -1277,6 +1290,7 @@ __global__ __launch_bounds__(64 * NSMAX, win_min_waves(64, 1)) void reduce_sqdis
     const uint32_t soffn = static_cast<uint32_t>(c0n * 4), nrecn = static_cast<uint32_t>((c0n + WC) * 4);
     int Kwn = (UNI ? un < units32 : fastn) ? K : 0;
     asm volatile("" : "+s"(Kwn));
+    stamp(0);
 #pragma unroll
     for (int i = 0; i < PF; ++i) xp[i] = UNI ? load_row(pvn, i, c0n, nn, Kwn) : load_fast(pvn, i, soffn, nrecn, Kwn);
     // the turn
@@ -1285,6 +1299,7 @@ __global__ __launch_bounds__(64 * NSMAX, win_min_waves(64, 1)) void reduce_sqdis
       wait_flag(h - 1, seq);
       a = part[h - 1][lane];
     }
+    stamp(2);
     __builtin_amdgcn_s_setprio(3);
     {
       float tc = mul_row_bcast<0>(wv[0], x[0]);
@@ -1302,6 +1317,7 @@ __global__ __launch_bounds__(64 * NSMAX, win_min_waves(64, 1)) void reduce_sqdis
       publish(NSMAX, seq);
       if (lane < n) out[out_off + c0 + lane] = a;
     }
+    stamp(3);
     if (h < ns - 1) {
       __builtin_amdgcn_s_setprio(0);
       wait_flag(NSMAX, seq);
@@ -1343,6 +1359,8 @@ __global__ __launch_bounds__(64 * NSMAX, win_min_waves(64, 1)) void reduce_sqdis
       load_slow(pvn, c0n, nn, Ks);
     }
     __builtin_amdgcn_s_setprio(0);
+    stamp(4);
+    ++wi;
     j = jn;
     c0 = c0n;
     n = nn;
@@ -1383,6 +1401,16 @@ inline bool seg_barrier_windows() {
 inline bool seg_split_two_paths() {
   static const bool on = [] {
     const char* e = std::getenv("FEDAVG_SEGWINF_TWO_PATHS");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
+// FEDAVG_SEGWINF_STAMPS=1: the hand-off kernel's timeline build (MODE 8;
+// the partials grow by winn_stamp_elems)
+inline bool seg_split_stamps() {
+  static const bool on = [] {
+    const char* e = std::getenv("FEDAVG_SEGWINF_STAMPS");
     return e && e[0] == '1';
   }();
   return on;
@@ -1694,6 +1722,15 @@ int launch_seg_fused(const SegFusedPlan& p, const SegKey* keys, const int64_t* t
       else
         hipLaunchKernelGGL((reduce_sqdist_segwinn_kernel<16>), grid, block, 0, s, keys, tptrs, n_keys, units, k32,
                            weights, out, partials);
+    } else if (seg_split_stamps()) {  // timeline probe
+      if (partial_elems < K * p.waves + winn_stamp_elems(16))
+        return set_error(FEDAVG_EINVAL, "%s: the timeline needs %lld more doubles", what, (long long)winn_stamp_elems(16));
+      if (ns <= 8)
+        hipLaunchKernelGGL((reduce_sqdist_segwinf_kernel<8, kSegWinfPF8, true, 8>), grid, block, 0, s, keys, tptrs,
+                           n_keys, units, k32, weights, out, partials);
+      else
+        hipLaunchKernelGGL((reduce_sqdist_segwinf_kernel<16, kSegWinfPF16, true, 8>), grid, block, 0, s, keys, tptrs,
+                           n_keys, units, k32, weights, out, partials);
     } else if (seg_split_two_paths()) {  // A/B: ragged windows reloaded after the squares
       if (ns <= 8)
         hipLaunchKernelGGL((reduce_sqdist_segwinf_kernel<8, kSegWinfPF8, false>), grid, block, 0, s, keys, tptrs,
@@ -1914,7 +1951,8 @@ int fedavg_client_sqdist_segments_f32(const int64_t* client_ptrs, const int64_t*
 // that out.  partials : fedavg_reduce_sqdist_segments_partials(K) doubles.
 int64_t fedavg_reduce_sqdist_segments_partials(int64_t K) {
   if (K <= 0 || K > kSegSplitMaxK) return 0;
-  if (K > kSegFusedMaxK) return K * segwinn_blocks(K, INT64_MAX / 2);  // the split-row windows (device round)
+  if (K > kSegFusedMaxK)  // the split-row windows (device round)
+    return K * segwinn_blocks(K, INT64_MAX / 2) + (seg_split_stamps() ? winn_stamp_elems(16) : 0);
   const int S = seg_fused_cols(K);
   const int per_cu = S == 32 ? seg_fused_per_cu_max<32>(K)
                      : (S == 64 ? seg_fused_per_cu_max<64>(K)
@@ -1923,7 +1961,7 @@ int64_t fedavg_reduce_sqdist_segments_partials(int64_t K) {
   const int64_t windows = K * segwin_waves_for(segwin_kmax(K), INT64_MAX / 2);  // a full window launch
   const int64_t split = K >= seg_split_min_k() ? K * segwinn_blocks(K, INT64_MAX / 2) : 0;  // 129-256: split windows
   const int64_t need = tiles > windows ? tiles : windows;
-  return need > split ? need : split;
+  return (need > split ? need : split) + (seg_split_stamps() ? winn_stamp_elems(16) : 0);
 }
 
 int fedavg_reduce_sqdist_segments_f32(const int64_t* client_ptrs, const int64_t* key_numel, const int64_t* key_offset,

@@ -33,6 +33,39 @@ MAGIC = 0x504D415453
 BLOCKS, WINS, SLOTS = 8, 48, 8
 
 
+def stamps_of(wv, K, G, nsmax, ns):
+    """The stamp block after the K x G partials: [blocks, waves, windows, slots]."""
+    st = wv[K * G + 1:K * G + 1 + BLOCKS * nsmax * WINS * SLOTS].reshape(BLOCKS, nsmax, WINS, SLOTS)
+    return st[:, :ns].astype(np.float64)
+
+
+def summarize(st, ns, wins):
+    """Median cycles per window over the steady-state windows 4..wins-2."""
+    sl = slice(4, wins - 1)
+    top, arr, turn, hand, sq, rel = (st[..., i] for i in range(6))
+    have = {n: bool((st[:, :, sl, i] != 0).all()) for i, n in enumerate(("top", "arr", "turn", "hand", "sq", "rel"))}
+    med = lambda a: round(float(np.median(a)), 1)
+    cyc = {"window_period": med((top[:, 0, 1:wins] - top[:, 0, :wins - 1])[:, 3:]),
+           "chain": med(hand[:, ns - 1, sl] - turn[:, 0, sl]), "turn": med((hand - turn)[:, :, sl]),
+           "squares_after_chain_mean": med((sq[:, :, sl] - hand[:, ns - 1, sl][:, None, :]).mean(axis=1)),
+           "squares_after_chain_max": med((sq[:, :, sl] - hand[:, ns - 1, sl][:, None, :]).max(axis=1)),
+           "top_to_turn_wave0": med(turn[:, 0, sl] - top[:, 0, sl]),
+           # the chain's start against the block's previous window: how far it overlaps the reloads
+           "turn0_after_last_squares_prev": med(turn[:, 0, 5:wins] - sq[:, :, 4:wins - 1].max(axis=1)),
+           "turn0_after_first_squares_prev": med(turn[:, 0, 5:wins] - sq[:, :, 4:wins - 1].min(axis=1))}
+    if ns > 1:
+        cyc["handoff"] = med(turn[:, 1:, sl] - hand[:, :-1, sl])
+    if have["arr"]:
+        wait_rows = (arr - top)[:, :, sl]
+        cyc.update(wait_own_rows=med(wait_rows), wait_own_rows_wave0=med(wait_rows[:, 0]),
+                   wait_own_rows_last_wave=med(wait_rows[:, ns - 1]),
+                   last_arrival_to_turn0=med(turn[:, 0, sl] - arr[:, :, sl].max(axis=1)))
+    if have["rel"]:
+        cyc.update(end_barrier=med(rel[:, :, sl] - sq[:, :, sl].max(axis=1)[:, None, :]),
+                   release_to_next_top=med(top[:, :, 5:wins] - rel[:, :, 4:wins - 1]))
+    return cyc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shapes", nargs="*", default=["1000x12500000", "500x11227812"])
@@ -76,35 +109,11 @@ def main():
             if G is None:
                 print(json.dumps({"K": K, "P": P, "code": code, "error": "no stamp header"}), flush=True)
                 continue
-            st = wv[K * G + 1:K * G + 1 + BLOCKS * args.nsmax * WINS * SLOTS].reshape(BLOCKS, args.nsmax, WINS, SLOTS)
-            st = st[:, :ns].astype(np.float64)
+            st = stamps_of(wv, K, G, args.nsmax, ns)
             raw[f"{K}x{P}_{code}"] = st
-            nwin = (P + 63) // 64
-            wins = min(WINS, nwin // G)
-            sl = slice(4, wins - 1)
-            top, arr, turn, hand, sq, rel = (st[..., i] for i in range(6))
-            have = {n: bool((st[:, :, sl, i] != 0).all()) for i, n in enumerate(("top", "arr", "turn", "hand", "sq", "rel"))}
-            med = lambda a: round(float(np.median(a)), 1)
-            cyc = {"window_period": med((top[:, 0, 1:wins] - top[:, 0, :wins - 1])[:, 3:]),
-                   "chain": med(hand[:, ns - 1, sl] - turn[:, 0, sl]), "turn": med((hand - turn)[:, :, sl]),
-                   "squares_after_chain_mean": med((sq[:, :, sl] - hand[:, ns - 1, sl][:, None, :]).mean(axis=1)),
-                   "squares_after_chain_max": med((sq[:, :, sl] - hand[:, ns - 1, sl][:, None, :]).max(axis=1)),
-                   "top_to_turn_wave0": med(turn[:, 0, sl] - top[:, 0, sl]),
-                   # the chain's start against the block's previous window: how far it overlaps the reloads
-                   "turn0_after_last_squares_prev": med(turn[:, 0, 5:wins] - sq[:, :, 4:wins - 1].max(axis=1)),
-                   "turn0_after_first_squares_prev": med(turn[:, 0, 5:wins] - sq[:, :, 4:wins - 1].min(axis=1))}
-            if ns > 1:
-                cyc["handoff"] = med(turn[:, 1:, sl] - hand[:, :-1, sl])
-            if have["arr"]:
-                wait_rows = (arr - top)[:, :, sl]
-                cyc.update(wait_own_rows=med(wait_rows), wait_own_rows_wave0=med(wait_rows[:, 0]),
-                           wait_own_rows_last_wave=med(wait_rows[:, ns - 1]),
-                           last_arrival_to_turn0=med(turn[:, 0, sl] - arr[:, :, sl].max(axis=1)))
-            if have["rel"]:
-                cyc.update(end_barrier=med(rel[:, :, sl] - sq[:, :, sl].max(axis=1)[:, None, :]),
-                           release_to_next_top=med(top[:, :, 5:wins] - rel[:, :, 4:wins - 1]))
-            rec = {"K": K, "P": P, "code": code, "grid": G, "windows_per_block": round(nwin / G, 1),
-                   "ms_median": round(float(np.median(ms)), 4), "cycles_median": cyc}
+            rec = {"K": K, "P": P, "code": code, "grid": G, "windows_per_block": round(((P + 63) // 64) / G, 1),
+                   "ms_median": round(float(np.median(ms)), 4),
+                   "cycles_median": summarize(st, ns, min(WINS, ((P + 63) // 64) // G))}
             print(json.dumps(rec), flush=True)
         del x, work
         torch.cuda.empty_cache()
