@@ -276,7 +276,21 @@ def test_legacy_fused_segments_entry_matches(K):
     """fedavg_reduce_sqdist_segments_f32 (the separate-table entry, integer
     keys converted inside the tiles, no unit map) gives the bits and sums of
     the one-call round on the same clients."""
-    counts, dicts = _clients(K, _SPECS, seed=50 + K)
+    _legacy_entry_matches(K, _SPECS, seed=50 + K)
+
+
+@pytest.mark.parametrize("K", [129, 200])
+def test_legacy_fused_segments_entry_split_windows(K):
+    """The separate-table entry on all-fp32 clients long enough for the
+    zero-copy split windows (129-256 clients, round 6): the one-call round's
+    bits and sums."""
+    specs = [((64, 3, 3, 3), torch.float32), ((127,), torch.float32), ((600_001,), torch.float32),
+             ((0,), torch.float32), ((40_001,), torch.float32)]
+    _legacy_entry_matches(K, specs, seed=70 + K)
+
+
+def _legacy_entry_matches(K, specs, seed):
+    counts, dicts = _clients(K, specs, seed=seed)
     r = _Round(counts, dicts)
     rc, out, sumsq = r.run()
     assert rc == 0
