@@ -1508,7 +1508,8 @@ int launch_fused_winn(const float* clients, int64_t K, int64_t P, int64_t ld, co
 // tests), never in a hung grid.  Weights by row broadcast (chain8_row_bcast).
 // MODE 8: the timeline stamps of the winn kernel.  Probes: MODE 1 polls
 // with s_sleep 1 (the first form), 2 keeps every priority at 0, 4 keeps the
-// turn at the squares' priority.
+// turn at the squares' priority, 16 runs every wave's squares at priority 2, 32 by
+// halves (waves 0-7 at 2, the rest at 1).
 // ---------------------------------------------------------------------------
 constexpr int kHandoffSpinMax = 1 << 16;  // x 16 polls of ~100 clocks (or x s_sleep 1): < 50 ms, a window is ~13 us
 
@@ -1652,7 +1653,14 @@ __global__ __launch_bounds__(64 * NSMAX, win_min_waves(64, 1)) void reduce_sqdis
       a = avg[lane];
     }
     // the squares, the next window's rows reloaded behind them: waves 0-3 first
-    if constexpr (kPrio) {
+    if constexpr ((MODE & 16) != 0) {  // probe: every wave's squares at priority 2
+      __builtin_amdgcn_s_setprio(2);
+    } else if constexpr ((MODE & 32) != 0) {  // probe: halves (waves 0-7 first)
+      if (h < 8)
+        __builtin_amdgcn_s_setprio(2);
+      else
+        __builtin_amdgcn_s_setprio(1);
+    } else if constexpr (kPrio) {
       if (h < 4)
         __builtin_amdgcn_s_setprio(2);
       else if (h < 8)
@@ -2697,6 +2705,10 @@ int fedavg_reduce_sqdist_f32_variant(const float* clients, int64_t K, int64_t P,
     FEDAVG_WINF_CASE(8, 8, 2)
     FEDAVG_WINF_CASE(8, 16, 1)
     FEDAVG_WINF_CASE(8, 8, 8)
+    FEDAVG_WINF_CASE(16, 16, 16)
+    FEDAVG_WINF_CASE(16, 16, 32)
+    FEDAVG_WINF_CASE(8, 8, 16)
+    FEDAVG_WINF_CASE(8, 8, 32)
 #undef FEDAVG_WINF_CASE
     default: return set_error(FEDAVG_EMODE, "%s: cols must be 32, 64, 128 or 256 (+1000: double-buffered)", what);
   }
